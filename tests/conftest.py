@@ -1,0 +1,19 @@
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libkarma_hip.so)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(REPO, "tests", "golden", "golden.json")) as f:
+        return json.load(f)
