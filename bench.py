@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""Benchmark: k-mer profile + shared-read graph build on MI355X (BASELINE.json metric).
+
+One step = the whole hot path over one batch of device-resident synthetic input
+(SURVEY.md §8(d)), per GPU:
+  k-mer profile of 200k contigs (mean 800 bp, k = 5p6): presence pass, column
+  table, dense float64 profile (N x M) written to HBM;
+  shared-read graph of 100M paired fragments (~340M (read, contig) records):
+  pair emission, bucket partition, LDS hash reduce, weights.
+Inputs (2-bit packed contigs + records) are resident in HBM before timing.
+
+Multi-GPU (torchrun, one rank per GPU): weak scaling — rank r owns contig rows
+[r*200k, (r+1)*200k) and fragments [r*100M, (r+1)*100M) of a global problem
+whose genes span all ranks; the step adds the presence OR-allreduce, the edge
+partial all-to-all (pre-reduced pairs routed to the owner of contig a) and the
+totals allgather over RCCL (karma_amd/distributed.py).
+
+Prints ONE JSON line on rank 0.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (seed, contigs per GPU, fragments per GPU, paired, kmer)
+    "config3": (3, 200_000, 100_000_000, True, "5p6"),
+    "config2": (2, 50_000, 10_000_000, True, "5p6"),
+    "config1": (1, 1_000, 100_000, False, 5),
+    "tiny": (7, 5_000, 500_000, True, "5p6"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-sample", type=float, default=0.1,
+                    help="fraction of the per-GPU workload the CPU baseline processes (0 disables)")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+
+    import torch
+
+    from karma_amd import _lib, engine
+    from karma_amd.distributed import Comm, ShardedBuild
+
+    seed, n_loc, f_loc, paired, kmer = CONFIGS[args.config]
+    comm = Comm.create(world, rank, local_rank)
+    ctx = _lib.Context(local_rank if world > 1 else 0)
+    torch.cuda.set_device(local_rank if world > 1 else 0)
+
+    # ---------------- synthetic input (host), then resident in HBM ----------------
+    t_gen = time.time()
+    n_glob, f_glob = n_loc * world, f_loc * world
+    c_lo = rank * n_loc
+    blob, offs, key_len = engine.synth_contigs(seed, n_loc, 400, 800, 0, first=c_lo)
+    genes = engine.synth_genes(seed, n_glob)
+    rec = engine.synth_records(seed, n_glob, rank * f_loc, (rank + 1) * f_loc, paired, genes=genes)
+    A = len(rec)
+    log(f"[rank {rank}] generated {n_loc} contigs ({int(offs[-1])} bases), {f_loc} fragments, {A} records "
+        f"in {time.time() - t_gen:.1f}s")
+
+    build = ShardedBuild(ctx, comm, engine.kmode_of(kmer), n_glob, c_lo, n_loc)  # sets the shared stream
+    store = engine.ContigStore(ctx, blob, offs, key_len)
+    rec_dev = torch.from_numpy(rec.view(np.int64).reshape(-1)).to(build.ops.dev)
+    torch.cuda.synchronize()
+    packed_bytes = int(np.sum((np.diff(offs) + 3) // 4))  # sum ceil(L/4)
+
+    def step(keep=False):
+        return build.run(store, rec_dev.data_ptr(), A, keep=keep)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    if not args.no_timing:
+        ctx.timing(True)
+        ctx.timing_reset()
+    comm.barrier()
+    torch.cuda.synchronize()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    comm.barrier()
+    t1 = time.perf_counter()
+    dt = comm.max_float(t1 - t0)
+    kern = ctx.timing_read() if not args.no_timing else {}
+    ctx.timing(False)
+    st = step(keep=True)  # untimed: sizes for the byte model
+    res.update({k: st[k] for k in ("entries", "pairs_local")})
+
+    units = world * (n_loc + f_loc) * args.steps
+    value = units / dt
+    M = res["M"]
+    E = comm.sum_int(res["E_local"])
+    # algorithmic bytes per launch, DESIGN.md §Measurement
+    per_kernel_bytes = {
+        "kmer_profile": packed_bytes + 8 * n_loc * M,
+        "kmer_presence": packed_bytes,
+        "graph_count": 8 * A,
+        "graph_scatter": 8 * A + 4 * res["entries"],
+        "graph_bucket_reduce": 4 * res["entries"] + 16 * res["pairs_local"],
+    }
+    roof = None
+    if kern:
+        dom = max((k for k in kern if k in per_kernel_bytes), key=lambda k: kern[k][0], default=None)
+        if dom:
+            ms, nl = kern[dom]
+            avg_s = ms / nl / 1e3
+            achieved = per_kernel_bytes[dom] / avg_s / 1e9
+            roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(dom),
+                    "bytes_per_launch": per_kernel_bytes[dom], "avg_launch_ms": round(ms / nl, 4)}
+    step_bytes = packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(seed, n_loc, f_loc, paired, kmer, args.cpu_sample, blob, offs, rec)
+
+    if rank == 0:
+        line = {
+            "metric": "contigs+reads/sec for k-mer vec + shared-read graph build; HBM GB/s vs roofline",
+            "value": round(value, 1),
+            "unit": "(contigs+fragments)/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 keys / i64 counts / f64 div",
+            "data": "synthetic (SplitMix64 generator, SURVEY.md §8(d))",
+            "config": {"workload": f"{args.config}: {n_loc} contigs (mean 800 bp) + {f_loc} "
+                                   f"{'paired' if paired else 'single-end'} fragments per GPU, k={kmer}",
+                       "contigs_per_gpu": n_loc, "fragments_per_gpu": f_loc, "records_per_gpu": A,
+                       "columns_M": M, "edges": E, "parallelism": f"contig+fragment shards x{world}"},
+            "roofline": roof,
+            "step_hbm_bytes_per_gpu": step_bytes,
+            "step_achieved_GBs_per_gpu": round(step_bytes / (dt / args.steps) / 1e9, 1),
+            "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in kern.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    build.close()
+    store.close()
+    comm.close()
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(seed, n_loc, f_loc, paired, kmer, frac, blob, offs, rec):
+    """Oracle (single-threaded C restatement, oracle/) on a bounded sample."""
+    try:
+        from collections import OrderedDict
+
+        from oracle import oracle
+    except Exception as e:  # oracle not built on this box
+        return {"error": f"oracle unavailable: {e}"}
+    ns = max(1, int(n_loc * frac))
+    fs = max(1, int(f_loc * frac))
+    seqs = OrderedDict((f">ctg{i}", bytes(blob[offs[i]:offs[i + 1]]).decode()) for i in range(ns))
+    t0 = time.perf_counter()
+    oracle.calc_kmer_profile(seqs, kmer)
+    t1 = time.perf_counter()
+    r = rec[rec[:, 0] < fs].astype(np.int64)
+    starts = np.flatnonzero(np.r_[True, r[1:, 0] != r[:-1, 0]])
+    off = np.r_[starts, len(r)]
+    t2 = time.perf_counter()
+    oracle.graph_groups(off, r[:, 1], None, None, n_loc, dedup=True)
+    t3 = time.perf_counter()
+    secs = (t1 - t0) + (t3 - t2)
+    return {"value": round((ns + fs) / secs, 1), "unit": "(contigs+fragments)/s", "cores": 1, "kind": "port",
+            "sample": f"{ns} contigs k={kmer} profile ({t1 - t0:.2f}s) + graph of {fs} fragments / {len(r)} records "
+                      f"({t3 - t2:.2f}s) = {frac:.0%} of the per-GPU workload, oracle/ C restatement, 1 thread"}
+
+
+if __name__ == "__main__":
+    main()

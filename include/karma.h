@@ -1,0 +1,171 @@
+/*
+ * karma.h — C ABI of libkarma_hip.so, the MI355X (gfx950) implementation of
+ * lmfaber/karma's k-mer profile + shared-read graph hot path.
+ *
+ * Plain C types only (pointers + sizes); no torch / HIP types in signatures
+ * (streams are passed as void*).  Every function returns an int status
+ * (KARMA_OK = 0, negative = error; message via karma_last_error()).
+ *
+ * Reference interfaces replaced (file:line under lmfaber/karma):
+ *   karma_contigs_*, karma_kmer_*   KmerClustering.__calc_kmer_profile   karma/kmer.py:199-264
+ *                                   (__extract_kmers :146-179, __kmers_of_seq :181-197,
+ *                                    __count_kmer_occurence :56-92, fill_array_for_contig :108-122,
+ *                                    is_palindrome :46-54)
+ *   karma_graph_records             ReadGraph.from_contigs               karma/read_graph.py:19-50
+ *                                   + Contig readsets                    karma/contig.py:4-35
+ *                                   and ReadGraph.update_graph           karma/read_graph.py:192-221
+ *   karma_graph_eq                  ReadGraph.from_equivalence_classes   karma/read_graph.py:61-148
+ *   karma_pairs_merge / _totals     (new) multi-GPU edge merge, SURVEY.md §8(e)
+ *   karma_edges_*                   the normalised weight (s/|A| + s/|B|)/2  read_graph.py:39-42, :128-130
+ *   karma_synth_*                   (new) deterministic synthetic inputs, SURVEY.md §8(d)
+ *
+ * The reference is pure Python and has no FFI; INTEGRATION.md shows the ctypes
+ * binding (karma_amd/_lib.py) that the Python classes mirroring the reference
+ * API (karma_amd/kmer.py, read_graph.py, contig.py) use.
+ */
+#ifndef KARMA_H
+#define KARMA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------- */
+#define KARMA_OK 0
+#define KARMA_ERR_ARG (-1)       /* invalid argument / unsupported size                       */
+#define KARMA_ERR_KMER (-2)      /* unsupported k (supported: 1..8 and "5p6")                 */
+#define KARMA_ERR_HIP (-3)       /* HIP runtime error (no device, launch failure, ...)        */
+#define KARMA_ERR_OOM (-4)       /* device allocation failed                                  */
+#define KARMA_ERR_ZERO_DIV (-5)  /* non-zero count over a zero normaliser (ZeroDivisionError) */
+#define KARMA_ERR_UNSORTED (-6)  /* records not grouped by read (read ids must not decrease)  */
+#define KARMA_ERR_STATE (-7)     /* call out of order (e.g. profile before finalize)          */
+
+#define KARMA_KMER_5P6 (-1) /* kmer.py:69 "5p6": all 5-mers + string-palindromic 6-mers */
+
+int karma_version(void);
+const char* karma_last_error(void);
+int karma_device_count(int* n);
+
+/* ---- context: one device, one HIP stream --------------------------------- */
+typedef struct karma_ctx karma_ctx;
+int karma_ctx_create(int device, karma_ctx** out);
+int karma_ctx_destroy(karma_ctx* ctx);
+/* Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int karma_ctx_set_stream(karma_ctx* ctx, void* hip_stream);
+int karma_ctx_sync(karma_ctx* ctx);
+/* Per-kernel HIP-event timing on the launch stream (for bench.py's roofline). */
+int karma_timing_enable(karma_ctx* ctx, int on);
+int karma_timing_reset(karma_ctx* ctx);
+/* Fills up to cap entries: name (NUL-separated into names[cap*64]), total ms, launches.
+ * Returns number of distinct kernels in *n. Synchronises the stream. */
+int karma_timing_read(karma_ctx* ctx, char* names, double* total_ms, int64_t* launches, int cap, int* n);
+
+/* ---- device memory helpers (for callers without their own allocator) ------ */
+int karma_dev_alloc(karma_ctx* ctx, size_t bytes, void** out);
+int karma_dev_free(karma_ctx* ctx, void* p);
+int karma_memcpy(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int kind /*0 H2D,1 D2H,2 D2D*/);
+
+/* ---- contig store (device-resident, 2-bit packed + exception mask) -------- */
+typedef struct karma_contigs karma_contigs;
+/* seq: concatenated sequence bytes (latin-1 code points of the reference's str
+ * values), offsets[n+1] into seq, key_len[n] = len(FASTA dict key) — the
+ * reference's normaliser (kmer.py:213 iterates the dict's keys).
+ * is_device = 0: host pointers, copied; 1: device pointers, referenced (must
+ * outlive the store).  Packs A,C,G,T to 2 bits on the device; any other byte is
+ * an exception base handled through a byte-key path. */
+int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offsets, const int32_t* key_len,
+                         int64_t n, int is_device, karma_contigs** out);
+int karma_contigs_destroy(karma_contigs* c);
+int karma_contigs_info(karma_contigs* c, int64_t* n, int64_t* total_bases, int64_t* exception_bases,
+                       int64_t* packed_bytes);
+
+/* ---- k-mer profile (kmer.py:146-264) -------------------------------------- */
+typedef struct karma_kmer_plan karma_kmer_plan;
+/* Presence pass over the (local) contig store. kmode: 1..8 or KARMA_KMER_5P6. */
+int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_kmer_plan** out);
+int karma_kmer_plan_destroy(karma_kmer_plan* p);
+/* Multi-rank exchange points: the ACGT presence bitmap (OR /
+ * max-reduce across ranks) and the non-ACGT ("exception") k-mer keys (union). */
+int karma_kmer_presence_words(karma_kmer_plan* p, int64_t* nwords);
+int karma_kmer_presence_get(karma_kmer_plan* p, uint32_t* dst_dev);
+int karma_kmer_presence_set(karma_kmer_plan* p, const uint32_t* src_dev);
+int karma_kmer_exceptions_count(karma_kmer_plan* p, int64_t* n);
+int karma_kmer_exceptions_get(karma_kmer_plan* p, uint64_t* dst_dev);
+int karma_kmer_exceptions_set(karma_kmer_plan* p, const uint64_t* src_dev, int64_t n);
+/* Column table = sorted() union of present k-mers (kmer.py:172-177). */
+int karma_kmer_plan_finalize(karma_kmer_plan* p, int64_t* M);
+/* Column keys: byte-packed u64, big-endian bytes from bit 63; for k < 8 and 5p6
+ * the low byte holds the k-mer length (so u64 order == Python str order). */
+int karma_kmer_columns(karma_kmer_plan* p, uint64_t* keys_host);
+/* Dense float64 profile, row r = contig r of the store, stride ld >= M:
+ * out[r*ld + col] = count / key_len[r] (kmer.py:120, :231-233), zeros written. */
+int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_device);
+/* Number of k-mer occurrences per contig (0 => the all-zero row of kmer.py:250-258). */
+int karma_kmer_row_totals(karma_kmer_plan* p, int64_t* dst_host);
+
+/* ---- shared-read graph ----------------------------------------------------- */
+/* A pair list: unique keys (a << 32 | b, a <= b) sorted ascending with int64
+ * counts (and, for eq classes, the first emission position). */
+typedef struct karma_pairs karma_pairs;
+#define KARMA_REC_SORTED 0   /* records grouped by read, read ids non-decreasing (SAM order) */
+#define KARMA_REC_UNSORTED 1 /* any order: sorted by read on the device first */
+/* records: n_records x {u32 read_id, u32 contig} interleaved.  Deduplicates
+ * (read, contig) (contig.py:11 keeps QNAMEs in a set); emits for every read's
+ * contig set S every pair a <= b of S: the diagonal (a, a) counts |readset(a)|,
+ * (a, b) counts |R_a ∩ R_b| (read_graph.py:34). */
+int karma_graph_records(karma_ctx* ctx, const uint32_t* records, int64_t n_records, int64_t n_contigs, int flags,
+                        int is_device, karma_pairs** out);
+/* Salmon eq classes (read_graph.py:75-114): cls_off[n_classes+1] into members
+ * (contig indices as listed, duplicates kept), counts[n_classes], pair_skip[c]=1
+ * when the eq_size token is "1" (read_graph.py:102).  Totals (read_graph.py:86-92)
+ * go to the pair list's totals array; pairs carry first-emission positions. */
+int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
+                   const uint8_t* pair_skip, int64_t n_classes, int64_t n_contigs, int is_device, karma_pairs** out);
+/* Merge (key, count) lists in any order into one sorted unique list (exchange merge). */
+int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, int64_t n, int is_device,
+                      karma_pairs** out);
+int karma_pairs_destroy(karma_pairs* p);
+int karma_pairs_count(karma_pairs* p, int64_t* n);
+/* Device pointers of the list (valid until destroy): keys u64[n], counts i64[n]. */
+int karma_pairs_device(karma_pairs* p, const uint64_t** keys, const int64_t** counts);
+int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* first, int is_device);
+/* Index of the first key with a >= bounds[r] for r = 0..nranks (host out). */
+int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts);
+/* totals[c] = count of the diagonal pair (c, c) (readset sizes) for c in [0, n_contigs). */
+int karma_pairs_totals(karma_pairs* p, int64_t* totals_dev, int64_t n_contigs);
+
+typedef struct karma_edges karma_edges;
+#define KARMA_MODE_READS 0 /* diagonal = readset sizes; off-diagonal = shared reads   */
+#define KARMA_MODE_EQ 1    /* totals from the eq pass; diagonal pairs are self-loops */
+/* Edges with non-zero shared count and weight (s/tot[a] + s/tot[b]) / 2.
+ * totals_dev: int64[n_contigs] device array, or NULL to take it from the pair
+ * list (diagonal in READS mode, eq totals in EQ mode). */
+int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64_t* totals_dev, int64_t n_contigs,
+                           karma_edges** out, int64_t* n_edges);
+int karma_edges_destroy(karma_edges* e);
+/* Any output pointer may be NULL. first is only meaningful in EQ mode. */
+int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* shared, double* weight, uint64_t* first,
+                    int is_device);
+int karma_edges_totals(karma_edges* e, int64_t* totals, int is_device);
+
+/* ---- synthetic inputs (spec in karma_amd/synth.py) ------- */
+int karma_synth_contig_lengths(uint64_t seed, int64_t n, int32_t len_min, int32_t len_span, int64_t* lengths);
+/* Fills seq[total] given offsets[n+1] (prefix sums of the lengths). */
+int karma_synth_contig_bases(uint64_t seed, const int64_t* offsets, int64_t n, int32_t n_rate, uint8_t* seq);
+int karma_synth_n_genes(uint64_t seed, int64_t n_contigs, int32_t gene_max, int64_t* n_genes);
+int karma_synth_genes(uint64_t seed, int64_t n_contigs, int32_t gene_max, int64_t* gene_first, int32_t* gene_size);
+/* Records of fragments [frag_lo, frag_hi): per-fragment record counts first
+ * (rec_count[frag_hi-frag_lo]), then the records themselves. */
+int karma_synth_read_counts(uint64_t seed, const int64_t* gene_first, const int32_t* gene_size, int64_t n_genes,
+                            int64_t frag_lo, int64_t frag_hi, int paired, int32_t* rec_count);
+int karma_synth_read_records(uint64_t seed, const int64_t* gene_first, const int32_t* gene_size, int64_t n_genes,
+                             int64_t frag_lo, int64_t frag_hi, int paired, const int64_t* rec_off, uint32_t* records);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KARMA_H */

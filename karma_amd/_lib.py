@@ -1,0 +1,199 @@
+"""ctypes binding of libkarma_hip.so (C ABI in include/karma.h).
+
+This is the ONLY way the package reaches the compute path: there is no CPU
+fallback.  If the library is missing or no gfx950 device is visible, every
+entry point raises KarmaError — loudly — instead of computing something else.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkarma_hip.so")
+
+KARMA_OK = 0
+KARMA_ERR_ARG = -1
+KARMA_ERR_KMER = -2
+KARMA_ERR_HIP = -3
+KARMA_ERR_OOM = -4
+KARMA_ERR_ZERO_DIV = -5
+KARMA_ERR_UNSORTED = -6
+KARMA_ERR_STATE = -7
+
+KARMA_KMER_5P6 = -1
+KARMA_REC_SORTED = 0
+KARMA_REC_UNSORTED = 1
+KARMA_MODE_READS = 0
+KARMA_MODE_EQ = 1
+
+_c_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_u64 = ctypes.c_uint64
+_PP = ctypes.POINTER(ctypes.c_void_p)
+_I64P = ctypes.POINTER(ctypes.c_int64)
+
+# name -> (restype is int status, argtypes)
+_SIGS = {
+    "karma_version": [],
+    "karma_device_count": [ctypes.POINTER(ctypes.c_int)],
+    "karma_ctx_create": [_i32, _PP],
+    "karma_ctx_destroy": [_c_p],
+    "karma_ctx_set_stream": [_c_p, _c_p],
+    "karma_ctx_sync": [_c_p],
+    "karma_timing_enable": [_c_p, _i32],
+    "karma_timing_reset": [_c_p],
+    "karma_timing_read": [_c_p, ctypes.c_char_p, _c_p, _c_p, _i32, ctypes.POINTER(ctypes.c_int)],
+    "karma_dev_alloc": [_c_p, ctypes.c_size_t, _PP],
+    "karma_dev_free": [_c_p, _c_p],
+    "karma_memcpy": [_c_p, _c_p, _c_p, ctypes.c_size_t, _i32],
+    "karma_contigs_create": [_c_p, _c_p, _c_p, _c_p, _i64, _i32, _PP],
+    "karma_contigs_destroy": [_c_p],
+    "karma_contigs_info": [_c_p, _I64P, _I64P, _I64P, _I64P],
+    "karma_kmer_plan_create": [_c_p, _c_p, _i32, _PP],
+    "karma_kmer_plan_destroy": [_c_p],
+    "karma_kmer_presence_words": [_c_p, _I64P],
+    "karma_kmer_presence_get": [_c_p, _c_p],
+    "karma_kmer_presence_set": [_c_p, _c_p],
+    "karma_kmer_exceptions_count": [_c_p, _I64P],
+    "karma_kmer_exceptions_get": [_c_p, _c_p],
+    "karma_kmer_exceptions_set": [_c_p, _c_p, _i64],
+    "karma_kmer_plan_finalize": [_c_p, _I64P],
+    "karma_kmer_columns": [_c_p, _c_p],
+    "karma_kmer_profile": [_c_p, _c_p, _i64, _i32],
+    "karma_kmer_row_totals": [_c_p, _c_p],
+    "karma_graph_records": [_c_p, _c_p, _i64, _i64, _i32, _i32, _PP],
+    "karma_graph_eq": [_c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i64, _i32, _PP],
+    "karma_pairs_merge": [_c_p, _c_p, _c_p, _i64, _i32, _PP],
+    "karma_pairs_destroy": [_c_p],
+    "karma_pairs_count": [_c_p, _I64P],
+    "karma_pairs_device": [_c_p, _PP, _PP],
+    "karma_pairs_get": [_c_p, _c_p, _c_p, _c_p, _i32],
+    "karma_pairs_split": [_c_p, _c_p, _i32, _c_p],
+    "karma_pairs_totals": [_c_p, _c_p, _i64],
+    "karma_edges_from_pairs": [_c_p, _c_p, _i32, _c_p, _i64, _PP, _I64P],
+    "karma_edges_destroy": [_c_p],
+    "karma_edges_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _i32],
+    "karma_edges_totals": [_c_p, _c_p, _i32],
+    "karma_synth_contig_lengths": [_u64, _i64, _i32, _i32, _c_p],
+    "karma_synth_contig_bases": [_u64, _c_p, _i64, _i32, _c_p],
+    "karma_synth_n_genes": [_u64, _i64, _i32, _I64P],
+    "karma_synth_genes": [_u64, _i64, _i32, _c_p, _c_p],
+    "karma_synth_read_counts": [_u64, _c_p, _c_p, _i64, _i64, _i64, _i32, _c_p],
+    "karma_synth_read_records": [_u64, _c_p, _c_p, _i64, _i64, _i64, _i32, _c_p, _c_p],
+}
+
+EXPORTED = tuple(_SIGS) + ("karma_last_error",)
+
+
+class KarmaError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libkarma_hip error {code}: {msg}")
+        self.code = code
+
+
+_LIB = None
+
+
+def load():
+    """Load libkarma_hip.so (no GPU needed to load; compute calls need one)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise KarmaError(KARMA_ERR_HIP, f"{LIB_PATH} not built — run `make -C karma_amd/csrc` "
+                                        "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    lib.karma_last_error.argtypes = []
+    lib.karma_last_error.restype = ctypes.c_char_p
+    _LIB = lib
+    return lib
+
+
+def check(rc):
+    if rc != KARMA_OK:
+        msg = load().karma_last_error().decode(errors="replace")
+        raise KarmaError(rc, msg)
+    return rc
+
+
+def call(name, *args):
+    return check(getattr(load(), name)(*args))
+
+
+def ptr(a):
+    """Host numpy array -> c_void_p (None for None)."""
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class Context:
+    """One HIP device + stream (karma_ctx).  Objects created from it must be
+    destroyed before it (they are, through their own close())."""
+
+    def __init__(self, device=0):
+        lib = load()
+        n = ctypes.c_int(0)
+        rc = lib.karma_device_count(ctypes.byref(n))
+        if rc != KARMA_OK or n.value == 0:
+            raise KarmaError(KARMA_ERR_HIP, "no HIP device visible: libkarma_hip needs an MI355X (gfx950); "
+                                            "there is no CPU fallback")
+        h = ctypes.c_void_p()
+        call("karma_ctx_create", device, ctypes.byref(h))
+        self.h = h
+        self.device = device
+
+    def set_stream(self, stream_ptr):
+        call("karma_ctx_set_stream", self.h, ctypes.c_void_p(stream_ptr) if stream_ptr else None)
+
+    def sync(self):
+        call("karma_ctx_sync", self.h)
+
+    def timing(self, on=True):
+        call("karma_timing_enable", self.h, 1 if on else 0)
+
+    def timing_reset(self):
+        call("karma_timing_reset", self.h)
+
+    def timing_read(self, cap=64):
+        names = ctypes.create_string_buffer(64 * cap)
+        ms = np.zeros(cap, np.float64)
+        cnt = np.zeros(cap, np.int64)
+        n = ctypes.c_int(0)
+        call("karma_timing_read", self.h, names, ptr(ms), ptr(cnt), cap, ctypes.byref(n))
+        out = {}
+        raw = names.raw
+        for i in range(min(n.value, cap)):
+            nm = raw[64 * i:64 * (i + 1)].split(b"\0", 1)[0].decode()
+            out[nm] = (float(ms[i]), int(cnt[i]))
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().karma_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+_DEFAULT_CTX = {}
+
+
+def default_context(device=0):
+    ctx = _DEFAULT_CTX.get(device)
+    if ctx is None:
+        ctx = _DEFAULT_CTX[device] = Context(device)
+    return ctx

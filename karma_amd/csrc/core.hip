@@ -1,0 +1,228 @@
+// core.hip — context, errors, caching allocator, per-kernel event timing.
+#include <cstdarg>
+#include <cstring>
+
+#include "karma_internal.h"
+
+namespace karma {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+int ctx_begin(karma_ctx* ctx) {
+    KARMA_CHECK(ctx, KARMA_ERR_ARG, "null karma_ctx");
+    KARMA_HIP(hipSetDevice(ctx->device));
+    return KARMA_OK;
+}
+
+int ctx_alloc(karma_ctx* ctx, size_t bytes, void** out) {
+    bytes = (bytes + 255) & ~size_t(255);
+    auto it = ctx->free_list.find(bytes);
+    if (it != ctx->free_list.end()) {
+        *out = it->second;
+        ctx->free_list.erase(it);
+        ctx->cached_bytes -= bytes;
+        ctx->live[*out] = bytes;
+        return KARMA_OK;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        // drop the cache and retry once
+        (void)hipGetLastError();
+        hipStreamSynchronize(ctx->stream);
+        for (auto& kv : ctx->free_list) hipFree(kv.second);
+        ctx->free_list.clear();
+        ctx->cached_bytes = 0;
+        e = hipMalloc(&p, bytes);
+    }
+    if (e != hipSuccess) {
+        set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        return KARMA_ERR_OOM;
+    }
+    ctx->live[p] = bytes;
+    *out = p;
+    return KARMA_OK;
+}
+
+void ctx_free(karma_ctx* ctx, void* p) {
+    if (!p || !ctx) return;
+    auto it = ctx->live.find(p);
+    if (it == ctx->live.end()) return;
+    // stream-ordered reuse: later work on the same stream runs after earlier frees' readers
+    ctx->free_list.emplace(it->second, p);
+    ctx->cached_bytes += it->second;
+    ctx->live.erase(it);
+}
+
+void timing_start(karma_ctx* ctx, const char* name, hipEvent_t* ev_stop) {
+    *ev_stop = nullptr;
+    if (!ctx->timing) return;
+    hipEvent_t a, b;
+    if (ctx->event_pool.size() >= 2) {
+        a = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        b = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+    } else {
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+    }
+    hipEventRecord(a, ctx->stream);
+    ctx->launches.push_back({name, a, b});
+    *ev_stop = b;
+}
+
+void timing_stop(karma_ctx* ctx, hipEvent_t ev_stop) {
+    if (ev_stop) hipEventRecord(ev_stop, ctx->stream);
+}
+
+}  // namespace karma
+
+using namespace karma;
+
+extern "C" {
+
+int karma_version(void) { return 1; }
+
+const char* karma_last_error(void) { return g_err.c_str(); }
+
+int karma_device_count(int* n) {
+    KARMA_CHECK(n, KARMA_ERR_ARG, "null out");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *n = 0;
+        set_error("hipGetDeviceCount: %s", hipGetErrorString(e));
+        return KARMA_ERR_HIP;
+    }
+    *n = c;
+    return KARMA_OK;
+}
+
+int karma_ctx_create(int device, karma_ctx** out) {
+    KARMA_CHECK(out, KARMA_ERR_ARG, "null out");
+    int n = 0;
+    KARMA_HIP(hipGetDeviceCount(&n));
+    KARMA_CHECK(device >= 0 && device < n, KARMA_ERR_ARG, "device %d out of range (%d devices)", device, n);
+    KARMA_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    KARMA_HIP(hipGetDeviceProperties(&prop, device));
+    KARMA_CHECK(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, KARMA_ERR_HIP,
+                "device %d is %s; libkarma_hip is built for gfx950 only", device, prop.gcnArchName);
+    karma_ctx* ctx = new karma_ctx();
+    ctx->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        set_error("hipStreamCreate: %s", hipGetErrorString(e));
+        return KARMA_ERR_HIP;
+    }
+    ctx->stream = ctx->own_stream;
+    *out = ctx;
+    return KARMA_OK;
+}
+
+int karma_ctx_destroy(karma_ctx* ctx) {
+    if (!ctx) return KARMA_OK;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->free_list) hipFree(kv.second);
+    for (auto& kv : ctx->live) hipFree(kv.first);
+    for (auto& l : ctx->launches) {
+        hipEventDestroy(l.start);
+        hipEventDestroy(l.stop);
+    }
+    for (auto e : ctx->event_pool) hipEventDestroy(e);
+    if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return KARMA_OK;
+}
+
+int karma_ctx_set_stream(karma_ctx* ctx, void* s) {
+    KARMA_CHECK(ctx, KARMA_ERR_ARG, "null ctx");
+    ctx->stream = s ? static_cast<hipStream_t>(s) : ctx->own_stream;
+    return KARMA_OK;
+}
+
+int karma_ctx_sync(karma_ctx* ctx) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    return KARMA_OK;
+}
+
+int karma_timing_enable(karma_ctx* ctx, int on) {
+    KARMA_CHECK(ctx, KARMA_ERR_ARG, "null ctx");
+    ctx->timing = on != 0;
+    return KARMA_OK;
+}
+
+int karma_timing_reset(karma_ctx* ctx) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    for (auto& l : ctx->launches) {
+        ctx->event_pool.push_back(l.start);
+        ctx->event_pool.push_back(l.stop);
+    }
+    ctx->launches.clear();
+    return KARMA_OK;
+}
+
+int karma_timing_read(karma_ctx* ctx, char* names, double* total_ms, int64_t* launches, int cap, int* n) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<std::string> order;
+    std::map<std::string, std::pair<double, int64_t>> acc;
+    for (auto& l : ctx->launches) {
+        float ms = 0.f;
+        KARMA_HIP(hipEventElapsedTime(&ms, l.start, l.stop));
+        auto it = acc.find(l.name);
+        if (it == acc.end()) {
+            order.push_back(l.name);
+            acc[l.name] = {ms, 1};
+        } else {
+            it->second.first += ms;
+            it->second.second += 1;
+        }
+    }
+    int k = 0;
+    for (auto& nm : order) {
+        if (k >= cap) break;
+        std::strncpy(names + 64 * k, nm.c_str(), 63);
+        names[64 * k + 63] = 0;
+        total_ms[k] = acc[nm].first;
+        launches[k] = acc[nm].second;
+        ++k;
+    }
+    *n = (int)order.size();
+    return KARMA_OK;
+}
+
+int karma_dev_alloc(karma_ctx* ctx, size_t bytes, void** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    return ctx_alloc(ctx, bytes, out);
+}
+
+int karma_dev_free(karma_ctx* ctx, void* p) {
+    KARMA_TRY(ctx_begin(ctx));
+    ctx_free(ctx, p);
+    return KARMA_OK;
+}
+
+int karma_memcpy(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {
+    KARMA_TRY(ctx_begin(ctx));
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    KARMA_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    return KARMA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,988 @@
+// graph.hip — contig x contig shared-read graph for gfx950.
+//
+// Reference (lmfaber/karma) being replaced:
+//   ReadGraph.from_contigs          karma/read_graph.py:19-50  (O(N^2) readset intersections)
+//   Contig readsets                 karma/contig.py:4-35       (QNAME set per contig)
+//   ReadGraph.update_graph          karma/read_graph.py:192-221
+//   ReadGraph.from_equivalence_classes karma/read_graph.py:61-148
+//
+// Read-record path (the hot one):
+//   records {u32 read, u32 contig}, grouped by read (SAM order)
+//   K1 graph_count    : per read, dedup its contig set S, count pairs a<=b of S
+//                       per (bucket of a, block)        -> hist[bucket][block]
+//   scan              : exclusive scan of hist (bucket-major)
+//   K3 graph_scatter  : same walk, writes 32-bit entries (a_local << bbits | b)
+//                       into the bucket-partitioned array (one write per pair)
+//   K4 bucket_reduce  : one block per bucket, LDS open-addressing hash (key ->
+//                       count), then LDS bitonic sort -> sorted unique (a,b,count)
+//   assemble          : concatenate buckets -> globally sorted (a << 32 | b, count)
+// The diagonal (a, a) counts |readset(a)| (the normaliser), so one mechanism
+// yields both the shared counts and the totals.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+
+#include "karma_internal.h"
+
+using namespace karma;
+
+struct karma_edges {
+    karma_ctx* ctx = nullptr;
+    int64_t E = 0, n_contigs = 0;
+    DevArray<uint32_t> a, b;
+    DevArray<int64_t> s;
+    DevArray<double> w;
+    DevArray<uint64_t> first;
+    DevArray<int64_t> totals;
+    bool has_first = false;
+};
+
+namespace {
+
+constexpr int kWalkBlock = 256;
+constexpr int kMaxFast = 8;          // register fast path: reads with <= 8 records
+constexpr int kReduceBlock = 512;
+constexpr int kTableCap = 4096;      // LDS hash slots per bucket block (32 KB)
+constexpr int kTile = kReduceBlock * 2;
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+struct Geo {
+    int bw;      // log2 bucket width (contigs per bucket)
+    int bbits;   // bits of b
+    int64_t n_buckets;
+};
+
+int make_geo(int64_t N, Geo* g) {
+    KARMA_CHECK(N >= 1 && N <= (int64_t(1) << 24), KARMA_ERR_ARG, "n_contigs %lld out of range [1, 2^24]",
+                (long long)N);
+    int bbits = 1;
+    while ((int64_t(1) << bbits) < N) ++bbits;
+    int bw = 4;
+    while ((N >> bw) > 2048 && bw + 1 + bbits <= 31) ++bw;
+    while (bw + bbits > 31) --bw;
+    KARMA_CHECK(bw >= 0, KARMA_ERR_ARG, "n_contigs too large for 32-bit entries");
+    g->bw = bw;
+    g->bbits = bbits;
+    g->n_buckets = (N + (int64_t(1) << bw) - 1) >> bw;
+    return KARMA_OK;
+}
+
+// ---- per-read pair walk -------------------------------------------------------
+// Calls emit(a, b) for every pair a <= b of the read's deduplicated contig set.
+template <typename Emit>
+__device__ __forceinline__ void read_pairs(const uint2* __restrict__ rec, int64_t A, int64_t i, Emit emit) {
+    const uint32_t rid = rec[i].x;
+    uint32_t m[kMaxFast];
+    int64_t j = i;
+#pragma unroll
+    for (int t = 0; t < kMaxFast; ++t) {
+        uint32_t v = kEmpty;
+        if (j < A) {
+            uint2 r = rec[j];
+            if (r.x == rid) {
+                v = r.y;
+                ++j;
+            }
+        }
+        m[t] = v;
+    }
+    const bool big = (j < A) && rec[j].x == rid;
+    if (!big) {
+        // sorting network (Batcher odd-even merge for 8), compile-time indices only
+#define CE(x, y)                                    \
+    {                                               \
+        uint32_t lo_ = min(m[x], m[y]), hi_ = max(m[x], m[y]); \
+        m[x] = lo_;                                 \
+        m[y] = hi_;                                 \
+    }
+        CE(0, 1) CE(2, 3) CE(4, 5) CE(6, 7)
+        CE(0, 2) CE(1, 3) CE(4, 6) CE(5, 7)
+        CE(1, 2) CE(5, 6)
+        CE(0, 4) CE(1, 5) CE(2, 6) CE(3, 7)
+        CE(2, 4) CE(3, 5)
+        CE(1, 2) CE(3, 4) CE(5, 6)
+#undef CE
+        bool keep[kMaxFast];
+#pragma unroll
+        for (int p = 0; p < kMaxFast; ++p) keep[p] = m[p] != kEmpty && (p == 0 || m[p] != m[p - 1]);
+#pragma unroll
+        for (int p = 0; p < kMaxFast; ++p) {
+#pragma unroll
+            for (int q = p; q < kMaxFast; ++q) {
+                if (keep[p] && keep[q]) emit(m[p], m[q]);
+            }
+        }
+        return;
+    }
+    // slow path: arbitrary read size, O(m^3) over global memory (rare: reads
+    // mapping to more than 8 records)
+    int64_t end = j;
+    while (end < A && rec[end].x == rid) ++end;
+    for (int64_t p = i; p < end; ++p) {
+        const uint32_t c = rec[p].y;
+        bool dup = false;
+        for (int64_t q = i; q < p && !dup; ++q) dup = rec[q].y == c;
+        if (dup) continue;
+        for (int64_t q = i; q < end; ++q) {
+            const uint32_t d = rec[q].y;
+            if (d < c) continue;
+            bool first = true;
+            for (int64_t r = i; r < q && first; ++r) first = rec[r].y != d;
+            if (first) emit(c, d);
+        }
+    }
+}
+
+template <bool SCATTER>
+__global__ void __launch_bounds__(kWalkBlock) walk_kernel(const uint2* __restrict__ rec, int64_t A, int64_t chunk,
+                                                          int bw, int bbits, int64_t n_buckets, int64_t n_blocks,
+                                                          uint32_t* __restrict__ hist,  // [bucket][block]
+                                                          const int64_t* __restrict__ offs,
+                                                          uint32_t* __restrict__ entries, int* __restrict__ unsorted,
+                                                          uint32_t n_contigs, int* __restrict__ bad_contig) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_cnt[];  // n_buckets
+    const int64_t blk = blockIdx.x;
+    for (int64_t b = threadIdx.x; b < n_buckets; b += blockDim.x)
+        lds_cnt[b] = SCATTER ? (unsigned long long)offs[b * n_blocks + blk] : 0ull;
+    __syncthreads();
+    const int64_t lo = blk * chunk, hi = min(A, lo + chunk);
+    const uint32_t wmask = (1u << bw) - 1u;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const uint2 r = rec[i];
+        bool start = true;
+        if (i > 0) {
+            const uint32_t prev = rec[i - 1].x;
+            start = prev != r.x;
+            if (!SCATTER && prev > r.x) *unsorted = 1;
+        }
+        if (!SCATTER && r.y >= n_contigs) *bad_contig = 1;
+        if (!start) continue;
+        read_pairs(rec, A, i, [&](uint32_t a, uint32_t b) {
+            if (a >= n_contigs || b >= n_contigs) return;
+            const uint32_t bucket = a >> bw;
+            if (SCATTER) {
+                const unsigned long long pos = atomicAdd(&lds_cnt[bucket], 1ull);
+                entries[pos] = ((a & wmask) << bbits) | b;
+            } else {
+                atomicAdd(&lds_cnt[bucket], 1ull);
+            }
+        });
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (int64_t b = threadIdx.x; b < n_buckets; b += blockDim.x) hist[b * n_blocks + blk] = (uint32_t)lds_cnt[b];
+    }
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+// Bitonic sort of (key, val) pairs in LDS, n = power of two <= kTableCap.
+__device__ void lds_bitonic(uint32_t* keys, uint32_t* vals, int n) {
+    for (int size = 2; size <= n; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < n / 2; t += blockDim.x) {
+                const int i = 2 * t - (t & (stride - 1));
+                const int j = i + stride;
+                const bool up = (i & size) == 0;
+                const uint32_t ki = keys[i], kj = keys[j];
+                if ((ki > kj) == up) {
+                    keys[i] = kj;
+                    keys[j] = ki;
+                    const uint32_t v = vals[i];
+                    vals[i] = vals[j];
+                    vals[j] = v;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// One block per bucket: aggregate entries with an LDS hash table, sort, emit
+// (global key, count).  Sets overflow[bucket] and bails out if the bucket has
+// more than kTableCap - kTile distinct pairs (handled by the generic path).
+__global__ void __launch_bounds__(kReduceBlock) bucket_reduce_kernel(
+    const uint32_t* __restrict__ entries, const int64_t* __restrict__ bstart, int bw, int bbits,
+    uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n,
+    uint8_t* __restrict__ overflow) {
+    __shared__ uint32_t keys[kTableCap];
+    __shared__ uint32_t vals[kTableCap];
+    __shared__ int nuniq;
+    __shared__ int ovf;
+    const int64_t bucket = blockIdx.x;
+    const int64_t s = bstart[bucket], e = bstart[bucket + 1];
+    for (int t = threadIdx.x; t < kTableCap; t += blockDim.x) {
+        keys[t] = kEmpty;
+        vals[t] = 0;
+    }
+    if (threadIdx.x == 0) {
+        nuniq = 0;
+        ovf = 0;
+    }
+    __syncthreads();
+    for (int64_t base = s; base < e; base += kTile) {
+        if (nuniq > kTableCap - kTile) {
+            if (threadIdx.x == 0) ovf = 1;
+            break;
+        }
+#pragma unroll
+        for (int u = 0; u < kTile / kReduceBlock; ++u) {
+            const int64_t i = base + u * kReduceBlock + threadIdx.x;
+            if (i < e) {
+                const uint32_t key = entries[i];
+                uint32_t h = hash32(key) & (kTableCap - 1);
+                while (true) {
+                    const uint32_t k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (k == key) {
+                        atomicAdd(&vals[h], 1u);
+                        break;
+                    }
+                    if (k == kEmpty) {
+                        const uint32_t old = atomicCAS(&keys[h], kEmpty, key);
+                        if (old == kEmpty || old == key) {
+                            if (old == kEmpty) atomicAdd(&nuniq, 1);
+                            atomicAdd(&vals[h], 1u);
+                            break;
+                        }
+                    }
+                    h = (h + 1) & (kTableCap - 1);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    if (ovf) {
+        if (threadIdx.x == 0) {
+            overflow[bucket] = 1;
+            out_n[bucket] = 0;
+        }
+        return;
+    }
+    // compact occupied slots to the front (keys stay in LDS)
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    uint32_t my_k[kTableCap / kReduceBlock], my_v[kTableCap / kReduceBlock];
+#pragma unroll
+    for (int u = 0; u < kTableCap / kReduceBlock; ++u) {
+        const int t = u * kReduceBlock + threadIdx.x;
+        my_k[u] = keys[t];
+        my_v[u] = vals[t];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kTableCap / kReduceBlock; ++u) {
+        if (my_k[u] != kEmpty) {
+            const int pos = atomicAdd(&cnt, 1);
+            keys[pos] = my_k[u];
+            vals[pos] = my_v[u];
+        }
+    }
+    __syncthreads();
+    const int n = cnt;
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    for (int t = n + threadIdx.x; t < p2; t += blockDim.x) {
+        keys[t] = kEmpty;
+        vals[t] = 0;
+    }
+    __syncthreads();
+    lds_bitonic(keys, vals, p2);
+    const uint32_t bmask = (1u << bbits) - 1u;
+    const uint64_t abase = (uint64_t)bucket << bw;
+    uint64_t* ok = out_keys + bucket * (int64_t)kTableCap;
+    int64_t* oc = out_counts + bucket * (int64_t)kTableCap;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const uint32_t k = keys[t];
+        ok[t] = ((abase + (k >> bbits)) << 32) | (k & bmask);
+        oc[t] = (int64_t)vals[t];
+    }
+    if (threadIdx.x == 0) out_n[bucket] = n;
+}
+
+// Copies each bucket's sorted list (from its slot region or an overflow buffer)
+// to its final offset.
+__global__ void assemble_kernel(const uint64_t* const* __restrict__ src_k, const int64_t* const* __restrict__ src_c,
+                                const int64_t* __restrict__ n_per, const int64_t* __restrict__ dst_off,
+                                uint64_t* __restrict__ keys, int64_t* __restrict__ counts) {
+    const int64_t b = blockIdx.x;
+    const int64_t n = n_per[b], d = dst_off[b];
+    const uint64_t* sk = src_k[b];
+    const int64_t* sc = src_c[b];
+    for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
+        keys[d + t] = sk[t];
+        counts[d + t] = sc[t];
+    }
+}
+
+__global__ void fill_ptrs_kernel(const uint64_t* base_k, const int64_t* base_c, int64_t n_buckets, int64_t stride,
+                                 const uint64_t** pk, const int64_t** pc) {
+    int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < n_buckets) {
+        pk[b] = base_k + b * stride;
+        pc[b] = base_c + b * stride;
+    }
+}
+
+// bucket b gets entries of every block: hist[b][*]; bstart = exclusive scan of bucket totals
+__global__ void bucket_bounds_kernel(const int64_t* __restrict__ offs, int64_t n_buckets, int64_t n_blocks,
+                                     int64_t total, int64_t* __restrict__ bstart) {
+    int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < n_buckets) bstart[b] = offs[b * n_blocks];
+    if (b == n_buckets) bstart[b] = total;
+}
+
+// Overflowed bucket -> u64 global keys (generic path input)
+__global__ void widen_kernel(const uint32_t* __restrict__ entries, int64_t s, int64_t n, uint64_t abase, int bbits,
+                             uint64_t* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint32_t k = entries[s + i];
+        out[i] = ((abase + (k >> bbits)) << 32) | (k & ((1u << bbits) - 1u));
+    }
+}
+
+__global__ void fill_ones_kernel(int64_t* __restrict__ v, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = 1;
+}
+
+// ---- generic sort + reduce (low-volume paths) ----------------------------------
+__global__ void iota_kernel(uint32_t* __restrict__ v, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (uint32_t)i;
+}
+
+__global__ void gather_kernel(const uint32_t* __restrict__ idx, const int64_t* __restrict__ c_in,
+                              const uint64_t* __restrict__ f_in, int64_t n, int64_t* __restrict__ c_out,
+                              uint64_t* __restrict__ f_out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint32_t j = idx[i];
+        c_out[i] = c_in ? c_in[j] : 1;
+        if (f_out) f_out[i] = f_in ? f_in[j] : (uint64_t)j;
+    }
+}
+
+struct MinOp {
+    __device__ __forceinline__ uint64_t operator()(const uint64_t& a, const uint64_t& b) const { return a < b ? a : b; }
+};
+
+// ---- eq classes -----------------------------------------------------------------
+__global__ void eq_totals_kernel(const int64_t* __restrict__ cls_off, const uint32_t* __restrict__ members,
+                                 const int64_t* __restrict__ counts, int64_t n_classes, uint32_t n_contigs,
+                                 unsigned long long* __restrict__ totals, int64_t* __restrict__ pair_cnt,
+                                 const uint8_t* __restrict__ skip, int* __restrict__ bad) {
+    int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_classes) return;
+    const int64_t s = cls_off[c], e = cls_off[c + 1], m = e - s;
+    const unsigned long long cnt = (unsigned long long)counts[c];
+    for (int64_t t = s; t < e; ++t) {
+        const uint32_t x = members[t];
+        if (x >= n_contigs) {
+            *bad = 1;
+            continue;
+        }
+        atomicAdd(&totals[x], cnt);  // two's complement: exact for negative counts too
+    }
+    pair_cnt[c] = (skip && skip[c]) ? 0 : m * (m - 1) / 2;
+}
+
+__global__ void eq_emit_kernel(const int64_t* __restrict__ cls_off, const uint32_t* __restrict__ members,
+                               const int64_t* __restrict__ counts, const int64_t* __restrict__ pair_off,
+                               int64_t n_classes, int64_t P, uint64_t* __restrict__ keys, int64_t* __restrict__ cnt_out) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    // class = last c with pair_off[c] <= p
+    int64_t lo = 0, hi = n_classes;
+    while (hi - lo > 1) {
+        int64_t mid = (lo + hi) >> 1;
+        if (pair_off[mid] <= p) lo = mid;
+        else hi = mid;
+    }
+    // skip empty classes that share the offset
+    int64_t c = lo;
+    const int64_t t = p - pair_off[c];
+    const int64_t s = cls_off[c], m = cls_off[c + 1] - s;
+    // combinations order: row i holds pairs (i, i+1..m-1); cum(i) = i*m - i*(i+1)/2
+    int64_t il = 0, ih = m - 1;
+    while (ih - il > 1) {
+        int64_t mid = (il + ih) >> 1;
+        if (mid * m - mid * (mid + 1) / 2 <= t) il = mid;
+        else ih = mid;
+    }
+    const int64_t i = il, j = i + 1 + (t - (i * m - i * (i + 1) / 2));
+    const uint32_t a = members[s + i], b = members[s + j];
+    const uint32_t lo2 = min(a, b), hi2 = max(a, b);
+    keys[p] = ((uint64_t)lo2 << 32) | hi2;
+    cnt_out[p] = counts[c];
+}
+
+// ---- finalize --------------------------------------------------------------------
+__global__ void diag_totals_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, int64_t n,
+                                   int64_t* __restrict__ totals) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint64_t k = keys[i];
+        const uint32_t a = (uint32_t)(k >> 32), b = (uint32_t)k;
+        if (a == b) totals[a] = counts[i];
+    }
+}
+
+__global__ void edge_flags_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, int64_t n,
+                                  int mode, int64_t* __restrict__ flags) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint64_t k = keys[i];
+        const bool diag = (uint32_t)(k >> 32) == (uint32_t)k;
+        flags[i] = (counts[i] != 0 && !(diag && mode == KARMA_MODE_READS)) ? 1 : 0;
+    }
+}
+
+__global__ void edge_write_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts,
+                                  const uint64_t* __restrict__ first, const int64_t* __restrict__ flags,
+                                  const int64_t* __restrict__ pos, int64_t n, const int64_t* __restrict__ totals,
+                                  uint32_t* __restrict__ ea, uint32_t* __restrict__ eb, int64_t* __restrict__ es,
+                                  double* __restrict__ ew, uint64_t* __restrict__ ef, int* __restrict__ zero_div) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flags[i]) return;
+    const int64_t o = pos[i];
+    const uint64_t k = keys[i];
+    const uint32_t a = (uint32_t)(k >> 32), b = (uint32_t)k;
+    const int64_t s = counts[i], ta = totals[a], tb = totals[b];
+    ea[o] = a;
+    eb[o] = b;
+    es[o] = s;
+    if (ef) ef[o] = first[i];
+    if (ta == 0 || tb == 0) {
+        *zero_div = 1;
+        ew[o] = 0.0;
+        return;
+    }
+    // read_graph.py:39-42 / :128-130: ((s / tA) + (s / tB)) / 2, IEEE binary64, no FMA
+    const double x = __ddiv_rn((double)s, (double)ta);
+    const double y = __ddiv_rn((double)s, (double)tb);
+    ew[o] = __dadd_rn(x, y) * 0.5;
+}
+
+int scan_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
+    size_t tb = 0;
+    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, ctx->stream));
+    DevArray<uint8_t> tmp;
+    KARMA_TRY(tmp.alloc(ctx, tb));
+    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.ptr, tb, in, out, n, ctx->stream));
+    return KARMA_OK;
+}
+
+__global__ void u32_to_i64_kernel(const uint32_t* __restrict__ in, int64_t* __restrict__ out, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+int grid1(int64_t n, int block = 256) { return (int)std::max<int64_t>(1, ceil_div(n, block)); }
+
+// Records path into a pair list (records already on the device, grouped by read).
+int records_to_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
+    Geo g;
+    KARMA_TRY(make_geo(N, &g));
+    const int64_t n_blocks = std::max<int64_t>(1, std::min<int64_t>(4096, ceil_div(A, 2048)));
+    const int64_t chunk = std::max<int64_t>(1, ceil_div(A, n_blocks));
+    const int64_t H = g.n_buckets * n_blocks;
+    DevArray<uint32_t> hist;
+    DevArray<int64_t> hist64, offs, bstart;
+    DevArray<int> flags;
+    KARMA_TRY(hist.alloc(ctx, H));
+    KARMA_TRY(hist64.alloc(ctx, H + 1));
+    KARMA_TRY(offs.alloc(ctx, H + 1));
+    KARMA_TRY(bstart.alloc(ctx, g.n_buckets + 1));
+    KARMA_TRY(flags.alloc(ctx, 2));
+    KARMA_HIP(hipMemsetAsync(flags.ptr, 0, 8, ctx->stream));
+    const size_t lds = g.n_buckets * sizeof(unsigned long long);
+    KARMA_CHECK(lds <= 160 * 1024, KARMA_ERR_ARG, "too many buckets (%lld)", (long long)g.n_buckets);
+    if (A > 0) {
+        KARMA_LAUNCH(ctx, "graph_count", walk_kernel<false>, n_blocks, kWalkBlock, lds, rec, A, chunk, g.bw, g.bbits,
+                     g.n_buckets, n_blocks, hist.ptr, (const int64_t*)nullptr, (uint32_t*)nullptr, flags.ptr,
+                     (uint32_t)N, flags.ptr + 1);
+    } else {
+        KARMA_HIP(hipMemsetAsync(hist.ptr, 0, H * 4, ctx->stream));
+    }
+    KARMA_LAUNCH(ctx, "hist_widen", u32_to_i64_kernel, grid1(H), 256, 0, hist.ptr, hist64.ptr, H);
+    KARMA_HIP(hipMemsetAsync(hist64.ptr + H, 0, 8, ctx->stream));
+    KARMA_TRY(scan_i64(ctx, hist64.ptr, offs.ptr, H + 1));
+    int hflags[2];
+    int64_t total = 0;
+    KARMA_HIP(hipMemcpyAsync(hflags, flags.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipMemcpyAsync(&total, offs.ptr + H, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_CHECK(!hflags[0], KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
+    KARMA_CHECK(!hflags[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
+    KARMA_LAUNCH(ctx, "bucket_bounds", bucket_bounds_kernel, grid1(g.n_buckets + 1), 256, 0, offs.ptr, g.n_buckets,
+                 n_blocks, total, bstart.ptr);
+    DevArray<uint32_t> entries;
+    KARMA_TRY(entries.alloc(ctx, total));
+    if (A > 0)
+        KARMA_LAUNCH(ctx, "graph_scatter", walk_kernel<true>, n_blocks, kWalkBlock, lds, rec, A, chunk, g.bw, g.bbits,
+                     g.n_buckets, n_blocks, (uint32_t*)nullptr, offs.ptr, entries.ptr, flags.ptr, (uint32_t)N,
+                     flags.ptr + 1);
+    // per-bucket reduction
+    DevArray<uint64_t> slot_k;
+    DevArray<int64_t> slot_c, n_per;
+    DevArray<uint8_t> ovf;
+    KARMA_TRY(slot_k.alloc(ctx, g.n_buckets * kTableCap));
+    KARMA_TRY(slot_c.alloc(ctx, g.n_buckets * kTableCap));
+    KARMA_TRY(n_per.alloc(ctx, g.n_buckets + 1));
+    KARMA_TRY(ovf.alloc(ctx, g.n_buckets));
+    KARMA_HIP(hipMemsetAsync(ovf.ptr, 0, g.n_buckets, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(n_per.ptr + g.n_buckets, 0, 8, ctx->stream));
+    KARMA_LAUNCH(ctx, "graph_bucket_reduce", bucket_reduce_kernel, g.n_buckets, kReduceBlock, 0, entries.ptr,
+                 bstart.ptr, g.bw, g.bbits, slot_k.ptr, slot_c.ptr, n_per.ptr, ovf.ptr);
+    std::vector<uint8_t> hovf(g.n_buckets);
+    KARMA_HIP(hipMemcpyAsync(hovf.data(), ovf.ptr, g.n_buckets, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    // source pointer table
+    DevArray<const uint64_t*> pk;
+    DevArray<const int64_t*> pc;
+    KARMA_TRY(pk.alloc(ctx, g.n_buckets));
+    KARMA_TRY(pc.alloc(ctx, g.n_buckets));
+    KARMA_LAUNCH(ctx, "bucket_ptrs", fill_ptrs_kernel, grid1(g.n_buckets), 256, 0, slot_k.ptr, slot_c.ptr,
+                 g.n_buckets, (int64_t)kTableCap, pk.ptr, pc.ptr);
+    // overflowed buckets: generic sort-reduce of their entries
+    std::vector<std::unique_ptr<DevArray<uint64_t>>> ovk;
+    std::vector<std::unique_ptr<DevArray<int64_t>>> ovc;
+    std::vector<int64_t> hbstart;
+    bool any_ovf = std::any_of(hovf.begin(), hovf.end(), [](uint8_t v) { return v != 0; });
+    if (any_ovf) {
+        hbstart.resize(g.n_buckets + 1);
+        KARMA_HIP(hipMemcpyAsync(hbstart.data(), bstart.ptr, (g.n_buckets + 1) * 8, hipMemcpyDeviceToHost,
+                                 ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        for (int64_t b = 0; b < g.n_buckets; ++b) {
+            if (!hovf[b]) continue;
+            const int64_t s = hbstart[b], n = hbstart[b + 1] - s;
+            DevArray<uint64_t> wide;
+            DevArray<int64_t> ones;
+            KARMA_TRY(wide.alloc(ctx, n));
+            KARMA_TRY(ones.alloc(ctx, n));
+            KARMA_LAUNCH(ctx, "bucket_widen", widen_kernel, grid1(n), 256, 0, entries.ptr, s, n,
+                         (uint64_t)b << g.bw, g.bbits, wide.ptr);
+            KARMA_LAUNCH(ctx, "fill_ones", fill_ones_kernel, grid1(n), 256, 0, ones.ptr, n);
+            ovk.emplace_back(new DevArray<uint64_t>());
+            ovc.emplace_back(new DevArray<int64_t>());
+            int64_t nu = 0;
+            KARMA_TRY(sort_reduce_pairs(ctx, wide.ptr, ones.ptr, nullptr, n, 64, *ovk.back(), *ovc.back(), nullptr,
+                                        &nu));
+            const uint64_t* kp = ovk.back()->ptr;
+            const int64_t* cp = ovc.back()->ptr;
+            KARMA_HIP(hipMemcpyAsync(pk.ptr + b, &kp, sizeof kp, hipMemcpyHostToDevice, ctx->stream));
+            KARMA_HIP(hipMemcpyAsync(pc.ptr + b, &cp, sizeof cp, hipMemcpyHostToDevice, ctx->stream));
+            KARMA_HIP(hipMemcpyAsync(n_per.ptr + b, &nu, 8, hipMemcpyHostToDevice, ctx->stream));
+            KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        }
+    }
+    DevArray<int64_t> dst;
+    KARMA_TRY(dst.alloc(ctx, g.n_buckets + 1));
+    KARMA_TRY(scan_i64(ctx, n_per.ptr, dst.ptr, g.n_buckets + 1));
+    int64_t U = 0;
+    KARMA_HIP(hipMemcpyAsync(&U, dst.ptr + g.n_buckets, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_TRY(out->keys.alloc(ctx, U));
+    KARMA_TRY(out->counts.alloc(ctx, U));
+    KARMA_LAUNCH(ctx, "bucket_assemble", assemble_kernel, g.n_buckets, 256, 0, pk.ptr, pc.ptr, n_per.ptr, dst.ptr,
+                 out->keys.ptr, out->counts.ptr);
+    out->n = U;
+    out->n_contigs = N;
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    return KARMA_OK;
+}
+
+__global__ void interleave_kernel(const uint32_t* __restrict__ rid, const uint32_t* __restrict__ cid, int64_t n,
+                                  uint2* __restrict__ out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = make_uint2(rid[i], cid[i]);
+}
+
+__global__ void deinterleave_kernel(const uint2* __restrict__ in, int64_t n, uint32_t* __restrict__ rid,
+                                    uint32_t* __restrict__ cid) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        rid[i] = in[i].x;
+        cid[i] = in[i].y;
+    }
+}
+
+}  // namespace
+
+namespace karma {
+
+int sort_reduce_pairs(karma_ctx* ctx, const uint64_t* keys_in, const int64_t* counts_in, const uint64_t* first_in,
+                      int64_t n, int key_bits, DevArray<uint64_t>& keys_out, DevArray<int64_t>& counts_out,
+                      DevArray<uint64_t>* first_out, int64_t* n_out) {
+    KARMA_CHECK(n < (int64_t(1) << 31), KARMA_ERR_ARG, "sort_reduce_pairs: %lld items exceed 2^31", (long long)n);
+    if (n == 0) {
+        KARMA_TRY(keys_out.alloc(ctx, 0));
+        KARMA_TRY(counts_out.alloc(ctx, 0));
+        if (first_out) KARMA_TRY(first_out->alloc(ctx, 0));
+        *n_out = 0;
+        return KARMA_OK;
+    }
+    DevArray<uint64_t> ks;
+    DevArray<uint32_t> idx, idx_s;
+    DevArray<int64_t> cs;
+    DevArray<uint64_t> fs;
+    KARMA_TRY(ks.alloc(ctx, n));
+    KARMA_TRY(idx.alloc(ctx, n));
+    KARMA_TRY(idx_s.alloc(ctx, n));
+    KARMA_TRY(cs.alloc(ctx, n));
+    if (first_out) KARMA_TRY(fs.alloc(ctx, n));
+    KARMA_LAUNCH(ctx, "iota", iota_kernel, grid1(n), 256, 0, idx.ptr, n);
+    size_t tb = 0;
+    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys_in, ks.ptr, idx.ptr, idx_s.ptr, (int)n, 0, key_bits,
+                                                 ctx->stream));
+    DevArray<uint8_t> tmp;
+    KARMA_TRY(tmp.alloc(ctx, tb));
+    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, keys_in, ks.ptr, idx.ptr, idx_s.ptr, (int)n, 0, key_bits,
+                                                 ctx->stream));
+    KARMA_LAUNCH(ctx, "gather", gather_kernel, grid1(n), 256, 0, idx_s.ptr, counts_in, first_in, n, cs.ptr,
+                 first_out ? fs.ptr : (uint64_t*)nullptr);
+    DevArray<uint64_t> uk;
+    DevArray<int64_t> uc, nruns;
+    KARMA_TRY(uk.alloc(ctx, n));
+    KARMA_TRY(uc.alloc(ctx, n));
+    KARMA_TRY(nruns.alloc(ctx, 1));
+    size_t tb2 = 0;
+    KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb2, ks.ptr, uk.ptr, cs.ptr, uc.ptr, nruns.ptr,
+                                                hipcub::Sum(), (int)n, ctx->stream));
+    DevArray<uint8_t> tmp2;
+    KARMA_TRY(tmp2.alloc(ctx, tb2));
+    KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(tmp2.ptr, tb2, ks.ptr, uk.ptr, cs.ptr, uc.ptr, nruns.ptr,
+                                                hipcub::Sum(), (int)n, ctx->stream));
+    DevArray<uint64_t> uf, uk2;
+    if (first_out) {
+        KARMA_TRY(uf.alloc(ctx, n));
+        KARMA_TRY(uk2.alloc(ctx, n));
+        size_t tb3 = 0;
+        KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb3, ks.ptr, uk2.ptr, fs.ptr, uf.ptr, nruns.ptr, MinOp(),
+                                                    (int)n, ctx->stream));
+        DevArray<uint8_t> tmp3;
+        KARMA_TRY(tmp3.alloc(ctx, tb3));
+        KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(tmp3.ptr, tb3, ks.ptr, uk2.ptr, fs.ptr, uf.ptr, nruns.ptr,
+                                                    MinOp(), (int)n, ctx->stream));
+    }
+    int64_t U = 0;
+    KARMA_HIP(hipMemcpyAsync(&U, nruns.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_TRY(keys_out.alloc(ctx, U));
+    KARMA_TRY(counts_out.alloc(ctx, U));
+    KARMA_HIP(hipMemcpyAsync(keys_out.ptr, uk.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    KARMA_HIP(hipMemcpyAsync(counts_out.ptr, uc.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    if (first_out) {
+        KARMA_TRY(first_out->alloc(ctx, U));
+        KARMA_HIP(hipMemcpyAsync(first_out->ptr, uf.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    *n_out = U;
+    return KARMA_OK;
+}
+
+}  // namespace karma
+
+extern "C" {
+
+int karma_graph_records(karma_ctx* ctx, const uint32_t* records, int64_t A, int64_t N, int flags, int is_device,
+                        karma_pairs** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && (records || A == 0) && A >= 0, KARMA_ERR_ARG, "karma_graph_records: bad arguments");
+    KARMA_CHECK(A < (int64_t(1) << 40), KARMA_ERR_ARG, "too many records");
+    auto* p = new karma_pairs();
+    p->ctx = ctx;
+    DevArray<uint2> own;
+    const uint2* rec = reinterpret_cast<const uint2*>(records);
+    int rc = KARMA_OK;
+    if (!is_device || flags == KARMA_REC_UNSORTED) {
+        if ((rc = own.alloc(ctx, A))) {
+            delete p;
+            return rc;
+        }
+        if (A) {
+            KARMA_HIP(hipMemcpyAsync(own.ptr, records, A * 8, is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                     ctx->stream));
+        }
+        rec = own.ptr;
+    }
+    if (flags == KARMA_REC_UNSORTED && A > 1) {
+        KARMA_CHECK(A < (int64_t(1) << 31), KARMA_ERR_ARG, "unsorted path limited to 2^31 records");
+        DevArray<uint32_t> rid, cid, rid2, cid2;
+        if ((rc = rid.alloc(ctx, A)) || (rc = cid.alloc(ctx, A)) || (rc = rid2.alloc(ctx, A)) ||
+            (rc = cid2.alloc(ctx, A))) {
+            delete p;
+            return rc;
+        }
+        KARMA_LAUNCH(ctx, "deinterleave", deinterleave_kernel, grid1(A), 256, 0, own.ptr, A, rid.ptr, cid.ptr);
+        size_t tb = 0;
+        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, rid.ptr, rid2.ptr, cid.ptr, cid2.ptr, (int)A, 0, 32,
+                                                     ctx->stream));
+        DevArray<uint8_t> tmp;
+        if ((rc = tmp.alloc(ctx, tb))) {
+            delete p;
+            return rc;
+        }
+        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, rid.ptr, rid2.ptr, cid.ptr, cid2.ptr, (int)A, 0, 32,
+                                                     ctx->stream));
+        KARMA_LAUNCH(ctx, "interleave", interleave_kernel, grid1(A), 256, 0, rid2.ptr, cid2.ptr, A, own.ptr);
+    }
+    rc = records_to_pairs(ctx, rec, A, N, p);
+    if (rc) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return KARMA_OK;
+}
+
+int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
+                   const uint8_t* pair_skip, int64_t C, int64_t N, int is_device, karma_pairs** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && cls_off && C >= 0 && N >= 0 && N < (int64_t(1) << 32), KARMA_ERR_ARG,
+                "karma_graph_eq: bad arguments");
+    int64_t n_mem = 0;
+    if (is_device) {
+        KARMA_HIP(hipMemcpyAsync(&n_mem, cls_off + C, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    } else {
+        n_mem = cls_off[C];
+    }
+    DevArray<int64_t> d_off, d_cnt;
+    DevArray<uint32_t> d_mem;
+    DevArray<uint8_t> d_skip;
+    KARMA_TRY(d_off.alloc(ctx, C + 1));
+    KARMA_TRY(d_cnt.alloc(ctx, C));
+    KARMA_TRY(d_mem.alloc(ctx, n_mem));
+    KARMA_TRY(d_skip.alloc(ctx, C));
+    const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    KARMA_HIP(hipMemcpyAsync(d_off.ptr, cls_off, (C + 1) * 8, kind, ctx->stream));
+    if (C) KARMA_HIP(hipMemcpyAsync(d_cnt.ptr, counts, C * 8, kind, ctx->stream));
+    if (n_mem) KARMA_HIP(hipMemcpyAsync(d_mem.ptr, members, n_mem * 4, kind, ctx->stream));
+    if (C) {
+        if (pair_skip) KARMA_HIP(hipMemcpyAsync(d_skip.ptr, pair_skip, C, kind, ctx->stream));
+        else KARMA_HIP(hipMemsetAsync(d_skip.ptr, 0, C, ctx->stream));
+    }
+    auto* p = new karma_pairs();
+    p->ctx = ctx;
+    p->n_contigs = N;
+    std::unique_ptr<karma_pairs> guard(p);
+    KARMA_TRY(p->totals.alloc(ctx, N));
+    p->has_totals = true;
+    if (N) KARMA_HIP(hipMemsetAsync(p->totals.ptr, 0, N * 8, ctx->stream));
+    DevArray<int64_t> pc, poff;
+    DevArray<int> bad;
+    KARMA_TRY(pc.alloc(ctx, C + 1));
+    KARMA_TRY(poff.alloc(ctx, C + 1));
+    KARMA_TRY(bad.alloc(ctx, 1));
+    KARMA_HIP(hipMemsetAsync(bad.ptr, 0, 4, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(pc.ptr + C, 0, 8, ctx->stream));
+    if (C)
+        KARMA_LAUNCH(ctx, "eq_totals", eq_totals_kernel, grid1(C), 256, 0, d_off.ptr, d_mem.ptr, d_cnt.ptr, C,
+                     (uint32_t)N, (unsigned long long*)p->totals.ptr, pc.ptr, d_skip.ptr, bad.ptr);
+    KARMA_TRY(scan_i64(ctx, pc.ptr, poff.ptr, C + 1));
+    int64_t P = 0;
+    int hbad = 0;
+    KARMA_HIP(hipMemcpyAsync(&P, poff.ptr + C, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipMemcpyAsync(&hbad, bad.ptr, 4, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_CHECK(!hbad, KARMA_ERR_ARG, "eq class member index >= n_contigs");
+    DevArray<uint64_t> keys;
+    DevArray<int64_t> cnts;
+    KARMA_TRY(keys.alloc(ctx, P));
+    KARMA_TRY(cnts.alloc(ctx, P));
+    if (P)
+        KARMA_LAUNCH(ctx, "eq_emit", eq_emit_kernel, grid1(P), 256, 0, d_off.ptr, d_mem.ptr, d_cnt.ptr, poff.ptr, C,
+                     P, keys.ptr, cnts.ptr);
+    int key_bits = 32;
+    while (key_bits < 64 && (int64_t(1) << (key_bits - 32)) < N) ++key_bits;
+    KARMA_TRY(sort_reduce_pairs(ctx, keys.ptr, cnts.ptr, nullptr, P, key_bits, p->keys, p->counts, &p->first, &p->n));
+    p->has_first = true;
+    *out = guard.release();
+    return KARMA_OK;
+}
+
+int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, int64_t n, int is_device,
+                      karma_pairs** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && n >= 0 && (n == 0 || (keys && counts)), KARMA_ERR_ARG, "karma_pairs_merge: bad arguments");
+    auto* p = new karma_pairs();
+    p->ctx = ctx;
+    std::unique_ptr<karma_pairs> guard(p);
+    DevArray<uint64_t> k;
+    DevArray<int64_t> c;
+    const uint64_t* kp = keys;
+    const int64_t* cp = counts;
+    if (!is_device && n) {
+        KARMA_TRY(k.alloc(ctx, n));
+        KARMA_TRY(c.alloc(ctx, n));
+        KARMA_HIP(hipMemcpyAsync(k.ptr, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(c.ptr, counts, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        kp = k.ptr;
+        cp = c.ptr;
+    }
+    KARMA_TRY(sort_reduce_pairs(ctx, kp, cp, nullptr, n, 64, p->keys, p->counts, nullptr, &p->n));
+    *out = guard.release();
+    return KARMA_OK;
+}
+
+int karma_pairs_destroy(karma_pairs* p) {
+    if (!p) return KARMA_OK;
+    hipSetDevice(p->ctx->device);
+    delete p;
+    return KARMA_OK;
+}
+
+int karma_pairs_count(karma_pairs* p, int64_t* n) {
+    KARMA_CHECK(p && n, KARMA_ERR_ARG, "null argument");
+    *n = p->n;
+    return KARMA_OK;
+}
+
+int karma_pairs_device(karma_pairs* p, const uint64_t** keys, const int64_t** counts) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
+    if (keys) *keys = p->keys.ptr;
+    if (counts) *counts = p->counts.ptr;
+    return KARMA_OK;
+}
+
+int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* first, int is_device) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
+    KARMA_TRY(ctx_begin(p->ctx));
+    const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (p->n) {
+        if (keys) KARMA_HIP(hipMemcpyAsync(keys, p->keys.ptr, p->n * 8, kind, p->ctx->stream));
+        if (counts) KARMA_HIP(hipMemcpyAsync(counts, p->counts.ptr, p->n * 8, kind, p->ctx->stream));
+        if (first && p->has_first) KARMA_HIP(hipMemcpyAsync(first, p->first.ptr, p->n * 8, kind, p->ctx->stream));
+    }
+    KARMA_HIP(hipStreamSynchronize(p->ctx->stream));
+    return KARMA_OK;
+}
+
+int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts) {
+    KARMA_CHECK(p && bounds && starts && nranks >= 1, KARMA_ERR_ARG, "bad arguments");
+    KARMA_TRY(ctx_begin(p->ctx));
+    std::vector<uint64_t> hk(p->n);
+    if (p->n) {
+        KARMA_HIP(hipMemcpyAsync(hk.data(), p->keys.ptr, p->n * 8, hipMemcpyDeviceToHost, p->ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(p->ctx->stream));
+    }
+    for (int r = 0; r <= nranks; ++r) {
+        const uint64_t lim = (uint64_t)bounds[r] << 32;
+        starts[r] = std::lower_bound(hk.begin(), hk.end(), lim) - hk.begin();
+    }
+    return KARMA_OK;
+}
+
+int karma_pairs_totals(karma_pairs* p, int64_t* totals_dev, int64_t N) {
+    KARMA_CHECK(p && totals_dev && N >= 0, KARMA_ERR_ARG, "bad arguments");
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    if (N) KARMA_HIP(hipMemsetAsync(totals_dev, 0, N * 8, ctx->stream));
+    if (p->n)
+        KARMA_LAUNCH(ctx, "diag_totals", diag_totals_kernel, grid1(p->n), 256, 0, p->keys.ptr, p->counts.ptr, p->n,
+                     totals_dev);
+    return KARMA_OK;
+}
+
+int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64_t* totals_dev, int64_t N,
+                           karma_edges** out, int64_t* n_edges) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(p && out && n_edges && N >= 0, KARMA_ERR_ARG, "karma_edges_from_pairs: bad arguments");
+    KARMA_CHECK(mode == KARMA_MODE_READS || mode == KARMA_MODE_EQ, KARMA_ERR_ARG, "bad mode");
+    auto* e = new karma_edges();
+    e->ctx = ctx;
+    e->n_contigs = N;
+    std::unique_ptr<karma_edges> guard(e);
+    KARMA_TRY(e->totals.alloc(ctx, N));
+    const int64_t* tot = totals_dev;
+    if (!tot) {
+        if (mode == KARMA_MODE_EQ) {
+            KARMA_CHECK(p->has_totals && p->n_contigs == N, KARMA_ERR_STATE, "eq pair list without totals");
+            if (N) KARMA_HIP(hipMemcpyAsync(e->totals.ptr, p->totals.ptr, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        } else {
+            KARMA_TRY(karma_pairs_totals(p, e->totals.ptr, N));
+        }
+    } else if (N) {
+        KARMA_HIP(hipMemcpyAsync(e->totals.ptr, tot, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    const int64_t n = p->n;
+    DevArray<int64_t> flags, pos;
+    DevArray<int> zd;
+    KARMA_TRY(flags.alloc(ctx, n + 1));
+    KARMA_TRY(pos.alloc(ctx, n + 1));
+    KARMA_TRY(zd.alloc(ctx, 1));
+    KARMA_HIP(hipMemsetAsync(zd.ptr, 0, 4, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(flags.ptr + n, 0, 8, ctx->stream));
+    if (n) KARMA_LAUNCH(ctx, "edge_flags", edge_flags_kernel, grid1(n), 256, 0, p->keys.ptr, p->counts.ptr, n, mode, flags.ptr);
+    KARMA_TRY(scan_i64(ctx, flags.ptr, pos.ptr, n + 1));
+    int64_t E = 0;
+    KARMA_HIP(hipMemcpyAsync(&E, pos.ptr + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_TRY(e->a.alloc(ctx, E));
+    KARMA_TRY(e->b.alloc(ctx, E));
+    KARMA_TRY(e->s.alloc(ctx, E));
+    KARMA_TRY(e->w.alloc(ctx, E));
+    e->has_first = p->has_first;
+    if (e->has_first) KARMA_TRY(e->first.alloc(ctx, E));
+    if (n)
+        KARMA_LAUNCH(ctx, "edge_weights", edge_write_kernel, grid1(n), 256, 0, p->keys.ptr, p->counts.ptr,
+                     p->has_first ? p->first.ptr : (const uint64_t*)nullptr, flags.ptr, pos.ptr, n, e->totals.ptr,
+                     e->a.ptr, e->b.ptr, e->s.ptr, e->w.ptr, e->has_first ? e->first.ptr : (uint64_t*)nullptr, zd.ptr);
+    int hz = 0;
+    KARMA_HIP(hipMemcpyAsync(&hz, zd.ptr, 4, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_CHECK(!hz, KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
+    e->E = E;
+    *n_edges = E;
+    *out = guard.release();
+    return KARMA_OK;
+}
+
+int karma_edges_destroy(karma_edges* e) {
+    if (!e) return KARMA_OK;
+    hipSetDevice(e->ctx->device);
+    delete e;
+    return KARMA_OK;
+}
+
+int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, double* w, uint64_t* first, int is_device) {
+    KARMA_CHECK(e, KARMA_ERR_ARG, "null edges");
+    KARMA_TRY(ctx_begin(e->ctx));
+    const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    hipStream_t st = e->ctx->stream;
+    if (e->E) {
+        if (a) KARMA_HIP(hipMemcpyAsync(a, e->a.ptr, e->E * 4, kind, st));
+        if (b) KARMA_HIP(hipMemcpyAsync(b, e->b.ptr, e->E * 4, kind, st));
+        if (s) KARMA_HIP(hipMemcpyAsync(s, e->s.ptr, e->E * 8, kind, st));
+        if (w) KARMA_HIP(hipMemcpyAsync(w, e->w.ptr, e->E * 8, kind, st));
+        if (first && e->has_first) KARMA_HIP(hipMemcpyAsync(first, e->first.ptr, e->E * 8, kind, st));
+    }
+    KARMA_HIP(hipStreamSynchronize(st));
+    return KARMA_OK;
+}
+
+int karma_edges_totals(karma_edges* e, int64_t* totals, int is_device) {
+    KARMA_CHECK(e && (totals || !e->n_contigs), KARMA_ERR_ARG, "bad arguments");
+    KARMA_TRY(ctx_begin(e->ctx));
+    if (e->n_contigs)
+        KARMA_HIP(hipMemcpyAsync(totals, e->totals.ptr, e->n_contigs * 8,
+                                 is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(e->ctx->stream));
+    return KARMA_OK;
+}
+
+}  // extern "C"

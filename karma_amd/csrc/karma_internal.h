@@ -1,0 +1,125 @@
+// karma_internal.h — shared host/device plumbing of libkarma_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/karma.h"
+
+namespace karma {
+
+void set_error(const char* fmt, ...);
+
+#define KARMA_HIP(expr)                                                                     \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess) {                                                             \
+            ::karma::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
+            return _e == hipErrorOutOfMemory ? KARMA_ERR_OOM : KARMA_ERR_HIP;               \
+        }                                                                                   \
+    } while (0)
+
+#define KARMA_CHECK(cond, code, ...)      \
+    do {                                  \
+        if (!(cond)) {                    \
+            ::karma::set_error(__VA_ARGS__); \
+            return (code);                \
+        }                                 \
+    } while (0)
+
+#define KARMA_TRY(expr)          \
+    do {                         \
+        int _rc = (expr);        \
+        if (_rc != KARMA_OK) return _rc; \
+    } while (0)
+
+struct TimedLaunch {
+    const char* name;
+    hipEvent_t start, stop;
+};
+
+}  // namespace karma
+
+struct karma_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    // exact-size caching allocator: repeated steps of identical shape never hipMalloc
+    std::multimap<size_t, void*> free_list;
+    std::map<void*, size_t> live;
+    size_t cached_bytes = 0;
+    // per-kernel event timing
+    bool timing = false;
+    std::vector<karma::TimedLaunch> launches;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace karma {
+
+int ctx_alloc(karma_ctx* ctx, size_t bytes, void** out);
+void ctx_free(karma_ctx* ctx, void* p);
+int ctx_begin(karma_ctx* ctx);  // hipSetDevice
+// Wrap a launch with HIP events when timing is on.
+void timing_start(karma_ctx* ctx, const char* name, hipEvent_t* ev_stop);
+void timing_stop(karma_ctx* ctx, hipEvent_t ev_stop);
+
+template <typename T>
+struct DevArray {
+    karma_ctx* ctx = nullptr;
+    T* ptr = nullptr;
+    size_t n = 0;
+    DevArray() = default;
+    DevArray(const DevArray&) = delete;
+    DevArray& operator=(const DevArray&) = delete;
+    ~DevArray() { release(); }
+    int alloc(karma_ctx* c, size_t count) {
+        release();
+        ctx = c;
+        n = count;
+        void* p = nullptr;
+        int rc = ctx_alloc(c, (count ? count : 1) * sizeof(T), &p);
+        ptr = static_cast<T*>(p);
+        return rc;
+    }
+    void release() {
+        if (ptr) ctx_free(ctx, ptr);
+        ptr = nullptr;
+        n = 0;
+    }
+};
+
+#define KARMA_LAUNCH(ctx, name, kernel, grid, block, shmem, ...)                         \
+    do {                                                                                \
+        hipEvent_t _stop = nullptr;                                                     \
+        ::karma::timing_start((ctx), (name), &_stop);                                   \
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), (shmem), (ctx)->stream, __VA_ARGS__); \
+        ::karma::timing_stop((ctx), _stop);                                             \
+        KARMA_HIP(hipGetLastError());                                                   \
+    } while (0)
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Generic (key u64, count i64[, first u64]) sort + reduce-by-key on the device.
+// Used by the low-volume paths (eq classes, exchange merge, bucket overflow).
+int sort_reduce_pairs(karma_ctx* ctx, const uint64_t* keys_in, const int64_t* counts_in, const uint64_t* first_in,
+                      int64_t n, int key_bits, DevArray<uint64_t>& keys_out, DevArray<int64_t>& counts_out,
+                      DevArray<uint64_t>* first_out, int64_t* n_out);
+
+}  // namespace karma
+
+struct karma_pairs {
+    karma_ctx* ctx = nullptr;
+    int64_t n = 0;
+    int64_t n_contigs = 0;
+    karma::DevArray<uint64_t> keys;
+    karma::DevArray<int64_t> counts;
+    karma::DevArray<uint64_t> first;   // eq path only
+    karma::DevArray<int64_t> totals;   // eq path only
+    bool has_first = false;
+    bool has_totals = false;
+};

@@ -1,0 +1,741 @@
+// kmer.hip — contig store + k-mer profile kernels for gfx950.
+//
+// Reference (lmfaber/karma, pure Python) being replaced:
+//   KmerClustering.__calc_kmer_profile   karma/kmer.py:199-264
+//   __extract_kmers (sorted column set)  karma/kmer.py:146-179
+//   __kmers_of_seq / is_palindrome       karma/kmer.py:181-197, :46-54
+//   __count_kmer_occurence               karma/kmer.py:56-92
+//   fill_array_for_contig (count/len)    karma/kmer.py:108-122 (len = len(FASTA key), :213)
+//
+// Device data layout:
+//   packed[w]  u32, 16 bases per word, FIRST base in bits 31:30 (so a 64-bit
+//              window of two words yields the k-mer's lexicographic 2-bit code);
+//              every contig starts on a word boundary (woff[c]); one pad word.
+//   mask[w]    u16, bit 15-j set when base j of word w is not one of A,C,G,T
+//              (an "exception" base: N, IUPAC, lowercase, '\r', ...).
+//   raw        original bytes, read only for k-mers that touch an exception.
+// Ordinals: k-mer code for integer k (4^k values); for "5p6" the 5-mer q has
+// ordinal 5q and the 6-mer (q, x) ordinal 5q + 1 + x, so ordinal order equals
+// Python str order (a proper prefix sorts first).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+
+#include "karma_internal.h"
+
+using namespace karma;
+
+struct karma_contigs {
+    karma_ctx* ctx = nullptr;
+    int64_t n = 0, total = 0, words = 0, exc_bases = 0;
+    DevArray<uint8_t> raw_own;
+    DevArray<int64_t> off_own;
+    DevArray<int32_t> keylen_own;
+    const uint8_t* raw = nullptr;
+    const int64_t* off = nullptr;
+    const int32_t* keylen = nullptr;
+    DevArray<int64_t> woff;
+    DevArray<uint32_t> packed;
+    DevArray<uint16_t> mask;
+    DevArray<uint8_t> has_exc;
+};
+
+struct karma_kmer_plan {
+    karma_ctx* ctx = nullptr;
+    karma_contigs* store = nullptr;
+    int kmode = 0;
+    int kmin = 0, kmax = 0;
+    uint32_t S = 0;  // ordinal space
+    int64_t nwords = 0;
+    DevArray<uint32_t> presence;
+    DevArray<uint64_t> exc_keys;  // sorted unique
+    int64_t n_exc = 0;
+    DevArray<int32_t> col_of_ord;
+    DevArray<int32_t> col_of_exc;
+    DevArray<uint64_t> col_keys;
+    DevArray<int64_t> row_tot;
+    int64_t M = -1;
+};
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ int base_code(uint8_t b) {
+    // A C G T -> 0 1 2 3 ; anything else -> -1 (exception)
+    return b == 'A' ? 0 : b == 'C' ? 1 : b == 'G' ? 2 : b == 'T' ? 3 : -1;
+}
+
+// ---------------------------------------------------------------- pack -------
+__global__ void __launch_bounds__(kBlock) pack_kernel(const uint8_t* __restrict__ raw, const int64_t* __restrict__ off,
+                                                      const int64_t* __restrict__ woff, int64_t n,
+                                                      uint32_t* __restrict__ packed, uint16_t* __restrict__ mask,
+                                                      uint8_t* __restrict__ has_exc,
+                                                      unsigned long long* __restrict__ exc_count) {
+    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
+        const int64_t s = off[c], L = off[c + 1] - s, w0 = woff[c], nw = woff[c + 1] - w0;
+        unsigned local_exc = 0;
+        for (int64_t w = threadIdx.x; w < nw; w += blockDim.x) {
+            uint32_t word = 0;
+            uint32_t m = 0;
+            const int64_t j0 = w * 16;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                int code = 0;
+                if (j0 + j < L) {
+                    int cc = base_code(raw[s + j0 + j]);
+                    if (cc < 0) {
+                        m |= 1u << (15 - j);
+                        ++local_exc;
+                    } else {
+                        code = cc;
+                    }
+                }
+                word |= (uint32_t)code << (30 - 2 * j);
+            }
+            packed[w0 + w] = word;
+            mask[w0 + w] = (uint16_t)m;
+        }
+        // block-wide OR of "has exception"
+        __shared__ unsigned blk_exc;
+        if (threadIdx.x == 0) blk_exc = 0;
+        __syncthreads();
+        if (local_exc) atomicAdd(&blk_exc, local_exc);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            has_exc[c] = blk_exc ? 1 : 0;
+            if (blk_exc) atomicAdd(exc_count, (unsigned long long)blk_exc);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void word_count_kernel(const int64_t* __restrict__ off, int64_t n, int64_t* __restrict__ wc) {
+    int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < n) wc[c] = (off[c + 1] - off[c] + 15) / 16;
+    if (c == n) wc[c] = 0;
+}
+
+// ------------------------------------------------------------- k-mer keys ----
+// Byte key of a k-mer: bytes big-endian from bit 63; the low byte holds the
+// length unless the mode is k = 8 (all keys one length, 8 bytes).
+__device__ __forceinline__ uint64_t key_from_bytes(const uint8_t* p, int len, bool with_len) {
+    uint64_t k = 0;
+    for (int j = 0; j < len; ++j) k |= (uint64_t)p[j] << (56 - 8 * j);
+    return with_len ? (k | (uint64_t)len) : k;
+}
+
+__device__ __forceinline__ uint64_t key_from_code(uint32_t code, int len, bool with_len) {
+    const uint64_t ACGT = 0x54474341ull;  // 'A','C','G','T' little-endian bytes
+    uint64_t k = 0;
+    for (int j = 0; j < len; ++j) {
+        uint32_t b = (code >> (2 * (len - 1 - j))) & 3u;
+        k |= ((ACGT >> (8 * b)) & 0xFF) << (56 - 8 * j);
+    }
+    return with_len ? (k | (uint64_t)len) : k;
+}
+
+__device__ __forceinline__ uint64_t ord_key(uint32_t o, bool p56, int k, bool with_len) {
+    if (!p56) return key_from_code(o, k, with_len);
+    uint32_t q = o / 5, r = o % 5;
+    return r == 0 ? key_from_code(q, 5, with_len) : key_from_code((q << 2) | (r - 1), 6, with_len);
+}
+
+__device__ __forceinline__ bool pal6_code(uint32_t c) {
+    return ((c >> 10) & 3) == (c & 3) && ((c >> 8) & 3) == ((c >> 2) & 3) && ((c >> 6) & 3) == ((c >> 4) & 3);
+}
+
+__device__ __forceinline__ bool pal_bytes(const uint8_t* p, int len) {
+    for (int j = 0; j < len / 2; ++j)
+        if (p[j] != p[len - 1 - j]) return false;
+    return true;
+}
+
+// lower_bound over a sorted device array (count of elements < key)
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* a, int64_t n, uint64_t key) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Window view of one contig position: 2-bit code of up to 8 bases + exception bits.
+struct Window {
+    uint64_t x;  // two packed words
+    uint32_t m;  // two mask halves
+    int o;       // base offset inside the first word
+    __device__ __forceinline__ uint32_t code(int k) const {
+        return (uint32_t)(x >> (64 - 2 * o - 2 * k)) & ((1u << (2 * k)) - 1u);
+    }
+    __device__ __forceinline__ bool clean(int k) const { return ((m >> (32 - o - k)) & ((1u << k) - 1u)) == 0; }
+};
+
+__device__ __forceinline__ Window load_window(const uint32_t* packed, const uint16_t* mask, int64_t w0, int64_t i,
+                                              bool need_mask) {
+    const int64_t w = w0 + (i >> 4);
+    Window v;
+    v.o = (int)(i & 15);
+    v.x = ((uint64_t)packed[w] << 32) | packed[w + 1];
+    v.m = need_mask ? (((uint32_t)mask[w] << 16) | mask[w + 1]) : 0u;
+    return v;
+}
+
+// ------------------------------------------------------------- presence ------
+// Sets the ACGT-ordinal presence bitmap (LDS-private per block, OR-flushed once)
+// and appends the byte keys of k-mers touching an exception base.
+template <bool P56>
+__global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __restrict__ packed,
+                                                          const uint16_t* __restrict__ mask,
+                                                          const uint8_t* __restrict__ has_exc,
+                                                          const int64_t* __restrict__ woff,
+                                                          const int64_t* __restrict__ off,
+                                                          const uint8_t* __restrict__ raw, int64_t n, int k,
+                                                          int nwords, bool with_len, uint32_t* __restrict__ presence,
+                                                          uint64_t* __restrict__ exc_buf, int64_t exc_cap,
+                                                          unsigned long long* __restrict__ exc_cnt,
+                                                          int64_t* __restrict__ row_tot) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
+    __shared__ unsigned long long blk_tot;
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) lds_bits[w] = 0;
+    const int kmin = P56 ? 5 : k;
+    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
+        if (threadIdx.x == 0) blk_tot = 0;
+        __syncthreads();
+        const int64_t L = off[c + 1] - off[c], w0 = woff[c];
+        const bool exc = has_exc[c] != 0;
+        unsigned my = 0;
+        for (int64_t i = threadIdx.x; i + kmin <= L; i += blockDim.x) {
+            Window v = load_window(packed, mask, w0, i, exc);
+            if (P56) {
+                // 5-mer at i (kmer.py:72-73)
+                if (v.clean(5)) {
+                    uint32_t o5 = v.code(5) * 5u;
+                    atomicOr(&lds_bits[o5 >> 5], 1u << (o5 & 31));
+                } else {
+                    uint64_t key = key_from_bytes(raw + off[c] + i, 5, true);
+                    unsigned long long slot = atomicAdd(exc_cnt, 1ull);
+                    if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
+                }
+                ++my;
+                // palindromic 6-mer at i (kmer.py:76-80)
+                if (i + 6 <= L) {
+                    if (v.clean(6)) {
+                        uint32_t c6 = v.code(6);
+                        if (pal6_code(c6)) {
+                            uint32_t o6 = (c6 >> 2) * 5u + 1u + (c6 & 3u);
+                            atomicOr(&lds_bits[o6 >> 5], 1u << (o6 & 31));
+                            ++my;
+                        }
+                    } else {
+                        const uint8_t* p = raw + off[c] + i;
+                        if (pal_bytes(p, 6)) {
+                            uint64_t key = key_from_bytes(p, 6, true);
+                            unsigned long long slot = atomicAdd(exc_cnt, 1ull);
+                            if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
+                            ++my;
+                        }
+                    }
+                }
+            } else {
+                if (v.clean(k)) {
+                    uint32_t o = v.code(k);
+                    atomicOr(&lds_bits[o >> 5], 1u << (o & 31));
+                } else {
+                    uint64_t key = key_from_bytes(raw + off[c] + i, k, with_len);
+                    unsigned long long slot = atomicAdd(exc_cnt, 1ull);
+                    if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
+                }
+                ++my;
+            }
+        }
+        if (my) atomicAdd(&blk_tot, (unsigned long long)my);
+        __syncthreads();
+        if (threadIdx.x == 0) row_tot[c] = (int64_t)blk_tot;
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
+        uint32_t b = lds_bits[w];
+        if (b) atomicOr(&presence[w], b);
+    }
+}
+
+// ----------------------------------------------------------- column table ---
+// One block: merges present ACGT ordinals with the sorted exception keys in
+// byte-key order (= Python sorted() over str, kmer.py:172).
+constexpr int kColBlock = 1024;
+
+__global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* __restrict__ presence, int nwords,
+                                                            uint32_t S, bool p56, int k, bool with_len,
+                                                            const uint64_t* __restrict__ exc, int64_t X,
+                                                            int32_t* __restrict__ col_of_ord,
+                                                            int32_t* __restrict__ col_of_exc,
+                                                            uint64_t* __restrict__ col_keys, int64_t* __restrict__ M_out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t prefix[];  // nwords + 1
+    // exclusive popcount prefix over the bitmap (nwords <= 2048)
+    __shared__ uint32_t chunk_sum[kColBlock];
+    const int per = (nwords + kColBlock - 1) / kColBlock;
+    const int lo = threadIdx.x * per, hi = min(nwords, lo + per);
+    uint32_t s = 0;
+    for (int w = lo; w < hi; ++w) s += __popc(presence[w]);
+    chunk_sum[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int t = 0; t < kColBlock; ++t) {
+            uint32_t v = chunk_sum[t];
+            chunk_sum[t] = run;
+            run += v;
+        }
+        prefix[nwords] = run;
+    }
+    __syncthreads();
+    uint32_t run = chunk_sum[threadIdx.x];
+    for (int w = lo; w < hi; ++w) {
+        prefix[w] = run;
+        run += __popc(presence[w]);
+    }
+    __syncthreads();
+    const uint32_t n_present = prefix[nwords];
+    for (uint32_t o = threadIdx.x; o < S; o += blockDim.x) {
+        uint32_t word = presence[o >> 5];
+        if ((word >> (o & 31)) & 1u) {
+            uint32_t rank = prefix[o >> 5] + __popc(word & ((1u << (o & 31)) - 1u));
+            uint64_t key = ord_key(o, p56, k, with_len);
+            int64_t col = (int64_t)rank + lower_bound_u64(exc, X, key);
+            col_of_ord[o] = (int32_t)col;
+            col_keys[col] = key;
+        } else {
+            col_of_ord[o] = -1;
+        }
+    }
+    for (int64_t x = threadIdx.x; x < X; x += blockDim.x) {
+        const uint64_t key = exc[x];
+        // number of ordinals whose key < exc key (ord_key is monotone in o)
+        uint32_t lo2 = 0, hi2 = S;
+        while (lo2 < hi2) {
+            uint32_t mid = (lo2 + hi2) >> 1;
+            if (ord_key(mid, p56, k, with_len) < key) lo2 = mid + 1;
+            else hi2 = mid;
+        }
+        uint32_t below = prefix[lo2 >> 5] + (lo2 < S ? __popc(presence[lo2 >> 5] & ((1u << (lo2 & 31)) - 1u)) : 0u);
+        if (lo2 >= S) below = n_present;
+        const int64_t col = x + below;
+        col_of_exc[x] = (int32_t)col;
+        col_keys[col] = key;
+    }
+    if (threadIdx.x == 0) *M_out = (int64_t)n_present + X;
+}
+
+// -------------------------------------------------------------- profile ------
+// One contig per block iteration: LDS histogram over the M columns, then the
+// dense row count/len(key) is streamed out (8*M bytes per contig).
+template <bool P56, bool LDS_COUNTS>
+__global__ void __launch_bounds__(kBlock) profile_kernel(
+    const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
+    const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
+    const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
+    const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
+    double* __restrict__ out, int64_t ld, uint32_t* __restrict__ scratch, int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_counts[];
+    uint32_t* counts = LDS_COUNTS ? lds_counts : scratch + (int64_t)blockIdx.x * M;
+    const int kmin = P56 ? 5 : k;
+    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
+        for (int64_t j = threadIdx.x; j < M; j += blockDim.x) counts[j] = 0;
+        __syncthreads();
+        const int64_t L = off[c + 1] - off[c], w0 = woff[c];
+        const bool excp = has_exc[c] != 0;
+        for (int64_t i = threadIdx.x; i + kmin <= L; i += blockDim.x) {
+            Window v = load_window(packed, mask, w0, i, excp);
+            if (P56) {
+                if (v.clean(5)) {
+                    atomicAdd(&counts[col_of_ord[v.code(5) * 5u]], 1u);
+                } else {
+                    uint64_t key = key_from_bytes(raw + off[c] + i, 5, true);
+                    atomicAdd(&counts[col_of_exc[lower_bound_u64(exc, X, key)]], 1u);
+                }
+                if (i + 6 <= L) {
+                    if (v.clean(6)) {
+                        uint32_t c6 = v.code(6);
+                        if (pal6_code(c6)) atomicAdd(&counts[col_of_ord[(c6 >> 2) * 5u + 1u + (c6 & 3u)]], 1u);
+                    } else {
+                        const uint8_t* p = raw + off[c] + i;
+                        if (pal_bytes(p, 6)) {
+                            uint64_t key = key_from_bytes(p, 6, true);
+                            atomicAdd(&counts[col_of_exc[lower_bound_u64(exc, X, key)]], 1u);
+                        }
+                    }
+                }
+            } else {
+                if (v.clean(k)) {
+                    atomicAdd(&counts[col_of_ord[v.code(k)]], 1u);
+                } else {
+                    uint64_t key = key_from_bytes(raw + off[c] + i, k, with_len);
+                    atomicAdd(&counts[col_of_exc[lower_bound_u64(exc, X, key)]], 1u);
+                }
+            }
+        }
+        __syncthreads();
+        const double len = (double)keylen[c];
+        double* row = out + c * ld;
+        for (int64_t j = threadIdx.x; j < M; j += blockDim.x) {
+            const uint32_t v = counts[j];
+            if (v && keylen[c] == 0) *err = 1;
+            row[j] = v ? (double)v / len : 0.0;  // IEEE correctly rounded (kmer.py:120)
+        }
+        __syncthreads();
+    }
+}
+
+int grid_for(int64_t n, int64_t cap) { return (int)std::max<int64_t>(1, std::min<int64_t>(n, cap)); }
+
+int kmer_shape(int kmode, int* kmin, int* kmax, uint32_t* S, bool* with_len) {
+    if (kmode == KARMA_KMER_5P6) {
+        *kmin = 5;
+        *kmax = 6;
+        *S = 1024u * 5u;
+        *with_len = true;
+        return KARMA_OK;
+    }
+    KARMA_CHECK(kmode >= 1 && kmode <= 8, KARMA_ERR_KMER, "unsupported k-mer size %d (supported: 1..8, 5p6)", kmode);
+    *kmin = *kmax = kmode;
+    *S = 1u << (2 * kmode);
+    *with_len = kmode < 8;
+    return KARMA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offsets, const int32_t* key_len, int64_t n,
+                         int is_device, karma_contigs** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && offsets && key_len && n >= 0, KARMA_ERR_ARG, "karma_contigs_create: bad arguments");
+    auto* c = new karma_contigs();
+    c->ctx = ctx;
+    c->n = n;
+    int64_t total = 0;
+    int rc = KARMA_OK;
+    if (is_device) {
+        KARMA_HIP(hipMemcpyAsync(&total, offsets + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        c->raw = seq;
+        c->off = offsets;
+        c->keylen = key_len;
+    } else {
+        total = offsets[n];
+        if ((rc = c->raw_own.alloc(ctx, (size_t)total + 16)) || (rc = c->off_own.alloc(ctx, n + 1)) ||
+            (rc = c->keylen_own.alloc(ctx, n ? n : 1))) {
+            delete c;
+            return rc;
+        }
+        if (total) KARMA_HIP(hipMemcpyAsync(c->raw_own.ptr, seq, total, hipMemcpyHostToDevice, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(c->off_own.ptr, offsets, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+        if (n) KARMA_HIP(hipMemcpyAsync(c->keylen_own.ptr, key_len, n * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+        c->raw = c->raw_own.ptr;
+        c->off = c->off_own.ptr;
+        c->keylen = c->keylen_own.ptr;
+    }
+    c->total = total;
+    // word offsets: exclusive scan of ceil(L/16)
+    DevArray<int64_t> wc;
+    if ((rc = wc.alloc(ctx, n + 1)) || (rc = c->woff.alloc(ctx, n + 1)) || (rc = c->has_exc.alloc(ctx, n ? n : 1))) {
+        delete c;
+        return rc;
+    }
+    KARMA_LAUNCH(ctx, "word_count", word_count_kernel, ceil_div(n + 1, 256), 256, 0, c->off, n, wc.ptr);
+    size_t tmp_bytes = 0;
+    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, wc.ptr, c->woff.ptr, (int)(n + 1), ctx->stream));
+    DevArray<uint8_t> tmp;
+    if ((rc = tmp.alloc(ctx, tmp_bytes))) {
+        delete c;
+        return rc;
+    }
+    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.ptr, tmp_bytes, wc.ptr, c->woff.ptr, (int)(n + 1), ctx->stream));
+    KARMA_HIP(hipMemcpyAsync(&c->words, c->woff.ptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = c->packed.alloc(ctx, c->words + 2)) || (rc = c->mask.alloc(ctx, c->words + 2))) {
+        delete c;
+        return rc;
+    }
+    KARMA_HIP(hipMemsetAsync(c->packed.ptr + c->words, 0, 2 * sizeof(uint32_t), ctx->stream));
+    KARMA_HIP(hipMemsetAsync(c->mask.ptr + c->words, 0, 2 * sizeof(uint16_t), ctx->stream));
+    DevArray<unsigned long long> exc;
+    if ((rc = exc.alloc(ctx, 1))) {
+        delete c;
+        return rc;
+    }
+    KARMA_HIP(hipMemsetAsync(exc.ptr, 0, sizeof(unsigned long long), ctx->stream));
+    if (n)
+        KARMA_LAUNCH(ctx, "pack_2bit", pack_kernel, grid_for(n, 8192), kBlock, 0, c->raw, c->off, c->woff.ptr, n,
+                     c->packed.ptr, c->mask.ptr, c->has_exc.ptr, exc.ptr);
+    unsigned long long ne = 0;
+    KARMA_HIP(hipMemcpyAsync(&ne, exc.ptr, sizeof ne, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    c->exc_bases = (int64_t)ne;
+    *out = c;
+    return KARMA_OK;
+}
+
+int karma_contigs_destroy(karma_contigs* c) {
+    if (!c) return KARMA_OK;
+    hipSetDevice(c->ctx->device);
+    delete c;
+    return KARMA_OK;
+}
+
+int karma_contigs_info(karma_contigs* c, int64_t* n, int64_t* total, int64_t* exc, int64_t* packed_bytes) {
+    KARMA_CHECK(c, KARMA_ERR_ARG, "null contigs");
+    if (n) *n = c->n;
+    if (total) *total = c->total;
+    if (exc) *exc = c->exc_bases;
+    if (packed_bytes) *packed_bytes = c->words * 4 + c->words * 2;
+    return KARMA_OK;
+}
+
+int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_kmer_plan** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(c && out, KARMA_ERR_ARG, "karma_kmer_plan_create: bad arguments");
+    int kmin, kmax;
+    uint32_t S;
+    bool with_len;
+    KARMA_TRY(kmer_shape(kmode, &kmin, &kmax, &S, &with_len));
+    auto* p = new karma_kmer_plan();
+    p->ctx = ctx;
+    p->store = c;
+    p->kmode = kmode;
+    p->kmin = kmin;
+    p->kmax = kmax;
+    p->S = S;
+    p->nwords = (S + 31) / 32;
+    int rc;
+    const int64_t exc_cap = c->exc_bases * (kmode == KARMA_KMER_5P6 ? 11 : kmax) + 1;
+    DevArray<uint64_t> exc_buf;
+    DevArray<unsigned long long> exc_cnt;
+    if ((rc = p->presence.alloc(ctx, p->nwords)) || (rc = p->row_tot.alloc(ctx, c->n ? c->n : 1)) ||
+        (rc = exc_buf.alloc(ctx, exc_cap)) || (rc = exc_cnt.alloc(ctx, 1))) {
+        delete p;
+        return rc;
+    }
+    KARMA_HIP(hipMemsetAsync(p->presence.ptr, 0, p->nwords * 4, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(exc_cnt.ptr, 0, 8, ctx->stream));
+    if (c->n) {
+        const int grid = grid_for(c->n, 2048);
+        const size_t lds = p->nwords * 4;
+        if (kmode == KARMA_KMER_5P6)
+            KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<true>, grid, kBlock, lds, c->packed.ptr, c->mask.ptr,
+                         c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->n, kmode, (int)p->nwords, with_len,
+                         p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, p->row_tot.ptr);
+        else
+            KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<false>, grid, kBlock, lds, c->packed.ptr, c->mask.ptr,
+                         c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->n, kmode, (int)p->nwords, with_len,
+                         p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, p->row_tot.ptr);
+    }
+    unsigned long long ninst = 0;
+    KARMA_HIP(hipMemcpyAsync(&ninst, exc_cnt.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_CHECK((int64_t)ninst <= exc_cap, KARMA_ERR_STATE, "exception k-mer buffer overflow (%llu > %lld)", ninst,
+                (long long)exc_cap);
+    if (ninst) {
+        // sort + unique the exception keys (low volume; hipCUB)
+        DevArray<uint64_t> sorted, uniq;
+        DevArray<int64_t> nsel;
+        if ((rc = sorted.alloc(ctx, ninst)) || (rc = uniq.alloc(ctx, ninst)) || (rc = nsel.alloc(ctx, 1))) {
+            delete p;
+            return rc;
+        }
+        size_t tb1 = 0, tb2 = 0;
+        KARMA_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb1, exc_buf.ptr, sorted.ptr, (int)ninst, 0, 64, ctx->stream));
+        KARMA_HIP(hipcub::DeviceSelect::Unique(nullptr, tb2, sorted.ptr, uniq.ptr, nsel.ptr, (int)ninst, ctx->stream));
+        DevArray<uint8_t> tmp;
+        if ((rc = tmp.alloc(ctx, std::max(tb1, tb2)))) {
+            delete p;
+            return rc;
+        }
+        KARMA_HIP(hipcub::DeviceRadixSort::SortKeys(tmp.ptr, tb1, exc_buf.ptr, sorted.ptr, (int)ninst, 0, 64, ctx->stream));
+        KARMA_HIP(hipcub::DeviceSelect::Unique(tmp.ptr, tb2, sorted.ptr, uniq.ptr, nsel.ptr, (int)ninst, ctx->stream));
+        int64_t nu = 0;
+        KARMA_HIP(hipMemcpyAsync(&nu, nsel.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        if ((rc = p->exc_keys.alloc(ctx, nu))) {
+            delete p;
+            return rc;
+        }
+        KARMA_HIP(hipMemcpyAsync(p->exc_keys.ptr, uniq.ptr, nu * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        p->n_exc = nu;
+    }
+    *out = p;
+    return KARMA_OK;
+}
+
+int karma_kmer_plan_destroy(karma_kmer_plan* p) {
+    if (!p) return KARMA_OK;
+    hipSetDevice(p->ctx->device);
+    delete p;
+    return KARMA_OK;
+}
+
+int karma_kmer_presence_words(karma_kmer_plan* p, int64_t* nwords) {
+    KARMA_CHECK(p && nwords, KARMA_ERR_ARG, "null argument");
+    *nwords = p->nwords;
+    return KARMA_OK;
+}
+
+int karma_kmer_presence_get(karma_kmer_plan* p, uint32_t* dst) {
+    KARMA_CHECK(p && dst, KARMA_ERR_ARG, "null argument");
+    KARMA_TRY(ctx_begin(p->ctx));
+    KARMA_HIP(hipMemcpyAsync(dst, p->presence.ptr, p->nwords * 4, hipMemcpyDeviceToDevice, p->ctx->stream));
+    return KARMA_OK;
+}
+
+int karma_kmer_presence_set(karma_kmer_plan* p, const uint32_t* src) {
+    KARMA_CHECK(p && src, KARMA_ERR_ARG, "null argument");
+    KARMA_TRY(ctx_begin(p->ctx));
+    KARMA_HIP(hipMemcpyAsync(p->presence.ptr, src, p->nwords * 4, hipMemcpyDeviceToDevice, p->ctx->stream));
+    p->M = -1;
+    return KARMA_OK;
+}
+
+int karma_kmer_exceptions_count(karma_kmer_plan* p, int64_t* n) {
+    KARMA_CHECK(p && n, KARMA_ERR_ARG, "null argument");
+    *n = p->n_exc;
+    return KARMA_OK;
+}
+
+int karma_kmer_exceptions_get(karma_kmer_plan* p, uint64_t* dst) {
+    KARMA_CHECK(p && (dst || !p->n_exc), KARMA_ERR_ARG, "null argument");
+    KARMA_TRY(ctx_begin(p->ctx));
+    if (p->n_exc)
+        KARMA_HIP(hipMemcpyAsync(dst, p->exc_keys.ptr, p->n_exc * 8, hipMemcpyDeviceToDevice, p->ctx->stream));
+    return KARMA_OK;
+}
+
+int karma_kmer_exceptions_set(karma_kmer_plan* p, const uint64_t* src, int64_t n) {
+    KARMA_CHECK(p && (src || n == 0) && n >= 0, KARMA_ERR_ARG, "bad argument");
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    p->M = -1;
+    if (n == 0) {
+        p->n_exc = 0;
+        return KARMA_OK;
+    }
+    DevArray<uint64_t> sorted, uniq;
+    DevArray<int64_t> nsel;
+    int rc;
+    if ((rc = sorted.alloc(ctx, n)) || (rc = uniq.alloc(ctx, n)) || (rc = nsel.alloc(ctx, 1))) return rc;
+    size_t tb1 = 0, tb2 = 0;
+    KARMA_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb1, src, sorted.ptr, (int)n, 0, 64, ctx->stream));
+    KARMA_HIP(hipcub::DeviceSelect::Unique(nullptr, tb2, sorted.ptr, uniq.ptr, nsel.ptr, (int)n, ctx->stream));
+    DevArray<uint8_t> tmp;
+    if ((rc = tmp.alloc(ctx, std::max(tb1, tb2)))) return rc;
+    KARMA_HIP(hipcub::DeviceRadixSort::SortKeys(tmp.ptr, tb1, src, sorted.ptr, (int)n, 0, 64, ctx->stream));
+    KARMA_HIP(hipcub::DeviceSelect::Unique(tmp.ptr, tb2, sorted.ptr, uniq.ptr, nsel.ptr, (int)n, ctx->stream));
+    int64_t nu = 0;
+    KARMA_HIP(hipMemcpyAsync(&nu, nsel.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = p->exc_keys.alloc(ctx, nu))) return rc;
+    KARMA_HIP(hipMemcpyAsync(p->exc_keys.ptr, uniq.ptr, nu * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    p->n_exc = nu;
+    return KARMA_OK;
+}
+
+int karma_kmer_plan_finalize(karma_kmer_plan* p, int64_t* M) {
+    KARMA_CHECK(p && M, KARMA_ERR_ARG, "null argument");
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    int kmin, kmax;
+    uint32_t S;
+    bool with_len;
+    KARMA_TRY(kmer_shape(p->kmode, &kmin, &kmax, &S, &with_len));
+    int rc;
+    DevArray<int64_t> m_dev;
+    if ((rc = p->col_of_ord.alloc(ctx, S)) || (rc = p->col_of_exc.alloc(ctx, p->n_exc ? p->n_exc : 1)) ||
+        (rc = p->col_keys.alloc(ctx, S + p->n_exc)) || (rc = m_dev.alloc(ctx, 1)))
+        return rc;
+    const size_t lds = (p->nwords + 1) * 4;
+    KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->presence.ptr, (int)p->nwords, S,
+                 p->kmode == KARMA_KMER_5P6, p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode, with_len, p->exc_keys.ptr,
+                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, m_dev.ptr);
+    KARMA_HIP(hipMemcpyAsync(&p->M, m_dev.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    *M = p->M;
+    return KARMA_OK;
+}
+
+int karma_kmer_columns(karma_kmer_plan* p, uint64_t* keys_host) {
+    KARMA_CHECK(p && p->M >= 0, KARMA_ERR_STATE, "karma_kmer_columns before finalize");
+    KARMA_TRY(ctx_begin(p->ctx));
+    if (p->M) {
+        KARMA_CHECK(keys_host, KARMA_ERR_ARG, "null keys");
+        KARMA_HIP(hipMemcpyAsync(keys_host, p->col_keys.ptr, p->M * 8, hipMemcpyDeviceToHost, p->ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(p->ctx->stream));
+    }
+    return KARMA_OK;
+}
+
+int karma_kmer_row_totals(karma_kmer_plan* p, int64_t* dst) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null plan");
+    KARMA_TRY(ctx_begin(p->ctx));
+    if (p->store->n) {
+        KARMA_CHECK(dst, KARMA_ERR_ARG, "null dst");
+        KARMA_HIP(hipMemcpyAsync(dst, p->row_tot.ptr, p->store->n * 8, hipMemcpyDeviceToHost, p->ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(p->ctx->stream));
+    }
+    return KARMA_OK;
+}
+
+int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_device) {
+    KARMA_CHECK(p && p->M >= 0, KARMA_ERR_STATE, "karma_kmer_profile before finalize");
+    karma_ctx* ctx = p->ctx;
+    karma_contigs* c = p->store;
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(ld >= p->M, KARMA_ERR_ARG, "ld (%lld) < M (%lld)", (long long)ld, (long long)p->M);
+    const int64_t n = c->n, M = p->M;
+    if (n == 0 || M == 0) {
+        if (n && M == 0) return KARMA_OK;
+        return KARMA_OK;
+    }
+    KARMA_CHECK(out, KARMA_ERR_ARG, "null out");
+    int rc;
+    DevArray<double> dev_out;
+    double* dst = out;
+    if (!out_is_device) {
+        if ((rc = dev_out.alloc(ctx, (size_t)n * ld))) return rc;
+        dst = dev_out.ptr;
+    }
+    DevArray<int> err;
+    if ((rc = err.alloc(ctx, 1))) return rc;
+    KARMA_HIP(hipMemsetAsync(err.ptr, 0, 4, ctx->stream));
+    bool with_len = p->kmode != 8;
+    const bool lds_ok = M * 4 <= 144 * 1024;
+    const int grid = grid_for(n, lds_ok ? 4096 : 1024);
+    DevArray<uint32_t> scratch;
+    if (!lds_ok && (rc = scratch.alloc(ctx, (size_t)grid * M))) return rc;
+    const size_t lds = lds_ok ? M * 4 : 0;
+    const int k = p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode;
+#define KARMA_PROFILE_LAUNCH(P56, LDS)                                                                           \
+    KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, LDS>), grid, kBlock, lds, c->packed.ptr, c->mask.ptr, \
+                 c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len, p->col_of_ord.ptr,       \
+                 p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err.ptr)
+    if (p->kmode == KARMA_KMER_5P6) {
+        if (lds_ok) KARMA_PROFILE_LAUNCH(true, true);
+        else KARMA_PROFILE_LAUNCH(true, false);
+    } else {
+        if (lds_ok) KARMA_PROFILE_LAUNCH(false, true);
+        else KARMA_PROFILE_LAUNCH(false, false);
+    }
+#undef KARMA_PROFILE_LAUNCH
+    int herr = 0;
+    KARMA_HIP(hipMemcpyAsync(&herr, err.ptr, 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (!out_is_device)
+        KARMA_HIP(hipMemcpyAsync(out, dst, (size_t)n * ld * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_CHECK(!herr, KARMA_ERR_ZERO_DIV, "division by zero: a contig with a zero-length key has k-mers");
+    return KARMA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,295 @@
+"""Multi-GPU (one process per GPU) sharded build — SURVEY.md §8(e).
+
+Sharding: rank r owns a contiguous block of contig rows and a contiguous
+range of fragments (read ids).  Two exchange steps exist in the path and only
+those use collectives (RCCL over xGMI through torch.distributed "nccl"):
+
+  k-mer profile  the column set is the GLOBAL sorted union of present k-mers
+                 (kmer.py:172): the ACGT presence bytes are MAX-allreduced
+                 (S <= 64 KiB) and the non-ACGT k-mer keys all-gathered; then
+                 every rank derives the identical column table and writes its
+                 own rows.
+  shared graph   each rank reduces its fragments' pairs locally (HIP bucket
+                 reduce), routes the pre-reduced (key, count) list to the owner
+                 of contig a (all-to-all-v), the owner merges, the readset
+                 sizes (diagonal counts) are SUM-allreduced so every owner can
+                 weight edges to contigs it does not own.
+All arithmetic is integer until the one weight formula, so the result is
+bit-identical to the single-GPU (and the reference) result.
+
+The compute backend is injectable (`ops`): HipOps drives libkarma_hip.so on
+the GPU; tests/test_distributed_cpu.py plugs an oracle-backed CPU backend into
+the same driver to cover the exchange logic with gloo at world size 2.
+"""
+
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+
+class Comm:
+    """Thin torch.distributed wrapper; world size 1 needs no process group."""
+
+    def __init__(self, world, rank, dist=None, device=None):
+        self.world, self.rank, self.dist, self.device = world, rank, dist, device
+
+    @classmethod
+    def create(cls, world, rank, local_rank=0, backend=None):
+        if world == 1:
+            return cls(1, 0)
+        import torch
+        import torch.distributed as dist
+
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            device = torch.device(f"cuda:{local_rank}")
+        else:
+            device = torch.device("cpu")
+        if not dist.is_initialized():
+            dist.init_process_group(backend, rank=rank, world_size=world)
+        return cls(world, rank, dist, device)
+
+    # scalar helpers (host values)
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def _scalar(self, x, dtype, op):
+        import torch
+
+        t = torch.tensor([x], dtype=dtype, device=self.device)
+        self.dist.all_reduce(t, op=op)
+        return t.item()
+
+    def max_float(self, x):
+        return x if not self.dist else self._scalar(float(x), __import__("torch").float64, self.dist.ReduceOp.MAX)
+
+    def sum_int(self, x):
+        return x if not self.dist else int(self._scalar(int(x), __import__("torch").int64, self.dist.ReduceOp.SUM))
+
+    # tensor collectives (in place / returning)
+    def allreduce_max_(self, t):
+        if self.dist:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return t
+
+    def allreduce_sum_(self, t):
+        if self.dist:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t
+
+    def all_gather_var(self, t):
+        """Concatenation of every rank's 1-D tensor (sizes may differ)."""
+        if not self.dist:
+            return t
+        import torch
+
+        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        self.dist.all_gather(sizes, n)
+        sizes = [int(s.item()) for s in sizes]
+        mx = max(sizes)
+        if mx == 0:
+            return t[:0]
+        pad = torch.zeros(mx, dtype=t.dtype, device=t.device)
+        pad[: t.numel()] = t
+        outs = [torch.empty_like(pad) for _ in range(self.world)]
+        self.dist.all_gather(outs, pad)
+        return torch.cat([o[:s] for o, s in zip(outs, sizes)])
+
+    def alltoallv(self, t, send_counts):
+        """1-D all-to-all-v: send_counts[r] consecutive elements go to rank r."""
+        if not self.dist:
+            return t
+        import torch
+
+        sc = torch.tensor(list(send_counts), dtype=torch.int64, device=t.device)
+        rc = torch.empty_like(sc)
+        self.dist.all_to_all_single(rc, sc)
+        recv_counts = [int(x) for x in rc.tolist()]
+        out = torch.empty(sum(recv_counts), dtype=t.dtype, device=t.device)
+        self.dist.all_to_all_single(out, t, output_split_sizes=recv_counts,
+                                    input_split_sizes=[int(x) for x in send_counts])
+        return out
+
+    def close(self):
+        if self.dist and self.dist.is_initialized():
+            self.dist.destroy_process_group()
+            self.dist = None
+
+
+class HipOps:
+    """Compute backend on libkarma_hip.so; exchange buffers are torch CUDA tensors."""
+
+    def __init__(self, ctx, device_index=None):
+        import torch
+
+        from . import engine
+
+        self.torch, self.engine = torch, engine
+        self.dev = torch.device(f"cuda:{torch.cuda.current_device() if device_index is None else device_index}")
+        # one stream shared by torch (collectives, buffers) and the HIP kernels
+        self.stream = torch.cuda.Stream(device=self.dev)
+        torch.cuda.set_stream(self.stream)
+        ctx.set_stream(self.stream.cuda_stream)
+        self.ctx = ctx
+
+    # -- k-mer --
+    def kmer_plan(self, store, kmode):
+        return self.engine.KmerPlan(self.ctx, store, kmode)
+
+    def presence_bytes(self, plan):
+        t = self.torch
+        nw = plan.presence_words()
+        words = t.empty(nw, dtype=t.int32, device=self.dev)
+        plan.presence_get(words.data_ptr())
+        bits = t.arange(32, device=self.dev, dtype=t.int64)
+        return ((words.to(t.int64).unsqueeze(1) >> bits) & 1).to(t.uint8).reshape(-1)
+
+    def set_presence_bytes(self, plan, pres):
+        t = self.torch
+        bits = t.arange(32, device=self.dev, dtype=t.int64)
+        w = (pres.reshape(-1, 32).to(t.int64) << bits).sum(1)
+        w = w - ((w >> 31) & 1) * (1 << 32)  # to signed 32-bit without overflow
+        words = w.to(t.int32).contiguous()
+        plan.presence_set(words.data_ptr())
+        self._keep = words
+
+    def exceptions(self, plan):
+        t = self.torch
+        n = plan.exceptions_count()
+        keys = t.empty(max(n, 1), dtype=t.int64, device=self.dev)
+        plan.exceptions_get(keys.data_ptr() if n else None)
+        return keys[:n]
+
+    def set_exceptions(self, plan, keys):
+        keys = keys.contiguous()
+        plan.exceptions_set(keys.data_ptr() if keys.numel() else None, keys.numel())
+        self._keep_exc = keys
+
+    def finalize(self, plan):
+        return plan.finalize()
+
+    def profile(self, plan, out):
+        if out.numel():
+            plan.profile_device(out.data_ptr(), out.shape[1])
+
+    def profile_buffer(self, n, M):
+        return self.torch.empty((n, M), dtype=self.torch.float64, device=self.dev)
+
+    # -- graph --
+    def graph_local(self, records, n_records, n_contigs):
+        return self.engine.Pairs.from_records(self.ctx, None, n_contigs, grouped=True, device_ptr=records,
+                                              n_records=n_records)
+
+    def pairs_split(self, pairs, bounds):
+        t = self.torch
+        starts = pairs.split(bounds)
+        n = pairs.count()
+        keys = t.empty(max(n, 1), dtype=t.int64, device=self.dev)
+        counts = t.empty(max(n, 1), dtype=t.int64, device=self.dev)
+        if n:
+            from ._lib import call
+            import ctypes
+            call("karma_pairs_get", pairs.h, ctypes.c_void_p(keys.data_ptr()), ctypes.c_void_p(counts.data_ptr()),
+                 None, 1)
+        return keys[:n], counts[:n], starts
+
+    def merge(self, keys, counts):
+        return self.engine.Pairs.merge(self.ctx, keys.data_ptr() if keys.numel() else None,
+                                       counts.data_ptr() if counts.numel() else None, device=True, n=keys.numel())
+
+    def totals(self, pairs, n_contigs):
+        tot = self.torch.zeros(n_contigs, dtype=self.torch.int64, device=self.dev)
+        pairs.totals_device(tot.data_ptr(), n_contigs)
+        return tot
+
+    def edges(self, pairs, n_contigs, totals=None):
+        from ._lib import KARMA_MODE_READS
+        return pairs.edges(KARMA_MODE_READS, n_contigs, totals.data_ptr() if totals is not None else None)
+
+    def edge_count(self, edges):
+        return edges.E
+
+    def edge_arrays(self, edges):
+        return edges.get()
+
+    def entries(self, pairs):
+        _, counts, _ = pairs.get()
+        return int(counts.sum())
+
+    def close(self, *objs):
+        for o in objs:
+            if o is not None:
+                o.close()
+
+
+class ShardedBuild:
+    """k-mer profile + shared-read graph over contig/fragment shards."""
+
+    def __init__(self, ctx, comm: Comm, kmode, n_glob, c_lo, n_loc, ops=None):
+        self.comm, self.kmode, self.n_glob, self.c_lo, self.n_loc = comm, kmode, n_glob, c_lo, n_loc
+        self.ops = ops if ops is not None else HipOps(ctx)
+        self._prof = None
+        bounds = np.zeros(comm.world + 1, np.int64)
+        if comm.world > 1:
+            import torch
+            dev = comm.device
+            t = torch.tensor([c_lo, c_lo + n_loc], dtype=torch.int64, device=dev)
+            allb = [torch.zeros_like(t) for _ in range(comm.world)]
+            comm.dist.all_gather(allb, t)
+            allb = [b.tolist() for b in allb]
+            for r in range(comm.world):
+                assert allb[r][0] == (allb[r - 1][1] if r else 0), "contig shards must be contiguous, in rank order"
+                bounds[r + 1] = allb[r][1]
+            assert bounds[-1] == n_glob
+        else:
+            bounds[1] = n_glob
+        self.bounds = bounds
+
+    def run(self, store, records, n_records, keep=False):
+        ops, comm = self.ops, self.comm
+        # ---- k-mer profile (kmer.py:199-233) ----
+        plan = ops.kmer_plan(store, self.kmode)
+        if comm.world > 1:
+            pres = comm.allreduce_max_(ops.presence_bytes(plan))
+            ops.set_presence_bytes(plan, pres)
+            ops.set_exceptions(plan, comm.all_gather_var(ops.exceptions(plan)))
+        M = ops.finalize(plan)
+        if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
+            self._prof = ops.profile_buffer(self.n_loc, M)
+        ops.profile(plan, self._prof)
+        # ---- shared-read graph (read_graph.py:19-50) ----
+        local = ops.graph_local(records, n_records, self.n_glob)
+        stats = {"M": M}
+        if keep:
+            stats["entries"] = ops.entries(local)
+            stats["pairs_local"] = local.count() if hasattr(local, "count") else None
+        if comm.world > 1:
+            keys, counts, starts = ops.pairs_split(local, self.bounds)
+            send = np.diff(starts)
+            rk = comm.alltoallv(keys, send)
+            rc = comm.alltoallv(counts, send)
+            merged = ops.merge(rk, rc)
+            tot = comm.allreduce_sum_(ops.totals(merged, self.n_glob))
+            edges = ops.edges(merged, self.n_glob, tot)
+            ops.close(local)
+            final_pairs = merged
+        else:
+            edges = ops.edges(local, self.n_glob)
+            final_pairs = local
+        stats["E_local"] = ops.edge_count(edges)
+        if keep:
+            stats["profile"] = self._prof
+            stats["edges"] = ops.edge_arrays(edges)
+            stats["columns"] = plan.columns() if hasattr(plan, "columns") else None
+        ops.close(edges, final_pairs, plan)
+        return stats
+
+    def close(self):
+        self._prof = None

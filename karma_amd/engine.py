@@ -1,0 +1,388 @@
+"""Host-side driver of the HIP hot path (thin layer over karma_amd._lib).
+
+Everything here moves host arrays to/from libkarma_hip.so; all compute is in
+the HIP kernels (karma_amd/csrc/*.hip).  The drop-in classes (kmer.py,
+read_graph.py, contig.py) call these functions.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import call, ptr
+
+KMODE_5P6 = _lib.KARMA_KMER_5P6
+
+
+def kmode_of(kmer_size) -> int:
+    """kmer.py:69 tests `kmer_size == "5p6"`; anything else is an int k
+    (cmd_parser.py:234-235 casts with int())."""
+    if kmer_size == "5p6":
+        return KMODE_5P6
+    return int(kmer_size)
+
+
+def encode_sequences(sequences):
+    """OrderedDict[str, str] -> (bytes blob, offsets int64[N+1], key_len int32[N]).
+
+    Sequences are compared/sliced as Python str; for code points < 256 latin-1
+    bytes preserve both length and ordering, so the byte kernels are exact.
+    """
+    vals = []
+    for v in sequences.values():
+        try:
+            vals.append(v.encode("latin-1"))
+        except UnicodeEncodeError as e:
+            raise ValueError("sequence contains a code point >= 256; libkarma_hip handles byte sequences "
+                             "(latin-1) only") from e
+    offs = np.zeros(len(vals) + 1, dtype=np.int64)
+    if vals:
+        np.cumsum([len(v) for v in vals], out=offs[1:])
+    blob = np.frombuffer(b"".join(vals) + b"\0" * 16, dtype=np.uint8)
+    key_len = np.array([len(k) for k in sequences.keys()], dtype=np.int32)
+    return blob, offs, key_len
+
+
+def decode_keys(keys: np.ndarray, kmode: int):
+    """u64 column keys (karma.h encoding) -> list[str] (latin-1)."""
+    out = []
+    for k in keys.tolist():
+        if kmode == 8:
+            ln = 8
+        else:
+            ln = k & 0xFF
+        b = k.to_bytes(8, "big")[:ln]
+        out.append(b.decode("latin-1"))
+    return out
+
+
+class ContigStore:
+    """Device-resident contigs (karma_contigs): 2-bit packed + exception mask."""
+
+    def __init__(self, ctx, blob, offsets, key_len, device_pointers=False, n=None):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        if device_pointers:
+            call("karma_contigs_create", ctx.h, ctypes.c_void_p(blob), ctypes.c_void_p(offsets),
+                 ctypes.c_void_p(key_len), n, 1, ctypes.byref(h))
+        else:
+            self._keep = (blob, offsets, key_len)
+            n = len(key_len)
+            call("karma_contigs_create", ctx.h, ptr(blob), ptr(offsets), ptr(key_len) if n else ptr(
+                np.zeros(1, np.int32)), n, 0, ctypes.byref(h))
+        self.h = h
+        self.n = n
+
+    def info(self):
+        v = [ctypes.c_int64() for _ in range(4)]
+        call("karma_contigs_info", self.h, *[ctypes.byref(x) for x in v])
+        return dict(n=v[0].value, total_bases=v[1].value, exception_bases=v[2].value, packed_bytes=v[3].value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.load().karma_contigs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class KmerPlan:
+    """Presence pass + column table + dense profile (karma_kmer_plan)."""
+
+    def __init__(self, ctx, store: ContigStore, kmode: int):
+        self.ctx, self.store, self.kmode = ctx, store, kmode
+        h = ctypes.c_void_p()
+        call("karma_kmer_plan_create", ctx.h, store.h, kmode, ctypes.byref(h))
+        self.h = h
+        self.M = None
+
+    # -- exchange points (multi-rank) --
+    def presence_words(self):
+        n = ctypes.c_int64()
+        call("karma_kmer_presence_words", self.h, ctypes.byref(n))
+        return n.value
+
+    def presence_get(self, dst_dev_ptr):
+        call("karma_kmer_presence_get", self.h, ctypes.c_void_p(dst_dev_ptr))
+
+    def presence_set(self, src_dev_ptr):
+        call("karma_kmer_presence_set", self.h, ctypes.c_void_p(src_dev_ptr))
+
+    def exceptions_count(self):
+        n = ctypes.c_int64()
+        call("karma_kmer_exceptions_count", self.h, ctypes.byref(n))
+        return n.value
+
+    def exceptions_get(self, dst_dev_ptr):
+        call("karma_kmer_exceptions_get", self.h, ctypes.c_void_p(dst_dev_ptr) if dst_dev_ptr else None)
+
+    def exceptions_set(self, src_dev_ptr, n):
+        call("karma_kmer_exceptions_set", self.h, ctypes.c_void_p(src_dev_ptr) if src_dev_ptr else None, n)
+
+    def finalize(self):
+        m = ctypes.c_int64()
+        call("karma_kmer_plan_finalize", self.h, ctypes.byref(m))
+        self.M = m.value
+        return self.M
+
+    def columns(self):
+        keys = np.zeros(max(self.M, 1), dtype=np.uint64)
+        call("karma_kmer_columns", self.h, ptr(keys))
+        return keys[: self.M]
+
+    def row_totals(self):
+        out = np.zeros(max(self.store.n, 1), dtype=np.int64)
+        call("karma_kmer_row_totals", self.h, ptr(out))
+        return out[: self.store.n]
+
+    def profile_host(self):
+        out = np.zeros((self.store.n, self.M), dtype=np.float64)
+        if out.size:
+            call("karma_kmer_profile", self.h, ptr(out), self.M, 0)
+        return out
+
+    def profile_device(self, dst_dev_ptr, ld=None):
+        call("karma_kmer_profile", self.h, ctypes.c_void_p(dst_dev_ptr), ld or self.M, 1)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.load().karma_kmer_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def kmer_profile(sequences, kmer_size, ctx=None):
+    """Full single-device k-mer profile of an OrderedDict (kmer.py:199-233).
+
+    Returns (profile float64[N, M], columns list[str], row_totals int64[N])."""
+    ctx = ctx or _lib.default_context()
+    kmode = kmode_of(kmer_size)
+    blob, offs, key_len = encode_sequences(sequences)
+    store = ContigStore(ctx, blob, offs, key_len)
+    try:
+        plan = KmerPlan(ctx, store, kmode)
+        try:
+            plan.finalize()
+            cols = decode_keys(plan.columns(), kmode)
+            prof = plan.profile_host()
+            tot = plan.row_totals()
+        finally:
+            plan.close()
+    finally:
+        store.close()
+    return prof, cols, tot
+
+
+# ---------------------------------------------------------------------------
+# Graph
+# ---------------------------------------------------------------------------
+
+class Pairs:
+    """Sorted unique (a << 32 | b, count) list (karma_pairs)."""
+
+    def __init__(self, ctx, h):
+        self.ctx, self.h = ctx, h
+
+    @classmethod
+    def from_records(cls, ctx, records, n_contigs, grouped=True, device_ptr=None, n_records=None):
+        h = ctypes.c_void_p()
+        flags = _lib.KARMA_REC_SORTED if grouped else _lib.KARMA_REC_UNSORTED
+        if device_ptr is not None:
+            call("karma_graph_records", ctx.h, ctypes.c_void_p(device_ptr), n_records, n_contigs, flags, 1,
+                 ctypes.byref(h))
+        else:
+            rec = np.ascontiguousarray(records, dtype=np.uint32).reshape(-1, 2)
+            call("karma_graph_records", ctx.h, ptr(rec) if len(rec) else None, len(rec), n_contigs, flags, 0,
+                 ctypes.byref(h))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_eq(cls, ctx, cls_off, members, counts, pair_skip, n_contigs):
+        h = ctypes.c_void_p()
+        cls_off = np.ascontiguousarray(cls_off, np.int64)
+        members = np.ascontiguousarray(members, np.uint32)
+        counts = np.ascontiguousarray(counts, np.int64)
+        skip = np.ascontiguousarray(pair_skip, np.uint8)
+        call("karma_graph_eq", ctx.h, ptr(cls_off), ptr(members) if len(members) else None,
+             ptr(counts) if len(counts) else None, ptr(skip) if len(skip) else None, len(cls_off) - 1, n_contigs, 0,
+             ctypes.byref(h))
+        return cls(ctx, h)
+
+    @classmethod
+    def merge(cls, ctx, keys, counts, device=False, n=None):
+        h = ctypes.c_void_p()
+        if device:
+            call("karma_pairs_merge", ctx.h, ctypes.c_void_p(keys) if keys else None,
+                 ctypes.c_void_p(counts) if counts else None, n, 1, ctypes.byref(h))
+        else:
+            keys = np.ascontiguousarray(keys, np.uint64)
+            counts = np.ascontiguousarray(counts, np.int64)
+            call("karma_pairs_merge", ctx.h, ptr(keys) if len(keys) else None, ptr(counts) if len(counts) else None,
+                 len(keys), 0, ctypes.byref(h))
+        return cls(ctx, h)
+
+    def count(self):
+        n = ctypes.c_int64()
+        call("karma_pairs_count", self.h, ctypes.byref(n))
+        return n.value
+
+    def device_ptrs(self):
+        k, c = ctypes.c_void_p(), ctypes.c_void_p()
+        call("karma_pairs_device", self.h, ctypes.byref(k), ctypes.byref(c))
+        return k.value, c.value
+
+    def get(self):
+        n = self.count()
+        keys = np.zeros(max(n, 1), np.uint64)
+        counts = np.zeros(max(n, 1), np.int64)
+        first = np.zeros(max(n, 1), np.uint64)
+        call("karma_pairs_get", self.h, ptr(keys), ptr(counts), ptr(first), 0)
+        return keys[:n], counts[:n], first[:n]
+
+    def split(self, bounds):
+        bounds = np.ascontiguousarray(bounds, np.int64)
+        starts = np.zeros(len(bounds), np.int64)
+        call("karma_pairs_split", self.h, ptr(bounds), len(bounds) - 1, ptr(starts))
+        return starts
+
+    def totals_device(self, dst_dev_ptr, n_contigs):
+        call("karma_pairs_totals", self.h, ctypes.c_void_p(dst_dev_ptr), n_contigs)
+
+    def edges(self, mode, n_contigs, totals_dev_ptr=None):
+        h = ctypes.c_void_p()
+        E = ctypes.c_int64()
+        call("karma_edges_from_pairs", self.ctx.h, self.h, mode,
+             ctypes.c_void_p(totals_dev_ptr) if totals_dev_ptr else None, n_contigs, ctypes.byref(h),
+             ctypes.byref(E))
+        return Edges(self.ctx, h, E.value, n_contigs)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.load().karma_pairs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+@dataclass
+class EdgeArrays:
+    a: np.ndarray
+    b: np.ndarray
+    shared: np.ndarray
+    weight: np.ndarray
+    first: np.ndarray
+    totals: np.ndarray
+
+
+class Edges:
+    def __init__(self, ctx, h, E, n_contigs):
+        self.ctx, self.h, self.E, self.n_contigs = ctx, h, E, n_contigs
+
+    def get(self) -> EdgeArrays:
+        E = self.E
+        a = np.zeros(max(E, 1), np.uint32)
+        b = np.zeros(max(E, 1), np.uint32)
+        s = np.zeros(max(E, 1), np.int64)
+        w = np.zeros(max(E, 1), np.float64)
+        f = np.zeros(max(E, 1), np.uint64)
+        call("karma_edges_get", self.h, ptr(a), ptr(b), ptr(s), ptr(w), ptr(f), 0)
+        t = np.zeros(max(self.n_contigs, 1), np.int64)
+        call("karma_edges_totals", self.h, ptr(t), 0)
+        return EdgeArrays(a[:E], b[:E], s[:E], w[:E], f[:E], t[: self.n_contigs])
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.load().karma_edges_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def graph_from_records(records, n_contigs, grouped=True, ctx=None) -> EdgeArrays:
+    """Shared-read edges from (read, contig) records (read_graph.py:19-50 semantics)."""
+    ctx = ctx or _lib.default_context()
+    p = Pairs.from_records(ctx, records, n_contigs, grouped=grouped)
+    try:
+        e = p.edges(_lib.KARMA_MODE_READS, n_contigs)
+        try:
+            return e.get()
+        finally:
+            e.close()
+    finally:
+        p.close()
+
+
+def graph_from_eq(cls_off, members, counts, pair_skip, n_contigs, ctx=None) -> EdgeArrays:
+    """Eq-class edges (read_graph.py:86-131 semantics), with first-emission order."""
+    ctx = ctx or _lib.default_context()
+    p = Pairs.from_eq(ctx, cls_off, members, counts, pair_skip, n_contigs)
+    try:
+        e = p.edges(_lib.KARMA_MODE_EQ, n_contigs)
+        try:
+            return e.get()
+        finally:
+            e.close()
+    finally:
+        p.close()
+
+
+# ---------------------------------------------------------------------------
+# Synthetic inputs through the native generator (twin of synth.py)
+# ---------------------------------------------------------------------------
+
+def synth_contigs(seed, n, len_min=400, len_span=800, n_rate=0, first=0):
+    """(blob uint8, offsets int64[n+1], key_len int32[n]) of contigs ">ctg<i>",
+    i in [first, first + n) of the global synthetic set (counter-based, so a
+    shard generates only its own rows)."""
+    lens = np.zeros(first + n, np.int64)
+    call("karma_synth_contig_lengths", seed, first + n, len_min, len_span, ptr(lens))
+    goffs = np.zeros(first + n + 1, np.int64)
+    np.cumsum(lens, out=goffs[1:])
+    gslice = np.ascontiguousarray(goffs[first:])
+    blob = np.zeros(int(gslice[-1] - gslice[0]) + 16, np.uint8)
+    call("karma_synth_contig_bases", seed, ptr(gslice), n, n_rate, ptr(blob))
+    offs = gslice - gslice[0]
+    key_len = _key_lens(first + n)[first:].copy()
+    return blob, offs, key_len
+
+
+def _key_lens(n):
+    i = np.arange(n)
+    digits = np.ones(n, np.int32)
+    p = 10
+    while p <= n:
+        digits += (i >= p)
+        p *= 10
+    return (4 + digits).astype(np.int32)
+
+
+def synth_genes(seed, n_contigs, gene_max=4):
+    ng = ctypes.c_int64()
+    call("karma_synth_n_genes", seed, n_contigs, gene_max, ctypes.byref(ng))
+    gf = np.zeros(ng.value, np.int64)
+    gs = np.zeros(ng.value, np.int32)
+    call("karma_synth_genes", seed, n_contigs, gene_max, ptr(gf), ptr(gs))
+    return gf, gs
+
+
+def synth_records(seed, n_contigs, frag_lo, frag_hi, paired, gene_max=4, genes=None):
+    """records uint32[A, 2] (read, contig) for fragments [frag_lo, frag_hi)."""
+    gf, gs = genes if genes is not None else synth_genes(seed, n_contigs, gene_max)
+    nf = frag_hi - frag_lo
+    cnt = np.zeros(max(nf, 1), np.int32)
+    call("karma_synth_read_counts", seed, ptr(gf), ptr(gs), len(gf), frag_lo, frag_hi, int(paired), ptr(cnt))
+    off = np.zeros(nf + 1, np.int64)
+    np.cumsum(cnt[:nf], out=off[1:])
+    rec = np.zeros((max(int(off[-1]), 1), 2), np.uint32)
+    call("karma_synth_read_records", seed, ptr(gf), ptr(gs), len(gf), frag_lo, frag_hi, int(paired), ptr(off),
+         ptr(rec))
+    return rec[: int(off[-1])]

@@ -1,0 +1,271 @@
+"""GPU parity: the HIP path (through libkarma_hip.so) vs the reference.
+
+Two references are used:
+  * tests/golden/golden.json — outputs of lmfaber/karma itself (captured by
+    tests/golden/make_golden.py), compared through the drop-in classes;
+  * oracle/ — the CPU restatement pinned by those goldens, for seeded inputs
+    larger than the goldens (bit-exact integer counts and f64 weights).
+Everything here is bit-exact: integer counts, and f64 values that are one IEEE
+division (profile) or two divisions, one add and one halving (weights).
+"""
+import hashlib
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+
+from karma_amd import _lib, engine, synth
+from karma_amd.contig import Contig
+from karma_amd.kmer import KmerClustering
+from karma_amd.read_graph import ReadGraph
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def calc(seqs, kmer):
+    k = KmerClustering(OrderedDict(seqs), "/tmp", kmer, 4)
+    return k, k._KmerClustering__calc_kmer_profile()
+
+
+def check_profile(out, seqs, kmer):
+    if "exit" in out:
+        with pytest.raises(SystemExit) as e:
+            calc(seqs, kmer)
+        assert e.value.code == out["exit"]
+        return
+    if "raises" in out:
+        with pytest.raises(Exception) as e:
+            calc(seqs, kmer)
+        assert type(e.value).__name__ == out["raises"]
+        return
+    k, prof = calc(seqs, kmer)
+    assert prof.dtype == np.float64
+    assert list(prof.shape) == out["shape"]
+    assert [km for km, _ in sorted(k.kmers.items(), key=lambda kv: kv[1])] == out["columns"]
+    assert k.sorted_kmer_set == []
+    assert hashlib.sha256(prof.astype("<f8").tobytes()).hexdigest() == out["sha256"]
+    if "nz" in out:
+        r, c = prof.nonzero()
+        assert [[int(a), int(b), float(prof[a, b])] for a, b in zip(r, c)] == out["nz"]
+
+
+def test_profile_golden_hand(golden):
+    for name, case in golden["profile_hand"].items():
+        check_profile(case["out"], [tuple(x) for x in case["seqs"]], case["kmer"])
+
+
+def test_profile_golden_random(golden):
+    for name, case in golden["profile_rand"].items():
+        seqs = synth.contig_sequences(case["seed"], case["n"], case["len_min"], case["len_span"], case["n_rate"])
+        check_profile(case["out"], list(seqs.items()), case["kmer"])
+
+
+def test_profile_golden_config1(golden):
+    case = golden["profile_config1"]
+    seqs = synth.contig_sequences(case["seed"], case["n"])
+    check_profile(case["out"], list(seqs.items()), case["kmer"])
+
+
+@pytest.mark.parametrize("kmer,n_rate", [("5p6", 0), ("5p6", 50), (5, 30), (7, 0), (7, 100), (3, 5), (1, 9),
+                                         (8, 0), (8, 200), (4, 0), (6, 64)])
+def test_profile_vs_oracle_seeded(kmer, n_rate):
+    seed = 100 + (hash(str(kmer)) % 7) + n_rate
+    blob, offs, key_len = engine.synth_contigs(seed, 1500, 20, 1500, n_rate)
+    seqs = OrderedDict((f">ctg{i}", bytes(blob[offs[i]:offs[i + 1]]).decode()) for i in range(1500))
+    prof, cols, tot = engine.kmer_profile(seqs, kmer)
+    oprof, ocols, ocounts = oracle.calc_kmer_profile(seqs, kmer)
+    assert cols == ocols
+    assert prof.shape == oprof.shape
+    assert np.array_equal(prof.view(np.uint64), oprof.view(np.uint64))
+    assert np.array_equal(tot, ocounts.sum(axis=1))
+
+
+def test_profile_lowercase_iupac_and_bytes():
+    rng = np.random.default_rng(5)
+    alphabet = np.frombuffer(b"ACGTACGTACGTNacgtRY\r-*", np.uint8)
+    seqs = OrderedDict()
+    for i in range(300):
+        L = int(rng.integers(6, 400))
+        seqs[f">s{i} desc"[: 2 + i % 9]] = bytes(alphabet[rng.integers(0, len(alphabet), L)]).decode("latin-1")
+    for kmer in ("5p6", 5, 2, 7, 8):
+        prof, cols, _ = engine.kmer_profile(seqs, kmer)
+        oprof, ocols, _ = oracle.calc_kmer_profile(seqs, kmer)
+        assert cols == ocols
+        assert np.array_equal(prof.view(np.uint64), oprof.view(np.uint64))
+
+
+def test_profile_long_contigs_and_large_k8_columns():
+    # k=8 with every 8-mer present -> M > LDS capacity: global-scratch variant
+    blob, offs, key_len = engine.synth_contigs(77, 40, 30000, 20000, 0)
+    seqs = OrderedDict((f">c{i}", bytes(blob[offs[i]:offs[i + 1]]).decode()) for i in range(40))
+    prof, cols, _ = engine.kmer_profile(seqs, 8)
+    oprof, ocols, _ = oracle.calc_kmer_profile(seqs, 8)
+    assert len(cols) > 36 * 1024
+    assert cols == ocols
+    assert np.array_equal(prof.view(np.uint64), oprof.view(np.uint64))
+
+
+def test_profile_unsupported_k_raises():
+    with pytest.raises(_lib.KarmaError):
+        engine.kmer_profile(OrderedDict([(">a", "ACGTACGTACGT")]), 9)
+
+
+# ---------------------------------------------------------------- graphs ----
+
+def dump(g):
+    return {"nodes": [str(n) for n in g.nodes()],
+            "edges": [[str(a), str(b), float(d["weight"])] for a, b, d in g.edges(data=True)]}
+
+
+def test_eq_graph_golden(golden, tmp_path):
+    for name, case in list(golden["eq_hand"].items()):
+        p = tmp_path / f"{name}.txt"
+        p.write_text(case["text"])
+        out = case["out"]
+        if "raises" in out:
+            with pytest.raises(Exception) as e:
+                ReadGraph.from_equivalence_classes(str(p), OrderedDict((k, "") for k in case["fasta"]))
+            assert type(e.value).__name__ == out["raises"], name
+            continue
+        g = ReadGraph.from_equivalence_classes(str(p), OrderedDict((k, "") for k in case["fasta"]))
+        assert isinstance(g, ReadGraph)
+        d = dump(g)
+        assert d["edges"] == out["edges"], name
+        n_txp = int(case["text"].split("\n")[0])
+        assert d["nodes"][:n_txp] == out["nodes"][:n_txp]
+        assert set(d["nodes"]) == set(out["nodes"])
+    for name, case in golden["eq_synth"].items():
+        classes = synth.eq_classes(case["seed"], case["n"], case["n_frags"], case["paired"])
+        names = [f"ctg{i}" for i in range(case["n"])]
+        p = tmp_path / f"{name}.txt"
+        p.write_text(synth.eq_file_text(names, classes))
+        d = dump(ReadGraph.from_equivalence_classes(str(p), OrderedDict((">" + x, "") for x in names)))
+        assert d["edges"] == case["out"]["edges"]
+        assert d["nodes"] == case["out"]["nodes"]
+
+
+def make_contigs(names, readsets):
+    out = []
+    for n, reads in zip(names, readsets):
+        c = Contig(n)
+        c.load_from_iterator([f"{r}\t0\t{n}\t1\t60\t*" for r in reads])
+        out.append(c)
+    return out
+
+
+def test_readset_graph_golden(golden):
+    for name, case in golden["readset_hand"].items():
+        g = ReadGraph.from_contigs(make_contigs(case["names"], case["readsets"]))
+        assert dump(g) == case["out"], name
+    for name, case in golden["readset_synth"].items():
+        recs = synth.read_records(case["seed"], case["n"], case["n_frags"], case["paired"])
+        sets = [[] for _ in range(case["n"])]
+        for r, c in recs:
+            sets[c].append(f"r{r}")
+        g = ReadGraph.from_contigs(make_contigs([f"ctg{i}" for i in range(case["n"])], sets))
+        assert dump(g) == case["out"], name
+
+
+def test_update_graph_golden(golden):
+    for name, case in golden["update_hand"].items():
+        g = ReadGraph()
+        for a, b, w in case["base_edges"]:
+            g.add_edge(a, b, weight=w)
+        g.set_original_contigs(make_contigs(case["orig_names"], case["orig_sets"]))
+        g.update_graph(make_contigs(case["new_names"], case["new_sets"]))
+        assert dump(g) == case["out"], name
+
+
+def check_records(rec, n, grouped=True):
+    e = engine.graph_from_records(rec, n, grouped=grouped)
+    rs = np.asarray(rec, dtype=np.int64)
+    order = np.argsort(rs[:, 0], kind="stable")
+    rs = rs[order]
+    starts = np.flatnonzero(np.r_[True, rs[1:, 0] != rs[:-1, 0]]) if len(rs) else np.zeros(0, np.int64)
+    off = np.r_[starts, len(rs)]
+    o = oracle.graph_groups(off, rs[:, 1] if len(rs) else np.zeros(0), None, None, n, dedup=True)
+    assert np.array_equal(e.a, o["a"])
+    assert np.array_equal(e.b, o["b"])
+    assert np.array_equal(e.shared, o["shared"])
+    assert np.array_equal(e.weight.view(np.uint64), o["weight"].view(np.uint64))
+    assert np.array_equal(e.totals, o["totals"])
+    return e
+
+
+@pytest.mark.parametrize("seed,n,nf,paired", [(2, 20_000, 400_000, True), (5, 3_000, 200_000, False),
+                                              (9, 777, 50_000, True), (4, 1, 1000, True)])
+def test_records_graph_vs_oracle(seed, n, nf, paired):
+    rec = engine.synth_records(seed, n, 0, nf, paired)
+    check_records(rec, n)
+
+
+def test_records_unsorted_and_detection():
+    rec = engine.synth_records(8, 5000, 0, 100_000, True)
+    rng = np.random.default_rng(0)
+    shuf = rec[rng.permutation(len(rec))]
+    e1 = check_records(shuf, 5000, grouped=False)
+    e2 = engine.graph_from_records(rec, 5000, grouped=True)
+    assert np.array_equal(e1.weight, e2.weight)
+    with pytest.raises(_lib.KarmaError) as ei:
+        engine.graph_from_records(shuf, 5000, grouped=True)
+    assert ei.value.code == _lib.KARMA_ERR_UNSORTED
+
+
+def test_records_bucket_overflow_path():
+    # every read hits 8 random contigs of 1000 -> > 3072 distinct pairs per bucket
+    rng = np.random.default_rng(1)
+    R = 60_000
+    reads = np.repeat(np.arange(R, dtype=np.uint32), 8)
+    contigs = rng.integers(0, 1000, R * 8).astype(np.uint32)
+    check_records(np.stack([reads, contigs], 1), 1000)
+
+
+def test_records_big_reads_and_duplicates():
+    rng = np.random.default_rng(2)
+    rows = []
+    for r in range(3000):
+        m = int(rng.choice([1, 2, 3, 9, 17, 40]))
+        for c in rng.integers(0, 200, m):
+            rows.append((r, int(c)))
+            if rng.random() < 0.3:
+                rows.append((r, int(c)))  # mate on the same contig
+    check_records(np.array(rows, np.uint32), 200)
+
+
+def test_records_empty_and_bad_contig():
+    e = engine.graph_from_records(np.zeros((0, 2), np.uint32), 10)
+    assert len(e.a) == 0 and e.totals.tolist() == [0] * 10
+    with pytest.raises(_lib.KarmaError):
+        engine.graph_from_records(np.array([[0, 12]], np.uint32), 10)
+
+
+def test_eq_vs_oracle_seeded():
+    classes = synth.eq_classes(31, 2000, 300_000, True)
+    names = [f"ctg{i}" for i in range(2000)]
+    off = np.r_[0, np.cumsum([len(c) for c, _ in classes])].astype(np.int64)
+    mem = np.array([x for c, _ in classes for x in c], np.uint32)
+    cnt = np.array([k for _, k in classes], np.int64)
+    skip = np.array([1 if len(c) == 1 else 0 for c, _ in classes], np.uint8)
+    e = engine.graph_from_eq(off, mem, cnt, skip, len(names))
+    o = oracle.graph_groups(off, mem, cnt, skip, len(names), dedup=False)
+    for k in ("a", "b", "shared", "first", "totals"):
+        assert np.array_equal(getattr(e, k), o[k]), k
+    assert np.array_equal(e.weight.view(np.uint64), o["weight"].view(np.uint64))
+
+
+def test_eq_path_equals_readset_path():
+    # eq-class graph == per-read graph when each fragment's dedup
+    # set is its class
+    seed, n, nf = 12, 4000, 200_000
+    rec = engine.synth_records(seed, n, 0, nf, True)
+    er = engine.graph_from_records(rec, n)
+    classes = synth.eq_classes(seed, n, nf, True)
+    off = np.r_[0, np.cumsum([len(c) for c, _ in classes])].astype(np.int64)
+    mem = np.array([x for c, _ in classes for x in c], np.uint32)
+    cnt = np.array([k for _, k in classes], np.int64)
+    skip = np.array([1 if len(c) == 1 else 0 for c, _ in classes], np.uint8)
+    ee = engine.graph_from_eq(off, mem, cnt, skip, n)
+    assert np.array_equal(er.a, ee.a) and np.array_equal(er.b, ee.b)
+    assert np.array_equal(er.weight.view(np.uint64), ee.weight.view(np.uint64))
+    assert np.array_equal(er.totals, ee.totals)
