@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <cstdlib>
 
 #include "karma_internal.h"
 
@@ -41,11 +42,11 @@ struct karma_edges {
 
 namespace {
 
-constexpr int kWalkBlock = 256;
+constexpr int kWT = 512;             // walk threads per block
+constexpr int kWalkTile = 2048;      // records staged in LDS per tile (4 per thread)
 constexpr int kMaxFast = 8;          // register fast path: reads with <= 8 records
 constexpr int kReduceBlock = 512;
-constexpr int kTableCap = 4096;      // LDS hash slots per bucket block (32 KB)
-constexpr int kTile = kReduceBlock * 2;
+constexpr int kTableCap = 8192;      // LDS hash slots per bucket block (64 KB)
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
 struct Geo {
@@ -59,10 +60,12 @@ int make_geo(int64_t N, Geo* g) {
                 (long long)N);
     int bbits = 1;
     while ((int64_t(1) << bbits) < N) ++bbits;
+    // ~<= 512 coarse buckets: few enough that every block's open write lines
+    // (blocks x buckets x 128 B) stay in its XCD's L2, few enough distinct
+    // pairs per bucket for one LDS hash table
     int bw = 4;
-    while ((N >> bw) > 2048 && bw + 1 + bbits <= 31) ++bw;
-    while (bw + bbits > 31) --bw;
-    KARMA_CHECK(bw >= 0, KARMA_ERR_ARG, "n_contigs too large for 32-bit entries");
+    while ((N >> bw) > 512) ++bw;
+    KARMA_CHECK(bw + bbits <= 31, KARMA_ERR_ARG, "n_contigs too large for 32-bit entries");
     g->bw = bw;
     g->bbits = bbits;
     g->n_buckets = (N + (int64_t(1) << bw) - 1) >> bw;
@@ -70,55 +73,62 @@ int make_geo(int64_t N, Geo* g) {
 }
 
 // ---- per-read pair walk -------------------------------------------------------
-// Calls emit(a, b) for every pair a <= b of the read's deduplicated contig set.
-template <typename Emit>
-__device__ __forceinline__ void read_pairs(const uint2* __restrict__ rec, int64_t A, int64_t i, Emit emit) {
-    const uint32_t rid = rec[i].x;
+// A read's contigs (<= 8 records, else it is a "big read") sorted by a fixed
+// network; keep[p] marks the first copy of each distinct contig and rank[p] is
+// its index among the kept ones, so the read emits u - rank[p] entries
+// (p, q >= p) with first contig m[p] (u = number of distinct contigs).
+struct ReadSet {
     uint32_t m[kMaxFast];
-    int64_t j = i;
+    bool keep[kMaxFast];
+    uint32_t rank[kMaxFast];
+    uint32_t u;
+};
+
+template <typename Get>
+__device__ __forceinline__ bool gather_read(uint32_t rid, Get get, ReadSet& s) {
+    bool more = true;
 #pragma unroll
     for (int t = 0; t < kMaxFast; ++t) {
         uint32_t v = kEmpty;
-        if (j < A) {
-            uint2 r = rec[j];
-            if (r.x == rid) {
-                v = r.y;
-                ++j;
-            }
+        if (more) {
+            const uint2 r = get(t);
+            if (r.x == rid) v = r.y;
+            else more = false;
         }
-        m[t] = v;
+        s.m[t] = v;
     }
-    const bool big = (j < A) && rec[j].x == rid;
-    if (!big) {
-        // sorting network (Batcher odd-even merge for 8), compile-time indices only
-#define CE(x, y)                                    \
-    {                                               \
-        uint32_t lo_ = min(m[x], m[y]), hi_ = max(m[x], m[y]); \
-        m[x] = lo_;                                 \
-        m[y] = hi_;                                 \
+    if (more && get(kMaxFast).x == rid) return false;  // > 8 records
+#define CE(x, y)                                                       \
+    {                                                                  \
+        uint32_t lo_ = min(s.m[x], s.m[y]), hi_ = max(s.m[x], s.m[y]); \
+        s.m[x] = lo_;                                                  \
+        s.m[y] = hi_;                                                  \
     }
-        CE(0, 1) CE(2, 3) CE(4, 5) CE(6, 7)
-        CE(0, 2) CE(1, 3) CE(4, 6) CE(5, 7)
-        CE(1, 2) CE(5, 6)
-        CE(0, 4) CE(1, 5) CE(2, 6) CE(3, 7)
-        CE(2, 4) CE(3, 5)
-        CE(1, 2) CE(3, 4) CE(5, 6)
+    // Batcher odd-even merge sort network, 8 inputs, 19 comparators
+    CE(0, 1) CE(2, 3) CE(4, 5) CE(6, 7)
+    CE(0, 2) CE(1, 3) CE(4, 6) CE(5, 7)
+    CE(1, 2) CE(5, 6)
+    CE(0, 4) CE(1, 5) CE(2, 6) CE(3, 7)
+    CE(2, 4) CE(3, 5)
+    CE(1, 2) CE(3, 4) CE(5, 6)
 #undef CE
-        bool keep[kMaxFast];
+    uint32_t u = 0;
 #pragma unroll
-        for (int p = 0; p < kMaxFast; ++p) keep[p] = m[p] != kEmpty && (p == 0 || m[p] != m[p - 1]);
-#pragma unroll
-        for (int p = 0; p < kMaxFast; ++p) {
-#pragma unroll
-            for (int q = p; q < kMaxFast; ++q) {
-                if (keep[p] && keep[q]) emit(m[p], m[q]);
-            }
-        }
-        return;
+    for (int p = 0; p < kMaxFast; ++p) {
+        s.keep[p] = s.m[p] != kEmpty && (p == 0 || s.m[p] != s.m[p - 1]);
+        s.rank[p] = u;
+        u += s.keep[p] ? 1u : 0u;
     }
-    // slow path: arbitrary read size, O(m^3) over global memory (rare: reads
-    // mapping to more than 8 records)
-    int64_t end = j;
+    s.u = u;
+    return true;
+}
+
+// Arbitrary read size (reads with more than 8 records; rare), O(m^3) over
+// global memory, one thread per read.
+template <typename Emit>
+__device__ void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_t i, Emit emit) {
+    const uint32_t rid = rec[i].x;
+    int64_t end = i;
     while (end < A && rec[end].x == rid) ++end;
     for (int64_t p = i; p < end; ++p) {
         const uint32_t c = rec[p].y;
@@ -135,45 +145,204 @@ __device__ __forceinline__ void read_pairs(const uint2* __restrict__ rec, int64_
     }
 }
 
-template <bool SCATTER>
-__global__ void __launch_bounds__(kWalkBlock) walk_kernel(const uint2* __restrict__ rec, int64_t A, int64_t chunk,
-                                                          int bw, int bbits, int64_t n_buckets, int64_t n_blocks,
-                                                          uint32_t* __restrict__ hist,  // [bucket][block]
-                                                          const int64_t* __restrict__ offs,
-                                                          uint32_t* __restrict__ entries, int* __restrict__ unsorted,
-                                                          uint32_t n_contigs, int* __restrict__ bad_contig) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long lds_cnt[];  // n_buckets
+// COUNT=true : entries per (bucket, block) + order/contig checks + big-read list
+// COUNT=false: writes the 32-bit entries (a_local << bbits | b) at bucket-major
+//              positions; one LDS cursor reservation per (read, bucket run).
+template <bool COUNT>
+__global__ void __launch_bounds__(kWT) walk_kernel(const uint2* __restrict__ rec, int64_t A, int64_t chunk, int bw,
+                                                   int bbits, int B, int nblk, uint32_t* __restrict__ hist,
+                                                   const int64_t* __restrict__ offs, uint32_t* __restrict__ entries,
+                                                   int* __restrict__ flags, uint32_t N, int64_t* __restrict__ big_list,
+                                                   unsigned* __restrict__ big_n) {
+    constexpr int TILE = kWalkTile;
+    __shared__ uint2 trec[TILE];
+    __shared__ uint16_t starts[TILE];
+    __shared__ uint32_t wave_cnt[kWT / 64];
+    __shared__ uint32_t n_starts;
+    __shared__ uint32_t prev_rid;
+    __shared__ int has_prev;
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    unsigned long long* cursor = reinterpret_cast<unsigned long long*>(dyn);  // !COUNT
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(dyn);                          // COUNT
+
     const int64_t blk = blockIdx.x;
-    for (int64_t b = threadIdx.x; b < n_buckets; b += blockDim.x)
-        lds_cnt[b] = SCATTER ? (unsigned long long)offs[b * n_blocks + blk] : 0ull;
-    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        if (COUNT) cnt[b] = 0;
+        else cursor[b] = (unsigned long long)offs[(int64_t)b * (nblk + 1) + blk];
+    }
     const int64_t lo = blk * chunk, hi = min(A, lo + chunk);
     const uint32_t wmask = (1u << bw) - 1u;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-        const uint2 r = rec[i];
-        bool start = true;
-        if (i > 0) {
-            const uint32_t prev = rec[i - 1].x;
-            start = prev != r.x;
-            if (!SCATTER && prev > r.x) *unsorted = 1;
-        }
-        if (!SCATTER && r.y >= n_contigs) *bad_contig = 1;
-        if (!start) continue;
-        read_pairs(rec, A, i, [&](uint32_t a, uint32_t b) {
-            if (a >= n_contigs || b >= n_contigs) return;
-            const uint32_t bucket = a >> bw;
-            if (SCATTER) {
-                const unsigned long long pos = atomicAdd(&lds_cnt[bucket], 1ull);
-                entries[pos] = ((a & wmask) << bbits) | b;
-            } else {
-                atomicAdd(&lds_cnt[bucket], 1ull);
+    int bad_order = 0, bad_contig = 0;
+    for (int64_t ts = lo; ts < hi; ts += TILE) {
+        const int tn = (int)min<int64_t>(TILE, hi - ts);
+        __syncthreads();  // previous tile fully consumed
+        // stage the tile: each wave loads 256 consecutive records (non-temporal:
+        // the stream is read once; L2 is left to the open write lines)
+        uint2 r4[TILE / kWT];
+#pragma unroll
+        for (int u = 0; u < TILE / kWT; ++u) {
+            const int j = wave * (TILE / (kWT / 64)) + u * 64 + lane;
+            uint2 r = make_uint2(kEmpty, kEmpty);
+            if (j < tn) {
+                const unsigned long long v =
+                    __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(rec + ts + j));
+                r = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+                trec[j] = r;
             }
-        });
-    }
-    if (!SCATTER) {
+            r4[u] = r;
+        }
+        if (threadIdx.x == 0) {
+            has_prev = ts > 0;
+            prev_rid = ts > 0 ? rec[ts - 1].x : 0u;
+        }
         __syncthreads();
-        for (int64_t b = threadIdx.x; b < n_buckets; b += blockDim.x) hist[b * n_blocks + blk] = (uint32_t)lds_cnt[b];
+        // read starts of this tile, compacted (block-wide, in tile order)
+        bool st[TILE / kWT];
+#pragma unroll
+        for (int u = 0; u < TILE / kWT; ++u) {
+            const int j = wave * (TILE / (kWT / 64)) + u * 64 + lane;
+            bool s = false;
+            if (j < tn) {
+                const uint2 r = r4[u];
+                const bool hp = j > 0 || has_prev;
+                const uint32_t p = j > 0 ? trec[j - 1].x : prev_rid;
+                if (COUNT) {
+                    if (hp && p > r.x) bad_order = 1;
+                    if (r.y >= N) bad_contig = 1;
+                }
+                s = !hp || p != r.x;
+            }
+            st[u] = s;
+        }
+        // wave-level exclusive offsets via ballots (tile order within the wave)
+        uint32_t wbase = 0;
+#pragma unroll
+        for (int u = 0; u < TILE / kWT; ++u) wbase += __popcll(__ballot(st[u]));
+        if (lane == 0) wave_cnt[wave] = wbase;
+        __syncthreads();
+        uint32_t off0 = 0;
+        for (int w = 0; w < wave; ++w) off0 += wave_cnt[w];
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < kWT / 64; ++w) t += wave_cnt[w];
+            n_starts = t;
+        }
+#pragma unroll
+        for (int u = 0; u < TILE / kWT; ++u) {
+            const unsigned long long bal = __ballot(st[u]);
+            if (st[u]) {
+                const int j = wave * (TILE / (kWT / 64)) + u * 64 + lane;
+                starts[off0 + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)j;
+            }
+            off0 += __popcll(bal);
+        }
+        __syncthreads();
+        const int ns = (int)n_starts;
+        // one lane per read
+        for (int s = threadIdx.x; s < ns; s += blockDim.x) {
+            const int j0 = starts[s];
+            const uint32_t rid = trec[j0].x;
+            ReadSet rs;
+            const bool fast = gather_read(rid, [&](int t) -> uint2 {
+                const int j = j0 + t;
+                if (j < tn) return trec[j];
+                const int64_t g = ts + j;
+                return g < A ? rec[g] : make_uint2(kEmpty, kEmpty);
+            }, rs);
+            if (!fast) {
+                if (COUNT) big_list[atomicAdd(big_n, 1u)] = ts + j0;
+                continue;
+            }
+            // runs of kept contigs in the same bucket (m[] is sorted)
+            uint32_t run_b = kEmpty, run_n = 0;
+            unsigned long long base[kMaxFast];
+#pragma unroll
+            for (int p = 0; p < kMaxFast; ++p) {
+                base[p] = 0;
+                if (rs.keep[p] && rs.m[p] < N) {
+                    const uint32_t b = rs.m[p] >> bw;
+                    if (b != run_b) {
+                        if (run_n) {
+                            if (COUNT) atomicAdd(&cnt[run_b], run_n);
+                        }
+                        run_b = b;
+                        run_n = 0;
+                    }
+                    run_n += rs.u - rs.rank[p];
+                }
+            }
+            if (run_n && COUNT) atomicAdd(&cnt[run_b], run_n);
+            if (!COUNT) {
+                // second sweep: reserve per run, then write the run's entries
+                uint32_t rb = kEmpty, rn = 0;
+                int rp0 = 0;
+#pragma unroll
+                for (int p = 0; p <= kMaxFast; ++p) {
+                    const bool valid = p < kMaxFast && rs.keep[p] && rs.m[p] < N;
+                    const uint32_t b = valid ? (rs.m[p] >> bw) : kEmpty;
+                    if (p == kMaxFast || (valid && b != rb)) {
+                        if (rn) {
+                            unsigned long long pos = atomicAdd(&cursor[rb], (unsigned long long)rn);
+#pragma unroll
+                            for (int q = 0; q < kMaxFast; ++q) {
+                                if (q >= rp0 && q < p && rs.keep[q] && rs.m[q] < N) {
+                                    base[q] = pos;
+                                    pos += rs.u - rs.rank[q];
+                                }
+                            }
+                        }
+                        if (valid) {
+                            rb = b;
+                            rn = 0;
+                            rp0 = p;
+                        }
+                    }
+                    if (valid) rn += rs.u - rs.rank[p];
+                }
+#pragma unroll
+                for (int p = 0; p < kMaxFast; ++p) {
+                    if (!(rs.keep[p] && rs.m[p] < N)) continue;
+                    const uint32_t a = rs.m[p];
+                    const uint32_t hi_key = (a & wmask) << bbits;
+                    unsigned long long pos = base[p];
+#pragma unroll
+                    for (int q = p; q < kMaxFast; ++q) {
+                        if (rs.keep[q] && rs.m[q] < N) entries[pos++] = hi_key | rs.m[q];
+                    }
+                }
+            }
+        }
     }
+    if (COUNT) {
+        if (bad_order) flags[0] = 1;
+        if (bad_contig) flags[1] = 1;
+        __syncthreads();
+        for (int b = threadIdx.x; b < B; b += blockDim.x) hist[(int64_t)b * (nblk + 1) + blk] = cnt[b];
+    }
+}
+
+// Reads with more than 8 records: one thread per read, the virtual last block
+// column of the histogram (global atomics; rare).
+template <bool SCATTER>
+__global__ void big_reads_kernel(const uint2* __restrict__ rec, int64_t A, const int64_t* __restrict__ big_list,
+                                 int64_t n_big, int bw, int bbits, int nblk, uint32_t* __restrict__ hist,
+                                 unsigned long long* __restrict__ cursor, uint32_t* __restrict__ entries, uint32_t N) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_big) return;
+    const uint32_t wmask = (1u << bw) - 1u;
+    read_pairs_slow(rec, A, big_list[k], [&](uint32_t a, uint32_t b) {
+        if (b >= N) return;
+        const uint32_t bucket = a >> bw;
+        if (SCATTER) entries[atomicAdd(&cursor[bucket], 1ull)] = ((a & wmask) << bbits) | b;
+        else atomicAdd(&hist[(int64_t)bucket * (nblk + 1) + nblk], 1u);
+    });
+}
+
+__global__ void big_cursor_kernel(const int64_t* __restrict__ offs, int B, int nblk,
+                                  unsigned long long* __restrict__ cursor) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < B) cursor[b] = (unsigned long long)offs[(int64_t)b * (nblk + 1) + nblk];
 }
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
@@ -209,7 +378,7 @@ __device__ void lds_bitonic(uint32_t* keys, uint32_t* vals, int n) {
 
 // One block per bucket: aggregate entries with an LDS hash table, sort, emit
 // (global key, count).  Sets overflow[bucket] and bails out if the bucket has
-// more than kTableCap - kTile distinct pairs (handled by the generic path).
+// more than kTableCap - 2048 distinct pairs (handled by the generic path).
 __global__ void __launch_bounds__(kReduceBlock) bucket_reduce_kernel(
     const uint32_t* __restrict__ entries, const int64_t* __restrict__ bstart, int bw, int bbits,
     uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n,
@@ -229,33 +398,44 @@ __global__ void __launch_bounds__(kReduceBlock) bucket_reduce_kernel(
         ovf = 0;
     }
     __syncthreads();
-    for (int64_t base = s; base < e; base += kTile) {
-        if (nuniq > kTableCap - kTile) {
+    // 16-byte loads (4 entries per lane), the next iteration's loads issued
+    // before the current one is inserted: ~16 KB in flight per block
+    const int64_t a0 = s & ~int64_t(3);
+    constexpr int64_t kIter = 4 * kReduceBlock;
+    auto load4 = [&](int64_t base) -> uint4 {
+        const int64_t i = base + 4 * threadIdx.x;
+        return i < e ? *reinterpret_cast<const uint4*>(entries + i) : make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
+    };
+    uint4 nxt = load4(a0);
+    for (int64_t base = a0; base < e; base += kIter) {
+        if (nuniq > kTableCap - kIter) {
             if (threadIdx.x == 0) ovf = 1;
             break;
         }
+        const uint4 cur = nxt;
+        nxt = load4(base + kIter);
+        const uint32_t v[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
-        for (int u = 0; u < kTile / kReduceBlock; ++u) {
-            const int64_t i = base + u * kReduceBlock + threadIdx.x;
-            if (i < e) {
-                const uint32_t key = entries[i];
-                uint32_t h = hash32(key) & (kTableCap - 1);
-                while (true) {
-                    const uint32_t k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (k == key) {
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + 4 * threadIdx.x + u;
+            if (i < s || i >= e) continue;
+            const uint32_t key = v[u];
+            uint32_t h = hash32(key) & (kTableCap - 1);
+            while (true) {
+                const uint32_t k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (k == key) {
+                    atomicAdd(&vals[h], 1u);
+                    break;
+                }
+                if (k == kEmpty) {
+                    const uint32_t old = atomicCAS(&keys[h], kEmpty, key);
+                    if (old == kEmpty || old == key) {
+                        if (old == kEmpty) atomicAdd(&nuniq, 1);
                         atomicAdd(&vals[h], 1u);
                         break;
                     }
-                    if (k == kEmpty) {
-                        const uint32_t old = atomicCAS(&keys[h], kEmpty, key);
-                        if (old == kEmpty || old == key) {
-                            if (old == kEmpty) atomicAdd(&nuniq, 1);
-                            atomicAdd(&vals[h], 1u);
-                            break;
-                        }
-                    }
-                    h = (h + 1) & (kTableCap - 1);
                 }
+                h = (h + 1) & (kTableCap - 1);
             }
         }
         __syncthreads();
@@ -495,45 +675,63 @@ int grid1(int64_t n, int block = 256) { return (int)std::max<int64_t>(1, ceil_di
 int records_to_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
     Geo g;
     KARMA_TRY(make_geo(N, &g));
-    const int64_t n_blocks = std::max<int64_t>(1, std::min<int64_t>(4096, ceil_div(A, 2048)));
-    const int64_t chunk = std::max<int64_t>(1, ceil_div(A, n_blocks));
-    const int64_t H = g.n_buckets * n_blocks;
+    const int B = (int)g.n_buckets;
+    constexpr int kTileCount = kWalkTile;
+    // persistent-style grid: <= 1024 blocks, each a contiguous run of whole tiles
+    int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(1024, ceil_div(A, kTileCount)));
+    const int64_t chunk = std::max<int64_t>(kTileCount, ceil_div(ceil_div(A, nblk), kTileCount) * kTileCount);
+    nblk = std::max<int64_t>(1, ceil_div(A, chunk));
+    const int64_t H = (int64_t)B * (nblk + 1);  // last column: reads with > 8 records
     DevArray<uint32_t> hist;
-    DevArray<int64_t> hist64, offs, bstart;
+    DevArray<int64_t> hist64, offs, bstart, big_list;
     DevArray<int> flags;
+    DevArray<unsigned> big_n;
     KARMA_TRY(hist.alloc(ctx, H));
     KARMA_TRY(hist64.alloc(ctx, H + 1));
     KARMA_TRY(offs.alloc(ctx, H + 1));
     KARMA_TRY(bstart.alloc(ctx, g.n_buckets + 1));
     KARMA_TRY(flags.alloc(ctx, 2));
+    KARMA_TRY(big_n.alloc(ctx, 1));
+    KARMA_TRY(big_list.alloc(ctx, A / (kMaxFast + 1) + 1));
     KARMA_HIP(hipMemsetAsync(flags.ptr, 0, 8, ctx->stream));
-    const size_t lds = g.n_buckets * sizeof(unsigned long long);
-    KARMA_CHECK(lds <= 160 * 1024, KARMA_ERR_ARG, "too many buckets (%lld)", (long long)g.n_buckets);
-    if (A > 0) {
-        KARMA_LAUNCH(ctx, "graph_count", walk_kernel<false>, n_blocks, kWalkBlock, lds, rec, A, chunk, g.bw, g.bbits,
-                     g.n_buckets, n_blocks, hist.ptr, (const int64_t*)nullptr, (uint32_t*)nullptr, flags.ptr,
-                     (uint32_t)N, flags.ptr + 1);
-    } else {
-        KARMA_HIP(hipMemsetAsync(hist.ptr, 0, H * 4, ctx->stream));
-    }
-    KARMA_LAUNCH(ctx, "hist_widen", u32_to_i64_kernel, grid1(H), 256, 0, hist.ptr, hist64.ptr, H);
-    KARMA_HIP(hipMemsetAsync(hist64.ptr + H, 0, 8, ctx->stream));
-    KARMA_TRY(scan_i64(ctx, hist64.ptr, offs.ptr, H + 1));
+    KARMA_HIP(hipMemsetAsync(big_n.ptr, 0, 4, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(hist.ptr, 0, H * 4, ctx->stream));
+    if (A > 0)
+        KARMA_LAUNCH(ctx, "graph_count", walk_kernel<true>, nblk, kWT, B * 4, rec, A, chunk, g.bw, g.bbits, B,
+                     (int)nblk, hist.ptr, (const int64_t*)nullptr, (uint32_t*)nullptr, flags.ptr, (uint32_t)N,
+                     big_list.ptr, big_n.ptr);
     int hflags[2];
-    int64_t total = 0;
+    unsigned n_big = 0;
     KARMA_HIP(hipMemcpyAsync(hflags, flags.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipMemcpyAsync(&total, offs.ptr + H, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipMemcpyAsync(&n_big, big_n.ptr, 4, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
     KARMA_CHECK(!hflags[0], KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
     KARMA_CHECK(!hflags[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
+    if (n_big)
+        KARMA_LAUNCH(ctx, "graph_big_count", big_reads_kernel<false>, grid1(n_big, 64), 64, 0, rec, A, big_list.ptr,
+                     (int64_t)n_big, g.bw, g.bbits, (int)nblk, hist.ptr, (unsigned long long*)nullptr,
+                     (uint32_t*)nullptr, (uint32_t)N);
+    KARMA_LAUNCH(ctx, "hist_widen", u32_to_i64_kernel, grid1(H), 256, 0, hist.ptr, hist64.ptr, H);
+    KARMA_HIP(hipMemsetAsync(hist64.ptr + H, 0, 8, ctx->stream));
+    KARMA_TRY(scan_i64(ctx, hist64.ptr, offs.ptr, H + 1));
+    int64_t total = 0;
+    KARMA_HIP(hipMemcpyAsync(&total, offs.ptr + H, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
     KARMA_LAUNCH(ctx, "bucket_bounds", bucket_bounds_kernel, grid1(g.n_buckets + 1), 256, 0, offs.ptr, g.n_buckets,
-                 n_blocks, total, bstart.ptr);
+                 nblk + 1, total, bstart.ptr);
     DevArray<uint32_t> entries;
-    KARMA_TRY(entries.alloc(ctx, total));
+    KARMA_TRY(entries.alloc(ctx, total + 4));  // +4: 16-byte loads past the end
     if (A > 0)
-        KARMA_LAUNCH(ctx, "graph_scatter", walk_kernel<true>, n_blocks, kWalkBlock, lds, rec, A, chunk, g.bw, g.bbits,
-                     g.n_buckets, n_blocks, (uint32_t*)nullptr, offs.ptr, entries.ptr, flags.ptr, (uint32_t)N,
-                     flags.ptr + 1);
+        KARMA_LAUNCH(ctx, "graph_scatter", walk_kernel<false>, nblk, kWT, B * 8, rec, A, chunk, g.bw, g.bbits, B,
+                     (int)nblk, (uint32_t*)nullptr, offs.ptr, entries.ptr, flags.ptr, (uint32_t)N, (int64_t*)nullptr,
+                     (unsigned*)nullptr);
+    if (n_big) {
+        DevArray<unsigned long long> cur;
+        KARMA_TRY(cur.alloc(ctx, B));
+        KARMA_LAUNCH(ctx, "big_cursor", big_cursor_kernel, grid1(B), 256, 0, offs.ptr, B, (int)nblk, cur.ptr);
+        KARMA_LAUNCH(ctx, "graph_big_scatter", big_reads_kernel<true>, grid1(n_big, 64), 64, 0, rec, A, big_list.ptr,
+                     (int64_t)n_big, g.bw, g.bbits, (int)nblk, (uint32_t*)nullptr, cur.ptr, entries.ptr, (uint32_t)N);
+    }
     // per-bucket reduction
     DevArray<uint64_t> slot_k;
     DevArray<int64_t> slot_c, n_per;

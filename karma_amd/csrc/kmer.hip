@@ -185,8 +185,14 @@ __device__ __forceinline__ Window load_window(const uint32_t* packed, const uint
 }
 
 // ------------------------------------------------------------- presence ------
-// Sets the ACGT-ordinal presence bitmap (LDS-private per block, OR-flushed once)
-// and appends the byte keys of k-mers touching an exception base.
+// One wave per contig.  Sets the ACGT-ordinal presence bitmap (LDS-private per
+// block, test-before-set so the hot bits stop costing atomics, OR-flushed once
+// per block) and appends the byte keys of k-mers touching an exception base.
+__device__ __forceinline__ void set_bit(uint32_t* bits, uint32_t o) {
+    const uint32_t m = 1u << (o & 31);
+    if (!(bits[o >> 5] & m)) atomicOr(&bits[o >> 5], m);
+}
+
 template <bool P56>
 __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __restrict__ packed,
                                                           const uint16_t* __restrict__ mask,
@@ -199,66 +205,53 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
                                                           unsigned long long* __restrict__ exc_cnt,
                                                           int64_t* __restrict__ row_tot) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
-    __shared__ unsigned long long blk_tot;
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) lds_bits[w] = 0;
+    __syncthreads();
     const int kmin = P56 ? 5 : k;
-    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
-        if (threadIdx.x == 0) blk_tot = 0;
-        __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+    auto push_exc = [&](uint64_t key) {
+        const unsigned long long slot = atomicAdd(exc_cnt, 1ull);
+        if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
+    };
+    for (int64_t c = (int64_t)blockIdx.x * wpb + wave; c < n; c += (int64_t)gridDim.x * wpb) {
         const int64_t L = off[c + 1] - off[c], w0 = woff[c];
         const bool exc = has_exc[c] != 0;
         unsigned my = 0;
-        for (int64_t i = threadIdx.x; i + kmin <= L; i += blockDim.x) {
-            Window v = load_window(packed, mask, w0, i, exc);
+        for (int64_t i = lane; i + kmin <= L; i += 64) {
+            const Window v = load_window(packed, mask, w0, i, exc);
             if (P56) {
-                // 5-mer at i (kmer.py:72-73)
-                if (v.clean(5)) {
-                    uint32_t o5 = v.code(5) * 5u;
-                    atomicOr(&lds_bits[o5 >> 5], 1u << (o5 & 31));
-                } else {
-                    uint64_t key = key_from_bytes(raw + off[c] + i, 5, true);
-                    unsigned long long slot = atomicAdd(exc_cnt, 1ull);
-                    if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
-                }
+                if (v.clean(5)) set_bit(lds_bits, v.code(5) * 5u);  // kmer.py:72-73
+                else push_exc(key_from_bytes(raw + off[c] + i, 5, true));
                 ++my;
-                // palindromic 6-mer at i (kmer.py:76-80)
-                if (i + 6 <= L) {
+                if (i + 6 <= L) {  // palindromic 6-mers, kmer.py:76-80
                     if (v.clean(6)) {
-                        uint32_t c6 = v.code(6);
+                        const uint32_t c6 = v.code(6);
                         if (pal6_code(c6)) {
-                            uint32_t o6 = (c6 >> 2) * 5u + 1u + (c6 & 3u);
-                            atomicOr(&lds_bits[o6 >> 5], 1u << (o6 & 31));
+                            set_bit(lds_bits, (c6 >> 2) * 5u + 1u + (c6 & 3u));
                             ++my;
                         }
                     } else {
                         const uint8_t* p = raw + off[c] + i;
                         if (pal_bytes(p, 6)) {
-                            uint64_t key = key_from_bytes(p, 6, true);
-                            unsigned long long slot = atomicAdd(exc_cnt, 1ull);
-                            if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
+                            push_exc(key_from_bytes(p, 6, true));
                             ++my;
                         }
                     }
                 }
             } else {
-                if (v.clean(k)) {
-                    uint32_t o = v.code(k);
-                    atomicOr(&lds_bits[o >> 5], 1u << (o & 31));
-                } else {
-                    uint64_t key = key_from_bytes(raw + off[c] + i, k, with_len);
-                    unsigned long long slot = atomicAdd(exc_cnt, 1ull);
-                    if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
-                }
+                if (v.clean(k)) set_bit(lds_bits, v.code(k));
+                else push_exc(key_from_bytes(raw + off[c] + i, k, with_len));
                 ++my;
             }
         }
-        if (my) atomicAdd(&blk_tot, (unsigned long long)my);
-        __syncthreads();
-        if (threadIdx.x == 0) row_tot[c] = (int64_t)blk_tot;
+        // wave sum of k-mer occurrences -> row_tot (0 = the all-zero row, kmer.py:250-258)
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) my += __shfl_xor(my, d);
+        if (lane == 0) row_tot[c] = (int64_t)my;
     }
     __syncthreads();
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
-        uint32_t b = lds_bits[w];
+        const uint32_t b = lds_bits[w];
         if (b) atomicOr(&presence[w], b);
     }
 }
@@ -331,9 +324,70 @@ __global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* __re
 }
 
 // -------------------------------------------------------------- profile ------
-// One contig per block iteration: LDS histogram over the M columns, then the
-// dense row count/len(key) is streamed out (8*M bytes per contig).
-template <bool P56, bool LDS_COUNTS>
+// WAVE=true : one wave per contig, its own LDS histogram (M <= kWaveMaxM),
+//             no block barriers; WAVE=false: one block per contig (large M,
+//             histogram in LDS or, past the LDS budget, in a global scratch row).
+// The dense row count / len(key) (kmer.py:120, :231-233) streams out with
+// 16-byte non-temporal stores when the row start is 16-byte aligned.
+constexpr int kWaveMaxM = 4096;
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+template <bool P56, typename Add>
+__device__ __forceinline__ void count_contig(const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask,
+                                             bool excp, int64_t w0, const uint8_t* __restrict__ craw, int64_t L,
+                                             int k, bool with_len, const int32_t* __restrict__ col_of_ord,
+                                             const uint64_t* __restrict__ exc, int64_t X,
+                                             const int32_t* __restrict__ col_of_exc, int64_t i0, int64_t step,
+                                             Add add) {
+    const int kmin = P56 ? 5 : k;
+    for (int64_t i = i0; i + kmin <= L; i += step) {
+        const Window v = load_window(packed, mask, w0, i, excp);
+        if (P56) {
+            if (v.clean(5)) add(col_of_ord[v.code(5) * 5u]);
+            else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 5, true))]);
+            if (i + 6 <= L) {
+                if (v.clean(6)) {
+                    const uint32_t c6 = v.code(6);
+                    if (pal6_code(c6)) add(col_of_ord[(c6 >> 2) * 5u + 1u + (c6 & 3u)]);
+                } else if (pal_bytes(craw + i, 6)) {
+                    add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 6, true))]);
+                }
+            }
+        } else {
+            if (v.clean(k)) add(col_of_ord[v.code(k)]);
+            else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
+        }
+    }
+}
+
+__device__ __forceinline__ void write_row(double* __restrict__ row, const uint32_t* __restrict__ counts, int64_t M,
+                                          int32_t klen, int* __restrict__ err, int t0, int step) {
+    const double len = (double)klen;
+    if ((reinterpret_cast<uintptr_t>(row) & 15) == 0) {
+        const int64_t M2 = M >> 1;
+        for (int64_t j = t0; j < M2; j += step) {
+            const uint32_t a = counts[2 * j], b = counts[2 * j + 1];
+            if ((a | b) && klen == 0) *err = 1;
+            d2 v;
+            v.x = a ? (double)a / len : 0.0;  // IEEE correctly rounded (kmer.py:120)
+            v.y = b ? (double)b / len : 0.0;
+            __builtin_nontemporal_store(v, reinterpret_cast<d2*>(row) + j);
+        }
+        if ((M & 1) && t0 == 0) {
+            const uint32_t a = counts[M - 1];
+            if (a && klen == 0) *err = 1;
+            __builtin_nontemporal_store(a ? (double)a / len : 0.0, row + M - 1);
+        }
+    } else {
+        for (int64_t j = t0; j < M; j += step) {
+            const uint32_t a = counts[j];
+            if (a && klen == 0) *err = 1;
+            __builtin_nontemporal_store(a ? (double)a / len : 0.0, row + j);
+        }
+    }
+}
+
+template <bool P56, bool WAVE, bool LDS_COUNTS>
 __global__ void __launch_bounds__(kBlock) profile_kernel(
     const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
     const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
@@ -341,52 +395,36 @@ __global__ void __launch_bounds__(kBlock) profile_kernel(
     const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
     double* __restrict__ out, int64_t ld, uint32_t* __restrict__ scratch, int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_counts[];
-    uint32_t* counts = LDS_COUNTS ? lds_counts : scratch + (int64_t)blockIdx.x * M;
-    const int kmin = P56 ? 5 : k;
-    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
-        for (int64_t j = threadIdx.x; j < M; j += blockDim.x) counts[j] = 0;
-        __syncthreads();
-        const int64_t L = off[c + 1] - off[c], w0 = woff[c];
-        const bool excp = has_exc[c] != 0;
-        for (int64_t i = threadIdx.x; i + kmin <= L; i += blockDim.x) {
-            Window v = load_window(packed, mask, w0, i, excp);
-            if (P56) {
-                if (v.clean(5)) {
-                    atomicAdd(&counts[col_of_ord[v.code(5) * 5u]], 1u);
-                } else {
-                    uint64_t key = key_from_bytes(raw + off[c] + i, 5, true);
-                    atomicAdd(&counts[col_of_exc[lower_bound_u64(exc, X, key)]], 1u);
-                }
-                if (i + 6 <= L) {
-                    if (v.clean(6)) {
-                        uint32_t c6 = v.code(6);
-                        if (pal6_code(c6)) atomicAdd(&counts[col_of_ord[(c6 >> 2) * 5u + 1u + (c6 & 3u)]], 1u);
-                    } else {
-                        const uint8_t* p = raw + off[c] + i;
-                        if (pal_bytes(p, 6)) {
-                            uint64_t key = key_from_bytes(p, 6, true);
-                            atomicAdd(&counts[col_of_exc[lower_bound_u64(exc, X, key)]], 1u);
-                        }
-                    }
-                }
-            } else {
-                if (v.clean(k)) {
-                    atomicAdd(&counts[col_of_ord[v.code(k)]], 1u);
-                } else {
-                    uint64_t key = key_from_bytes(raw + off[c] + i, k, with_len);
-                    atomicAdd(&counts[col_of_exc[lower_bound_u64(exc, X, key)]], 1u);
-                }
-            }
+    if (WAVE) {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+        uint32_t* counts = lds_counts + wave * M;
+        for (int64_t c = (int64_t)blockIdx.x * wpb + wave; c < n; c += (int64_t)gridDim.x * wpb) {
+            for (int64_t j = lane; j < M; j += 64) counts[j] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const int64_t s = off[c];
+            count_contig<P56>(packed, mask, has_exc[c] != 0, woff[c], raw + s, off[c + 1] - s, k, with_len,
+                              col_of_ord, exc, X, col_of_exc, lane, 64,
+                              [&](int32_t col) { atomicAdd(&counts[col], 1u); });
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            write_row(out + c * ld, counts, M, keylen[c], err, lane, 64);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
-        __syncthreads();
-        const double len = (double)keylen[c];
-        double* row = out + c * ld;
-        for (int64_t j = threadIdx.x; j < M; j += blockDim.x) {
-            const uint32_t v = counts[j];
-            if (v && keylen[c] == 0) *err = 1;
-            row[j] = v ? (double)v / len : 0.0;  // IEEE correctly rounded (kmer.py:120)
+    } else {
+        uint32_t* counts = LDS_COUNTS ? lds_counts : scratch + (int64_t)blockIdx.x * M;
+        for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
+            for (int64_t j = threadIdx.x; j < M; j += blockDim.x) counts[j] = 0;
+            __syncthreads();
+            const int64_t s = off[c];
+            count_contig<P56>(packed, mask, has_exc[c] != 0, woff[c], raw + s, off[c + 1] - s, k, with_len,
+                              col_of_ord, exc, X, col_of_exc, threadIdx.x, blockDim.x,
+                              [&](int32_t col) { atomicAdd(&counts[col], 1u); });
+            __syncthreads();
+            write_row(out + c * ld, counts, M, keylen[c], err, threadIdx.x, blockDim.x);
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 
@@ -524,7 +562,7 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
     KARMA_HIP(hipMemsetAsync(p->presence.ptr, 0, p->nwords * 4, ctx->stream));
     KARMA_HIP(hipMemsetAsync(exc_cnt.ptr, 0, 8, ctx->stream));
     if (c->n) {
-        const int grid = grid_for(c->n, 2048);
+        const int grid = grid_for(ceil_div(c->n, kBlock / 64), 2048);
         const size_t lds = p->nwords * 4;
         if (kmode == KARMA_KMER_5P6)
             KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<true>, grid, kBlock, lds, c->packed.ptr, c->mask.ptr,
@@ -711,22 +749,25 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
     if ((rc = err.alloc(ctx, 1))) return rc;
     KARMA_HIP(hipMemsetAsync(err.ptr, 0, 4, ctx->stream));
     bool with_len = p->kmode != 8;
+    const bool wave = M <= kWaveMaxM;
     const bool lds_ok = M * 4 <= 144 * 1024;
-    const int grid = grid_for(n, lds_ok ? 4096 : 1024);
+    const int grid = wave ? grid_for(ceil_div(n, kBlock / 64), 2048) : grid_for(n, lds_ok ? 4096 : 1024);
     DevArray<uint32_t> scratch;
-    if (!lds_ok && (rc = scratch.alloc(ctx, (size_t)grid * M))) return rc;
-    const size_t lds = lds_ok ? M * 4 : 0;
+    if (!wave && !lds_ok && (rc = scratch.alloc(ctx, (size_t)grid * M))) return rc;
+    const size_t lds = wave ? (kBlock / 64) * M * 4 : (lds_ok ? M * 4 : 0);
     const int k = p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode;
-#define KARMA_PROFILE_LAUNCH(P56, LDS)                                                                           \
-    KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, LDS>), grid, kBlock, lds, c->packed.ptr, c->mask.ptr, \
-                 c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len, p->col_of_ord.ptr,       \
-                 p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err.ptr)
+#define KARMA_PROFILE_LAUNCH(P56, W, LDS)                                                                        \
+    KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, W, LDS>), grid, kBlock, lds, c->packed.ptr,           \
+                 c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len,            \
+                 p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err.ptr)
     if (p->kmode == KARMA_KMER_5P6) {
-        if (lds_ok) KARMA_PROFILE_LAUNCH(true, true);
-        else KARMA_PROFILE_LAUNCH(true, false);
+        if (wave) KARMA_PROFILE_LAUNCH(true, true, true);
+        else if (lds_ok) KARMA_PROFILE_LAUNCH(true, false, true);
+        else KARMA_PROFILE_LAUNCH(true, false, false);
     } else {
-        if (lds_ok) KARMA_PROFILE_LAUNCH(false, true);
-        else KARMA_PROFILE_LAUNCH(false, false);
+        if (wave) KARMA_PROFILE_LAUNCH(false, true, true);
+        else if (lds_ok) KARMA_PROFILE_LAUNCH(false, false, true);
+        else KARMA_PROFILE_LAUNCH(false, false, false);
     }
 #undef KARMA_PROFILE_LAUNCH
     int herr = 0;
