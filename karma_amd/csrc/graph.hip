@@ -42,8 +42,11 @@ struct karma_edges {
 
 namespace {
 
-constexpr int kWT = 512;             // walk threads per block
-constexpr int kWalkTile = 2048;      // records staged in LDS per tile (4 per thread)
+constexpr int kWT = 1024;            // walk threads per block
+constexpr int kWalkTile = 4096;      // records per block-chunk granule
+// <= 256 walk blocks (32 per XCD): blocks x buckets x 128-B open write lines
+// (~1.6 MB per XCD at 391 buckets) stay inside the XCD's 4 MB L2
+constexpr int kMaxWalkBlocks = 256;
 constexpr int kMaxFast = 8;          // register fast path: reads with <= 8 records
 constexpr int kReduceBlock = 512;
 constexpr int kTableCap = 8192;      // LDS hash slots per bucket block (64 KB)
@@ -84,20 +87,7 @@ struct ReadSet {
     uint32_t u;
 };
 
-template <typename Get>
-__device__ __forceinline__ bool gather_read(uint32_t rid, Get get, ReadSet& s) {
-    bool more = true;
-#pragma unroll
-    for (int t = 0; t < kMaxFast; ++t) {
-        uint32_t v = kEmpty;
-        if (more) {
-            const uint2 r = get(t);
-            if (r.x == rid) v = r.y;
-            else more = false;
-        }
-        s.m[t] = v;
-    }
-    if (more && get(kMaxFast).x == rid) return false;  // > 8 records
+__device__ __forceinline__ void sort_dedup(ReadSet& s) {
 #define CE(x, y)                                                       \
     {                                                                  \
         uint32_t lo_ = min(s.m[x], s.m[y]), hi_ = max(s.m[x], s.m[y]); \
@@ -120,7 +110,6 @@ __device__ __forceinline__ bool gather_read(uint32_t rid, Get get, ReadSet& s) {
         u += s.keep[p] ? 1u : 0u;
     }
     s.u = u;
-    return true;
 }
 
 // Arbitrary read size (reads with more than 8 records; rare), O(m^3) over
@@ -148,19 +137,23 @@ __device__ void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_
 // COUNT=true : entries per (bucket, block) + order/contig checks + big-read list
 // COUNT=false: writes the 32-bit entries (a_local << bbits | b) at bucket-major
 //              positions; one LDS cursor reservation per (read, bucket run).
+// Every wave walks its own contiguous record range in tiles of 256 records plus
+// an 8-record halo (so the <= 9 records a read needs are one unconditional LDS
+// gather), with the next tile's loads in flight; waves of a block share only
+// the per-bucket counters, so the main loop has no block barrier.
+constexpr int kWaveTile = 256;
+constexpr int kHalo = kMaxFast;
+
 template <bool COUNT>
 __global__ void __launch_bounds__(kWT) walk_kernel(const uint2* __restrict__ rec, int64_t A, int64_t chunk, int bw,
                                                    int bbits, int B, int nblk, uint32_t* __restrict__ hist,
                                                    const int64_t* __restrict__ offs, uint32_t* __restrict__ entries,
                                                    int* __restrict__ flags, uint32_t N, int64_t* __restrict__ big_list,
                                                    unsigned* __restrict__ big_n) {
-    constexpr int TILE = kWalkTile;
-    __shared__ uint2 trec[TILE];
-    __shared__ uint16_t starts[TILE];
-    __shared__ uint32_t wave_cnt[kWT / 64];
-    __shared__ uint32_t n_starts;
-    __shared__ uint32_t prev_rid;
-    __shared__ int has_prev;
+    constexpr int WPB = kWT / 64;
+    constexpr int PER = kWaveTile / 64;
+    __shared__ uint2 wrec[WPB][kWaveTile + kHalo];
+    __shared__ uint16_t wstart[WPB][kWaveTile];
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     unsigned long long* cursor = reinterpret_cast<unsigned long long*>(dyn);  // !COUNT
     uint32_t* cnt = reinterpret_cast<uint32_t*>(dyn);                          // COUNT
@@ -171,110 +164,101 @@ __global__ void __launch_bounds__(kWT) walk_kernel(const uint2* __restrict__ rec
         if (COUNT) cnt[b] = 0;
         else cursor[b] = (unsigned long long)offs[(int64_t)b * (nblk + 1) + blk];
     }
-    const int64_t lo = blk * chunk, hi = min(A, lo + chunk);
+    __syncthreads();
+    const int64_t blo = blk * chunk, bhi = min(A, blo + chunk);
+    const int64_t wchunk = (bhi - blo + WPB - 1) / WPB;
+    const int64_t lo = min(bhi, blo + wave * wchunk), hi = min(bhi, lo + wchunk);
     const uint32_t wmask = (1u << bw) - 1u;
+    uint2* tr = wrec[wave];
+    uint16_t* st_list = wstart[wave];
     int bad_order = 0, bad_contig = 0;
-    for (int64_t ts = lo; ts < hi; ts += TILE) {
-        const int tn = (int)min<int64_t>(TILE, hi - ts);
-        __syncthreads();  // previous tile fully consumed
-        // stage the tile: each wave loads 256 consecutive records (non-temporal:
-        // the stream is read once; L2 is left to the open write lines)
-        uint2 r4[TILE / kWT];
+
+    auto ld = [&](int64_t g) -> uint2 {
+        if (g >= A) return make_uint2(kEmpty, kEmpty);
+        const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(rec + g));
+        return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+    };
+    uint2 nxt[PER], nxt_h = make_uint2(kEmpty, kEmpty);
+    auto prefetch = [&](int64_t t0) {
+        // tile records t0 .. t0+255 (owned if < hi) and halo t0+256 .. +263
 #pragma unroll
-        for (int u = 0; u < TILE / kWT; ++u) {
-            const int j = wave * (TILE / (kWT / 64)) + u * 64 + lane;
-            uint2 r = make_uint2(kEmpty, kEmpty);
-            if (j < tn) {
-                const unsigned long long v =
-                    __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(rec + ts + j));
-                r = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-                trec[j] = r;
-            }
-            r4[u] = r;
-        }
-        if (threadIdx.x == 0) {
-            has_prev = ts > 0;
-            prev_rid = ts > 0 ? rec[ts - 1].x : 0u;
-        }
-        __syncthreads();
-        // read starts of this tile, compacted (block-wide, in tile order)
-        bool st[TILE / kWT];
+        for (int u = 0; u < PER; ++u) nxt[u] = (t0 < hi) ? ld(t0 + u * 64 + lane) : make_uint2(kEmpty, kEmpty);
+        nxt_h = (t0 < hi && lane < kHalo) ? ld(t0 + kWaveTile + lane) : make_uint2(kEmpty, kEmpty);
+    };
+    uint32_t prev = lo > 0 ? rec[lo - 1].x : 0u;
+    bool has_prev = lo > 0;
+    prefetch(lo);
+    for (int64_t ts = lo; ts < hi; ts += kWaveTile) {
+        const int tn = (int)min<int64_t>(kWaveTile, hi - ts);
 #pragma unroll
-        for (int u = 0; u < TILE / kWT; ++u) {
-            const int j = wave * (TILE / (kWT / 64)) + u * 64 + lane;
+        for (int u = 0; u < PER; ++u) tr[u * 64 + lane] = nxt[u];
+        if (lane < kHalo) tr[kWaveTile + lane] = nxt_h;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        prefetch(ts + kWaveTile);
+        // a record past the owned range belongs to the next tile/wave even if
+        // it lies in this tile's slots (tn < 256): mask it out of the starts
+        int ns = 0;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int j = u * 64 + lane;
+            const uint2 r = tr[j];
             bool s = false;
             if (j < tn) {
-                const uint2 r = r4[u];
                 const bool hp = j > 0 || has_prev;
-                const uint32_t p = j > 0 ? trec[j - 1].x : prev_rid;
+                const uint32_t p = j > 0 ? tr[j - 1].x : prev;
                 if (COUNT) {
                     if (hp && p > r.x) bad_order = 1;
                     if (r.y >= N) bad_contig = 1;
                 }
                 s = !hp || p != r.x;
             }
-            st[u] = s;
+            const unsigned long long bal = __ballot(s);
+            if (s) st_list[ns + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)j;
+            ns += __popcll(bal);
         }
-        // wave-level exclusive offsets via ballots (tile order within the wave)
-        uint32_t wbase = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int s = lane; s < ns; s += 64) {
+            const int j0 = st_list[s];
+            // records j0 .. j0+8 are in the tile or its halo (j0 <= 255)
+            uint2 r[kMaxFast + 1];
 #pragma unroll
-        for (int u = 0; u < TILE / kWT; ++u) wbase += __popcll(__ballot(st[u]));
-        if (lane == 0) wave_cnt[wave] = wbase;
-        __syncthreads();
-        uint32_t off0 = 0;
-        for (int w = 0; w < wave; ++w) off0 += wave_cnt[w];
-        if (threadIdx.x == 0) {
-            uint32_t t = 0;
-            for (int w = 0; w < kWT / 64; ++w) t += wave_cnt[w];
-            n_starts = t;
-        }
-#pragma unroll
-        for (int u = 0; u < TILE / kWT; ++u) {
-            const unsigned long long bal = __ballot(st[u]);
-            if (st[u]) {
-                const int j = wave * (TILE / (kWT / 64)) + u * 64 + lane;
-                starts[off0 + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)j;
-            }
-            off0 += __popcll(bal);
-        }
-        __syncthreads();
-        const int ns = (int)n_starts;
-        // one lane per read
-        for (int s = threadIdx.x; s < ns; s += blockDim.x) {
-            const int j0 = starts[s];
-            const uint32_t rid = trec[j0].x;
+            for (int t = 0; t <= kMaxFast; ++t) r[t] = tr[j0 + t];
+            const uint32_t rid = r[0].x;
             ReadSet rs;
-            const bool fast = gather_read(rid, [&](int t) -> uint2 {
-                const int j = j0 + t;
-                if (j < tn) return trec[j];
-                const int64_t g = ts + j;
-                return g < A ? rec[g] : make_uint2(kEmpty, kEmpty);
-            }, rs);
-            if (!fast) {
+            bool v = true;
+#pragma unroll
+            for (int t = 0; t < kMaxFast; ++t) {
+                v = v && (t == 0 || r[t].x == rid);
+                rs.m[t] = v ? r[t].y : kEmpty;
+            }
+            const bool big = v && r[kMaxFast].x == rid;
+            if (big) {
                 if (COUNT) big_list[atomicAdd(big_n, 1u)] = ts + j0;
                 continue;
             }
-            // runs of kept contigs in the same bucket (m[] is sorted)
+            sort_dedup(rs);
             uint32_t run_b = kEmpty, run_n = 0;
             unsigned long long base[kMaxFast];
+            if (COUNT) {
 #pragma unroll
-            for (int p = 0; p < kMaxFast; ++p) {
-                base[p] = 0;
-                if (rs.keep[p] && rs.m[p] < N) {
-                    const uint32_t b = rs.m[p] >> bw;
-                    if (b != run_b) {
-                        if (run_n) {
-                            if (COUNT) atomicAdd(&cnt[run_b], run_n);
+                for (int p = 0; p < kMaxFast; ++p) {
+                    if (rs.keep[p] && rs.m[p] < N) {
+                        const uint32_t b = rs.m[p] >> bw;
+                        if (b != run_b) {
+                            if (run_n) atomicAdd(&cnt[run_b], run_n);
+                            run_b = b;
+                            run_n = 0;
                         }
-                        run_b = b;
-                        run_n = 0;
+                        run_n += rs.u - rs.rank[p];
                     }
-                    run_n += rs.u - rs.rank[p];
                 }
-            }
-            if (run_n && COUNT) atomicAdd(&cnt[run_b], run_n);
-            if (!COUNT) {
-                // second sweep: reserve per run, then write the run's entries
+                if (run_n) atomicAdd(&cnt[run_b], run_n);
+            } else {
+                // reserve per run of one bucket, then write each element's entries
                 uint32_t rb = kEmpty, rn = 0;
                 int rp0 = 0;
 #pragma unroll
@@ -303,8 +287,7 @@ __global__ void __launch_bounds__(kWT) walk_kernel(const uint2* __restrict__ rec
 #pragma unroll
                 for (int p = 0; p < kMaxFast; ++p) {
                     if (!(rs.keep[p] && rs.m[p] < N)) continue;
-                    const uint32_t a = rs.m[p];
-                    const uint32_t hi_key = (a & wmask) << bbits;
+                    const uint32_t hi_key = (rs.m[p] & wmask) << bbits;
                     unsigned long long pos = base[p];
 #pragma unroll
                     for (int q = p; q < kMaxFast; ++q) {
@@ -313,6 +296,11 @@ __global__ void __launch_bounds__(kWT) walk_kernel(const uint2* __restrict__ rec
                 }
             }
         }
+        prev = tr[tn - 1].x;
+        has_prev = true;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     if (COUNT) {
         if (bad_order) flags[0] = 1;
@@ -376,32 +364,112 @@ __device__ void lds_bitonic(uint32_t* keys, uint32_t* vals, int n) {
     }
 }
 
-// One block per bucket: aggregate entries with an LDS hash table, sort, emit
-// (global key, count).  Sets overflow[bucket] and bails out if the bucket has
-// more than kTableCap - 2048 distinct pairs (handled by the generic path).
-__global__ void __launch_bounds__(kReduceBlock) bucket_reduce_kernel(
-    const uint32_t* __restrict__ entries, const int64_t* __restrict__ bstart, int bw, int bbits,
+// ---- bucket reduction ----------------------------------------------------------
+// LDS open-addressing table (key -> count) of kTableCap slots.  A block inserts
+// at most kIter keys between capacity checks, so it never fills up: past
+// kTableCap - kIter distinct keys it raises the bucket's overflow flag and the
+// bucket goes to the generic sort-reduce path.
+constexpr int64_t kIter = 4 * kReduceBlock;
+constexpr int64_t kSlice = 131072;  // entries per slice block (load balance)
+
+struct Table {
+    uint32_t* keys;
+    uint32_t* vals;
+    int* nuniq;
+    __device__ void init() {
+        for (int t = threadIdx.x; t < kTableCap; t += blockDim.x) {
+            keys[t] = kEmpty;
+            vals[t] = 0;
+        }
+        if (threadIdx.x == 0) *nuniq = 0;
+    }
+    __device__ __forceinline__ void insert(uint32_t key, uint32_t c) {
+        uint32_t h = hash32(key) & (kTableCap - 1);
+        while (true) {
+            const uint32_t k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (k == key) {
+                atomicAdd(&vals[h], c);
+                return;
+            }
+            if (k == kEmpty) {
+                const uint32_t old = atomicCAS(&keys[h], kEmpty, key);
+                if (old == kEmpty || old == key) {
+                    if (old == kEmpty) atomicAdd(nuniq, 1);
+                    atomicAdd(&vals[h], c);
+                    return;
+                }
+            }
+            h = (h + 1) & (kTableCap - 1);
+        }
+    }
+    // compact occupied slots to the front; returns their number (all threads)
+    __device__ int compact(int* cnt) {
+        if (threadIdx.x == 0) *cnt = 0;
+        __syncthreads();
+        uint32_t my_k[kTableCap / kReduceBlock], my_v[kTableCap / kReduceBlock];
+#pragma unroll
+        for (int u = 0; u < kTableCap / kReduceBlock; ++u) {
+            const int t = u * kReduceBlock + threadIdx.x;
+            my_k[u] = keys[t];
+            my_v[u] = vals[t];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kTableCap / kReduceBlock; ++u) {
+            if (my_k[u] != kEmpty) {
+                const int pos = atomicAdd(cnt, 1);
+                keys[pos] = my_k[u];
+                vals[pos] = my_v[u];
+            }
+        }
+        __syncthreads();
+        return *cnt;
+    }
+};
+
+// sorted (global key, count) list of a bucket into its slot region
+__device__ void emit_sorted(Table& t, int n, int64_t bucket, int bw, int bbits, uint64_t* __restrict__ out_keys,
+                           int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n) {
+    int p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    for (int i = n + threadIdx.x; i < p2; i += blockDim.x) {
+        t.keys[i] = kEmpty;
+        t.vals[i] = 0;
+    }
+    __syncthreads();
+    lds_bitonic(t.keys, t.vals, p2);
+    const uint32_t bmask = (1u << bbits) - 1u;
+    const uint64_t abase = (uint64_t)bucket << bw;
+    uint64_t* ok = out_keys + bucket * (int64_t)kTableCap;
+    int64_t* oc = out_counts + bucket * (int64_t)kTableCap;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t k = t.keys[i];
+        ok[i] = ((abase + (k >> bbits)) << 32) | (k & bmask);
+        oc[i] = (int64_t)t.vals[i];
+    }
+    if (threadIdx.x == 0) out_n[bucket] = n;
+}
+
+// One block per slice [s, e) of a bucket's entries.  A bucket with one slice
+// is finalised here; otherwise the slice's partial (key, count) list goes to
+// part_* for bucket_merge_kernel.
+__global__ void __launch_bounds__(kReduceBlock) slice_reduce_kernel(
+    const uint32_t* __restrict__ entries, const int64_t* __restrict__ sl_bucket, const int64_t* __restrict__ sl_lo,
+    const int64_t* __restrict__ sl_hi, const uint8_t* __restrict__ single, int bw, int bbits,
     uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n,
+    uint32_t* __restrict__ part_keys, uint32_t* __restrict__ part_cnt, int* __restrict__ part_n,
     uint8_t* __restrict__ overflow) {
     __shared__ uint32_t keys[kTableCap];
     __shared__ uint32_t vals[kTableCap];
-    __shared__ int nuniq;
-    __shared__ int ovf;
-    const int64_t bucket = blockIdx.x;
-    const int64_t s = bstart[bucket], e = bstart[bucket + 1];
-    for (int t = threadIdx.x; t < kTableCap; t += blockDim.x) {
-        keys[t] = kEmpty;
-        vals[t] = 0;
-    }
-    if (threadIdx.x == 0) {
-        nuniq = 0;
-        ovf = 0;
-    }
+    __shared__ int nuniq, cnt, ovf;
+    Table t{keys, vals, &nuniq};
+    const int64_t sl = blockIdx.x, bucket = sl_bucket[sl], s = sl_lo[sl], e = sl_hi[sl];
+    t.init();
+    if (threadIdx.x == 0) ovf = 0;
     __syncthreads();
     // 16-byte loads (4 entries per lane), the next iteration's loads issued
-    // before the current one is inserted: ~16 KB in flight per block
+    // before the current one is inserted
     const int64_t a0 = s & ~int64_t(3);
-    constexpr int64_t kIter = 4 * kReduceBlock;
     auto load4 = [&](int64_t base) -> uint4 {
         const int64_t i = base + 4 * threadIdx.x;
         return i < e ? *reinterpret_cast<const uint4*>(entries + i) : make_uint4(kEmpty, kEmpty, kEmpty, kEmpty);
@@ -418,76 +486,56 @@ __global__ void __launch_bounds__(kReduceBlock) bucket_reduce_kernel(
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int64_t i = base + 4 * threadIdx.x + u;
-            if (i < s || i >= e) continue;
-            const uint32_t key = v[u];
-            uint32_t h = hash32(key) & (kTableCap - 1);
-            while (true) {
-                const uint32_t k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (k == key) {
-                    atomicAdd(&vals[h], 1u);
-                    break;
-                }
-                if (k == kEmpty) {
-                    const uint32_t old = atomicCAS(&keys[h], kEmpty, key);
-                    if (old == kEmpty || old == key) {
-                        if (old == kEmpty) atomicAdd(&nuniq, 1);
-                        atomicAdd(&vals[h], 1u);
-                        break;
-                    }
-                }
-                h = (h + 1) & (kTableCap - 1);
-            }
+            if (i >= s && i < e) t.insert(v[u], 1u);
         }
         __syncthreads();
     }
     __syncthreads();
     if (ovf) {
-        if (threadIdx.x == 0) {
-            overflow[bucket] = 1;
-            out_n[bucket] = 0;
-        }
+        if (threadIdx.x == 0) overflow[bucket] = 1;
         return;
     }
-    // compact occupied slots to the front (keys stay in LDS)
-    __shared__ int cnt;
-    if (threadIdx.x == 0) cnt = 0;
-    __syncthreads();
-    uint32_t my_k[kTableCap / kReduceBlock], my_v[kTableCap / kReduceBlock];
-#pragma unroll
-    for (int u = 0; u < kTableCap / kReduceBlock; ++u) {
-        const int t = u * kReduceBlock + threadIdx.x;
-        my_k[u] = keys[t];
-        my_v[u] = vals[t];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kTableCap / kReduceBlock; ++u) {
-        if (my_k[u] != kEmpty) {
-            const int pos = atomicAdd(&cnt, 1);
-            keys[pos] = my_k[u];
-            vals[pos] = my_v[u];
+    const int n = t.compact(&cnt);
+    if (single[sl]) {
+        emit_sorted(t, n, bucket, bw, bbits, out_keys, out_counts, out_n);
+    } else {
+        uint32_t* pk = part_keys + sl * (int64_t)kTableCap;
+        uint32_t* pc = part_cnt + sl * (int64_t)kTableCap;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            pk[i] = keys[i];
+            pc[i] = vals[i];
         }
+        if (threadIdx.x == 0) part_n[sl] = n;
     }
+}
+
+// One block per multi-slice bucket: merge its slices' partial lists.
+__global__ void __launch_bounds__(kReduceBlock) bucket_merge_kernel(
+    const int64_t* __restrict__ mb_bucket, const int64_t* __restrict__ mb_s0, const int64_t* __restrict__ mb_s1,
+    int bw, int bbits, const uint32_t* __restrict__ part_keys, const uint32_t* __restrict__ part_cnt,
+    const int* __restrict__ part_n, uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_counts,
+    int64_t* __restrict__ out_n, uint8_t* __restrict__ overflow) {
+    __shared__ uint32_t keys[kTableCap];
+    __shared__ uint32_t vals[kTableCap];
+    __shared__ int nuniq, cnt;
+    Table t{keys, vals, &nuniq};
+    const int64_t bucket = mb_bucket[blockIdx.x], s0 = mb_s0[blockIdx.x], s1 = mb_s1[blockIdx.x];
+    if (overflow[bucket]) return;  // a slice overflowed: generic path
+    t.init();
     __syncthreads();
-    const int n = cnt;
-    int p2 = 1;
-    while (p2 < n) p2 <<= 1;
-    for (int t = n + threadIdx.x; t < p2; t += blockDim.x) {
-        keys[t] = kEmpty;
-        vals[t] = 0;
+    for (int64_t sl = s0; sl < s1; ++sl) {
+        const int n = part_n[sl];
+        if (nuniq > kTableCap - n) {
+            __syncthreads();
+            if (threadIdx.x == 0) overflow[bucket] = 1;
+            return;
+        }
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            t.insert(part_keys[sl * (int64_t)kTableCap + i], part_cnt[sl * (int64_t)kTableCap + i]);
+        __syncthreads();
     }
-    __syncthreads();
-    lds_bitonic(keys, vals, p2);
-    const uint32_t bmask = (1u << bbits) - 1u;
-    const uint64_t abase = (uint64_t)bucket << bw;
-    uint64_t* ok = out_keys + bucket * (int64_t)kTableCap;
-    int64_t* oc = out_counts + bucket * (int64_t)kTableCap;
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        const uint32_t k = keys[t];
-        ok[t] = ((abase + (k >> bbits)) << 32) | (k & bmask);
-        oc[t] = (int64_t)vals[t];
-    }
-    if (threadIdx.x == 0) out_n[bucket] = n;
+    const int n = t.compact(&cnt);
+    emit_sorted(t, n, bucket, bw, bbits, out_keys, out_counts, out_n);
 }
 
 // Copies each bucket's sorted list (from its slot region or an overflow buffer)
@@ -678,7 +726,7 @@ int records_to_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, kar
     const int B = (int)g.n_buckets;
     constexpr int kTileCount = kWalkTile;
     // persistent-style grid: <= 1024 blocks, each a contiguous run of whole tiles
-    int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(1024, ceil_div(A, kTileCount)));
+    int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(kMaxWalkBlocks, ceil_div(A, kTileCount)));
     const int64_t chunk = std::max<int64_t>(kTileCount, ceil_div(ceil_div(A, nblk), kTileCount) * kTileCount);
     nblk = std::max<int64_t>(1, ceil_div(A, chunk));
     const int64_t H = (int64_t)B * (nblk + 1);  // last column: reads with > 8 records
@@ -742,8 +790,53 @@ int records_to_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, kar
     KARMA_TRY(ovf.alloc(ctx, g.n_buckets));
     KARMA_HIP(hipMemsetAsync(ovf.ptr, 0, g.n_buckets, ctx->stream));
     KARMA_HIP(hipMemsetAsync(n_per.ptr + g.n_buckets, 0, 8, ctx->stream));
-    KARMA_LAUNCH(ctx, "graph_bucket_reduce", bucket_reduce_kernel, g.n_buckets, kReduceBlock, 0, entries.ptr,
-                 bstart.ptr, g.bw, g.bbits, slot_k.ptr, slot_c.ptr, n_per.ptr, ovf.ptr);
+    {
+        // slices of <= kSlice entries; buckets with one slice finish in the slice kernel
+        std::vector<int64_t> hb(g.n_buckets + 1);
+        KARMA_HIP(hipMemcpyAsync(hb.data(), bstart.ptr, (g.n_buckets + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        std::vector<int64_t> sb, slo, shi, mb, m0, m1;
+        std::vector<uint8_t> single;
+        for (int64_t b = 0; b < g.n_buckets; ++b) {
+            const int64_t len = hb[b + 1] - hb[b];
+            const int64_t ns = std::max<int64_t>(1, ceil_div(len, kSlice));
+            const int64_t first = (int64_t)sb.size();
+            for (int64_t k = 0; k < ns; ++k) {
+                sb.push_back(b);
+                slo.push_back(hb[b] + len * k / ns);
+                shi.push_back(hb[b] + len * (k + 1) / ns);
+                single.push_back(ns == 1);
+            }
+            if (ns > 1) {
+                mb.push_back(b);
+                m0.push_back(first);
+                m1.push_back(first + ns);
+            }
+        }
+        const int64_t NS = (int64_t)sb.size(), NM = (int64_t)mb.size();
+        DevArray<int64_t> d_sl;  // [sb | slo | shi | mb | m0 | m1]
+        DevArray<uint8_t> d_single;
+        DevArray<uint32_t> part_k, part_c;
+        DevArray<int> part_n;
+        KARMA_TRY(d_sl.alloc(ctx, 3 * NS + 3 * NM + 1));
+        KARMA_TRY(d_single.alloc(ctx, NS));
+        KARMA_TRY(part_k.alloc(ctx, (NM ? NS : 1) * (int64_t)kTableCap));
+        KARMA_TRY(part_c.alloc(ctx, (NM ? NS : 1) * (int64_t)kTableCap));
+        KARMA_TRY(part_n.alloc(ctx, NS));
+        std::vector<int64_t> packed_tab;
+        packed_tab.reserve(3 * NS + 3 * NM);
+        for (auto* v : {&sb, &slo, &shi, &mb, &m0, &m1}) packed_tab.insert(packed_tab.end(), v->begin(), v->end());
+        KARMA_HIP(hipMemcpyAsync(d_sl.ptr, packed_tab.data(), packed_tab.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(d_single.ptr, single.data(), NS, hipMemcpyHostToDevice, ctx->stream));
+        KARMA_LAUNCH(ctx, "graph_bucket_reduce", slice_reduce_kernel, NS, kReduceBlock, 0, entries.ptr, d_sl.ptr,
+                     d_sl.ptr + NS, d_sl.ptr + 2 * NS, d_single.ptr, g.bw, g.bbits, slot_k.ptr, slot_c.ptr, n_per.ptr,
+                     part_k.ptr, part_c.ptr, part_n.ptr, ovf.ptr);
+        if (NM)
+            KARMA_LAUNCH(ctx, "graph_bucket_merge", bucket_merge_kernel, NM, kReduceBlock, 0, d_sl.ptr + 3 * NS,
+                         d_sl.ptr + 3 * NS + NM, d_sl.ptr + 3 * NS + 2 * NM, g.bw, g.bbits, part_k.ptr, part_c.ptr,
+                         part_n.ptr, slot_k.ptr, slot_c.ptr, n_per.ptr, ovf.ptr);
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));  // tables above die at scope end
+    }
     std::vector<uint8_t> hovf(g.n_buckets);
     KARMA_HIP(hipMemcpyAsync(hovf.data(), ovf.ptr, g.n_buckets, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));

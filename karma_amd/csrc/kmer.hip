@@ -61,6 +61,7 @@ struct karma_kmer_plan {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kPadWords = 80;    // zero words after the store (stages may read past the last contig)
 
 __device__ __forceinline__ int base_code(uint8_t b) {
     // A C G T -> 0 1 2 3 ; anything else -> -1 (exception)
@@ -184,6 +185,41 @@ __device__ __forceinline__ Window load_window(const uint32_t* packed, const uint
     return v;
 }
 
+// ------------------------------------------------------------- staging -------
+// A wave walks its contig in stages of 1024 positions: the 65 packed words
+// (and, for contigs with exception bases, the 65 mask half-words) of a stage
+// are loaded once, coalesced, into the wave's LDS slice; every k-mer window is
+// then read from LDS.
+template <typename Body>
+__device__ __forceinline__ void for_each_window(const uint32_t* __restrict__ packed,
+                                                const uint16_t* __restrict__ mask, bool excp, int64_t w0,
+                                                int64_t npos, uint32_t* wbuf, uint16_t* mbuf, int lane, Body body) {
+    for (int64_t base = 0; base < npos; base += 1024) {
+        const int64_t wb = w0 + (base >> 4);
+        wbuf[lane] = packed[wb + lane];
+        if (lane == 0) wbuf[64] = packed[wb + 64];
+        if (excp) {
+            mbuf[lane] = mask[wb + lane];
+            if (lane == 0) mbuf[64] = mask[wb + 64];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int64_t lim = min(npos, base + 1024);
+        for (int64_t i = base + lane; i < lim; i += 64) {
+            const int l = (int)(i - base), w = l >> 4;
+            Window v;
+            v.o = l & 15;
+            v.x = ((uint64_t)wbuf[w] << 32) | wbuf[w + 1];
+            v.m = excp ? (((uint32_t)mbuf[w] << 16) | mbuf[w + 1]) : 0u;
+            body(i, v);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 // ------------------------------------------------------------- presence ------
 // One wave per contig.  Sets the ACGT-ordinal presence bitmap (LDS-private per
 // block, test-before-set so the hot bits stop costing atomics, OR-flushed once
@@ -203,57 +239,64 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
                                                           int nwords, bool with_len, uint32_t* __restrict__ presence,
                                                           uint64_t* __restrict__ exc_buf, int64_t exc_cap,
                                                           unsigned long long* __restrict__ exc_cnt,
-                                                          int64_t* __restrict__ row_tot) {
+                                                          int64_t c_begin, const int* __restrict__ full) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+    // once every ACGT ordinal is present, only contigs with exception bases can
+    // still add columns (tested between the two launches, see saturation_kernel)
+    const bool saturated = full != nullptr && *full != 0;
+    uint32_t* wbuf = lds_bits + nwords + wave * 80;
+    uint16_t* mbuf = reinterpret_cast<uint16_t*>(lds_bits + nwords + wpb * 80) + wave * 80;
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) lds_bits[w] = 0;
     __syncthreads();
     const int kmin = P56 ? 5 : k;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     auto push_exc = [&](uint64_t key) {
         const unsigned long long slot = atomicAdd(exc_cnt, 1ull);
         if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
     };
-    for (int64_t c = (int64_t)blockIdx.x * wpb + wave; c < n; c += (int64_t)gridDim.x * wpb) {
-        const int64_t L = off[c + 1] - off[c], w0 = woff[c];
-        const bool exc = has_exc[c] != 0;
-        unsigned my = 0;
-        for (int64_t i = lane; i + kmin <= L; i += 64) {
-            const Window v = load_window(packed, mask, w0, i, exc);
+    for (int64_t c = c_begin + (int64_t)blockIdx.x * wpb + wave; c < n; c += (int64_t)gridDim.x * wpb) {
+        if (saturated && !has_exc[c]) continue;
+        const int64_t L = off[c + 1] - off[c];
+        const uint8_t* craw = raw + off[c];
+        for_each_window(packed, mask, has_exc[c] != 0, woff[c], L - kmin + 1, wbuf, mbuf, lane,
+                        [&](int64_t i, const Window& v) {
             if (P56) {
                 if (v.clean(5)) set_bit(lds_bits, v.code(5) * 5u);  // kmer.py:72-73
-                else push_exc(key_from_bytes(raw + off[c] + i, 5, true));
-                ++my;
+                else push_exc(key_from_bytes(craw + i, 5, true));
                 if (i + 6 <= L) {  // palindromic 6-mers, kmer.py:76-80
                     if (v.clean(6)) {
                         const uint32_t c6 = v.code(6);
-                        if (pal6_code(c6)) {
-                            set_bit(lds_bits, (c6 >> 2) * 5u + 1u + (c6 & 3u));
-                            ++my;
-                        }
-                    } else {
-                        const uint8_t* p = raw + off[c] + i;
-                        if (pal_bytes(p, 6)) {
-                            push_exc(key_from_bytes(p, 6, true));
-                            ++my;
-                        }
+                        if (pal6_code(c6)) set_bit(lds_bits, (c6 >> 2) * 5u + 1u + (c6 & 3u));
+                    } else if (pal_bytes(craw + i, 6)) {
+                        push_exc(key_from_bytes(craw + i, 6, true));
                     }
                 }
             } else {
                 if (v.clean(k)) set_bit(lds_bits, v.code(k));
-                else push_exc(key_from_bytes(raw + off[c] + i, k, with_len));
-                ++my;
+                else push_exc(key_from_bytes(craw + i, k, with_len));
             }
-        }
-        // wave sum of k-mer occurrences -> row_tot (0 = the all-zero row, kmer.py:250-258)
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) my += __shfl_xor(my, d);
-        if (lane == 0) row_tot[c] = (int64_t)my;
+        });
     }
     __syncthreads();
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
         const uint32_t b = lds_bits[w];
         if (b) atomicOr(&presence[w], b);
     }
+}
+
+// Sets *full when every ACGT ordinal that can occur is present: all 4^k codes,
+// or for 5p6 the 1024 5-mers and the 64 palindromic 6-mers.
+__global__ void saturation_kernel(const uint32_t* __restrict__ presence, uint32_t S, bool p56, int* __restrict__ full) {
+    __shared__ int missing;
+    if (threadIdx.x == 0) missing = 0;
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < S; o += blockDim.x) {
+        bool can = true;
+        if (p56 && o % 5 != 0) can = pal6_code(((o / 5) << 2) | (o % 5 - 1));
+        if (can && !((presence[o >> 5] >> (o & 31)) & 1u)) missing = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *full = missing ? 0 : 1;
 }
 
 // ----------------------------------------------------------- column table ---
@@ -393,21 +436,55 @@ __global__ void __launch_bounds__(kBlock) profile_kernel(
     const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
     const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
     const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
-    double* __restrict__ out, int64_t ld, uint32_t* __restrict__ scratch, int* __restrict__ err) {
+    double* __restrict__ out, int64_t ld, uint32_t* __restrict__ scratch, int* __restrict__ err, int S,
+    int64_t* __restrict__ row_tot) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_counts[];
     if (WAVE) {
+        // LDS: [col table u16, S rounded to 8][per wave: counts M (even) | words 80 | mask 80 u16]
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
-        uint32_t* counts = lds_counts + wave * M;
+        uint16_t* col = reinterpret_cast<uint16_t*>(lds_counts);
+        const int s_pad = (S + 7) & ~7;
+        const int m_pad = (int)((M + 3) & ~3);
+        uint32_t* base = lds_counts + s_pad / 2 + wave * (m_pad + 80 + 40);
+        uint32_t* counts = base;
+        uint32_t* wbuf = base + m_pad;
+        uint16_t* mbuf = reinterpret_cast<uint16_t*>(base + m_pad + 80);
+        for (int o = threadIdx.x; o < S; o += blockDim.x) col[o] = (uint16_t)col_of_ord[o];
+        __syncthreads();
+        const int kmin = P56 ? 5 : k;
         for (int64_t c = (int64_t)blockIdx.x * wpb + wave; c < n; c += (int64_t)gridDim.x * wpb) {
             for (int64_t j = lane; j < M; j += 64) counts[j] = 0;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            const int64_t s = off[c];
-            count_contig<P56>(packed, mask, has_exc[c] != 0, woff[c], raw + s, off[c + 1] - s, k, with_len,
-                              col_of_ord, exc, X, col_of_exc, lane, 64,
-                              [&](int32_t col) { atomicAdd(&counts[col], 1u); });
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+            const int64_t s = off[c], L = off[c + 1] - s;
+            const uint8_t* craw = raw + s;
+            unsigned my = 0;
+            auto add = [&](uint32_t cl) {
+                atomicAdd(&counts[cl], 1u);
+                ++my;
+            };
+            for_each_window(packed, mask, has_exc[c] != 0, woff[c], L - kmin + 1, wbuf, mbuf, lane,
+                            [&](int64_t i, const Window& v) {
+                if (P56) {
+                    if (v.clean(5)) add(col[v.code(5) * 5u]);
+                    else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 5, true))]);
+                    if (i + 6 <= L) {
+                        if (v.clean(6)) {
+                            const uint32_t c6 = v.code(6);
+                            if (pal6_code(c6)) add(col[(c6 >> 2) * 5u + 1u + (c6 & 3u)]);
+                        } else if (pal_bytes(craw + i, 6)) {
+                            add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 6, true))]);
+                        }
+                    }
+                } else {
+                    if (v.clean(k)) add(col[v.code(k)]);
+                    else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
+                }
+            });
+            // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) my += __shfl_xor(my, d);
+            if (lane == 0) row_tot[c] = (int64_t)my;
             write_row(out + c * ld, counts, M, keylen[c], err, lane, 64);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -419,8 +496,10 @@ __global__ void __launch_bounds__(kBlock) profile_kernel(
             __syncthreads();
             const int64_t s = off[c];
             count_contig<P56>(packed, mask, has_exc[c] != 0, woff[c], raw + s, off[c + 1] - s, k, with_len,
-                              col_of_ord, exc, X, col_of_exc, threadIdx.x, blockDim.x,
-                              [&](int32_t col) { atomicAdd(&counts[col], 1u); });
+                              col_of_ord, exc, X, col_of_exc, threadIdx.x, blockDim.x, [&](int32_t col) {
+                                  atomicAdd(&counts[col], 1u);
+                                  atomicAdd(reinterpret_cast<unsigned long long*>(row_tot + c), 1ull);
+                              });
             __syncthreads();
             write_row(out + c * ld, counts, M, keylen[c], err, threadIdx.x, blockDim.x);
             __syncthreads();
@@ -496,12 +575,12 @@ int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offs
     KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.ptr, tmp_bytes, wc.ptr, c->woff.ptr, (int)(n + 1), ctx->stream));
     KARMA_HIP(hipMemcpyAsync(&c->words, c->woff.ptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    if ((rc = c->packed.alloc(ctx, c->words + 2)) || (rc = c->mask.alloc(ctx, c->words + 2))) {
+    if ((rc = c->packed.alloc(ctx, c->words + kPadWords)) || (rc = c->mask.alloc(ctx, c->words + kPadWords))) {
         delete c;
         return rc;
     }
-    KARMA_HIP(hipMemsetAsync(c->packed.ptr + c->words, 0, 2 * sizeof(uint32_t), ctx->stream));
-    KARMA_HIP(hipMemsetAsync(c->mask.ptr + c->words, 0, 2 * sizeof(uint16_t), ctx->stream));
+    KARMA_HIP(hipMemsetAsync(c->packed.ptr + c->words, 0, kPadWords * sizeof(uint32_t), ctx->stream));
+    KARMA_HIP(hipMemsetAsync(c->mask.ptr + c->words, 0, kPadWords * sizeof(uint16_t), ctx->stream));
     DevArray<unsigned long long> exc;
     if ((rc = exc.alloc(ctx, 1))) {
         delete c;
@@ -561,17 +640,35 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
     }
     KARMA_HIP(hipMemsetAsync(p->presence.ptr, 0, p->nwords * 4, ctx->stream));
     KARMA_HIP(hipMemsetAsync(exc_cnt.ptr, 0, 8, ctx->stream));
+    DevArray<int> full;
+    if ((rc = full.alloc(ctx, 1))) {
+        delete p;
+        return rc;
+    }
     if (c->n) {
-        const int grid = grid_for(ceil_div(c->n, kBlock / 64), 2048);
-        const size_t lds = p->nwords * 4;
-        if (kmode == KARMA_KMER_5P6)
-            KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<true>, grid, kBlock, lds, c->packed.ptr, c->mask.ptr,
-                         c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->n, kmode, (int)p->nwords, with_len,
-                         p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, p->row_tot.ptr);
-        else
-            KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<false>, grid, kBlock, lds, c->packed.ptr, c->mask.ptr,
-                         c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->n, kmode, (int)p->nwords, with_len,
-                         p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, p->row_tot.ptr);
+        // phase A over a prefix, saturation test, phase B over the rest (only
+        // contigs with exception bases once the ACGT ordinals are saturated)
+        const int64_t nA = std::min<int64_t>(c->n, 4096);
+        const size_t lds = p->nwords * 4 + (kBlock / 64) * 80 * (4 + 2);
+        const bool p56 = kmode == KARMA_KMER_5P6;
+        auto launch = [&](int64_t lo, int64_t hi, const int* f) -> int {
+            if (hi <= lo) return KARMA_OK;
+            const int grid = grid_for(ceil_div(hi - lo, kBlock / 64), 2048);
+            if (p56)
+                KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<true>, grid, kBlock, lds, c->packed.ptr,
+                             c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, hi, kmode, (int)p->nwords,
+                             with_len, p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, f);
+            else
+                KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<false>, grid, kBlock, lds, c->packed.ptr,
+                             c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, hi, kmode, (int)p->nwords,
+                             with_len, p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, f);
+            return KARMA_OK;
+        };
+        KARMA_TRY(launch(0, nA, nullptr));
+        if (nA < c->n) {
+            KARMA_LAUNCH(ctx, "kmer_saturation", saturation_kernel, 1, 1024, 0, p->presence.ptr, S, p56, full.ptr);
+            KARMA_TRY(launch(nA, c->n, full.ptr));
+        }
     }
     unsigned long long ninst = 0;
     KARMA_HIP(hipMemcpyAsync(&ninst, exc_cnt.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -748,18 +845,21 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
     DevArray<int> err;
     if ((rc = err.alloc(ctx, 1))) return rc;
     KARMA_HIP(hipMemsetAsync(err.ptr, 0, 4, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(p->row_tot.ptr, 0, n * 8, ctx->stream));
     bool with_len = p->kmode != 8;
-    const bool wave = M <= kWaveMaxM;
+    const bool wave = M <= kWaveMaxM && p->S <= 8192;
     const bool lds_ok = M * 4 <= 144 * 1024;
     const int grid = wave ? grid_for(ceil_div(n, kBlock / 64), 2048) : grid_for(n, lds_ok ? 4096 : 1024);
     DevArray<uint32_t> scratch;
     if (!wave && !lds_ok && (rc = scratch.alloc(ctx, (size_t)grid * M))) return rc;
-    const size_t lds = wave ? (kBlock / 64) * M * 4 : (lds_ok ? M * 4 : 0);
+    const size_t lds = wave ? (size_t)((p->S + 7) & ~7) * 2 + (kBlock / 64) * (((M + 3) & ~3) + 120) * 4
+                            : (lds_ok ? M * 4 : 0);
     const int k = p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode;
 #define KARMA_PROFILE_LAUNCH(P56, W, LDS)                                                                        \
     KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, W, LDS>), grid, kBlock, lds, c->packed.ptr,           \
                  c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len,            \
-                 p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err.ptr)
+                 p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err.ptr,  \
+                 (int)p->S, p->row_tot.ptr)
     if (p->kmode == KARMA_KMER_5P6) {
         if (wave) KARMA_PROFILE_LAUNCH(true, true, true);
         else if (lds_ok) KARMA_PROFILE_LAUNCH(true, false, true);

@@ -269,3 +269,17 @@ def test_eq_path_equals_readset_path():
     assert np.array_equal(er.a, ee.a) and np.array_equal(er.b, ee.b)
     assert np.array_equal(er.weight.view(np.uint64), ee.weight.view(np.uint64))
     assert np.array_equal(er.totals, ee.totals)
+
+
+@pytest.mark.parametrize("kmer,n_rate", [("5p6", 700), (3, 300), (7, 0), (6, 2000)])
+def test_profile_presence_two_phase(kmer, n_rate):
+    # > 4096 contigs: phase B of the presence pass runs (saturated or not),
+    # exception k-mers appear only in late contigs for the high n_rate cases
+    n = 6000
+    blob, offs, key_len = engine.synth_contigs(900 + n_rate, n, 40, 200, n_rate)
+    seqs = OrderedDict((f">ctg{i}", bytes(blob[offs[i]:offs[i + 1]]).decode()) for i in range(n))
+    prof, cols, tot = engine.kmer_profile(seqs, kmer)
+    oprof, ocols, ocounts = oracle.calc_kmer_profile(seqs, kmer)
+    assert cols == ocols
+    assert np.array_equal(prof.view(np.uint64), oprof.view(np.uint64))
+    assert np.array_equal(tot, ocounts.sum(axis=1))
