@@ -70,9 +70,12 @@ def main():
     from karma_amd.distributed import Comm, ShardedBuild
 
     seed, n_loc, f_loc, paired, kmer = CONFIGS[args.config]
-    comm = Comm.create(world, rank, local_rank)
-    ctx = _lib.Context(local_rank if world > 1 else 0)
-    torch.cuda.set_device(local_rank if world > 1 else 0)
+    # KARMA_FORCE_DEVICE pins every rank to one device (multi-rank rehearsal on
+    # a 1-GPU box together with KARMA_DIST_BACKEND=gloo); unset in real runs
+    dev_index = int(os.environ.get("KARMA_FORCE_DEVICE", local_rank if world > 1 else 0))
+    comm = Comm.create(world, rank, dev_index)
+    ctx = _lib.Context(dev_index)
+    torch.cuda.set_device(dev_index)
 
     # ---------------- synthetic input (host), then resident in HBM ----------------
     t_gen = time.time()

@@ -66,8 +66,10 @@ int make_geo(int64_t N, Geo* g) {
     // ~<= 512 coarse buckets: few enough that every block's open write lines
     // (blocks x buckets x 128 B) stay in its XCD's L2, few enough distinct
     // pairs per bucket for one LDS hash table
+    int target = 512;
+    if (const char* v = getenv("KARMA_BUCKETS_TARGET")) target = std::max(1, atoi(v));
     int bw = 4;
-    while ((N >> bw) > 512) ++bw;
+    while ((N >> bw) > target) ++bw;
     KARMA_CHECK(bw + bbits <= 31, KARMA_ERR_ARG, "n_contigs too large for 32-bit entries");
     g->bw = bw;
     g->bbits = bbits;
@@ -523,16 +525,21 @@ __global__ void __launch_bounds__(kReduceBlock) bucket_merge_kernel(
     if (overflow[bucket]) return;  // a slice overflowed: generic path
     t.init();
     __syncthreads();
+    // insert the partial lists in chunks of <= kIter keys with the same
+    // capacity test as the slice kernel
     for (int64_t sl = s0; sl < s1; ++sl) {
         const int n = part_n[sl];
-        if (nuniq > kTableCap - n) {
+        for (int c0 = 0; c0 < n; c0 += (int)kIter) {
+            if (nuniq > kTableCap - kIter) {
+                __syncthreads();
+                if (threadIdx.x == 0) overflow[bucket] = 1;
+                return;
+            }
+            const int c1 = min(n, c0 + (int)kIter);
+            for (int i = c0 + threadIdx.x; i < c1; i += blockDim.x)
+                t.insert(part_keys[sl * (int64_t)kTableCap + i], part_cnt[sl * (int64_t)kTableCap + i]);
             __syncthreads();
-            if (threadIdx.x == 0) overflow[bucket] = 1;
-            return;
         }
-        for (int i = threadIdx.x; i < n; i += blockDim.x)
-            t.insert(part_keys[sl * (int64_t)kTableCap + i], part_cnt[sl * (int64_t)kTableCap + i]);
-        __syncthreads();
     }
     const int n = t.compact(&cnt);
     emit_sorted(t, n, bucket, bw, bbits, out_keys, out_counts, out_n);

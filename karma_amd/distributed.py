@@ -30,10 +30,23 @@ import numpy as np
 
 
 class Comm:
-    """Thin torch.distributed wrapper; world size 1 needs no process group."""
+    """Thin torch.distributed wrapper; world size 1 needs no process group.
 
-    def __init__(self, world, rank, dist=None, device=None):
-        self.world, self.rank, self.dist, self.device = world, rank, dist, device
+    With backend "gloo", device tensors are staged through host memory (used
+    to run several GPU ranks on one device in tests; production multi-GPU runs
+    use "nccl" = RCCL over xGMI on the device tensors directly)."""
+
+    def __init__(self, world, rank, dist=None, device=None, backend=None):
+        self.world, self.rank, self.dist, self.device, self.backend = world, rank, dist, device, backend
+
+    def _h(self, t):
+        return t.cpu() if self.backend == "gloo" and t.device.type != "cpu" else t
+
+    def _back(self, h, like):
+        if h is like:
+            return like
+        like.copy_(h)
+        return like
 
     @classmethod
     def create(cls, world, rank, local_rank=0, backend=None):
@@ -43,7 +56,8 @@ class Comm:
         import torch.distributed as dist
 
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # KARMA_DIST_BACKEND=gloo: rehearse several GPU ranks on one device
+            backend = os.environ.get("KARMA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             torch.cuda.set_device(local_rank)
@@ -52,7 +66,7 @@ class Comm:
             device = torch.device("cpu")
         if not dist.is_initialized():
             dist.init_process_group(backend, rank=rank, world_size=world)
-        return cls(world, rank, dist, device)
+        return cls(world, rank, dist, device, backend)
 
     # scalar helpers (host values)
     def barrier(self):
@@ -75,12 +89,16 @@ class Comm:
     # tensor collectives (in place / returning)
     def allreduce_max_(self, t):
         if self.dist:
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            h = self._h(t)
+            self.dist.all_reduce(h, op=self.dist.ReduceOp.MAX)
+            self._back(h, t)
         return t
 
     def allreduce_sum_(self, t):
         if self.dist:
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+            h = self._h(t)
+            self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM)
+            self._back(h, t)
         return t
 
     def all_gather_var(self, t):
@@ -89,18 +107,20 @@ class Comm:
             return t
         import torch
 
+        dev = t.device
+        t = self._h(t)
         n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
         sizes = [torch.zeros_like(n) for _ in range(self.world)]
         self.dist.all_gather(sizes, n)
         sizes = [int(s.item()) for s in sizes]
         mx = max(sizes)
         if mx == 0:
-            return t[:0]
+            return t[:0].to(dev)
         pad = torch.zeros(mx, dtype=t.dtype, device=t.device)
         pad[: t.numel()] = t
         outs = [torch.empty_like(pad) for _ in range(self.world)]
         self.dist.all_gather(outs, pad)
-        return torch.cat([o[:s] for o, s in zip(outs, sizes)])
+        return torch.cat([o[:s] for o, s in zip(outs, sizes)]).to(dev)
 
     def alltoallv(self, t, send_counts):
         """1-D all-to-all-v: send_counts[r] consecutive elements go to rank r."""
@@ -108,6 +128,8 @@ class Comm:
             return t
         import torch
 
+        dev = t.device
+        t = self._h(t)
         sc = torch.tensor(list(send_counts), dtype=torch.int64, device=t.device)
         rc = torch.empty_like(sc)
         self.dist.all_to_all_single(rc, sc)
@@ -115,7 +137,7 @@ class Comm:
         out = torch.empty(sum(recv_counts), dtype=t.dtype, device=t.device)
         self.dist.all_to_all_single(out, t, output_split_sizes=recv_counts,
                                     input_split_sizes=[int(x) for x in send_counts])
-        return out
+        return out.to(dev)
 
     def close(self):
         if self.dist and self.dist.is_initialized():
@@ -175,6 +197,9 @@ class HipOps:
     def finalize(self, plan):
         return plan.finalize()
 
+    def columns(self, plan):
+        return plan.columns()
+
     def profile(self, plan, out):
         if out.numel():
             plan.profile_device(out.data_ptr(), out.shape[1])
@@ -218,6 +243,9 @@ class HipOps:
 
     def edge_arrays(self, edges):
         return edges.get()
+
+    def pair_count(self, pairs):
+        return pairs.count()
 
     def entries(self, pairs):
         _, counts, _ = pairs.get()
@@ -269,7 +297,7 @@ class ShardedBuild:
         stats = {"M": M}
         if keep:
             stats["entries"] = ops.entries(local)
-            stats["pairs_local"] = local.count() if hasattr(local, "count") else None
+            stats["pairs_local"] = ops.pair_count(local)
         if comm.world > 1:
             keys, counts, starts = ops.pairs_split(local, self.bounds)
             send = np.diff(starts)
@@ -287,7 +315,7 @@ class ShardedBuild:
         if keep:
             stats["profile"] = self._prof
             stats["edges"] = ops.edge_arrays(edges)
-            stats["columns"] = plan.columns() if hasattr(plan, "columns") else None
+            stats["columns"] = ops.columns(plan)
         ops.close(edges, final_pairs, plan)
         return stats
 
