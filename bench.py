@@ -5,8 +5,9 @@ One step = the whole hot path over one batch of device-resident synthetic input
 (SURVEY.md §8(d)), per GPU:
   k-mer profile of 200k contigs (mean 800 bp, k = 5p6): presence pass, column
   table, dense float64 profile (N x M) written to HBM;
-  shared-read graph of 100M paired fragments (~340M (read, contig) records):
-  pair emission, bucket partition, LDS hash reduce, weights.
+  shared-read graph of 100M paired fragments (~309M (read, contig) records):
+  one partition pass (a read -> one 2-byte (m0, M) code, or its pairs),
+  LDS histogram / hash reduces, per-bucket merge, weights.
 Inputs (2-bit packed contigs + records) are resident in HBM before timing.
 
 Multi-GPU (torchrun, one rank per GPU): weak scaling — rank r owns contig rows
@@ -116,8 +117,7 @@ def main():
     dt = comm.max_float(t1 - t0)
     kern = ctx.timing_read() if not args.no_timing else {}
     ctx.timing(False)
-    st = step(keep=True)  # untimed: sizes for the byte model
-    res.update({k: st[k] for k in ("entries", "pairs_local")})
+    n_reads = int(np.count_nonzero(rec[1:, 0] != rec[:-1, 0])) + 1 if A else 0
 
     units = world * (n_loc + f_loc) * args.steps
     value = units / dt
@@ -127,9 +127,9 @@ def main():
     per_kernel_bytes = {
         "kmer_profile": packed_bytes + 8 * n_loc * M,
         "kmer_presence": packed_bytes,
-        "graph_count": 8 * A,
-        "graph_scatter": 8 * A + 4 * res["entries"],
-        "graph_bucket_reduce": 4 * res["entries"] + 16 * res["pairs_local"],
+        # records read once + one 2-byte code written per read (compact reads)
+        "graph_partition": 8 * A + 2 * n_reads,
+        "graph_code_reduce": 2 * n_reads,
     }
     roof = None
     if kern:

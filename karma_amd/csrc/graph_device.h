@@ -1,0 +1,100 @@
+// graph_device.h — device helpers of the read-record graph pipeline
+// (graph_sets.hip): the per-read sort/dedup network, the generic walk of reads
+// with more than 8 records, a 32-bit mix hash and an LDS bitonic sort.
+// Included inside an anonymous namespace.
+#pragma once
+
+constexpr int kMaxFast = 8;          // register fast path: reads with <= 8 records
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+
+// ---- per-read pair walk -------------------------------------------------------
+// A read's contigs (<= 8 records, else it is a "big read") sorted by a fixed
+// network; keep[p] marks the first copy of each distinct contig and rank[p] is
+// its index among the kept ones, so the read emits u - rank[p] entries
+// (p, q >= p) with first contig m[p] (u = number of distinct contigs).
+struct ReadSet {
+    uint32_t m[kMaxFast];
+    bool keep[kMaxFast];
+    uint32_t rank[kMaxFast];
+    uint32_t u;
+};
+
+__device__ __forceinline__ void sort_dedup(ReadSet& s) {
+#define CE(x, y)                                                       \
+    {                                                                  \
+        uint32_t lo_ = min(s.m[x], s.m[y]), hi_ = max(s.m[x], s.m[y]); \
+        s.m[x] = lo_;                                                  \
+        s.m[y] = hi_;                                                  \
+    }
+    // Batcher odd-even merge sort network, 8 inputs, 19 comparators
+    CE(0, 1) CE(2, 3) CE(4, 5) CE(6, 7)
+    CE(0, 2) CE(1, 3) CE(4, 6) CE(5, 7)
+    CE(1, 2) CE(5, 6)
+    CE(0, 4) CE(1, 5) CE(2, 6) CE(3, 7)
+    CE(2, 4) CE(3, 5)
+    CE(1, 2) CE(3, 4) CE(5, 6)
+#undef CE
+    uint32_t u = 0;
+#pragma unroll
+    for (int p = 0; p < kMaxFast; ++p) {
+        s.keep[p] = s.m[p] != kEmpty && (p == 0 || s.m[p] != s.m[p - 1]);
+        s.rank[p] = u;
+        u += s.keep[p] ? 1u : 0u;
+    }
+    s.u = u;
+}
+
+
+// Arbitrary read size (reads with more than 8 records; rare), O(m^3) over
+// global memory, one thread per read.
+template <typename Emit>
+__device__ void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_t i, Emit emit) {
+    const uint32_t rid = rec[i].x;
+    int64_t end = i;
+    while (end < A && rec[end].x == rid) ++end;
+    for (int64_t p = i; p < end; ++p) {
+        const uint32_t c = rec[p].y;
+        bool dup = false;
+        for (int64_t q = i; q < p && !dup; ++q) dup = rec[q].y == c;
+        if (dup) continue;
+        for (int64_t q = i; q < end; ++q) {
+            const uint32_t d = rec[q].y;
+            if (d < c) continue;
+            bool first = true;
+            for (int64_t r = i; r < q && first; ++r) first = rec[r].y != d;
+            if (first) emit(c, d);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+// Bitonic sort of (key, val) pairs in LDS, n a power of two.
+__device__ void lds_bitonic(uint32_t* keys, uint32_t* vals, int n) {
+    for (int size = 2; size <= n; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < n / 2; t += blockDim.x) {
+                const int i = 2 * t - (t & (stride - 1));
+                const int j = i + stride;
+                const bool up = (i & size) == 0;
+                const uint32_t ki = keys[i], kj = keys[j];
+                if ((ki > kj) == up) {
+                    keys[i] = kj;
+                    keys[j] = ki;
+                    const uint32_t v = vals[i];
+                    vals[i] = vals[j];
+                    vals[j] = v;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}

@@ -123,3 +123,8 @@ struct karma_pairs {
     bool has_first = false;
     bool has_totals = false;
 };
+
+namespace karma {
+// set-partition records pipeline (graph_sets.hip)
+int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out);
+}  // namespace karma

@@ -221,6 +221,36 @@ def test_records_bucket_overflow_path():
     check_records(np.stack([reads, contigs], 1), 1000)
 
 
+def test_records_overflow_with_compact_reads():
+    # a bucket that overflows its hash table also holds compact reads (span < 4):
+    # the generic fallback must regenerate their pairs from the code histogram
+    rng = np.random.default_rng(5)
+    rows = []
+    for r in range(40_000):
+        if r % 2:
+            for c in rng.integers(0, 1000, 8):
+                rows.append((r, int(c)))
+        else:
+            m0 = int(rng.integers(0, 996))
+            for c in m0 + rng.integers(0, 4, int(rng.integers(1, 6))):
+                rows.append((r, int(c)))
+    check_records(np.array(rows, np.uint32), 1000)
+
+
+def test_records_compact_spans_and_bucket_edges():
+    # spans 0..5 placed on and across pair-bucket boundaries (16 contigs per
+    # bucket at n_contigs = 300): compact codes, bucket-crossing and wide reads
+    rng = np.random.default_rng(6)
+    rows = []
+    for r in range(30_000):
+        span = int(rng.integers(0, 6))
+        m0 = int(rng.choice([15, 16, 30, 31, 32, 47, 100, 294])) - int(rng.integers(0, 3))
+        cs = [m0, min(m0 + span, 299)] + [m0 + int(x) for x in rng.integers(0, span + 1, int(rng.integers(0, 4)))]
+        for c in rng.permutation(cs):
+            rows.append((r, min(int(c), 299)))
+    check_records(np.array(rows, np.uint32), 300)
+
+
 def test_records_big_reads_and_duplicates():
     rng = np.random.default_rng(2)
     rows = []

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""profiles/pmc_traffic.json: HBM bytes per launch of the bench's kernels.
+
+Input: the per-kernel JSON of profiles/pmc_summary.py (rocprofv3 FETCH_SIZE and
+WRITE_SIZE passes, KiB per dispatch, reported there as MB).  Correction as
+MI355X_MICROARCH.md §HBM prescribes: on gfx950 FETCH_SIZE reports 1/2 of a
+wide (16 B/lane) streaming read, so reads are doubled; WRITE_SIZE is exact for
+16-B stores.  Both graph_partition and kmer_profile read/write 16 B per lane.
+
+Usage: python tools/pmc_traffic.py pmc_summary.json [out.json]
+"""
+import json
+import sys
+
+# rocprof kernel name -> bench.py kernel (KARMA_LAUNCH) name
+NAMES = {
+    "partition_kernel": "graph_partition",
+    "code_reduce_kernel": "graph_code_reduce",
+    "profile_kernel<true, true, true>": "kmer_profile",
+    "presence_kernel<true>": "kmer_presence",
+}
+
+
+def main():
+    src = json.load(open(sys.argv[1]))
+    out = {}
+    for k, v in src.items():
+        if k in NAMES and v.get("fetch_MB") == v.get("fetch_MB"):  # skip NaN
+            out[NAMES[k]] = int(round((2 * v["fetch_MB"] + v["write_MB"]) * 1024 * 1024))
+    dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
+    json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
