@@ -43,7 +43,6 @@ namespace {
 constexpr int kPT = 1024;                           // partition threads per block (16 waves)
 constexpr int kSuperTile = 8192;                    // records per LDS-resident super-tile
 constexpr int kPerWave = kSuperTile / (kPT / 64);   // 512 records per wave
-constexpr int kSlots = kPerWave / 64;               // 8 records per lane
 constexpr int kCBuf = 16384;                        // codes buffered in LDS (64 KB)
 constexpr int kMaxPartBlocks = 256;
 constexpr int kMaxB = 512;                          // pair buckets
@@ -78,12 +77,6 @@ int make_geo(int64_t N, Geo* g) {
         g->Bc = 0;
     }
     return KARMA_OK;
-}
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
@@ -131,8 +124,8 @@ __global__ void __launch_bounds__(kPT) partition_kernel(PartArgs P) {
     __shared__ uint32_t chist[kMaxBc + 1];
     __shared__ uint32_t ctoff[kMaxBc + 1];
     __shared__ uint32_t ccur[kMaxBc];
-    __shared__ uint32_t prev_rid_s, tile_reads, cbuf_n;
-    __shared__ int has_prev_s, cap_fail;
+    __shared__ uint32_t tile_reads[2], cbuf_n;
+    __shared__ int cap_fail;
     __shared__ int64_t base_s, fbase_s;
     __shared__ unsigned fidx_s;
 
@@ -145,11 +138,12 @@ __global__ void __launch_bounds__(kPT) partition_kernel(PartArgs P) {
     for (int b = threadIdx.x; b <= g.B; b += kPT) hist[b] = 0;
     for (int b = threadIdx.x; b <= g.Bc; b += kPT) chist[b] = 0;
     for (int b = threadIdx.x; b < g.Bc; b += kPT) ccur[b] = 0;
+    for (int b = threadIdx.x; b < g.B; b += kPT) cur[b] = 0;
     if (threadIdx.x == 0) {
-        has_prev_s = lo > 0;
-        prev_rid_s = lo > 0 ? P.rec[lo - 1].x : 0u;
         cbuf_n = 0;
+        tile_reads[0] = tile_reads[1] = 0;
     }
+    __syncthreads();
     int bad_order = 0, bad_contig = 0;
     int64_t used = 0, cused = 0;  // pair / code entries this block has written (uniform)
 
@@ -215,13 +209,18 @@ __global__ void __launch_bounds__(kPT) partition_kernel(PartArgs P) {
         __syncthreads();
     };
 
-    // register prefetch of the next super-tile: 16 B per lane per step (2 records)
-    constexpr int PER = kSuperTile / (2 * kPT);
+    // Register prefetch of a super-tile.  Wave w owns records [w0, w0 + 512)
+    // of the tile: unit u, lane l holds records 128u + 2l and 128u + 2l + 1
+    // (16 B), plus the record before the slice (its read-boundary carry); wave
+    // 15 also fetches the 8 records after the tile (the halo).
+    constexpr int PER = kPerWave / 128;
+    const int w0 = wave * kPerWave;
     u32x4 nxt[PER];
+    uint2 nxc = make_uint2(kEmpty, kEmpty), nxh = make_uint2(kEmpty, kEmpty);
     auto prefetch = [&](int64_t t0) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int64_t gi = t0 + 2 * ((int64_t)u * kPT + threadIdx.x);
+            const int64_t gi = t0 + w0 + 128 * u + 2 * lane;
             u32x4 v = {kEmpty, kEmpty, kEmpty, kEmpty};
             if (t0 < hi) {
                 if (gi + 1 < P.A) {
@@ -233,67 +232,60 @@ __global__ void __launch_bounds__(kPT) partition_kernel(PartArgs P) {
             }
             nxt[u] = v;
         }
+        const int64_t gc = t0 + w0 - 1;
+        nxc = t0 < hi && gc >= 0 && gc < P.A ? P.rec[gc] : make_uint2(kEmpty, kEmpty);
+        if (wave == kPT / 64 - 1 && lane < kMaxFast) {
+            const int64_t gh = t0 + kSuperTile + lane;
+            nxh = t0 < hi && gh < P.A ? P.rec[gh] : make_uint2(kEmpty, kEmpty);
+        }
     };
     prefetch(lo);
     int st = 0;
     for (int64_t ts = lo; ts < hi; ts += kSuperTile, ++st) {
         const int tn = (int)min<int64_t>(kSuperTile, hi - ts);
-        __syncthreads();  // previous super-tile fully consumed
-        for (int b = threadIdx.x; b < g.B; b += kPT) {
-            hist[b] = 0;
-            cur[b] = 0;
-        }
-        if (threadIdx.x == 0) tile_reads = 0;
+        // ---- read starts of this wave's slice, from registers (DPP wave_shr) ----
+        // (records past tn are the following ones: they close the last read)
+        uint32_t carry = nxc.x;
+        const bool carry_valid = ts + w0 > 0;
+        int ns = 0;
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int j = 2 * (u * kPT + threadIdx.x);
+            const int j = 128 * u + 2 * lane;  // slice index of the lane's first record
+            const uint32_t x0 = nxt[u].x, x1 = nxt[u].z;
+            uint32_t p = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)x1, 0x138, 0xF, 0xF, false);
+            if (lane == 0) p = carry;  // lane 0 takes the previous unit's last record
+            bool s0 = false, s1 = false;
+            if (w0 + j < tn) {
+                const bool hp = j > 0 || carry_valid;
+                if (hp && p > x0) bad_order = 1;
+                if (nxt[u].y >= P.N) bad_contig = 1;
+                s0 = !hp || p != x0;
+            }
+            if (w0 + j + 1 < tn) {
+                if (x0 > x1) bad_order = 1;
+                if (nxt[u].w >= P.N) bad_contig = 1;
+                s1 = x0 != x1;
+            }
+            const unsigned long long b0 = __ballot(s0), b1 = __ballot(s1), lower = (1ull << lane) - 1ull;
+            const int pos = ns + __popcll(b0 & lower) + __popcll(b1 & lower);
+            if (s0) wstart[wave][pos] = (uint16_t)j;
+            if (s1) wstart[wave][pos + (s0 ? 1 : 0)] = (uint16_t)(j + 1);
+            ns += __popcll(b0) + __popcll(b1);
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)x1, 63);
+        }
+        if (lane == 0 && ns) atomicAdd(&tile_reads[st & 1], (uint32_t)ns);
+        if (threadIdx.x == 0) tile_reads[(st + 1) & 1] = 0;  // read at tile st - 1, next written at st + 1
+        // ---- stage the slice in LDS (every wave is past the previous tile) ----
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int j = w0 + 128 * u + 2 * lane;
             srec[j] = make_uint2(nxt[u].x, nxt[u].y);
             srec[j + 1] = make_uint2(nxt[u].z, nxt[u].w);
         }
-        if (threadIdx.x < kMaxFast) {  // halo: the records after the super-tile
-            const int64_t gi = ts + kSuperTile + threadIdx.x;
-            srec[kSuperTile + threadIdx.x] = gi < P.A ? P.rec[gi] : make_uint2(kEmpty, kEmpty);
-        }
-        __syncthreads();
-        if (tn < kSuperTile) {  // short tail: the records after tn are the next ones
-            for (int j = tn + threadIdx.x; j < tn + kMaxFast; j += kPT) {
-                const int64_t gi = ts + j;
-                srec[j] = gi < P.A ? P.rec[gi] : make_uint2(kEmpty, kEmpty);
-            }
-            __syncthreads();
-        }
+        if (wave == kPT / 64 - 1 && lane < kMaxFast) srec[kSuperTile + lane] = nxh;
         prefetch(ts + kSuperTile);
-
-        // ---- read starts of this wave's slice, from registers (DPP wave_shr) ----
-        const int w0 = wave * kPerWave;
-        uint2 rr[kSlots];
-#pragma unroll
-        for (int u = 0; u < kSlots; ++u) rr[u] = srec[w0 + u * 64 + lane];
-        uint32_t carry = w0 > 0 ? srec[w0 - 1].x : prev_rid_s;
-        const bool carry_valid = w0 > 0 || has_prev_s;
-        int ns = 0;
-#pragma unroll
-        for (int u = 0; u < kSlots; ++u) {
-            const int j = w0 + u * 64 + lane;
-            const uint32_t x = rr[u].x;
-            uint32_t p = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)x, 0x138, 0xF, 0xF, false);
-            if (lane == 0) p = carry;  // lane 0 takes the previous slot's last record
-            const bool hp = j > 0 || carry_valid;
-            bool s = false;
-            if (j < tn) {
-                if (hp && p > x) bad_order = 1;
-                if (rr[u].y >= P.N) bad_contig = 1;
-                s = !hp || p != x;
-            }
-            const unsigned long long bal = __ballot(s);
-            if (s) wstart[wave][ns + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(j - w0);
-            ns += __popcll(bal);
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-        }
-        if (lane == 0 && ns) atomicAdd(&tile_reads, (uint32_t)ns);
-        wave_sync();
-        __syncthreads();  // every wave reads neighbours' slots below
-        if (cbuf_n + tile_reads > (uint32_t)kCBuf) flush(false);  // rare: a tile of many short reads
+        __syncthreads();  // tile staged, read starts counted
+        if (cbuf_n + tile_reads[st & 1] > (uint32_t)kCBuf) flush(false);  // rare: a tile of many short reads
 
         // ---- pass A: one lane per read: a code, or dedup + cache + count pairs ----
         int ng = 0;  // general reads of this wave, compacted to the front of wstart
@@ -371,95 +363,98 @@ __global__ void __launch_bounds__(kPT) partition_kernel(PartArgs P) {
             if (gen) wstart[wave][ng + __popcll(gb & ((1ull << lane) - 1ull))] = (uint16_t)(j0 - w0);
             ng += __popcll(gb);
         }
-        __syncthreads();
-        // ---- pairs of general reads: scan, region slice, directory ----
-        if (wave == 0) {
-            uint32_t c2 = 0;
-            for (int base = 0; base < g.B; base += 64) {
-                const uint32_t val = base + lane < g.B ? hist[base + lane] : 0u;
-                uint32_t x = val;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(x, d);
-                    if (lane >= d) x += y;
-                }
-                if (base + lane < g.B) toff[base + lane] = c2 + x - val;
-                c2 += __shfl(x, 63);
-            }
-            if (lane == 0) {
-                toff[g.B] = c2;
-                cap_fail = used + (int64_t)c2 > P.region_cap;
-                if (cap_fail) P.flags[2] = 1;  // the host reruns with room for every entry
-                base_s = blk * P.region_cap + used;
-            }
-        }
-        __syncthreads();
-        const uint32_t total = toff[g.B];
         const int64_t slot = blk * P.nst + st;
-        if (total == 0 || cap_fail) {
+        if (!__syncthreads_or(ng > 0)) {  // no general read in this super-tile: no pairs
             if (threadIdx.x == 0) P.st_base[slot] = -1;
         } else {
-            if (threadIdx.x == 0) P.st_base[slot] = base_s;
-            for (int b = threadIdx.x; b <= g.B; b += kPT) P.st_off[(int64_t)b * P.n_slots + slot] = toff[b];
-            // ---- pass B: write the pairs (m[p], m[q]), q >= p, of every general read ----
-            uint32_t* dst = P.ent + base_s;
-            for (int k = lane; k < ng; k += 64) {
-                const int j0 = w0 + wstart[wave][k];
-                uint2 r[kMaxFast];
+            // ---- pairs of general reads: scan, region slice, directory ----
+            if (wave == 0) {
+                uint32_t c2 = 0;
+                for (int base = 0; base < g.B; base += 64) {
+                    const uint32_t val = base + lane < g.B ? hist[base + lane] : 0u;
+                    uint32_t x = val;
 #pragma unroll
-                for (int t = 0; t < kMaxFast; ++t) r[t] = srec[j0 + t];
-                const uint32_t rid = r[0].x;
-                uint32_t m[kMaxFast];
-                bool v = true;
-                uint32_t u = 0;
-#pragma unroll
-                for (int t = 0; t < kMaxFast; ++t) {
-                    v = v && (t == 0 || r[t].x == rid) && r[t].y != kEmpty;
-                    m[t] = r[t].y;
-                    u += v ? 1u : 0u;
-                }
-                // runs of one bucket: reserve, then write
-                uint32_t rb = kEmpty, rn = 0;
-                int rp0 = 0;
-                uint32_t base[kMaxFast];
-#pragma unroll
-                for (int p = 0; p <= kMaxFast; ++p) {
-                    const bool in = p < kMaxFast && (uint32_t)p < u;
-                    const uint32_t b = in ? (m[p] >> g.bw) : kEmpty;
-                    if (p == kMaxFast || (in && b != rb)) {
-                        if (rn && rb < (uint32_t)g.B) {
-                            uint32_t pos = toff[rb] + atomicAdd(&cur[rb], rn);
-#pragma unroll
-                            for (int q = 0; q < kMaxFast; ++q) {
-                                if (q >= rp0 && q < p && (uint32_t)q < u) {
-                                    base[q] = pos;
-                                    pos += u - q;
-                                }
-                            }
-                        }
-                        if (in) {
-                            rb = b;
-                            rn = 0;
-                            rp0 = p;
-                        }
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = __shfl_up(x, d);
+                        if (lane >= d) x += y;
                     }
-                    if (in) rn += u - p;
+                    if (base + lane < g.B) toff[base + lane] = c2 + x - val;
+                    c2 += __shfl(x, 63);
                 }
-#pragma unroll
-                for (int p = 0; p < kMaxFast; ++p) {
-                    if ((uint32_t)p >= u || (m[p] >> g.bw) >= (uint32_t)g.B) continue;
-                    const uint32_t hk = (m[p] & wmask) << g.bbits;
-#pragma unroll
-                    for (int q = p; q < kMaxFast; ++q)
-                        if ((uint32_t)q < u) dst[base[p] + (q - p)] = hk | m[q];
+                if (lane == 0) {
+                    toff[g.B] = c2;
+                    cap_fail = used + (int64_t)c2 > P.region_cap;
+                    if (cap_fail) P.flags[2] = 1;  // the host reruns with room for every entry
+                    base_s = blk * P.region_cap + used;
                 }
             }
-        }
-        if (total) used += total;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            prev_rid_s = srec[tn - 1].x;
-            has_prev_s = 1;
+            __syncthreads();
+            const uint32_t total = toff[g.B];
+            if (total == 0 || cap_fail) {
+                if (threadIdx.x == 0) P.st_base[slot] = -1;
+            } else {
+                if (threadIdx.x == 0) P.st_base[slot] = base_s;
+                for (int b = threadIdx.x; b <= g.B; b += kPT) P.st_off[(int64_t)b * P.n_slots + slot] = toff[b];
+                // ---- pass B: write the pairs (m[p], m[q]), q >= p, of every general read ----
+                uint32_t* dst = P.ent + base_s;
+                for (int k = lane; k < ng; k += 64) {
+                    const int j0 = w0 + wstart[wave][k];
+                    uint2 r[kMaxFast];
+#pragma unroll
+                    for (int t = 0; t < kMaxFast; ++t) r[t] = srec[j0 + t];
+                    const uint32_t rid = r[0].x;
+                    uint32_t m[kMaxFast];
+                    bool v = true;
+                    uint32_t u = 0;
+#pragma unroll
+                    for (int t = 0; t < kMaxFast; ++t) {
+                        v = v && (t == 0 || r[t].x == rid) && r[t].y != kEmpty;
+                        m[t] = r[t].y;
+                        u += v ? 1u : 0u;
+                    }
+                    // runs of one bucket: reserve, then write
+                    uint32_t rb = kEmpty, rn = 0;
+                    int rp0 = 0;
+                    uint32_t base[kMaxFast];
+#pragma unroll
+                    for (int p = 0; p <= kMaxFast; ++p) {
+                        const bool in = p < kMaxFast && (uint32_t)p < u;
+                        const uint32_t b = in ? (m[p] >> g.bw) : kEmpty;
+                        if (p == kMaxFast || (in && b != rb)) {
+                            if (rn && rb < (uint32_t)g.B) {
+                                uint32_t pos = toff[rb] + atomicAdd(&cur[rb], rn);
+#pragma unroll
+                                for (int q = 0; q < kMaxFast; ++q) {
+                                    if (q >= rp0 && q < p && (uint32_t)q < u) {
+                                        base[q] = pos;
+                                        pos += u - q;
+                                    }
+                                }
+                            }
+                            if (in) {
+                                rb = b;
+                                rn = 0;
+                                rp0 = p;
+                            }
+                        }
+                        if (in) rn += u - p;
+                    }
+#pragma unroll
+                    for (int p = 0; p < kMaxFast; ++p) {
+                        if ((uint32_t)p >= u || (m[p] >> g.bw) >= (uint32_t)g.B) continue;
+                        const uint32_t hk = (m[p] & wmask) << g.bbits;
+#pragma unroll
+                        for (int q = p; q < kMaxFast; ++q)
+                            if ((uint32_t)q < u) dst[base[p] + (q - p)] = hk | m[q];
+                    }
+                }
+            }
+            if (total) used += total;
+            __syncthreads();  // pass B done with srec, toff and cur
+            for (int b = threadIdx.x; b < g.B; b += kPT) {
+                hist[b] = 0;
+                cur[b] = 0;
+            }
         }
         if (cbuf_n > (uint32_t)kCBuf - kFlushSlack) flush(true);  // srec is free until the next tile
     }
@@ -933,9 +928,11 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     const int64_t nb = std::max<int64_t>(1, ceil_div(A, chunk));
     const int nst = (int)(chunk / kSuperTile);
     const int64_t n_slots = nb * nst;
-    const int64_t max_flush = nb * (nst + 2);
-    // codes <= reads <= records, plus < 8 codes of padding per run of a flush
-    const int64_t code_region = chunk + (int64_t)(nst + 2) * 8 * g.Bc;
+    // <= 2 flushes per super-tile (before pass A when a tile of short reads would
+    // not fit, and at its end) + the last; codes <= reads <= records, plus < 8
+    // codes of padding per run of a flush
+    const int64_t max_flush = nb * (2 * nst + 1);
+    const int64_t code_region = chunk + (int64_t)(2 * nst + 1) * 8 * g.Bc;
     DevArray<int64_t> st_base, big_list, cf_base;
     DevArray<uint32_t> st_off, ent, cf_off;
     DevArray<uint16_t> cent;
