@@ -5,26 +5,32 @@
 // sorted unique (a << 32 | b, count) list over pairs a <= b of contigs sharing
 // reads; the diagonal (a, a) counts |readset(a)|, the weight normaliser.
 //
-// A read's distinct contigs are "compact" when they lie in [m0, m0 + 3]: contigs that share reads are isoforms of one gene, which
-// assemblers list next to each other (Trinity: TRINITY_DNx_cy_gz_i1, _i2, ...),
-// so nearly every read is compact.  Such a read is one 15-bit code (m0, M),
-// bit i of (1 | M << 1) marking contig m0 + i; dedup and order come for free.
-// Other reads (wider spans) take the general path: sort network, dedup, every
-// pair (p <= q).
+// A read's distinct contigs are "compact" when they lie in [m0, m0 + 3].
+// Contigs that share reads are isoforms of one gene, which assemblers list next
+// to each other (Trinity: TRINITY_DNx_cy_gz_i1, _i2, ...), so nearly every read
+// is compact.  A compact read is one code (m0, M), bit i of (1 | M << 1)
+// marking contig m0 + i: dedup and order come for free.  Other reads (wider
+// spans) take the general path: sort network, dedup, every pair (p <= q).
 //
-//   partition   one pass over the records.  A block stages super-tiles of 8192
-//               records in LDS.  Codes accumulate in a 64 KB LDS buffer across
-//               super-tiles and are flushed bucket-major (code buckets of
-//               2^bwc contigs) when full, so a code bucket's run in one flush is
-//               ~300 codes.  General reads' pairs are written per super-tile,
-//               bucket-major (pair buckets of 2^bw contigs).
+//   classify    one wave per chunk of 8192 records, no block barriers: stages
+//               512 records at a time in its own LDS slice, finds read starts
+//               with DPP, and writes one u32 code per compact read (coalesced,
+//               into the chunk's own region); general reads' starts go to the
+//               region's tail, reads of > 8 records to the big-read list.
+//   general     one wave per chunk with general reads: pairs as u64 keys into
+//               the chunk's pair list.
+//   partition   (codes, pairs) consecutive chunk lists fill a 64 KB LDS buffer;
+//               a full buffer is counting-sorted by bucket in LDS and written
+//               as 16-byte-aligned padded runs, one directory row per flush.
 //   code reduce per (code bucket, group of flushes): direct-mapped LDS
-//               histogram over (m0, M) — one no-return LDS add per read.
-//   pair reduce per (pair bucket, group of super-tiles): band counters for
+//               histogram over (m0, M), one no-return LDS add per read.
+//   pair reduce per (pair bucket, group of flushes): band counters for
 //               b - a < 8 and an LDS hash table for the rest.
 //   final       per pair bucket: sums the partials, expands the code histogram
 //               into band pairs, merges the hash lists, writes the sorted list.
 //   big reads   (> 8 records): separate generic path, merged at the end.
+// Device-side counters size every grid-stride loop, so the common path has
+// one host synchronisation (flags, overflow, output size) at the end.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -40,14 +46,11 @@ namespace {
 
 #include "graph_device.h"
 
-constexpr int kPT = 1024;                           // partition threads per block (16 waves)
-constexpr int kSuperTile = 8192;                    // records per LDS-resident super-tile
-constexpr int kPerWave = kSuperTile / (kPT / 64);   // 512 records per wave
-constexpr int kCBuf = 16384;                        // codes buffered in LDS (64 KB)
-constexpr int kMaxPartBlocks = 256;
-constexpr int kMaxB = 512;                          // pair buckets
-constexpr int kMaxBc = 128;                         // code buckets
-constexpr int kMaxBwCompact = 10;                   // compact reads need 2^(bw+3) band counters <= kBand
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kMaxB = 512;            // pair buckets
+constexpr int kMaxBc = 128;           // code buckets
+constexpr int kMaxBwCompact = 10;     // compact reads need 2^(bw+3) band counters <= kBand
 
 struct Geo {
     int bw, bbits, B;  // pair buckets of 2^bw contigs; pair keys a_local << bbits | b
@@ -79,150 +82,61 @@ int make_geo(int64_t N, Geo* g) {
     return KARMA_OK;
 }
 
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-constexpr uint16_t kPadCode = 0xFFFF;               // code-run padding (codes are < 2^15)
-constexpr uint32_t kFlushSlack = 4096;              // flush at a tile's end above kCBuf - this
+// ---- classify -------------------------------------------------------------------
+constexpr int kCW = 256;                // classify threads per block (4 independent waves)
+constexpr int kCIter = 512;             // records per wave step (8 per lane)
+constexpr int kCPer = kCIter / 128;     // 16-byte units per lane per step
+constexpr int64_t kCChunk = 8192;       // records per wave chunk (16 steps)
 
-struct PartArgs {
+struct ClassArgs {
     const uint2* rec;
-    int64_t A, chunk;
-    int nst;
-    Geo g;
+    int64_t A;
     uint32_t N;
-    // pair stream: per super-tile slot, bucket-major; st_base = -1 for a slot without pairs
-    uint32_t* ent;
-    int64_t region_cap;
-    int64_t n_slots;
-    int64_t* st_base;
-    uint32_t* st_off;  // [B + 1][n_slots]
-    // code stream: per flush, bucket-major; a block's codes go to [blk * code_region, ...)
-    uint16_t* cent;
-    int64_t code_region;
-    int64_t* cf_base;
-    uint32_t* cf_off;  // [max_flush][Bc + 1]
-    unsigned* n_flush;
-    int64_t max_flush;
-    int* flags;  // 0 order, 1 contig range, 2 pair region full, 3 flush directory full
+    int compact;
+    uint32_t* codes;    // chunk c: [c * kCChunk, +n_codes[c]) codes, general starts from the end down
+    uint32_t* n_codes;  // per chunk
+    uint32_t* n_gen;    // per chunk
     int64_t* big_list;
     unsigned* big_n;
-    unsigned long long* n_pairs;  // pair entries written (all blocks)
+    int* flags;  // 0 order, 1 contig range
 };
 
-__global__ void __launch_bounds__(kPT) partition_kernel(PartArgs P) {
-    __shared__ uint2 srec[kSuperTile + kMaxFast];
-    __shared__ uint16_t wstart[kPT / 64][kPerWave];
-    __shared__ uint32_t cbuf[kCBuf];
-    __shared__ uint32_t hist[kMaxB + 1];
-    __shared__ uint32_t toff[kMaxB + 1];
-    __shared__ uint32_t cur[kMaxB];
-    __shared__ uint32_t chist[kMaxBc + 1];
-    __shared__ uint32_t ctoff[kMaxBc + 1];
-    __shared__ uint32_t ccur[kMaxBc];
-    __shared__ uint32_t tile_reads[2], cbuf_n;
-    __shared__ int cap_fail;
-    __shared__ int64_t base_s, fbase_s;
-    __shared__ unsigned fidx_s;
-
-    const Geo g = P.g;
+// code (m0 | M << 24) of a compact read, or general / big
+__global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
+    __shared__ uint2 srec[kCW / 64][kCIter + kMaxFast];
+    __shared__ uint16_t wst[kCW / 64][kCIter];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t blk = blockIdx.x;
-    const int64_t lo = blk * P.chunk, hi = min(P.A, lo + P.chunk);
-    const uint32_t wmask = (1u << g.bw) - 1u, cmask = (1u << g.bwc) - 1u;
-    const bool compact_ok = g.bwc > 0;
-    for (int b = threadIdx.x; b <= g.B; b += kPT) hist[b] = 0;
-    for (int b = threadIdx.x; b <= g.Bc; b += kPT) chist[b] = 0;
-    for (int b = threadIdx.x; b < g.Bc; b += kPT) ccur[b] = 0;
-    for (int b = threadIdx.x; b < g.B; b += kPT) cur[b] = 0;
-    if (threadIdx.x == 0) {
-        cbuf_n = 0;
-        tile_reads[0] = tile_reads[1] = 0;
-    }
-    __syncthreads();
-    int bad_order = 0, bad_contig = 0;
-    int64_t used = 0, cused = 0;  // pair / code entries this block has written (uniform)
+    const int64_t chunk = (int64_t)blockIdx.x * (kCW / 64) + wave;
+    const int64_t c_lo = chunk * kCChunk;
+    if (c_lo >= P.A) return;  // this kernel has no block barrier: waves are independent
+    const int64_t c_hi = min(P.A, c_lo + kCChunk);
+    uint2* sr = srec[wave];
+    uint16_t* ws = wst[wave];
+    uint32_t* out = P.codes + c_lo;
+    const unsigned long long lower = (1ull << lane) - 1ull;
 
-    // codes in cbuf -> the code stream (all threads call this): one flush is
-    // the runs of the code buckets, each padded with kPadCode to a multiple of
-    // 8 codes (16-byte aligned).  `staged`: counting-sort into the free srec
-    // area, then 16-byte stores; otherwise scattered 2-byte stores.
-    auto flush = [&](bool staged) {
-        __syncthreads();
-        const uint32_t n = cbuf_n;
-        if (n == 0) return;
-        if (wave == 0) {
-            uint32_t c2 = 0;
-            for (int base = 0; base < g.Bc; base += 64) {
-                const uint32_t val = base + lane < g.Bc ? (chist[base + lane] + 7u) & ~7u : 0u;
-                uint32_t x = val;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(x, d);
-                    if (lane >= d) x += y;
-                }
-                if (base + lane < g.Bc) ctoff[base + lane] = c2 + x - val;
-                c2 += __shfl(x, 63);
-            }
-            if (lane == 0) {
-                ctoff[g.Bc] = c2;
-                const unsigned f = atomicAdd(P.n_flush, 1u);
-                fidx_s = f;
-                fbase_s = blk * P.code_region + cused;
-                if ((int64_t)f < P.max_flush) P.cf_base[f] = fbase_s;
-                else P.flags[3] = 1;
-            }
-        }
-        __syncthreads();
-        const unsigned f = fidx_s;
-        const int64_t fb = fbase_s;
-        const uint32_t total = ctoff[g.Bc];
-        if ((int64_t)f < P.max_flush) {
-            uint16_t* sorted = reinterpret_cast<uint16_t*>(srec);
-            uint16_t* out = staged ? sorted : P.cent + fb;
-            for (int b = threadIdx.x; b <= g.Bc; b += kPT) P.cf_off[(int64_t)f * (g.Bc + 1) + b] = ctoff[b];
-            for (int b = threadIdx.x; b < g.Bc; b += kPT)
-                for (uint32_t i = ctoff[b] + chist[b]; i < ctoff[b + 1]; ++i) out[i] = kPadCode;
-            for (uint32_t i = threadIdx.x; i < n; i += kPT) {
-                const uint32_t c = cbuf[i], m0 = c & 0xFFFFFFu, b = m0 >> g.bwc;
-                const uint32_t pos = ctoff[b] + atomicAdd(&ccur[b], 1u);
-                out[pos] = (uint16_t)(((m0 & cmask) << 3) | (c >> 24));
-            }
-            if (staged) {
-                __syncthreads();
-                u32x4* dst = reinterpret_cast<u32x4*>(P.cent + fb);
-                const u32x4* src = reinterpret_cast<const u32x4*>(sorted);
-                for (uint32_t i = threadIdx.x; i < total / 8; i += kPT) dst[i] = src[i];
-            }
-        }
-        cused += total;
-        __syncthreads();
-        for (int b = threadIdx.x; b < g.Bc; b += kPT) {
-            chist[b] = 0;
-            ccur[b] = 0;
-        }
-        if (threadIdx.x == 0) cbuf_n = 0;
-        __syncthreads();
-    };
-
-    // Register prefetch of a super-tile.  Wave w owns records [w0, w0 + 512)
-    // of the tile: unit u, lane l holds records 128u + 2l and 128u + 2l + 1
-    // (16 B), plus the record before the slice (its read-boundary carry); wave
-    // 15 also fetches the 8 records after the tile (the halo).
-    constexpr int PER = kPerWave / 128;
-    const int w0 = wave * kPerWave;
-    u32x4 nxt[PER];
+    // register prefetch of a step: unit u, lane l holds records 128u + 2l, +1;
+    // plus the record before the step (read-boundary carry) and the 8 after it
+    u32x4 nxt[kCPer];
     uint2 nxc = make_uint2(kEmpty, kEmpty), nxh = make_uint2(kEmpty, kEmpty);
     auto prefetch = [&](int64_t t0) {
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int64_t gi = t0 + w0 + 128 * u + 2 * lane;
+        for (int u = 0; u < kCPer; ++u) {
+            const int64_t gi = t0 + 128 * u + 2 * lane;
             u32x4 v = {kEmpty, kEmpty, kEmpty, kEmpty};
-            if (t0 < hi) {
+            if (t0 < c_hi) {
                 if (gi + 1 < P.A) {
                     v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.rec + gi));
                 } else if (gi < P.A) {
@@ -232,250 +146,348 @@ __global__ void __launch_bounds__(kPT) partition_kernel(PartArgs P) {
             }
             nxt[u] = v;
         }
-        const int64_t gc = t0 + w0 - 1;
-        nxc = t0 < hi && gc >= 0 && gc < P.A ? P.rec[gc] : make_uint2(kEmpty, kEmpty);
-        if (wave == kPT / 64 - 1 && lane < kMaxFast) {
-            const int64_t gh = t0 + kSuperTile + lane;
-            nxh = t0 < hi && gh < P.A ? P.rec[gh] : make_uint2(kEmpty, kEmpty);
-        }
+        nxc = t0 < c_hi && t0 > 0 ? P.rec[t0 - 1] : make_uint2(kEmpty, kEmpty);
+        const int64_t gh = t0 + kCIter + lane;
+        nxh = t0 < c_hi && lane < kMaxFast && gh < P.A ? P.rec[gh] : make_uint2(kEmpty, kEmpty);
     };
-    prefetch(lo);
-    int st = 0;
-    for (int64_t ts = lo; ts < hi; ts += kSuperTile, ++st) {
-        const int tn = (int)min<int64_t>(kSuperTile, hi - ts);
-        // ---- read starts of this wave's slice, from registers (DPP wave_shr) ----
-        // (records past tn are the following ones: they close the last read)
+    prefetch(c_lo);
+    uint32_t nc = 0, ng = 0;
+    int bad_order = 0, bad_contig = 0;
+    for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) {
+        const int tn = (int)min<int64_t>(kCIter, c_hi - t0);
+        // ---- read starts (records past tn are the following ones) ----
         uint32_t carry = nxc.x;
-        const bool carry_valid = ts + w0 > 0;
+        const bool carry_valid = t0 > 0;
         int ns = 0;
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int j = 128 * u + 2 * lane;  // slice index of the lane's first record
+        for (int u = 0; u < kCPer; ++u) {
+            const int j = 128 * u + 2 * lane;
             const uint32_t x0 = nxt[u].x, x1 = nxt[u].z;
             uint32_t p = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)x1, 0x138, 0xF, 0xF, false);
             if (lane == 0) p = carry;  // lane 0 takes the previous unit's last record
             bool s0 = false, s1 = false;
-            if (w0 + j < tn) {
+            if (j < tn) {
                 const bool hp = j > 0 || carry_valid;
                 if (hp && p > x0) bad_order = 1;
                 if (nxt[u].y >= P.N) bad_contig = 1;
                 s0 = !hp || p != x0;
             }
-            if (w0 + j + 1 < tn) {
+            if (j + 1 < tn) {
                 if (x0 > x1) bad_order = 1;
                 if (nxt[u].w >= P.N) bad_contig = 1;
                 s1 = x0 != x1;
             }
-            const unsigned long long b0 = __ballot(s0), b1 = __ballot(s1), lower = (1ull << lane) - 1ull;
+            const unsigned long long b0 = __ballot(s0), b1 = __ballot(s1);
             const int pos = ns + __popcll(b0 & lower) + __popcll(b1 & lower);
-            if (s0) wstart[wave][pos] = (uint16_t)j;
-            if (s1) wstart[wave][pos + (s0 ? 1 : 0)] = (uint16_t)(j + 1);
+            if (s0) ws[pos] = (uint16_t)j;
+            if (s1) ws[pos + (s0 ? 1 : 0)] = (uint16_t)(j + 1);
             ns += __popcll(b0) + __popcll(b1);
             carry = (uint32_t)__builtin_amdgcn_readlane((int)x1, 63);
         }
-        if (lane == 0 && ns) atomicAdd(&tile_reads[st & 1], (uint32_t)ns);
-        if (threadIdx.x == 0) tile_reads[(st + 1) & 1] = 0;  // read at tile st - 1, next written at st + 1
-        // ---- stage the slice in LDS (every wave is past the previous tile) ----
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int j = w0 + 128 * u + 2 * lane;
-            srec[j] = make_uint2(nxt[u].x, nxt[u].y);
-            srec[j + 1] = make_uint2(nxt[u].z, nxt[u].w);
+        for (int u = 0; u < kCPer; ++u) {
+            const int j = 128 * u + 2 * lane;
+            sr[j] = make_uint2(nxt[u].x, nxt[u].y);
+            sr[j + 1] = make_uint2(nxt[u].z, nxt[u].w);
         }
-        if (wave == kPT / 64 - 1 && lane < kMaxFast) srec[kSuperTile + lane] = nxh;
-        prefetch(ts + kSuperTile);
-        __syncthreads();  // tile staged, read starts counted
-        if (cbuf_n + tile_reads[st & 1] > (uint32_t)kCBuf) flush(false);  // rare: a tile of many short reads
-
-        // ---- pass A: one lane per read: a code, or dedup + cache + count pairs ----
-        int ng = 0;  // general reads of this wave, compacted to the front of wstart
+        if (lane < kMaxFast) sr[kCIter + lane] = nxh;
+        prefetch(t0 + kCIter);
+        wave_sync();
+        // ---- one lane per read ----
         for (int kb = 0; kb < ns; kb += 64) {
             const int k = kb + lane;
             uint32_t code = kEmpty;
             bool gen = false;
             int j0 = 0;
             if (k < ns) {
-                j0 = w0 + wstart[wave][k];
+                j0 = ws[k];
                 uint2 r[kMaxFast + 1];
 #pragma unroll
-                for (int t = 0; t <= kMaxFast; ++t) r[t] = srec[j0 + t];
+                for (int t = 0; t <= kMaxFast; ++t) r[t] = sr[j0 + t];
                 const uint32_t rid = r[0].x;
-                ReadSet rs;
                 bool v = true;
-                bool valid[kMaxFast];
                 uint32_t mn = kEmpty, mx = 0;
 #pragma unroll
                 for (int t = 0; t < kMaxFast; ++t) {
                     v = v && (t == 0 || r[t].x == rid);
-                    valid[t] = v;
-                    rs.m[t] = v ? r[t].y : kEmpty;
                     if (v) {
                         mn = min(mn, r[t].y);
                         mx = max(mx, r[t].y);
                     }
                 }
                 if (v && r[kMaxFast].x == rid) {  // > 8 records: generic path
-                    P.big_list[atomicAdd(P.big_n, 1u)] = ts + j0;
-                } else if (compact_ok && mx - mn < 4u && mx < P.N) {
+                    P.big_list[atomicAdd(P.big_n, 1u)] = t0 + j0;
+                } else if (P.compact && mx - mn < 4u && mx < P.N) {
                     uint32_t M = 0;
-#pragma unroll
-                    for (int t = 0; t < kMaxFast; ++t)
-                        if (valid[t]) M |= 1u << (rs.m[t] - mn);
-                    code = (M >> 1) << 24 | mn;
-                    atomicAdd(&chist[mn >> g.bwc], 1u);
-                } else {
-                    gen = true;
-                    sort_dedup(rs);
-                    // the read's slots now hold its sorted distinct contigs, then
-                    // kEmpty (.x keeps the read id for the read boundary)
-#pragma unroll
-                    for (int p = 0; p < kMaxFast; ++p)
-                        if (rs.keep[p]) srec[j0 + rs.rank[p]].y = rs.m[p];
-#pragma unroll
-                    for (int q = 1; q < kMaxFast; ++q)
-                        if (valid[q] && (uint32_t)q >= rs.u) srec[j0 + q].y = kEmpty;
-                    uint32_t run_b = kEmpty, run_n = 0;
-#pragma unroll
-                    for (int p = 0; p < kMaxFast; ++p) {
-                        if (rs.keep[p]) {
-                            const uint32_t b = rs.m[p] >> g.bw;
-                            if (b != run_b) {
-                                if (run_n && run_b < (uint32_t)g.B) atomicAdd(&hist[run_b], run_n);
-                                run_b = b;
-                                run_n = 0;
-                            }
-                            run_n += rs.u - rs.rank[p];
-                        }
-                    }
-                    if (run_n && run_b < (uint32_t)g.B) atomicAdd(&hist[run_b], run_n);
-                }
-            }
-            // wave-aggregated append of the codes; general reads compacted in place
-            // (index ng + rank <= k: every lane has read its slot before these writes)
-            const unsigned long long cb = __ballot(code != kEmpty);
-            if (cb) {
-                uint32_t at = 0;
-                if (lane == 0) at = atomicAdd(&cbuf_n, (uint32_t)__popcll(cb));
-                at = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
-                if (code != kEmpty) cbuf[at + __popcll(cb & ((1ull << lane) - 1ull))] = code;
-            }
-            const unsigned long long gb = __ballot(gen);
-            if (gen) wstart[wave][ng + __popcll(gb & ((1ull << lane) - 1ull))] = (uint16_t)(j0 - w0);
-            ng += __popcll(gb);
-        }
-        const int64_t slot = blk * P.nst + st;
-        if (!__syncthreads_or(ng > 0)) {  // no general read in this super-tile: no pairs
-            if (threadIdx.x == 0) P.st_base[slot] = -1;
-        } else {
-            // ---- pairs of general reads: scan, region slice, directory ----
-            if (wave == 0) {
-                uint32_t c2 = 0;
-                for (int base = 0; base < g.B; base += 64) {
-                    const uint32_t val = base + lane < g.B ? hist[base + lane] : 0u;
-                    uint32_t x = val;
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t y = __shfl_up(x, d);
-                        if (lane >= d) x += y;
-                    }
-                    if (base + lane < g.B) toff[base + lane] = c2 + x - val;
-                    c2 += __shfl(x, 63);
-                }
-                if (lane == 0) {
-                    toff[g.B] = c2;
-                    cap_fail = used + (int64_t)c2 > P.region_cap;
-                    if (cap_fail) P.flags[2] = 1;  // the host reruns with room for every entry
-                    base_s = blk * P.region_cap + used;
-                }
-            }
-            __syncthreads();
-            const uint32_t total = toff[g.B];
-            if (total == 0 || cap_fail) {
-                if (threadIdx.x == 0) P.st_base[slot] = -1;
-            } else {
-                if (threadIdx.x == 0) P.st_base[slot] = base_s;
-                for (int b = threadIdx.x; b <= g.B; b += kPT) P.st_off[(int64_t)b * P.n_slots + slot] = toff[b];
-                // ---- pass B: write the pairs (m[p], m[q]), q >= p, of every general read ----
-                uint32_t* dst = P.ent + base_s;
-                for (int k = lane; k < ng; k += 64) {
-                    const int j0 = w0 + wstart[wave][k];
-                    uint2 r[kMaxFast];
-#pragma unroll
-                    for (int t = 0; t < kMaxFast; ++t) r[t] = srec[j0 + t];
-                    const uint32_t rid = r[0].x;
-                    uint32_t m[kMaxFast];
-                    bool v = true;
-                    uint32_t u = 0;
+                    v = true;
 #pragma unroll
                     for (int t = 0; t < kMaxFast; ++t) {
-                        v = v && (t == 0 || r[t].x == rid) && r[t].y != kEmpty;
-                        m[t] = r[t].y;
-                        u += v ? 1u : 0u;
+                        v = v && (t == 0 || r[t].x == rid);
+                        if (v) M |= 1u << (r[t].y - mn);
                     }
-                    // runs of one bucket: reserve, then write
-                    uint32_t rb = kEmpty, rn = 0;
-                    int rp0 = 0;
-                    uint32_t base[kMaxFast];
-#pragma unroll
-                    for (int p = 0; p <= kMaxFast; ++p) {
-                        const bool in = p < kMaxFast && (uint32_t)p < u;
-                        const uint32_t b = in ? (m[p] >> g.bw) : kEmpty;
-                        if (p == kMaxFast || (in && b != rb)) {
-                            if (rn && rb < (uint32_t)g.B) {
-                                uint32_t pos = toff[rb] + atomicAdd(&cur[rb], rn);
-#pragma unroll
-                                for (int q = 0; q < kMaxFast; ++q) {
-                                    if (q >= rp0 && q < p && (uint32_t)q < u) {
-                                        base[q] = pos;
-                                        pos += u - q;
-                                    }
-                                }
-                            }
-                            if (in) {
-                                rb = b;
-                                rn = 0;
-                                rp0 = p;
-                            }
-                        }
-                        if (in) rn += u - p;
-                    }
-#pragma unroll
-                    for (int p = 0; p < kMaxFast; ++p) {
-                        if ((uint32_t)p >= u || (m[p] >> g.bw) >= (uint32_t)g.B) continue;
-                        const uint32_t hk = (m[p] & wmask) << g.bbits;
-#pragma unroll
-                        for (int q = p; q < kMaxFast; ++q)
-                            if ((uint32_t)q < u) dst[base[p] + (q - p)] = hk | m[q];
-                    }
+                    code = (M >> 1) << 24 | mn;
+                } else {
+                    gen = true;
                 }
             }
-            if (total) used += total;
-            __syncthreads();  // pass B done with srec, toff and cur
-            for (int b = threadIdx.x; b < g.B; b += kPT) {
-                hist[b] = 0;
-                cur[b] = 0;
-            }
+            const unsigned long long cb = __ballot(code != kEmpty), gb = __ballot(gen);
+            if (code != kEmpty) out[nc + __popcll(cb & lower)] = code;
+            if (gen) out[kCChunk - 1 - (ng + __popcll(gb & lower))] = (uint32_t)(t0 - c_lo + j0);
+            nc += __popcll(cb);
+            ng += __popcll(gb);
         }
-        if (cbuf_n > (uint32_t)kCBuf - kFlushSlack) flush(true);  // srec is free until the next tile
+        wave_sync();  // every lane is done with the slice
     }
-    flush(true);
-    if (threadIdx.x == 0 && used) atomicAdd(P.n_pairs, (unsigned long long)used);
-    // slots of this block past its last super-tile (chunk shorter than nst)
-    for (int s2 = st + threadIdx.x; s2 < P.nst; s2 += kPT) P.st_base[blk * P.nst + s2] = -1;
+    if (lane == 0) {
+        P.n_codes[chunk] = nc;
+        P.n_gen[chunk] = ng;
+    }
     if (bad_order) P.flags[0] = 1;
     if (bad_contig) P.flags[1] = 1;
 }
 
+// ---- general reads -----------------------------------------------------------------
+constexpr int kGW = 256;  // general-kernel threads (4 waves, one chunk each)
+
+// One wave per chunk: every pair (p <= q) of each general read's distinct
+// contigs, as (a << 32 | b), appended to the chunk's pair list.
+__global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ rec, int64_t A, uint32_t N,
+                                                       const uint32_t* __restrict__ codes,
+                                                       const uint32_t* __restrict__ n_gen, int64_t n_chunks,
+                                                       uint64_t* __restrict__ pairs, int64_t pcap,
+                                                       uint32_t* __restrict__ n_pairs, int* __restrict__ flags) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t chunk = (int64_t)blockIdx.x * (kGW / 64) + wave;
+    if (chunk >= n_chunks) return;
+    const uint32_t ng = n_gen[chunk];
+    uint32_t np = 0;
+    uint64_t* out = pairs + chunk * pcap;
+    const int64_t c_lo = chunk * kCChunk;
+    bool full = false;
+    for (uint32_t kb = 0; kb < ng; kb += 64) {
+        const uint32_t k = kb + lane;
+        ReadSet rs;
+        rs.u = 0;
+#pragma unroll
+        for (int t = 0; t < kMaxFast; ++t) rs.keep[t] = false;
+        if (k < ng) {
+            const int64_t s = c_lo + codes[c_lo + kCChunk - 1 - k];
+            const uint32_t rid = rec[s].x;
+            bool v = true;
+#pragma unroll
+            for (int t = 0; t < kMaxFast; ++t) {
+                uint2 r = make_uint2(kEmpty, kEmpty);
+                if (v && s + t < A) r = rec[s + t];
+                v = v && r.x == rid;
+                rs.m[t] = v && r.y < N ? r.y : kEmpty;
+            }
+            sort_dedup(rs);
+        }
+        const uint32_t cnt = rs.u * (rs.u + 1) / 2;
+        uint32_t x = cnt;  // wave inclusive scan of the pair counts
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+        if ((int64_t)np + total > pcap) {
+            full = true;
+            break;
+        }
+        uint64_t* o = out + np + (x - cnt);
+#pragma unroll
+        for (int p = 0; p < kMaxFast; ++p) {
+            if (!rs.keep[p]) continue;
+#pragma unroll
+            for (int q = p; q < kMaxFast; ++q)
+                if (rs.keep[q]) *o++ = ((uint64_t)rs.m[p] << 32) | rs.m[q];
+        }
+        np += total;
+    }
+    if (lane == 0) n_pairs[chunk] = np;
+    if (full && lane == 0) flags[2] = 1;  // the host reruns with room for every pair
+}
+
+// ---- partition: chunk lists -> bucket-major padded runs ---------------------------
+constexpr int kPT = 512;                 // partition threads (several blocks per CU overlap their phases)
+constexpr int kMaxListsPerBlock = 64;    // chunk lists per partition block, at most (a power of 2)
+
+// compact-read codes: u32 (m0 | M << 24) -> u16 (m0_local << 3 | M) per code bucket
+struct CodeStream {
+    using S = uint32_t;
+    using D = uint16_t;
+    static constexpr int kCap = 8192;   // codes per flush (32 KB of LDS)
+    static constexpr int kPad = 8;      // 16 B of u16
+    static constexpr int kMaxNb = kMaxBc;
+    static constexpr D kPadV = 0xFFFF;  // codes are < 2^15
+    __device__ static int nb(const Geo& g) { return g.Bc; }
+    __device__ static uint32_t bucket(S s, const Geo& g) { return (s & 0xFFFFFFu) >> g.bwc; }
+    __device__ static D value(S s, const Geo& g) {
+        return (D)(((s & 0xFFFFFFu) & ((1u << g.bwc) - 1u)) << 3 | (s >> 24));
+    }
+};
+
+// general pairs: u64 (a << 32 | b) -> u32 (a_local << bbits | b) per pair bucket
+struct PairStream {
+    using S = uint64_t;
+    using D = uint32_t;
+    static constexpr int kCap = 4096;
+    static constexpr int kPad = 4;
+    static constexpr int kMaxNb = kMaxB;
+    static constexpr D kPadV = kEmpty;  // pair keys are < 2^31
+    __device__ static int nb(const Geo& g) { return g.B; }
+    __device__ static uint32_t bucket(S s, const Geo& g) { return (uint32_t)(s >> 32) >> g.bw; }
+    __device__ static D value(S s, const Geo& g) {
+        return (((uint32_t)(s >> 32) & ((1u << g.bw) - 1u)) << g.bbits) | (uint32_t)s;
+    }
+};
+
+struct RunDir {
+    int64_t* base;               // per flush: start of its runs in the stream
+    uint32_t* off;               // per flush: nb + 1 run offsets
+    unsigned* n;                 // flushes written
+    int64_t max;                 // directory rows
+    unsigned long long* cursor;  // stream bump allocator
+    int64_t cap;                 // stream capacity
+};
+
+template <class T>
+__global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __restrict__ lists, int64_t list_cap,
+                                                         const uint32_t* __restrict__ list_n, int64_t n_lists,
+                                                         int per_block, Geo g, typename T::D* __restrict__ out,
+                                                         RunDir dir, int* __restrict__ flags) {
+    using S = typename T::S;
+    using D = typename T::D;
+    constexpr int kPer = T::kCap / kPT;  // items per thread per fill
+    __shared__ S buf[T::kCap];
+    __shared__ D sorted[T::kCap + T::kMaxNb * (T::kPad - 1)];
+    __shared__ uint32_t hist[2][T::kMaxNb + 1];  // by fill parity: reset while the other fills
+    __shared__ uint32_t toff[T::kMaxNb + 1];
+    __shared__ uint32_t cur[T::kMaxNb];
+    __shared__ uint32_t lpre[kMaxListsPerBlock + 1];
+    __shared__ int64_t fbase_s;
+    __shared__ unsigned fidx_s;
+    __shared__ int ok_s;
+    const int nb = T::nb(g);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int b = threadIdx.x; b <= nb; b += kPT) hist[0][b] = hist[1][b] = 0;
+
+    // the block's lists as one concatenated range: prefix of their lengths
+    const int64_t l_lo = (int64_t)blockIdx.x * per_block;
+    const int nl = (int)min<int64_t>(per_block, n_lists - l_lo);
+    if (wave == 0) {
+        uint32_t carry = 0;
+        for (int base = 0; base < nl; base += 64) {
+            const uint32_t v = base + lane < nl ? list_n[l_lo + base + lane] : 0u;
+            uint32_t x = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            if (base + lane < nl) lpre[base + lane] = carry + x - v;
+            carry += __shfl(x, 63);
+        }
+        for (int i = nl + lane; i <= kMaxListsPerBlock; i += 64) lpre[i] = carry;  // pad: fixed-step search
+    }
+    __syncthreads();
+    const uint32_t items = lpre[nl];
+    // items [base, base + kCap) of the range into registers (thread t: t + k * kPT)
+    S v[kPer];
+    auto load = [&](uint32_t base) {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t gi = base + threadIdx.x + k * kPT;
+            if (gi < items) {
+                int lo = 0;  // list L: lpre[L] <= gi < lpre[L + 1], fixed steps
+#pragma unroll
+                for (int step = kMaxListsPerBlock / 2; step >= 1; step >>= 1)
+                    if (lpre[lo + step] <= gi) lo += step;
+                v[k] = lists[(l_lo + lo) * list_cap + (gi - lpre[lo])];
+            }
+        }
+    };
+    load(0);
+    int parity = 0;
+    for (uint32_t base = 0; base < items; base += T::kCap, parity ^= 1) {
+        const uint32_t n = min(items - base, (uint32_t)T::kCap);
+        uint32_t* h = hist[parity];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kPT;
+            if (i < n) {
+                buf[i] = v[k];
+                atomicAdd(&h[T::bucket(v[k], g)], 1u);
+            }
+        }
+        load(base + T::kCap);  // the next fill's loads overlap this flush
+        // ---- flush: counting sort of buf by bucket into padded runs ----
+        __syncthreads();
+        for (int b = threadIdx.x; b < nb; b += kPT) cur[b] = 0;
+        if (wave == 0) {
+            uint32_t c2 = 0;
+            for (int b0 = 0; b0 < nb; b0 += 64) {
+                const uint32_t val =
+                    b0 + lane < nb ? (h[b0 + lane] + (T::kPad - 1)) & ~(uint32_t)(T::kPad - 1) : 0u;
+                uint32_t x = val;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(x, d);
+                    if (lane >= d) x += y;
+                }
+                if (b0 + lane < nb) toff[b0 + lane] = c2 + x - val;
+                c2 += __shfl(x, 63);
+            }
+            if (lane == 0) {
+                toff[nb] = c2;
+                const unsigned f = atomicAdd(dir.n, 1u);
+                const unsigned long long at = atomicAdd(dir.cursor, (unsigned long long)c2);
+                const bool ok = (int64_t)f < dir.max && (int64_t)(at + c2) <= dir.cap;
+                if (!ok) flags[3] = 1;  // the host reruns with a larger stream
+                else dir.base[f] = (int64_t)at;
+                fidx_s = f;
+                fbase_s = (int64_t)at;
+                ok_s = ok;
+            }
+        }
+        __syncthreads();
+        const bool ok = ok_s;
+        const uint32_t total = toff[nb];
+        if (ok) {
+            const unsigned f = fidx_s;
+            for (int b = threadIdx.x; b <= nb; b += kPT) dir.off[(int64_t)f * (nb + 1) + b] = toff[b];
+            for (int b = threadIdx.x; b < nb; b += kPT)
+                for (uint32_t i = toff[b] + h[b]; i < toff[b + 1]; ++i) sorted[i] = T::kPadV;
+            for (uint32_t i = threadIdx.x; i < n; i += kPT) {
+                const S x = buf[i];
+                const uint32_t b = T::bucket(x, g);
+                sorted[toff[b] + atomicAdd(&cur[b], 1u)] = T::value(x, g);
+            }
+        }
+        __syncthreads();
+        // buf, h and cur are free: the next fill may start once this block's
+        // 16-byte stores are issued (their completion is never waited for)
+        for (int b = threadIdx.x; b < nb; b += kPT) h[b] = 0;
+        if (ok) {
+            u32x4* dst = reinterpret_cast<u32x4*>(out + fbase_s);
+            const u32x4* src = reinterpret_cast<const u32x4*>(sorted);
+            const uint32_t nv = total * (uint32_t)sizeof(D) / 16u;
+            for (uint32_t i = threadIdx.x; i < nv; i += kPT) dst[i] = src[i];
+        }
+    }
+}
+
 // ---- run streams ------------------------------------------------------------------
-// A reduce block reads the runs of one bucket from a range of slots (super-tiles
-// or flushes).  Each wave takes batches of 64 runs (lane i holds run i) and
-// reads them as one stream of T entries, 64 consecutive entries per load; the
-// runs a window of 64 overlaps are found with wave-uniform (scalar) loops over
-// the lanes' run table, and kWin windows are in flight before they are counted.
+// A reduce block reads the runs of one bucket from a range of flushes.  Each
+// wave takes batches of 64 runs (lane i holds run i) and reads them as one
+// stream of 16-byte vectors, 64 consecutive vectors per load; the runs a
+// window of 64 overlaps are found with wave-uniform (scalar) loops over the
+// lanes' run table, and kWin windows are in flight before they are counted.
 constexpr int kWin = 16;
 
-template <typename T, typename Bounds, typename Count>
-__device__ __forceinline__ void stream_runs(const T* __restrict__ data, int64_t r_lo, int64_t r_hi, int threads,
+template <typename Bounds, typename Count>
+__device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int64_t r_lo, int64_t r_hi, int threads,
                                             Bounds bounds, Count count, bool* stop) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int64_t r0 = r_lo + (int64_t)wave * 64; r0 - (int64_t)wave * 64 < r_hi; r0 += (int64_t)threads) {
@@ -490,11 +502,11 @@ __device__ __forceinline__ void stream_runs(const T* __restrict__ data, int64_t 
             if (lane >= d) incl += y;
         }
         const uint32_t excl = incl - len;
-        const int64_t roff = beg - (int64_t)excl;  // element j of run r: data[roff + j]
+        const int64_t roff = beg - (int64_t)excl;  // vector j of run r: data[roff + j]
         const uint32_t Tn = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         int rlo = 0;
         for (uint32_t j0 = 0; j0 < Tn; j0 += 64u * kWin) {
-            T e[kWin];
+            u32x4 e[kWin];
 #pragma unroll
             for (int u = 0; u < kWin; ++u) {
                 const uint32_t w0 = j0 + 64u * u, j = w0 + lane;
@@ -517,32 +529,38 @@ __device__ __forceinline__ void stream_runs(const T* __restrict__ data, int64_t 
     }
 }
 
+// flushes [f_lo, f_hi) of group `grp` when n_flush (device) is split into n_groups
+__device__ __forceinline__ void group_range(const unsigned* n_flush, int n_groups, int grp, int64_t* f_lo,
+                                            int64_t* f_hi) {
+    const int64_t nf = *n_flush;
+    const int64_t per = (nf + n_groups - 1) / n_groups;
+    *f_lo = min(nf, grp * per);
+    *f_hi = min(nf, *f_lo + per);
+}
+
 // ---- code reduce --------------------------------------------------------------------
 constexpr int kCRT = 1024;
 constexpr int kHistMax = 1 << (kMaxBwCompact + 2 + 3);  // 32768 counters (128 KB)
 
 // One block per (code bucket, group of flushes): histogram of (m0_local, M).
-__global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __restrict__ cent,
-                                                           const int64_t* __restrict__ cf_base,
-                                                           const uint32_t* __restrict__ cf_off, int64_t n_flush,
-                                                           int Bc, int bwc, int n_cg, int64_t per_group,
-                                                           uint32_t* __restrict__ part_ch) {
+__global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __restrict__ cent, RunDir dir, int Bc,
+                                                           int bwc, int n_cg, uint32_t* __restrict__ part_ch) {
     __shared__ uint32_t h[kHistMax];
     const int bucket = blockIdx.x / n_cg, grp = blockIdx.x % n_cg;
     const int hn = 1 << (bwc + 3);
     for (int i = threadIdx.x; i < hn; i += kCRT) h[i] = 0;
     __syncthreads();
-    const int64_t f_lo = (int64_t)grp * per_group, f_hi = min(n_flush, f_lo + per_group);
+    int64_t f_lo, f_hi;
+    group_range(dir.n, n_cg, grp, &f_lo, &f_hi);
     bool stop = false;
-    // runs are 16-byte aligned and padded: stream them as vectors of 8 codes
     auto add = [&](uint32_t c) {
-        if (c != kPadCode) __hip_atomic_fetch_add(&h[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (c != CodeStream::kPadV) __hip_atomic_fetch_add(&h[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     stream_runs(
         reinterpret_cast<const u32x4*>(cent), f_lo, f_hi, kCRT,
         [&](int64_t f, int64_t* beg, uint32_t* len) {
-            const uint32_t* o = cf_off + f * (Bc + 1) + bucket;
-            *beg = (cf_base[f] + o[0]) >> 3;
+            const uint32_t* o = dir.off + f * (Bc + 1) + bucket;
+            *beg = (dir.base[f] + o[0]) >> 3;
             *len = (o[1] - o[0]) >> 3;
         },
         [&](const u32x4 v) {
@@ -560,7 +578,6 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
 //   band   dense counters band[a_local * D + (b - a)] for b - a < D = 2^dbits
 //   hash   open addressing (key = a_local << bbits | b) for the other pairs.
 constexpr int kRT = 1024;               // pair-reduce threads (16 waves)
-constexpr int kGroup = 4096;            // super-tile slots per pair-reduce block
 constexpr int kBand = 8192;             // band counters per bucket (32 KB)
 constexpr int kHashR = 4096;            // hash slots per pair-reduce block
 constexpr int kHashF = 8192;            // hash slots per final (per-bucket) block
@@ -624,43 +641,52 @@ struct HTab {
     }
 };
 
-// One block per (pair bucket, group of kGroup super-tile slots).  Output: the
-// group's dense band counters and its compacted hash list.
-__global__ void __launch_bounds__(kRT) pair_reduce_kernel(
-    const uint32_t* __restrict__ ent, const int64_t* __restrict__ st_base, const uint32_t* __restrict__ st_off,
-    int64_t n_slots, int n_groups, int bw, int bbits, int dbits, uint32_t* __restrict__ part_band,
-    uint32_t* __restrict__ part_keys, uint32_t* __restrict__ part_cnt, int* __restrict__ part_n,
-    uint8_t* __restrict__ overflow) {
+// One block per (pair bucket, group of flushes).  Output: the group's dense
+// band counters and its compacted hash list (part_n = -1: no flush in group).
+__global__ void __launch_bounds__(kRT) pair_reduce_kernel(const uint32_t* __restrict__ pent, RunDir dir,
+                                                          int n_pg, int bw, int bbits, int dbits, int B,
+                                                          uint32_t* __restrict__ part_band,
+                                                          uint32_t* __restrict__ part_keys,
+                                                          uint32_t* __restrict__ part_cnt, int* __restrict__ part_n,
+                                                          uint8_t* __restrict__ overflow) {
     __shared__ uint32_t band[kBand];
     __shared__ uint32_t hkeys[kHashR];
     __shared__ uint32_t hvals[kHashR];
     __shared__ int nuniq, cnt, ovf;
     HTab<kHashR, kRT> t{hkeys, hvals, &nuniq};
-    const int bucket = blockIdx.x / n_groups, grp = blockIdx.x % n_groups;
+    const int bucket = blockIdx.x / n_pg, grp = blockIdx.x % n_pg;
     const int band_n = dbits >= 0 ? (1 << (bw + dbits)) : 0;
     const uint32_t D = dbits >= 0 ? (1u << dbits) : 0u;
+    int64_t f_lo, f_hi;
+    group_range(dir.n, n_pg, grp, &f_lo, &f_hi);
+    const int64_t sl = blockIdx.x;
+    if (f_lo >= f_hi) {  // no pairs in this group (uniform)
+        if (threadIdx.x == 0) part_n[sl] = -1;
+        return;
+    }
     t.init();
     for (int i = threadIdx.x; i < band_n; i += kRT) band[i] = 0;
     if (threadIdx.x == 0) ovf = 0;
     __syncthreads();
-    const int64_t s_lo = (int64_t)grp * kGroup, s_hi = min(n_slots, s_lo + kGroup);
     const uint32_t bmask = (1u << bbits) - 1u, abase = (uint32_t)bucket << bw;
     bool full = false;
+    auto add = [&](uint32_t e) {
+        if (e == kEmpty) return;
+        const uint32_t al = e >> bbits, d = (e & bmask) - (abase + al);
+        if (d < D)
+            __hip_atomic_fetch_add(&band[(al << dbits) | d], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+            full |= !t.insert(e, 1u);
+    };
     stream_runs(
-        ent, s_lo, s_hi, kRT,
-        [&](int64_t r, int64_t* beg, uint32_t* len) {
-            const int64_t sb = st_base[r];
-            if (sb < 0) return;
-            const uint32_t o0 = st_off[(int64_t)bucket * n_slots + r], o1 = st_off[(int64_t)(bucket + 1) * n_slots + r];
-            *beg = sb + o0;
-            *len = o1 - o0;
+        reinterpret_cast<const u32x4*>(pent), f_lo, f_hi, kRT,
+        [&](int64_t f, int64_t* beg, uint32_t* len) {
+            const uint32_t* o = dir.off + f * (B + 1) + bucket;
+            *beg = (dir.base[f] + o[0]) >> 2;
+            *len = (o[1] - o[0]) >> 2;
         },
-        [&](const uint32_t e) {
-            const uint32_t al = e >> bbits, d = (e & bmask) - (abase + al);
-            if (d < D)
-                __hip_atomic_fetch_add(&band[(al << dbits) | d], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-                full |= !t.insert(e, 1u);
+        [&](const u32x4 v) {
+            add(v.x), add(v.y), add(v.z), add(v.w);
             if (nuniq > kHashR - kHashR / 8) full = true;  // early out: the bucket goes generic
         },
         &full);
@@ -670,7 +696,6 @@ __global__ void __launch_bounds__(kRT) pair_reduce_kernel(
         if (threadIdx.x == 0) overflow[bucket] = 1;
         return;
     }
-    const int64_t sl = blockIdx.x;
     uint32_t* pb = part_band + sl * (int64_t)kBand;
     for (int i = threadIdx.x; i < band_n; i += kRT) pb[i] = band[i];
     const int n = t.compact(&cnt);
@@ -684,8 +709,7 @@ __global__ void __launch_bounds__(kRT) pair_reduce_kernel(
 }
 
 // Summed code histogram entry gi = (m0 << 3 | M), m0 a global contig index.
-__device__ __forceinline__ uint32_t code_count(const uint32_t* __restrict__ part_ch, int n_cg, int bw, int bwc,
-                                               int gi) {
+__device__ __forceinline__ uint32_t code_count(const uint32_t* __restrict__ part_ch, int n_cg, int bwc, int gi) {
     const int bc = gi >> (bwc + 3), i = gi & ((8 << bwc) - 1);
     const int hn = 8 << bwc;
     uint32_t k = 0;
@@ -699,7 +723,7 @@ __device__ __forceinline__ uint32_t code_count(const uint32_t* __restrict__ part
 // position is its rank in its own sorted list plus the number of smaller keys
 // in the other one.
 __global__ void __launch_bounds__(kFT) final_kernel(
-    int n_groups, int n_cg, int bw, int bbits, int dbits, int bwc, const uint32_t* __restrict__ part_band,
+    int n_pg, int n_cg, int bw, int bbits, int dbits, int bwc, const uint32_t* __restrict__ part_band,
     const uint32_t* __restrict__ part_ch, const uint32_t* __restrict__ part_keys,
     const uint32_t* __restrict__ part_cnt, const int* __restrict__ part_n, uint64_t* __restrict__ out_keys,
     int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n, uint8_t* __restrict__ overflow) {
@@ -716,7 +740,10 @@ __global__ void __launch_bounds__(kFT) final_kernel(
     t.init();
     for (int i = threadIdx.x; i < band_n; i += kFT) {
         uint32_t v = 0;
-        for (int gi = 0; gi < n_groups; ++gi) v += part_band[((int64_t)bucket * n_groups + gi) * kBand + i];
+        for (int gi = 0; gi < n_pg; ++gi) {
+            const int64_t sl = (int64_t)bucket * n_pg + gi;
+            if (part_n[sl] >= 0) v += part_band[sl * kBand + i];
+        }
         bsum[i] = v;
     }
     __syncthreads();
@@ -726,7 +753,7 @@ __global__ void __launch_bounds__(kFT) final_kernel(
     if (n_cg > 0) {
         const int first = bucket > 0 ? -24 : 0;  // 3 contigs x 8 codes before the bucket
         for (int i = first + (int)threadIdx.x; i < (8 << bw); i += kFT) {
-            const uint32_t k = code_count(part_ch, n_cg, bw, bwc, (bucket << (bw + 3)) + i);
+            const uint32_t k = code_count(part_ch, n_cg, bwc, (bucket << (bw + 3)) + i);
             if (!k) continue;
             const int m0l = i >> 3;  // may be -3..-1
             const uint32_t bits = 1u | ((uint32_t)i & 7u) << 1;
@@ -740,8 +767,8 @@ __global__ void __launch_bounds__(kFT) final_kernel(
         }
         __syncthreads();
     }
-    for (int gi = 0; gi < n_groups; ++gi) {
-        const int64_t sl = (int64_t)bucket * n_groups + gi;
+    for (int gi = 0; gi < n_pg; ++gi) {
+        const int64_t sl = (int64_t)bucket * n_pg + gi;
         const int n = part_n[sl];
         bool full = false;
         for (int i = threadIdx.x; i < n; i += kFT)
@@ -813,13 +840,15 @@ __global__ void __launch_bounds__(kFT) final_kernel(
 }
 
 // ---- overflow fallback: every pair of one bucket as (key, count), generic sort ----
-__global__ void bucket_widen_kernel(const uint32_t* __restrict__ ent, const int64_t* __restrict__ st_base,
-                                    const uint32_t* __restrict__ st_off, int64_t n_slots, int bucket, int bw,
+// Thread t handles pair-stream flush t (this bucket's run) and compact-read
+// code t of the bucket (codes with m0 in [start - 3, end)).
+__global__ void bucket_widen_kernel(const uint32_t* __restrict__ pent, RunDir dir, int B, int bucket, int bw,
                                     int bbits, const uint32_t* __restrict__ part_ch, int n_cg, int bwc,
                                     uint64_t* __restrict__ out_k, int64_t* __restrict__ out_c,
                                     unsigned long long* __restrict__ n_out, int count_only) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t abase = (uint64_t)bucket << bw;
+    const int64_t n_fl = *dir.n;
     unsigned long long n = 0, at = 0;
     for (int pass = count_only ? 1 : 0; pass < 2; ++pass) {
         // pass 0 counts this thread's pairs, pass 1 emits (or only counts)
@@ -836,17 +865,17 @@ __global__ void bucket_widen_kernel(const uint32_t* __restrict__ ent, const int6
             if (!n) return;
             at = atomicAdd(n_out, n);
         }
-        if (t < n_slots && st_base[t] >= 0) {  // pair entries of slot t
-            const int64_t beg = st_base[t] + st_off[(int64_t)bucket * n_slots + t];
-            const uint32_t len = st_off[(int64_t)(bucket + 1) * n_slots + t] - st_off[(int64_t)bucket * n_slots + t];
-            for (uint32_t i = 0; i < len; ++i) {
-                const uint32_t k = ent[beg + i];
-                emit(((abase + (k >> bbits)) << 32) | (k & ((1u << bbits) - 1u)), 1);
+        if (t < n_fl) {  // pair entries of flush t
+            const uint32_t* o = dir.off + t * (B + 1) + bucket;
+            const int64_t beg = dir.base[t] + o[0];
+            for (uint32_t i = 0; i < o[1] - o[0]; ++i) {
+                const uint32_t k = pent[beg + i];
+                if (k != kEmpty) emit(((abase + (k >> bbits)) << 32) | (k & ((1u << bbits) - 1u)), 1);
             }
         }
         const int64_t ci = t - (bucket > 0 ? 24 : 0);  // code index relative to the bucket start
-        if (n_cg > 0 && t < (8 << bw) + (bucket > 0 ? 24 : 0)) {  // compact reads with m0 = start + (ci >> 3)
-            const uint32_t k = code_count(part_ch, n_cg, bw, bwc, (int)((int64_t)(bucket << (bw + 3)) + ci));
+        if (n_cg > 0 && t < (8 << bw) + (bucket > 0 ? 24 : 0)) {
+            const uint32_t k = code_count(part_ch, n_cg, bwc, (int)((int64_t)(bucket << (bw + 3)) + ci));
             if (k) {
                 const int64_t m0 = (int64_t)abase + (ci >> 3);
                 const uint32_t bits = 1u | ((uint32_t)ci & 7u) << 1;
@@ -914,6 +943,8 @@ int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
     return KARMA_OK;
 }
 
+constexpr int kListsPerBlock = 32;  // chunk lists per partition block (<= kMaxListsPerBlock)
+
 }  // namespace
 
 namespace karma {
@@ -923,104 +954,115 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     Geo g;
     KARMA_TRY(make_geo(N, &g));
     const int B = g.B;
-    const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(kMaxPartBlocks, ceil_div(A, kSuperTile)));
-    const int64_t chunk = ceil_div(ceil_div(std::max<int64_t>(A, 1), nblk), kSuperTile) * kSuperTile;
-    const int64_t nb = std::max<int64_t>(1, ceil_div(A, chunk));
-    const int nst = (int)(chunk / kSuperTile);
-    const int64_t n_slots = nb * nst;
-    // <= 2 flushes per super-tile (before pass A when a tile of short reads would
-    // not fit, and at its end) + the last; codes <= reads <= records, plus < 8
-    // codes of padding per run of a flush
-    const int64_t max_flush = nb * (2 * nst + 1);
-    const int64_t code_region = chunk + (int64_t)(2 * nst + 1) * 8 * g.Bc;
-    DevArray<int64_t> st_base, big_list, cf_base;
-    DevArray<uint32_t> st_off, ent, cf_off;
-    DevArray<uint16_t> cent;
+    const int64_t n_chunks = std::max<int64_t>(1, ceil_div(A, kCChunk));
+    const int64_t n_pblk = ceil_div(n_chunks, kListsPerBlock);
+    // per-step scratch
+    DevArray<uint32_t> codes, n_codes, n_gen, n_pl;
+    DevArray<int64_t> big_list;
     DevArray<int> flags;
-    DevArray<unsigned> counters;  // 0 big reads, 1 flushes
-    DevArray<unsigned long long> n_pairs;
-    KARMA_TRY(st_base.alloc(ctx, n_slots));
-    KARMA_TRY(st_off.alloc(ctx, (int64_t)(B + 1) * n_slots));
-    KARMA_TRY(flags.alloc(ctx, 4));
-    KARMA_TRY(counters.alloc(ctx, 2));
-    KARMA_TRY(n_pairs.alloc(ctx, 1));
+    DevArray<unsigned> counters;           // 0 big reads, 1 code flushes, 2 pair flushes
+    DevArray<unsigned long long> cursors;  // 0 code stream, 1 pair stream
+    KARMA_TRY(codes.alloc(ctx, n_chunks * kCChunk));
+    KARMA_TRY(n_codes.alloc(ctx, n_chunks));
+    KARMA_TRY(n_gen.alloc(ctx, n_chunks));
+    KARMA_TRY(n_pl.alloc(ctx, n_chunks));
     KARMA_TRY(big_list.alloc(ctx, A / (kMaxFast + 1) + 1));
+    KARMA_TRY(flags.alloc(ctx, 4));
+    KARMA_TRY(counters.alloc(ctx, 3));
+    KARMA_TRY(cursors.alloc(ctx, 2));
+    // code stream: <= one code per record + < 8 padding codes per run; a block
+    // flushes only a full buffer, and once at its end
+    const int64_t max_cflush = n_pblk + ceil_div(A, CodeStream::kCap) + 1;
+    const int64_t ccap = A + max_cflush * 8 * (int64_t)std::max(g.Bc, 1);
+    DevArray<uint16_t> cent;
+    DevArray<int64_t> cf_base;
+    DevArray<uint32_t> cf_off;
     if (g.Bc > 0) {
-        KARMA_TRY(cent.alloc(ctx, nb * code_region));
-        KARMA_TRY(cf_base.alloc(ctx, max_flush));
-        KARMA_TRY(cf_off.alloc(ctx, max_flush * (g.Bc + 1)));
+        KARMA_TRY(cent.alloc(ctx, ccap + 16));
+        KARMA_TRY(cf_base.alloc(ctx, max_cflush));
+        KARMA_TRY(cf_off.alloc(ctx, max_cflush * (g.Bc + 1)));
     }
-    // Each block owns a region of the pair array.  Pairs (incl. the diagonal)
-    // of general reads with <= 8 records are <= 4.5 per record; start at 1.5
-    // per record and rerun once with the bound.
-    int64_t region = chunk * 3 / 2 + 4;
-    unsigned hc[2] = {0, 0};
-    unsigned long long h_pairs = 0;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        KARMA_TRY(ent.alloc(ctx, nb * region + 8));
-        KARMA_HIP(hipMemsetAsync(flags.ptr, 0, 16, ctx->stream));
-        KARMA_HIP(hipMemsetAsync(counters.ptr, 0, 8, ctx->stream));
-        KARMA_HIP(hipMemsetAsync(n_pairs.ptr, 0, 8, ctx->stream));
-        if (A > 0) {
-            PartArgs P{rec, A, chunk, nst, g, (uint32_t)N, ent.ptr, region, n_slots, st_base.ptr, st_off.ptr,
-                       cent.ptr, code_region, cf_base.ptr, cf_off.ptr, counters.ptr + 1, max_flush, flags.ptr, big_list.ptr,
-                       counters.ptr, n_pairs.ptr};
-            KARMA_LAUNCH(ctx, "graph_partition", partition_kernel, nb, kPT, 0, P);
-        } else {
-            KARMA_HIP(hipMemsetAsync(st_base.ptr, 0xFF, n_slots * 8, ctx->stream));
-        }
-        int hf[4];
-        KARMA_HIP(hipMemcpyAsync(hf, flags.ptr, 16, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipMemcpyAsync(hc, counters.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipMemcpyAsync(&h_pairs, n_pairs.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipStreamSynchronize(ctx->stream));
-        KARMA_CHECK(!hf[0], KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
-        KARMA_CHECK(!hf[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
-        KARMA_CHECK(!hf[3], KARMA_ERR_STATE, "code flush directory full");
-        if (!hf[2]) break;
-        KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "entry region capacity exceeded twice");
-        region = chunk * 9 / 2 + 4;
-    }
-    const unsigned n_big = hc[0];
-    const int64_t n_flush = hc[1];
-    // code reduce: per (code bucket, group of flushes)
-    int n_cg = 0;
-    int64_t per_group = 1;
-    DevArray<uint32_t> part_ch;
-    if (g.Bc > 0 && n_flush > 0) {
-        n_cg = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(512, g.Bc), ceil_div(n_flush, 32)));
-        per_group = ceil_div(n_flush, n_cg);
-        n_cg = (int)ceil_div(n_flush, per_group);
-        KARMA_TRY(part_ch.alloc(ctx, (int64_t)g.Bc * n_cg * (int64_t(8) << g.bwc)));
-        KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr,
-                     cf_base.ptr, cf_off.ptr, n_flush, g.Bc, g.bwc, n_cg, per_group, part_ch.ptr);
-    }
-    // pair reduce: per (pair bucket, group of super-tile slots), then per bucket
-    const int n_groups = h_pairs ? (int)std::max<int64_t>(1, ceil_div(n_slots, kGroup)) : 0;
-    const int64_t nsl = (int64_t)B * n_groups;
-    DevArray<uint64_t> slot_k;
-    DevArray<int64_t> slot_c, n_per;
-    DevArray<uint8_t> ovf;
-    DevArray<uint32_t> part_b, part_k, part_c;
+    // pair lists: general reads' pairs per chunk; start with room for 1/8 pair
+    // per record and rerun with the bound (4.5 per record) when short
+    int64_t pcap = kCChunk / 8;
+    DevArray<uint64_t> plist;
+    DevArray<uint32_t> pent, pf_off;
+    DevArray<int64_t> pf_base;
+    unsigned hc[3] = {0, 0, 0};
+    int hf[4] = {0, 0, 0, 0};
+    // reduce geometry: grids fixed here, flush ranges from device counters
+    const int n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, ceil_div(512, g.Bc)) : 0;
+    const int n_pg = (int)std::max<int64_t>(1, ceil_div(256, B));
+    const int64_t nsl = (int64_t)B * n_pg;
+    DevArray<uint32_t> part_ch, part_b, part_k, part_c;
     DevArray<int> part_n;
-    KARMA_TRY(slot_k.alloc(ctx, (int64_t)B * kSlotCap));
-    KARMA_TRY(slot_c.alloc(ctx, (int64_t)B * kSlotCap));
-    KARMA_TRY(n_per.alloc(ctx, B + 1));
-    KARMA_TRY(ovf.alloc(ctx, B));
-    KARMA_TRY(part_b.alloc(ctx, std::max<int64_t>(nsl, 1) * (int64_t)kBand));
+    DevArray<uint64_t> slot_k;
+    DevArray<int64_t> slot_c, n_per, dst;
+    DevArray<uint8_t> ovf;
+    if (n_cg) KARMA_TRY(part_ch.alloc(ctx, (int64_t)g.Bc * n_cg * (int64_t(8) << g.bwc)));
+    KARMA_TRY(part_b.alloc(ctx, nsl * (int64_t)kBand));
     KARMA_TRY(part_k.alloc(ctx, nsl * (int64_t)kHashR));
     KARMA_TRY(part_c.alloc(ctx, nsl * (int64_t)kHashR));
     KARMA_TRY(part_n.alloc(ctx, nsl));
-    KARMA_HIP(hipMemsetAsync(ovf.ptr, 0, B, ctx->stream));
-    KARMA_HIP(hipMemsetAsync(n_per.ptr, 0, (B + 1) * 8, ctx->stream));
-    if (nsl) KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, ent.ptr, st_base.ptr, st_off.ptr,
-                 n_slots, n_groups, g.bw, g.bbits, g.dbits, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf.ptr);
-    KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel, B, kFT, 0, n_groups, n_cg, g.bw, g.bbits, g.dbits, g.bwc,
-                 part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per.ptr,
-                 ovf.ptr);
+    KARMA_TRY(slot_k.alloc(ctx, (int64_t)B * kSlotCap));
+    KARMA_TRY(slot_c.alloc(ctx, (int64_t)B * kSlotCap));
+    KARMA_TRY(n_per.alloc(ctx, B + 1));
+    KARMA_TRY(dst.alloc(ctx, B + 1));
+    KARMA_TRY(ovf.alloc(ctx, B));
+    RunDir pdir{};
     std::vector<uint8_t> hovf(B);
-    KARMA_HIP(hipMemcpyAsync(hovf.data(), ovf.ptr, B, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    int64_t U = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        const int64_t max_pflush = n_pblk + ceil_div(n_chunks * pcap, PairStream::kCap) + 1;
+        const int64_t pscap = n_chunks * pcap + max_pflush * 4 * (int64_t)B;
+        KARMA_TRY(plist.alloc(ctx, n_chunks * pcap));
+        KARMA_TRY(pent.alloc(ctx, pscap + 8));
+        KARMA_TRY(pf_base.alloc(ctx, max_pflush));
+        KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
+        KARMA_HIP(hipMemsetAsync(flags.ptr, 0, 16, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(counters.ptr, 0, 12, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(cursors.ptr, 0, 16, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(ovf.ptr, 0, B, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(n_per.ptr, 0, (B + 1) * 8, ctx->stream));
+        if (A > 0) {
+            ClassArgs C{rec, A, (uint32_t)N, g.Bc > 0, codes.ptr, n_codes.ptr, n_gen.ptr, big_list.ptr, counters.ptr,
+                        flags.ptr};
+            KARMA_LAUNCH(ctx, "graph_classify", classify_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+        } else {
+            KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
+            KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
+        }
+        KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
+                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, flags.ptr);
+        const RunDir cdir{cf_base.ptr, cf_off.ptr, counters.ptr + 1, max_cflush, cursors.ptr, ccap};
+        pdir = RunDir{pf_base.ptr, pf_off.ptr, counters.ptr + 2, max_pflush, cursors.ptr + 1, pscap};
+        if (g.Bc > 0) {
+            KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr,
+                         kCChunk, n_codes.ptr, n_chunks, kListsPerBlock, g, cent.ptr, cdir, flags.ptr);
+            KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
+                         g.Bc, g.bwc, n_cg, part_ch.ptr);
+        }
+        KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
+                     n_pl.ptr, n_chunks, kListsPerBlock, g, pent.ptr, pdir, flags.ptr);
+        KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
+                     g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf.ptr);
+        KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits, g.bwc,
+                     part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per.ptr,
+                     ovf.ptr);
+        KARMA_TRY(scan_excl_i64(ctx, n_per.ptr, dst.ptr, B + 1));
+        // the one synchronisation of the common path
+        KARMA_HIP(hipMemcpyAsync(hf, flags.ptr, 16, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(hc, counters.ptr, 12, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(hovf.data(), ovf.ptr, B, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(&U, dst.ptr + B, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        KARMA_CHECK(!hf[0], KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
+        KARMA_CHECK(!hf[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
+        if (!hf[2] && !hf[3]) break;
+        KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "pair list or run stream capacity exceeded twice");
+        pcap = kCChunk * 9 / 2;  // every read with <= 8 records fits
+    }
+    const unsigned n_big = hc[0];
     DevArray<const uint64_t*> pk;
     DevArray<const int64_t*> pc;
     KARMA_TRY(pk.alloc(ctx, B));
@@ -1029,16 +1071,17 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
                  (int64_t)kSlotCap, pk.ptr, pc.ptr);
     std::vector<std::unique_ptr<DevArray<uint64_t>>> keep_k;
     std::vector<std::unique_ptr<DevArray<int64_t>>> keep_c;
-    const int64_t widen_threads = std::max<int64_t>(n_slots, (int64_t(8) << g.bw) + 24);
+    const int64_t widen_threads = std::max<int64_t>(hc[2], (int64_t(8) << g.bw) + 24);
+    bool any_ovf = false;
     for (int b = 0; b < B; ++b) {
         if (!hovf[b]) continue;
+        any_ovf = true;
         // generic path for a bucket whose distinct pairs exceed the LDS tables
         DevArray<unsigned long long> np;
         KARMA_TRY(np.alloc(ctx, 1));
         KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
-        KARMA_LAUNCH(ctx, "bucket_widen", bucket_widen_kernel, grid_n(widen_threads, 64), 64, 0, ent.ptr,
-                     st_base.ptr, st_off.ptr, n_slots, b, g.bw, g.bbits, part_ch.ptr, n_cg, g.bwc,
-                     (uint64_t*)nullptr, (int64_t*)nullptr, np.ptr, 1);
+        KARMA_LAUNCH(ctx, "bucket_widen", bucket_widen_kernel, grid_n(widen_threads, 64), 64, 0, pent.ptr, pdir, B,
+                     b, g.bw, g.bbits, part_ch.ptr, n_cg, g.bwc, (uint64_t*)nullptr, (int64_t*)nullptr, np.ptr, 1);
         unsigned long long hp = 0;
         KARMA_HIP(hipMemcpyAsync(&hp, np.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
@@ -1047,9 +1090,8 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         KARMA_TRY(wide.alloc(ctx, hp));
         KARMA_TRY(wc.alloc(ctx, hp));
         KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
-        KARMA_LAUNCH(ctx, "bucket_widen", bucket_widen_kernel, grid_n(widen_threads, 64), 64, 0, ent.ptr,
-                     st_base.ptr, st_off.ptr, n_slots, b, g.bw, g.bbits, part_ch.ptr, n_cg, g.bwc, wide.ptr, wc.ptr,
-                     np.ptr, 0);
+        KARMA_LAUNCH(ctx, "bucket_widen", bucket_widen_kernel, grid_n(widen_threads, 64), 64, 0, pent.ptr, pdir, B,
+                     b, g.bw, g.bbits, part_ch.ptr, n_cg, g.bwc, wide.ptr, wc.ptr, np.ptr, 0);
         keep_k.emplace_back(new DevArray<uint64_t>());
         keep_c.emplace_back(new DevArray<int64_t>());
         int64_t nu = 0;
@@ -1062,12 +1104,11 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         KARMA_HIP(hipMemcpyAsync(n_per.ptr + b, &nu, 8, hipMemcpyHostToDevice, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
     }
-    DevArray<int64_t> dst;
-    KARMA_TRY(dst.alloc(ctx, B + 1));
-    KARMA_TRY(scan_excl_i64(ctx, n_per.ptr, dst.ptr, B + 1));
-    int64_t U = 0;
-    KARMA_HIP(hipMemcpyAsync(&U, dst.ptr + B, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    if (any_ovf) {
+        KARMA_TRY(scan_excl_i64(ctx, n_per.ptr, dst.ptr, B + 1));
+        KARMA_HIP(hipMemcpyAsync(&U, dst.ptr + B, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    }
     DevArray<uint64_t> mk;
     DevArray<int64_t> mc;
     const bool merge_big = n_big > 0;
