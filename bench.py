@@ -98,25 +98,37 @@ def main():
     def step(keep=False):
         return build.run(store, rec_dev.data_ptr(), A, keep=keep)
 
+    ctxs = build.contexts()  # main context (+ the concurrent graph build's)
+
+    def sync_all():
+        for c in ctxs:
+            c.sync()
+
     for _ in range(args.warmup):
         step()
-    ctx.sync()
+    sync_all()
     if not args.no_timing:
-        ctx.timing(True)
-        ctx.timing_reset()
+        for c in ctxs:
+            c.timing(True)
+            c.timing_reset()
     comm.barrier()
     torch.cuda.synchronize()
-    ctx.sync()
+    sync_all()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
-    ctx.sync()
+    sync_all()
     torch.cuda.synchronize()
     comm.barrier()
     t1 = time.perf_counter()
     dt = comm.max_float(t1 - t0)
-    kern = ctx.timing_read() if not args.no_timing else {}
-    ctx.timing(False)
+    kern = {}
+    if not args.no_timing:
+        for c in ctxs:
+            for name, (ms, nl) in c.timing_read().items():
+                prev = kern.get(name, (0.0, 0))
+                kern[name] = (prev[0] + ms, prev[1] + nl)
+            c.timing(False)
     n_reads = int(np.count_nonzero(rec[1:, 0] != rec[:-1, 0])) + 1 if A else 0
 
     units = world * (n_loc + f_loc) * args.steps
@@ -127,8 +139,10 @@ def main():
     per_kernel_bytes = {
         "kmer_profile": packed_bytes + 8 * n_loc * M,
         "kmer_presence": packed_bytes,
-        # records read once + one 2-byte code written per read (compact reads)
-        "graph_partition": 8 * A + 2 * n_reads,
+        # records read once, one 4-byte code per (compact) read written
+        "graph_classify": 8 * A + 4 * n_reads,
+        # codes read, 2-byte bucket-local codes written
+        "graph_code_partition": 6 * n_reads,
         "graph_code_reduce": 2 * n_reads,
     }
     roof = None

@@ -129,6 +129,10 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
 int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, int64_t n, int is_device,
                       karma_pairs** out);
 int karma_pairs_destroy(karma_pairs* p);
+/* Later kernels on p run on ctx's stream (after p's current stream is drained);
+ * p's memory stays with the allocator that made it.  Lets a list built on a
+ * second context (concurrent graph build) join the main stream's exchange. */
+int karma_pairs_rebind(karma_pairs* p, karma_ctx* ctx);
 int karma_pairs_count(karma_pairs* p, int64_t* n);
 /* Device pointers of the list (valid until destroy): keys u64[n], counts i64[n]. */
 int karma_pairs_device(karma_pairs* p, const uint64_t** keys, const int64_t** counts);

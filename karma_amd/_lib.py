@@ -70,6 +70,7 @@ _SIGS = {
     "karma_graph_eq": [_c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i64, _i32, _PP],
     "karma_pairs_merge": [_c_p, _c_p, _c_p, _i64, _i32, _PP],
     "karma_pairs_destroy": [_c_p],
+    "karma_pairs_rebind": [_c_p, _c_p],
     "karma_pairs_count": [_c_p, _I64P],
     "karma_pairs_device": [_c_p, _PP, _PP],
     "karma_pairs_get": [_c_p, _c_p, _c_p, _c_p, _i32],

@@ -1,4 +1,5 @@
 // core.hip — context, errors, caching allocator, per-kernel event timing.
+#include <algorithm>
 #include <cstdarg>
 #include <cstring>
 
@@ -85,6 +86,19 @@ void timing_stop(karma_ctx* ctx, hipEvent_t ev_stop) {
     if (ev_stop) hipEventRecord(ev_stop, ctx->stream);
 }
 
+int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out) {
+    if (ctx->pinned_bytes < bytes) {
+        if (ctx->pinned) KARMA_HIP(hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        const size_t want = std::max<size_t>(bytes, 64 * 1024);
+        KARMA_HIP(hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault));
+        ctx->pinned_bytes = want;
+    }
+    *out = ctx->pinned;
+    return KARMA_OK;
+}
+
 }  // namespace karma
 
 using namespace karma;
@@ -143,6 +157,7 @@ int karma_ctx_destroy(karma_ctx* ctx) {
     }
     for (auto e : ctx->event_pool) hipEventDestroy(e);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+    if (ctx->pinned) hipHostFree(ctx->pinned);
     delete ctx;
     return KARMA_OK;
 }

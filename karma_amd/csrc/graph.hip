@@ -416,6 +416,15 @@ int karma_pairs_destroy(karma_pairs* p) {
     return KARMA_OK;
 }
 
+int karma_pairs_rebind(karma_pairs* p, karma_ctx* ctx) {
+    KARMA_CHECK(p && ctx, KARMA_ERR_ARG, "null argument");
+    KARMA_CHECK(p->ctx->device == ctx->device, KARMA_ERR_ARG, "pairs and context are on different devices");
+    KARMA_TRY(ctx_begin(p->ctx));
+    KARMA_HIP(hipStreamSynchronize(p->ctx->stream));
+    p->ctx = ctx;
+    return KARMA_OK;
+}
+
 int karma_pairs_count(karma_pairs* p, int64_t* n) {
     KARMA_CHECK(p && n, KARMA_ERR_ARG, "null argument");
     *n = p->n;
@@ -490,32 +499,34 @@ int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64
         KARMA_HIP(hipMemcpyAsync(e->totals.ptr, tot, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
     }
     const int64_t n = p->n;
-    DevArray<int64_t> flags, pos;
-    DevArray<int> zd;
+    DevArray<int64_t> flags, pos, st;  // st: 0 zero-division flag, 1 edge count
     KARMA_TRY(flags.alloc(ctx, n + 1));
     KARMA_TRY(pos.alloc(ctx, n + 1));
-    KARMA_TRY(zd.alloc(ctx, 1));
-    KARMA_HIP(hipMemsetAsync(zd.ptr, 0, 4, ctx->stream));
+    KARMA_TRY(st.alloc(ctx, 2));
+    KARMA_HIP(hipMemsetAsync(st.ptr, 0, 16, ctx->stream));
     KARMA_HIP(hipMemsetAsync(flags.ptr + n, 0, 8, ctx->stream));
     if (n) KARMA_LAUNCH(ctx, "edge_flags", edge_flags_kernel, grid1(n), 256, 0, p->keys.ptr, p->counts.ptr, n, mode, flags.ptr);
     KARMA_TRY(scan_i64(ctx, flags.ptr, pos.ptr, n + 1));
-    int64_t E = 0;
-    KARMA_HIP(hipMemcpyAsync(&E, pos.ptr + n, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    KARMA_TRY(e->a.alloc(ctx, E));
-    KARMA_TRY(e->b.alloc(ctx, E));
-    KARMA_TRY(e->s.alloc(ctx, E));
-    KARMA_TRY(e->w.alloc(ctx, E));
+    // edges <= pairs: write them before the count is known on the host
+    KARMA_TRY(e->a.alloc(ctx, n));
+    KARMA_TRY(e->b.alloc(ctx, n));
+    KARMA_TRY(e->s.alloc(ctx, n));
+    KARMA_TRY(e->w.alloc(ctx, n));
     e->has_first = p->has_first;
-    if (e->has_first) KARMA_TRY(e->first.alloc(ctx, E));
+    if (e->has_first) KARMA_TRY(e->first.alloc(ctx, n));
     if (n)
         KARMA_LAUNCH(ctx, "edge_weights", edge_write_kernel, grid1(n), 256, 0, p->keys.ptr, p->counts.ptr,
                      p->has_first ? p->first.ptr : (const uint64_t*)nullptr, flags.ptr, pos.ptr, n, e->totals.ptr,
-                     e->a.ptr, e->b.ptr, e->s.ptr, e->w.ptr, e->has_first ? e->first.ptr : (uint64_t*)nullptr, zd.ptr);
-    int hz = 0;
-    KARMA_HIP(hipMemcpyAsync(&hz, zd.ptr, 4, hipMemcpyDeviceToHost, ctx->stream));
+                     e->a.ptr, e->b.ptr, e->s.ptr, e->w.ptr, e->has_first ? e->first.ptr : (uint64_t*)nullptr,
+                     reinterpret_cast<int*>(st.ptr));
+    KARMA_HIP(hipMemcpyAsync(st.ptr + 1, pos.ptr + n, 8, hipMemcpyDeviceToDevice, ctx->stream));
+    void* hpin = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, 16, &hpin));
+    KARMA_HIP(hipMemcpyAsync(hpin, st.ptr, 16, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    KARMA_CHECK(!hz, KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
+    const int64_t* hs = static_cast<const int64_t*>(hpin);
+    KARMA_CHECK(!(int)hs[0], KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
+    const int64_t E = hs[1];
     e->E = E;
     *n_edges = E;
     *out = guard.release();

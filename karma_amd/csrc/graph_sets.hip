@@ -99,6 +99,7 @@ constexpr int kCW = 256;                // classify threads per block (4 indepen
 constexpr int kCIter = 512;             // records per wave step (8 per lane)
 constexpr int kCPer = kCIter / 128;     // 16-byte units per lane per step
 constexpr int64_t kCChunk = 8192;       // records per wave chunk (16 steps)
+constexpr int kListsPerBlock = 32;      // chunk lists per partition block (<= kMaxListsPerBlock)
 
 struct ClassArgs {
     const uint2* rec;
@@ -108,9 +109,10 @@ struct ClassArgs {
     uint32_t* codes;    // chunk c: [c * kCChunk, +n_codes[c]) codes, general starts from the end down
     uint32_t* n_codes;  // per chunk
     uint32_t* n_gen;    // per chunk
+    unsigned long long* blk_items;  // per partition block (kListsPerBlock chunks): codes
     int64_t* big_list;
     unsigned* big_n;
-    int* flags;  // 0 order, 1 contig range
+    int* flags;  // 0 order, 1 contig range (2: general pair list full)
 };
 
 // code (m0 | M << 24) of a compact read, or general / big
@@ -241,6 +243,7 @@ __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
     if (lane == 0) {
         P.n_codes[chunk] = nc;
         P.n_gen[chunk] = ng;
+        if (nc) atomicAdd(P.blk_items + chunk / kListsPerBlock, (unsigned long long)nc);
     }
     if (bad_order) P.flags[0] = 1;
     if (bad_contig) P.flags[1] = 1;
@@ -255,7 +258,9 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
                                                        const uint32_t* __restrict__ codes,
                                                        const uint32_t* __restrict__ n_gen, int64_t n_chunks,
                                                        uint64_t* __restrict__ pairs, int64_t pcap,
-                                                       uint32_t* __restrict__ n_pairs, int* __restrict__ flags) {
+                                                       uint32_t* __restrict__ n_pairs,
+                                                       unsigned long long* __restrict__ blk_items,
+                                                       int* __restrict__ flags) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t chunk = (int64_t)blockIdx.x * (kGW / 64) + wave;
     if (chunk >= n_chunks) return;
@@ -305,8 +310,11 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
         }
         np += total;
     }
-    if (lane == 0) n_pairs[chunk] = np;
-    if (full && lane == 0) flags[2] = 1;  // the host reruns with room for every pair
+    if (lane == 0) {
+        n_pairs[chunk] = np;
+        if (np) atomicAdd(blk_items + chunk / kListsPerBlock, (unsigned long long)np);
+        if (full) flags[2] = 1;  // the host reruns with room for every pair
+    }
 }
 
 // ---- partition: chunk lists -> bucket-major padded runs ---------------------------
@@ -344,19 +352,27 @@ struct PairStream {
 };
 
 struct RunDir {
-    int64_t* base;               // per flush: start of its runs in the stream
-    uint32_t* off;               // per flush: nb + 1 run offsets
-    unsigned* n;                 // flushes written
-    int64_t max;                 // directory rows
-    unsigned long long* cursor;  // stream bump allocator
-    int64_t cap;                 // stream capacity
+    int64_t* base;                        // per flush: start of its runs in the stream
+    uint32_t* off;                        // per flush: nb + 1 run offsets
+    unsigned* n;                          // flushes (directory rows) in all
+    const unsigned long long* blk_items;  // per partition block: items (from the producers)
 };
+
+// A partition block's items (blk_items, summed by the producers), flushes
+// (every flush but the last holds cap items) and an output bound (items + <
+// pad per run): the bases of block b are these sums over blocks < b, so each
+// block derives its own directory rows and stream slice (no atomics, no plan
+// launch).
+__device__ __forceinline__ void part_need(uint64_t items, int cap, int nb, int pad, int64_t* outs, int64_t* rows) {
+    *rows = ((int64_t)items + cap - 1) / cap;
+    *outs = ((int64_t)items + *rows * (int64_t)nb * (pad - 1) + pad - 1) / pad * pad;
+}
 
 template <class T>
 __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __restrict__ lists, int64_t list_cap,
                                                          const uint32_t* __restrict__ list_n, int64_t n_lists,
                                                          int per_block, Geo g, typename T::D* __restrict__ out,
-                                                         RunDir dir, int* __restrict__ flags) {
+                                                         RunDir dir) {
     using S = typename T::S;
     using D = typename T::D;
     constexpr int kPer = T::kCap / kPT;  // items per thread per fill
@@ -366,10 +382,40 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
     __shared__ uint32_t toff[T::kMaxNb + 1];
     __shared__ uint32_t cur[T::kMaxNb];
     __shared__ uint32_t lpre[kMaxListsPerBlock + 1];
-    __shared__ int64_t fbase_s;
-    __shared__ unsigned fidx_s;
-    __shared__ int ok_s;
+    __shared__ int64_t red_s[2][kPT / 64];
     const int nb = T::nb(g);
+    int64_t used = 0;  // stream items of this block's flushes so far (uniform)
+    int row = 0;       // directory rows of this block so far (uniform)
+    int64_t out0, row0;  // this block's stream slice and first directory row
+    {
+        int64_t so = 0, sr = 0;
+        for (int64_t b = threadIdx.x; b < (int64_t)blockIdx.x; b += kPT) {
+            int64_t o, r;
+            part_need(dir.blk_items[b], T::kCap, nb, T::kPad, &o, &r);
+            so += o;
+            sr += r;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            so += __shfl_xor(so, d);
+            sr += __shfl_xor(sr, d);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            red_s[0][threadIdx.x >> 6] = so;
+            red_s[1][threadIdx.x >> 6] = sr;
+        }
+        __syncthreads();
+        out0 = row0 = 0;
+        for (int w = 0; w < kPT / 64; ++w) {
+            out0 += red_s[0][w];
+            row0 += red_s[1][w];
+        }
+        if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {  // the last block knows the row total
+            int64_t o, r;
+            part_need(dir.blk_items[blockIdx.x], T::kCap, nb, T::kPad, &o, &r);
+            *dir.n = (unsigned)(row0 + r);
+        }
+    }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int b = threadIdx.x; b <= nb; b += kPT) hist[0][b] = hist[1][b] = 0;
 
@@ -439,23 +485,16 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
                 if (b0 + lane < nb) toff[b0 + lane] = c2 + x - val;
                 c2 += __shfl(x, 63);
             }
-            if (lane == 0) {
-                toff[nb] = c2;
-                const unsigned f = atomicAdd(dir.n, 1u);
-                const unsigned long long at = atomicAdd(dir.cursor, (unsigned long long)c2);
-                const bool ok = (int64_t)f < dir.max && (int64_t)(at + c2) <= dir.cap;
-                if (!ok) flags[3] = 1;  // the host reruns with a larger stream
-                else dir.base[f] = (int64_t)at;
-                fidx_s = f;
-                fbase_s = (int64_t)at;
-                ok_s = ok;
-            }
+            if (lane == 0) toff[nb] = c2;
         }
         __syncthreads();
-        const bool ok = ok_s;
+        const unsigned f = (unsigned)(row0 + row);
+        const int64_t at = out0 + used;
         const uint32_t total = toff[nb];
-        if (ok) {
-            const unsigned f = fidx_s;
+        if (threadIdx.x == 0) dir.base[f] = at;
+        ++row;
+        used += total;
+        {
             for (int b = threadIdx.x; b <= nb; b += kPT) dir.off[(int64_t)f * (nb + 1) + b] = toff[b];
             for (int b = threadIdx.x; b < nb; b += kPT)
                 for (uint32_t i = toff[b] + h[b]; i < toff[b + 1]; ++i) sorted[i] = T::kPadV;
@@ -469,12 +508,10 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
         // buf, h and cur are free: the next fill may start once this block's
         // 16-byte stores are issued (their completion is never waited for)
         for (int b = threadIdx.x; b < nb; b += kPT) h[b] = 0;
-        if (ok) {
-            u32x4* dst = reinterpret_cast<u32x4*>(out + fbase_s);
-            const u32x4* src = reinterpret_cast<const u32x4*>(sorted);
-            const uint32_t nv = total * (uint32_t)sizeof(D) / 16u;
-            for (uint32_t i = threadIdx.x; i < nv; i += kPT) dst[i] = src[i];
-        }
+        u32x4* dst = reinterpret_cast<u32x4*>(out + at);
+        const u32x4* src = reinterpret_cast<const u32x4*>(sorted);
+        const uint32_t nv = total * (uint32_t)sizeof(D) / 16u;
+        for (uint32_t i = threadIdx.x; i < nv; i += kPT) dst[i] = src[i];
     }
 }
 
@@ -943,7 +980,6 @@ int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
     return KARMA_OK;
 }
 
-constexpr int kListsPerBlock = 32;  // chunk lists per partition block (<= kMaxListsPerBlock)
 
 }  // namespace
 
@@ -959,24 +995,34 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     // per-step scratch
     DevArray<uint32_t> codes, n_codes, n_gen, n_pl;
     DevArray<int64_t> big_list;
-    DevArray<int> flags;
-    DevArray<unsigned> counters;           // 0 big reads, 1 code flushes, 2 pair flushes
-    DevArray<unsigned long long> cursors;  // 0 code stream, 1 pair stream
     KARMA_TRY(codes.alloc(ctx, n_chunks * kCChunk));
     KARMA_TRY(n_codes.alloc(ctx, n_chunks));
     KARMA_TRY(n_gen.alloc(ctx, n_chunks));
     KARMA_TRY(n_pl.alloc(ctx, n_chunks));
     KARMA_TRY(big_list.alloc(ctx, A / (kMaxFast + 1) + 1));
-    KARMA_TRY(flags.alloc(ctx, 4));
-    KARMA_TRY(counters.alloc(ctx, 3));
-    KARMA_TRY(cursors.alloc(ctx, 2));
+    // control block, cleared by one memset and read back by one copy:
+    // flags[4] | counters[3] (big reads, code flushes, pair flushes) | spare[2]
+    // | pairs per bucket[B+1] | their exclusive scan[B+1] | overflow[B]
+    const int64_t ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8);
+    DevArray<int64_t> ctrl;
+    KARMA_TRY(ctrl.alloc(ctx, ctrl_words));
+    int* const flags = reinterpret_cast<int*>(ctrl.ptr);
+    unsigned* const counters = reinterpret_cast<unsigned*>(ctrl.ptr + 2);
+    int64_t* const n_per = ctrl.ptr + 6;
+    int64_t* const dst = n_per + (B + 1);
+    uint8_t* const ovf = reinterpret_cast<uint8_t*>(dst + (B + 1));
+    void* hpin = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, ctrl_words * 8, &hpin));
+    const int64_t* const hctrl = static_cast<const int64_t*>(hpin);
     // code stream: <= one code per record + < 8 padding codes per run; a block
     // flushes only a full buffer, and once at its end
     const int64_t max_cflush = n_pblk + ceil_div(A, CodeStream::kCap) + 1;
-    const int64_t ccap = A + max_cflush * 8 * (int64_t)std::max(g.Bc, 1);
+    const int64_t ccap = A + max_cflush * (8 * (int64_t)g.Bc + 8);
     DevArray<uint16_t> cent;
     DevArray<int64_t> cf_base;
     DevArray<uint32_t> cf_off;
+    DevArray<unsigned long long> blk_items;       // per partition block: codes, pairs
+    KARMA_TRY(blk_items.alloc(ctx, 2 * n_pblk));
     if (g.Bc > 0) {
         KARMA_TRY(cent.alloc(ctx, ccap + 16));
         KARMA_TRY(cf_base.alloc(ctx, max_cflush));
@@ -989,7 +1035,6 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     DevArray<uint32_t> pent, pf_off;
     DevArray<int64_t> pf_base;
     unsigned hc[3] = {0, 0, 0};
-    int hf[4] = {0, 0, 0, 0};
     // reduce geometry: grids fixed here, flush ranges from device counters
     const int n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, ceil_div(512, g.Bc)) : 0;
     const int n_pg = (int)std::max<int64_t>(1, ceil_div(256, B));
@@ -997,8 +1042,7 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     DevArray<uint32_t> part_ch, part_b, part_k, part_c;
     DevArray<int> part_n;
     DevArray<uint64_t> slot_k;
-    DevArray<int64_t> slot_c, n_per, dst;
-    DevArray<uint8_t> ovf;
+    DevArray<int64_t> slot_c;
     if (n_cg) KARMA_TRY(part_ch.alloc(ctx, (int64_t)g.Bc * n_cg * (int64_t(8) << g.bwc)));
     KARMA_TRY(part_b.alloc(ctx, nsl * (int64_t)kBand));
     KARMA_TRY(part_k.alloc(ctx, nsl * (int64_t)kHashR));
@@ -1006,60 +1050,55 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     KARMA_TRY(part_n.alloc(ctx, nsl));
     KARMA_TRY(slot_k.alloc(ctx, (int64_t)B * kSlotCap));
     KARMA_TRY(slot_c.alloc(ctx, (int64_t)B * kSlotCap));
-    KARMA_TRY(n_per.alloc(ctx, B + 1));
-    KARMA_TRY(dst.alloc(ctx, B + 1));
-    KARMA_TRY(ovf.alloc(ctx, B));
     RunDir pdir{};
     std::vector<uint8_t> hovf(B);
     int64_t U = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         const int64_t max_pflush = n_pblk + ceil_div(n_chunks * pcap, PairStream::kCap) + 1;
-        const int64_t pscap = n_chunks * pcap + max_pflush * 4 * (int64_t)B;
+        const int64_t pscap = n_chunks * pcap + max_pflush * (4 * (int64_t)B + 4);
         KARMA_TRY(plist.alloc(ctx, n_chunks * pcap));
         KARMA_TRY(pent.alloc(ctx, pscap + 8));
         KARMA_TRY(pf_base.alloc(ctx, max_pflush));
         KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
-        KARMA_HIP(hipMemsetAsync(flags.ptr, 0, 16, ctx->stream));
-        KARMA_HIP(hipMemsetAsync(counters.ptr, 0, 12, ctx->stream));
-        KARMA_HIP(hipMemsetAsync(cursors.ptr, 0, 16, ctx->stream));
-        KARMA_HIP(hipMemsetAsync(ovf.ptr, 0, B, ctx->stream));
-        KARMA_HIP(hipMemsetAsync(n_per.ptr, 0, (B + 1) * 8, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, ctrl_words * 8, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(blk_items.ptr, 0, 2 * n_pblk * 8, ctx->stream));
         if (A > 0) {
-            ClassArgs C{rec, A, (uint32_t)N, g.Bc > 0, codes.ptr, n_codes.ptr, n_gen.ptr, big_list.ptr, counters.ptr,
-                        flags.ptr};
+            ClassArgs C{rec,      A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
+                        n_gen.ptr, blk_items.ptr, big_list.ptr, counters, flags};
             KARMA_LAUNCH(ctx, "graph_classify", classify_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         } else {
             KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
             KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
-                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, flags.ptr);
-        const RunDir cdir{cf_base.ptr, cf_off.ptr, counters.ptr + 1, max_cflush, cursors.ptr, ccap};
-        pdir = RunDir{pf_base.ptr, pf_off.ptr, counters.ptr + 2, max_pflush, cursors.ptr + 1, pscap};
+                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_pblk, flags);
+        const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items.ptr};
+        pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items.ptr + n_pblk};
         if (g.Bc > 0) {
             KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr,
-                         kCChunk, n_codes.ptr, n_chunks, kListsPerBlock, g, cent.ptr, cdir, flags.ptr);
+                         kCChunk, n_codes.ptr, n_chunks, kListsPerBlock, g, cent.ptr, cdir);
             KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
                          g.Bc, g.bwc, n_cg, part_ch.ptr);
         }
         KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
-                     n_pl.ptr, n_chunks, kListsPerBlock, g, pent.ptr, pdir, flags.ptr);
+                     n_pl.ptr, n_chunks, kListsPerBlock, g, pent.ptr, pdir);
         KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
-                     g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf.ptr);
+                     g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
         KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits, g.bwc,
-                     part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per.ptr,
-                     ovf.ptr);
-        KARMA_TRY(scan_excl_i64(ctx, n_per.ptr, dst.ptr, B + 1));
+                     part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
+                     ovf);
+        KARMA_TRY(scan_excl_i64(ctx, n_per, dst, B + 1));
         // the one synchronisation of the common path
-        KARMA_HIP(hipMemcpyAsync(hf, flags.ptr, 16, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipMemcpyAsync(hc, counters.ptr, 12, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipMemcpyAsync(hovf.data(), ovf.ptr, B, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipMemcpyAsync(&U, dst.ptr + B, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(hpin, ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        const int* hf = reinterpret_cast<const int*>(hctrl);
+        std::memcpy(hc, hctrl + 2, sizeof hc);
+        std::memcpy(hovf.data(), hctrl + 6 + 2 * (B + 1), B);
+        U = hctrl[6 + (B + 1) + B];
         KARMA_CHECK(!hf[0], KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
         KARMA_CHECK(!hf[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
-        if (!hf[2] && !hf[3]) break;
-        KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "pair list or run stream capacity exceeded twice");
+        if (!hf[2]) break;
+        KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "pair list capacity exceeded twice");
         pcap = kCChunk * 9 / 2;  // every read with <= 8 records fits
     }
     const unsigned n_big = hc[0];
@@ -1101,12 +1140,12 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         const int64_t* cp = keep_c.back()->ptr;
         KARMA_HIP(hipMemcpyAsync(pk.ptr + b, &kp, sizeof kp, hipMemcpyHostToDevice, ctx->stream));
         KARMA_HIP(hipMemcpyAsync(pc.ptr + b, &cp, sizeof cp, hipMemcpyHostToDevice, ctx->stream));
-        KARMA_HIP(hipMemcpyAsync(n_per.ptr + b, &nu, 8, hipMemcpyHostToDevice, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(n_per + b, &nu, 8, hipMemcpyHostToDevice, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
     }
     if (any_ovf) {
-        KARMA_TRY(scan_excl_i64(ctx, n_per.ptr, dst.ptr, B + 1));
-        KARMA_HIP(hipMemcpyAsync(&U, dst.ptr + B, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_TRY(scan_excl_i64(ctx, n_per, dst, B + 1));
+        KARMA_HIP(hipMemcpyAsync(&U, dst + B, 8, hipMemcpyDeviceToHost, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
     }
     DevArray<uint64_t> mk;
@@ -1114,7 +1153,7 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     const bool merge_big = n_big > 0;
     KARMA_TRY((merge_big ? mk : out->keys).alloc(ctx, U));
     KARMA_TRY((merge_big ? mc : out->counts).alloc(ctx, U));
-    KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, pk.ptr, pc.ptr, n_per.ptr, dst.ptr,
+    KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, pk.ptr, pc.ptr, n_per, dst,
                  (merge_big ? mk : out->keys).ptr, (merge_big ? mc : out->counts).ptr);
     out->n = U;
     out->n_contigs = N;

@@ -57,6 +57,9 @@ struct karma_ctx {
     bool timing = false;
     std::vector<karma::TimedLaunch> launches;
     std::vector<hipEvent_t> event_pool;
+    // pinned host scratch for small status readbacks (one async copy + one sync)
+    void* pinned = nullptr;
+    size_t pinned_bytes = 0;
 };
 
 namespace karma {
@@ -64,6 +67,8 @@ namespace karma {
 int ctx_alloc(karma_ctx* ctx, size_t bytes, void** out);
 void ctx_free(karma_ctx* ctx, void* p);
 int ctx_begin(karma_ctx* ctx);  // hipSetDevice
+// Pinned host scratch of >= bytes (valid until the next call on this ctx).
+int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out);
 // Wrap a launch with HIP events when timing is on.
 void timing_start(karma_ctx* ctx, const char* name, hipEvent_t* ev_stop);
 void timing_stop(karma_ctx* ctx, hipEvent_t ev_stop);

@@ -29,6 +29,7 @@ using namespace karma;
 struct karma_contigs {
     karma_ctx* ctx = nullptr;
     int64_t n = 0, total = 0, words = 0, exc_bases = 0;
+    int64_t zero_key_maxlen = -1;  // longest contig with an empty FASTA key (-1: none)
     DevArray<uint8_t> raw_own;
     DevArray<int64_t> off_own;
     DevArray<int32_t> keylen_own;
@@ -509,6 +510,14 @@ __global__ void __launch_bounds__(kBlock) profile_kernel(
 
 int grid_for(int64_t n, int64_t cap) { return (int)std::max<int64_t>(1, std::min<int64_t>(n, cap)); }
 
+// longest contig whose key is empty: it divides by zero iff it has k-mers
+// (kmer.py:213), so karma_kmer_profile can refuse before launching
+__global__ void zero_key_kernel(const int64_t* __restrict__ off, const int32_t* __restrict__ keylen, int64_t n,
+                                unsigned long long* __restrict__ maxlen_plus1) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && keylen[i] == 0) atomicMax(maxlen_plus1, (unsigned long long)(off[i + 1] - off[i] + 1));
+}
+
 int kmer_shape(int kmode, int* kmin, int* kmax, uint32_t* S, bool* with_len) {
     if (kmode == KARMA_KMER_5P6) {
         *kmin = 5;
@@ -581,19 +590,22 @@ int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offs
     }
     KARMA_HIP(hipMemsetAsync(c->packed.ptr + c->words, 0, kPadWords * sizeof(uint32_t), ctx->stream));
     KARMA_HIP(hipMemsetAsync(c->mask.ptr + c->words, 0, kPadWords * sizeof(uint16_t), ctx->stream));
-    DevArray<unsigned long long> exc;
-    if ((rc = exc.alloc(ctx, 1))) {
+    DevArray<unsigned long long> stat;  // 0 exception bases, 1 zero-key max length + 1
+    if ((rc = stat.alloc(ctx, 2))) {
         delete c;
         return rc;
     }
-    KARMA_HIP(hipMemsetAsync(exc.ptr, 0, sizeof(unsigned long long), ctx->stream));
-    if (n)
+    KARMA_HIP(hipMemsetAsync(stat.ptr, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    if (n) {
         KARMA_LAUNCH(ctx, "pack_2bit", pack_kernel, grid_for(n, 8192), kBlock, 0, c->raw, c->off, c->woff.ptr, n,
-                     c->packed.ptr, c->mask.ptr, c->has_exc.ptr, exc.ptr);
-    unsigned long long ne = 0;
-    KARMA_HIP(hipMemcpyAsync(&ne, exc.ptr, sizeof ne, hipMemcpyDeviceToHost, ctx->stream));
+                     c->packed.ptr, c->mask.ptr, c->has_exc.ptr, stat.ptr);
+        KARMA_LAUNCH(ctx, "zero_key", zero_key_kernel, ceil_div(n, 256), 256, 0, c->off, c->keylen, n, stat.ptr + 1);
+    }
+    unsigned long long hs[2] = {0, 0};
+    KARMA_HIP(hipMemcpyAsync(hs, stat.ptr, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    c->exc_bases = (int64_t)ne;
+    c->exc_bases = (int64_t)hs[0];
+    c->zero_key_maxlen = (int64_t)hs[1] - 1;
     *out = c;
     return KARMA_OK;
 }
@@ -671,8 +683,10 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
         }
     }
     unsigned long long ninst = 0;
-    KARMA_HIP(hipMemcpyAsync(&ninst, exc_cnt.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    if (c->exc_bases) {  // exception k-mers exist only in contigs with non-ACGT bases
+        KARMA_HIP(hipMemcpyAsync(&ninst, exc_cnt.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    }
     KARMA_CHECK((int64_t)ninst <= exc_cap, KARMA_ERR_STATE, "exception k-mer buffer overflow (%llu > %lld)", ninst,
                 (long long)exc_cap);
     if (ninst) {
@@ -795,8 +809,11 @@ int karma_kmer_plan_finalize(karma_kmer_plan* p, int64_t* M) {
     KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->presence.ptr, (int)p->nwords, S,
                  p->kmode == KARMA_KMER_5P6, p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode, with_len, p->exc_keys.ptr,
                  p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, m_dev.ptr);
-    KARMA_HIP(hipMemcpyAsync(&p->M, m_dev.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    void* hpin = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, 8, &hpin));
+    KARMA_HIP(hipMemcpyAsync(hpin, m_dev.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    p->M = *static_cast<const int64_t*>(hpin);
     *M = p->M;
     return KARMA_OK;
 }
@@ -835,6 +852,8 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
         return KARMA_OK;
     }
     KARMA_CHECK(out, KARMA_ERR_ARG, "null out");
+    KARMA_CHECK(c->zero_key_maxlen < p->kmin, KARMA_ERR_ZERO_DIV,
+                "division by zero: a contig with a zero-length key has k-mers");
     int rc;
     DevArray<double> dev_out;
     double* dst = out;
@@ -870,12 +889,10 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
         else KARMA_PROFILE_LAUNCH(false, false, false);
     }
 #undef KARMA_PROFILE_LAUNCH
-    int herr = 0;
-    KARMA_HIP(hipMemcpyAsync(&herr, err.ptr, 4, hipMemcpyDeviceToHost, ctx->stream));
-    if (!out_is_device)
+    if (!out_is_device) {
         KARMA_HIP(hipMemcpyAsync(out, dst, (size_t)n * ld * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    KARMA_CHECK(!herr, KARMA_ERR_ZERO_DIV, "division by zero: a contig with a zero-length key has k-mers");
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    }
     return KARMA_OK;
 }
 

@@ -148,16 +148,21 @@ class Comm:
 class HipOps:
     """Compute backend on libkarma_hip.so; exchange buffers are torch CUDA tensors."""
 
-    def __init__(self, ctx, device_index=None):
+    def __init__(self, ctx, device_index=None, make_current=True):
         import torch
 
         from . import engine
 
         self.torch, self.engine = torch, engine
         self.dev = torch.device(f"cuda:{torch.cuda.current_device() if device_index is None else device_index}")
-        # one stream shared by torch (collectives, buffers) and the HIP kernels
-        self.stream = torch.cuda.Stream(device=self.dev)
-        torch.cuda.set_stream(self.stream)
+        # one stream shared by torch (collectives, buffers) and the HIP kernels;
+        # a second ops object (concurrent graph build) keeps its own stream and
+        # leaves torch's current stream alone
+        # the main stream runs the k-mer kernels (short prologue, then the
+        # profile): high priority, so its blocks dispatch first when CUs free up
+        self.stream = torch.cuda.Stream(device=self.dev, priority=-1 if make_current else 0)
+        if make_current:
+            torch.cuda.set_stream(self.stream)
         ctx.set_stream(self.stream.cuda_stream)
         self.ctx = ctx
 
@@ -208,6 +213,11 @@ class HipOps:
         return self.torch.empty((n, M), dtype=self.torch.float64, device=self.dev)
 
     # -- graph --
+    def adopt(self, pairs):
+        """Continue work on a pair list built by another HipOps on this stream."""
+        pairs.rebind(self.ctx)
+        return pairs
+
     def graph_local(self, records, n_records, n_contigs):
         return self.engine.Pairs.from_records(self.ctx, None, n_contigs, grouped=True, device_ptr=records,
                                               n_records=n_records)
@@ -260,10 +270,24 @@ class HipOps:
 class ShardedBuild:
     """k-mer profile + shared-read graph over contig/fragment shards."""
 
-    def __init__(self, ctx, comm: Comm, kmode, n_glob, c_lo, n_loc, ops=None):
+    def __init__(self, ctx, comm: Comm, kmode, n_glob, c_lo, n_loc, ops=None, overlap=None):
         self.comm, self.kmode, self.n_glob, self.c_lo, self.n_loc = comm, kmode, n_glob, c_lo, n_loc
         self.ops = ops if ops is not None else HipOps(ctx)
         self._prof = None
+        # The local graph build (records -> pair list) shares nothing with the
+        # k-mer profile: with overlap it runs from a worker thread on a second
+        # context/stream while this thread drives the profile; every collective
+        # stays on this thread, in the same order on every rank.
+        if overlap is None:
+            overlap = ops is None and os.environ.get("KARMA_OVERLAP", "1") != "0"
+        self.gctx = self.gops = self._pool = None
+        if overlap:
+            from concurrent.futures import ThreadPoolExecutor
+
+            from . import _lib
+            self.gctx = _lib.Context(ctx.device)
+            self.gops = HipOps(self.gctx, ctx.device, make_current=False)
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="karma-graph")
         bounds = np.zeros(comm.world + 1, np.int64)
         if comm.world > 1:
             import torch
@@ -280,20 +304,32 @@ class ShardedBuild:
             bounds[1] = n_glob
         self.bounds = bounds
 
+    def contexts(self):
+        """The karma contexts this build launches on (per-kernel timing)."""
+        return [c for c in (self.ops.ctx if hasattr(self.ops, "ctx") else None, self.gctx) if c is not None]
+
     def run(self, store, records, n_records, keep=False):
         ops, comm = self.ops, self.comm
-        # ---- k-mer profile (kmer.py:199-233) ----
-        plan = ops.kmer_plan(store, self.kmode)
-        if comm.world > 1:
-            pres = comm.allreduce_max_(ops.presence_bytes(plan))
-            ops.set_presence_bytes(plan, pres)
-            ops.set_exceptions(plan, comm.all_gather_var(ops.exceptions(plan)))
-        M = ops.finalize(plan)
-        if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
-            self._prof = ops.profile_buffer(self.n_loc, M)
-        ops.profile(plan, self._prof)
-        # ---- shared-read graph (read_graph.py:19-50) ----
-        local = ops.graph_local(records, n_records, self.n_glob)
+        fut = None
+        if self._pool is not None:  # ---- shared-read graph, concurrent (read_graph.py:19-50) ----
+            fut = self._pool.submit(self.gops.graph_local, records, n_records, self.n_glob)
+        try:
+            # ---- k-mer profile (kmer.py:199-233) ----
+            plan = ops.kmer_plan(store, self.kmode)
+            if comm.world > 1:
+                pres = comm.allreduce_max_(ops.presence_bytes(plan))
+                ops.set_presence_bytes(plan, pres)
+                ops.set_exceptions(plan, comm.all_gather_var(ops.exceptions(plan)))
+            M = ops.finalize(plan)
+            if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
+                self._prof = ops.profile_buffer(self.n_loc, M)
+            ops.profile(plan, self._prof)
+        finally:
+            local = fut.result() if fut is not None else None  # joined on every path
+        if local is None:  # ---- shared-read graph (read_graph.py:19-50) ----
+            local = ops.graph_local(records, n_records, self.n_glob)
+        else:
+            local = ops.adopt(local)
         stats = {"M": M}
         if keep:
             stats["entries"] = ops.entries(local)
@@ -321,3 +357,10 @@ class ShardedBuild:
 
     def close(self):
         self._prof = None
+        if self._pool is not None:
+            self._pool.shutdown()
+            self._pool = None
+        if self.gctx is not None:
+            self.gops = None
+            self.gctx.close()
+            self.gctx = None

@@ -263,6 +263,11 @@ class Pairs:
              ctypes.byref(E))
         return Edges(self.ctx, h, E.value, n_contigs)
 
+    def rebind(self, ctx):
+        """Run later kernels on this list on ``ctx``'s stream (karma_pairs_rebind)."""
+        call("karma_pairs_rebind", self.h, ctx.h)
+        self.ctx = ctx
+
     def close(self):
         if getattr(self, "h", None):
             _lib.load().karma_pairs_destroy(self.h)
