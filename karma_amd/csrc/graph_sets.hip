@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <type_traits>
 
 #include "karma_internal.h"
 
@@ -118,7 +119,8 @@ struct ClassArgs {
 // code (m0 | M << 24) of a compact read, or general / big
 __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
     __shared__ uint2 srec[kCW / 64][kCIter + kMaxFast];
-    __shared__ uint16_t wst[kCW / 64][kCIter];
+    __shared__ uint16_t wst[kCW / 64][kCIter + 1];  // read starts (+ the end of the last read)
+    __shared__ uint16_t wcl[kCW / 64][kCIter];      // reads by size class
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t chunk = (int64_t)blockIdx.x * (kCW / 64) + wave;
     const int64_t c_lo = chunk * kCChunk;
@@ -126,6 +128,7 @@ __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
     const int64_t c_hi = min(P.A, c_lo + kCChunk);
     uint2* sr = srec[wave];
     uint16_t* ws = wst[wave];
+    uint16_t* cl = wcl[wave];
     uint32_t* out = P.codes + c_lo;
     const unsigned long long lower = (1ull << lane) - 1ull;
 
@@ -195,48 +198,93 @@ __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
         if (lane < kMaxFast) sr[kCIter + lane] = nxh;
         prefetch(t0 + kCIter);
         wave_sync();
-        // ---- one lane per read ----
+        // ---- read sizes: the gap to the next read start (the last read's end
+        // is found in the slice + halo; 9 means more than 8 records) ----
+        if (lane == 0 && ns > 0) {
+            const int jl = ws[ns - 1];
+            const uint32_t rid = sr[jl].x;
+            int j = jl + 1;
+            while (j < jl + kMaxFast + 1 && sr[j].x == rid) ++j;
+            ws[ns] = (uint16_t)j;
+        }
+        wave_sync();
+        // split: small reads (<= 4 records) from the front of cl, large ones
+        // (5..9) from the back; an entry is j0 | size << 10
+        int n_s = 0, n_l = 0;
         for (int kb = 0; kb < ns; kb += 64) {
             const int k = kb + lane;
-            uint32_t code = kEmpty;
-            bool gen = false;
-            int j0 = 0;
+            int j0 = 0, sz = 0;
             if (k < ns) {
                 j0 = ws[k];
-                uint2 r[kMaxFast + 1];
-#pragma unroll
-                for (int t = 0; t <= kMaxFast; ++t) r[t] = sr[j0 + t];
-                const uint32_t rid = r[0].x;
-                bool v = true;
-                uint32_t mn = kEmpty, mx = 0;
-#pragma unroll
-                for (int t = 0; t < kMaxFast; ++t) {
-                    v = v && (t == 0 || r[t].x == rid);
-                    if (v) {
-                        mn = min(mn, r[t].y);
-                        mx = max(mx, r[t].y);
-                    }
-                }
-                if (v && r[kMaxFast].x == rid) {  // > 8 records: generic path
-                    P.big_list[atomicAdd(P.big_n, 1u)] = t0 + j0;
-                } else if (P.compact && mx - mn < 4u && mx < P.N) {
-                    uint32_t M = 0;
-                    v = true;
-#pragma unroll
-                    for (int t = 0; t < kMaxFast; ++t) {
-                        v = v && (t == 0 || r[t].x == rid);
-                        if (v) M |= 1u << (r[t].y - mn);
-                    }
-                    code = (M >> 1) << 24 | mn;
-                } else {
-                    gen = true;
-                }
+                sz = min((int)ws[k + 1] - j0, kMaxFast + 1);
             }
+            const bool sm = k < ns && sz <= 4, lg = k < ns && sz > 4;
+            const unsigned long long bs = __ballot(sm), bl = __ballot(lg);
+            const uint16_t e = (uint16_t)(j0 | sz << 10);
+            if (sm) cl[n_s + __popcll(bs & lower)] = e;
+            if (lg) cl[kCIter - 1 - (n_l + __popcll(bl & lower))] = e;
+            n_s += __popcll(bs);
+            n_l += __popcll(bl);
+        }
+        wave_sync();
+        // a read's code, or general: min/max of its contigs (ids only, the
+        // records past its size are replaced by its first contig)
+        auto classify = [&](auto width, int j0, int sz, uint32_t* code, bool* gen) {
+            constexpr int W = decltype(width)::value;
+            uint32_t y[W];
+            y[0] = sr[j0].y;
+#pragma unroll
+            for (int t = 1; t < W; ++t) {
+                const uint32_t v = sr[j0 + t].y;
+                y[t] = t < sz ? v : y[0];
+            }
+            uint32_t mn = y[0], mx = y[0];
+#pragma unroll
+            for (int t = 1; t < W; ++t) {
+                mn = min(mn, y[t]);
+                mx = max(mx, y[t]);
+            }
+            if (P.compact && mx - mn < 4u && mx < P.N) {
+                uint32_t M = 0;
+#pragma unroll
+                for (int t = 0; t < W; ++t) M |= 1u << (y[t] - mn);
+                *code = (M >> 1) << 24 | mn;
+            } else {
+                *gen = true;
+            }
+        };
+        auto emit = [&](uint32_t code, bool gen, int j0) {
             const unsigned long long cb = __ballot(code != kEmpty), gb = __ballot(gen);
             if (code != kEmpty) out[nc + __popcll(cb & lower)] = code;
             if (gen) out[kCChunk - 1 - (ng + __popcll(gb & lower))] = (uint32_t)(t0 - c_lo + j0);
             nc += __popcll(cb);
             ng += __popcll(gb);
+        };
+        for (int kb = 0; kb < n_s; kb += 64) {
+            const int k = kb + lane;
+            uint32_t code = kEmpty;
+            bool gen = false;
+            int j0 = 0;
+            if (k < n_s) {
+                const uint32_t e = cl[k];
+                j0 = e & 1023;
+                classify(std::integral_constant<int, 4>{}, j0, (int)(e >> 10), &code, &gen);
+            }
+            emit(code, gen, j0);
+        }
+        for (int kb = 0; kb < n_l; kb += 64) {
+            const int k = kb + lane;
+            uint32_t code = kEmpty;
+            bool gen = false;
+            int j0 = 0;
+            if (k < n_l) {
+                const uint32_t e = cl[kCIter - 1 - k];
+                j0 = e & 1023;
+                const int sz = (int)(e >> 10);
+                if (sz > kMaxFast) P.big_list[atomicAdd(P.big_n, 1u)] = t0 + j0;  // > 8 records: generic path
+                else classify(std::integral_constant<int, kMaxFast>{}, j0, sz, &code, &gen);
+            }
+            emit(code, gen, j0);
         }
         wave_sync();  // every lane is done with the slice
     }
