@@ -86,6 +86,13 @@ void timing_stop(karma_ctx* ctx, hipEvent_t ev_stop) {
     if (ev_stop) hipEventRecord(ev_stop, ctx->stream);
 }
 
+int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int64_t work) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(work, (int64_t)per_cu * ctx->cu_count));
+}
+
 int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out) {
     if (ctx->pinned_bytes < bytes) {
         if (ctx->pinned) KARMA_HIP(hipHostFree(ctx->pinned));
@@ -134,6 +141,7 @@ int karma_ctx_create(int device, karma_ctx** out) {
                 "device %d is %s; libkarma_hip is built for gfx950 only", device, prop.gcnArchName);
     karma_ctx* ctx = new karma_ctx();
     ctx->device = device;
+    ctx->cu_count = prop.multiProcessorCount;
     hipError_t e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete ctx;

@@ -47,6 +47,7 @@ struct TimedLaunch {
 
 struct karma_ctx {
     int device = 0;
+    int cu_count = 256;  // compute units of the device
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     // exact-size caching allocator: repeated steps of identical shape never hipMalloc
@@ -67,6 +68,9 @@ namespace karma {
 int ctx_alloc(karma_ctx* ctx, size_t bytes, void** out);
 void ctx_free(karma_ctx* ctx, void* p);
 int ctx_begin(karma_ctx* ctx);  // hipSetDevice
+// Grid of one round: blocks that fit on the device at once for this kernel,
+// block size and dynamic LDS (at least 1, at most `work` blocks).
+int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int64_t work);
 // Pinned host scratch of >= bytes (valid until the next call on this ctx).
 int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out);
 // Wrap a launch with HIP events when timing is on.

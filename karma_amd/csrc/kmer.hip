@@ -62,6 +62,7 @@ struct karma_kmer_plan {
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kPBlock = 512;  // profile: 8 waves share one LDS column table
 constexpr int kPadWords = 80;    // zero words after the store (stages may read past the last contig)
 
 __device__ __forceinline__ int base_code(uint8_t b) {
@@ -192,32 +193,66 @@ __device__ __forceinline__ Window load_window(const uint32_t* packed, const uint
 // are loaded once, coalesced, into the wave's LDS slice; every k-mer window is
 // then read from LDS.
 template <typename Body>
+__device__ __forceinline__ void window_round(int64_t base, int64_t npos, bool excp, const uint32_t* wbuf,
+                                             const uint16_t* mbuf, int lane, Body& body) {
+    const int64_t lim = min(npos, base + 1024);
+    for (int64_t i = base + lane; i < lim; i += 64) {
+        const int l = (int)(i - base), w = l >> 4;
+        Window v;
+        v.o = l & 15;
+        v.x = ((uint64_t)wbuf[w] << 32) | wbuf[w + 1];
+        v.m = excp ? (((uint32_t)mbuf[w] << 16) | mbuf[w + 1]) : 0u;
+        body(i, v);
+    }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The 65 packed words (and mask half-words) of one 1024-position stage, held
+// in registers: lane l has word l, lane 0 also word 64.
+struct Stage {
+    uint32_t w = 0, w64 = 0;
+    uint16_t m = 0, m64 = 0;
+    __device__ __forceinline__ void load(const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask,
+                                         bool excp, int64_t wb, int lane) {
+        w = packed[wb + lane];
+        if (lane == 0) w64 = packed[wb + 64];
+        if (excp) {
+            m = mask[wb + lane];
+            if (lane == 0) m64 = mask[wb + 64];
+        }
+    }
+    __device__ __forceinline__ void put(uint32_t* wbuf, uint16_t* mbuf, bool excp, int lane) const {
+        wbuf[lane] = w;
+        if (lane == 0) wbuf[64] = w64;
+        if (excp) {
+            mbuf[lane] = m;
+            if (lane == 0) mbuf[64] = m64;
+        }
+    }
+};
+
+// A wave walks its contig in stages of 1024 positions: the 65 packed words
+// (and, for contigs with exception bases, the 65 mask half-words) of a stage
+// are loaded once, coalesced, into the wave's LDS slice; every k-mer window is
+// then read from LDS.  `first`, when given, is stage 0 already in registers.
+template <typename Body>
 __device__ __forceinline__ void for_each_window(const uint32_t* __restrict__ packed,
                                                 const uint16_t* __restrict__ mask, bool excp, int64_t w0,
-                                                int64_t npos, uint32_t* wbuf, uint16_t* mbuf, int lane, Body body) {
+                                                int64_t npos, uint32_t* wbuf, uint16_t* mbuf, int lane, Body body,
+                                                const Stage* first = nullptr) {
     for (int64_t base = 0; base < npos; base += 1024) {
-        const int64_t wb = w0 + (base >> 4);
-        wbuf[lane] = packed[wb + lane];
-        if (lane == 0) wbuf[64] = packed[wb + 64];
-        if (excp) {
-            mbuf[lane] = mask[wb + lane];
-            if (lane == 0) mbuf[64] = mask[wb + 64];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int64_t lim = min(npos, base + 1024);
-        for (int64_t i = base + lane; i < lim; i += 64) {
-            const int l = (int)(i - base), w = l >> 4;
-            Window v;
-            v.o = l & 15;
-            v.x = ((uint64_t)wbuf[w] << 32) | wbuf[w + 1];
-            v.m = excp ? (((uint32_t)mbuf[w] << 16) | mbuf[w + 1]) : 0u;
-            body(i, v);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        Stage st;
+        if (first && base == 0) st = *first;
+        else st.load(packed, mask, excp, w0 + (base >> 4), lane);
+        st.put(wbuf, mbuf, excp, lane);
+        wave_lds_sync();
+        window_round(base, npos, excp, wbuf, mbuf, lane, body);
+        wave_lds_sync();
     }
 }
 
@@ -432,7 +467,7 @@ __device__ __forceinline__ void write_row(double* __restrict__ row, const uint32
 }
 
 template <bool P56, bool WAVE, bool LDS_COUNTS>
-__global__ void __launch_bounds__(kBlock) profile_kernel(
+__global__ void __launch_bounds__(kPBlock) profile_kernel(
     const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
     const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
     const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
@@ -453,18 +488,41 @@ __global__ void __launch_bounds__(kBlock) profile_kernel(
         for (int o = threadIdx.x; o < S; o += blockDim.x) col[o] = (uint16_t)col_of_ord[o];
         __syncthreads();
         const int kmin = P56 ? 5 : k;
-        for (int64_t c = (int64_t)blockIdx.x * wpb + wave; c < n; c += (int64_t)gridDim.x * wpb) {
+        // software pipeline over this wave's contigs: the next contig's offsets
+        // load at the top of the current one, and its first stage of packed
+        // words before the current row is written
+        struct Meta {
+            int64_t s = 0, L = 0, w0 = 0;
+            int32_t klen = 0;
+            bool exc = false;
+        };
+        auto meta = [&](int64_t cc, Meta& m) {
+            if (cc < n) {
+                m.s = off[cc];
+                m.L = off[cc + 1] - m.s;
+                m.w0 = woff[cc];
+                m.klen = keylen[cc];
+                m.exc = has_exc[cc] != 0;
+            }
+        };
+        const int64_t stride = (int64_t)gridDim.x * wpb;
+        int64_t c = (int64_t)blockIdx.x * wpb + wave;
+        Meta cur, nxt;
+        Stage st0;
+        meta(c, cur);
+        if (c < n) st0.load(packed, mask, cur.exc, cur.w0, lane);
+        for (; c < n; c += stride) {
+            meta(c + stride, nxt);
             for (int64_t j = lane; j < M; j += 64) counts[j] = 0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            const int64_t s = off[c], L = off[c + 1] - s;
-            const uint8_t* craw = raw + s;
+            wave_lds_sync();
+            const int64_t L = cur.L;
+            const uint8_t* craw = raw + cur.s;
             unsigned my = 0;
             auto add = [&](uint32_t cl) {
                 atomicAdd(&counts[cl], 1u);
                 ++my;
             };
-            for_each_window(packed, mask, has_exc[c] != 0, woff[c], L - kmin + 1, wbuf, mbuf, lane,
+            for_each_window(packed, mask, cur.exc, cur.w0, L - kmin + 1, wbuf, mbuf, lane,
                             [&](int64_t i, const Window& v) {
                 if (P56) {
                     if (v.clean(5)) add(col[v.code(5) * 5u]);
@@ -481,14 +539,16 @@ __global__ void __launch_bounds__(kBlock) profile_kernel(
                     if (v.clean(k)) add(col[v.code(k)]);
                     else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
                 }
-            });
+            }, &st0);
+            if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
             // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
 #pragma unroll
             for (int d = 32; d > 0; d >>= 1) my += __shfl_xor(my, d);
             if (lane == 0) row_tot[c] = (int64_t)my;
-            write_row(out + c * ld, counts, M, keylen[c], err, lane, 64);
+            write_row(out + c * ld, counts, M, cur.klen, err, lane, 64);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
+            cur = nxt;
         }
     } else {
         uint32_t* counts = LDS_COUNTS ? lds_counts : scratch + (int64_t)blockIdx.x * M;
@@ -868,17 +928,23 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
     bool with_len = p->kmode != 8;
     const bool wave = M <= kWaveMaxM && p->S <= 8192;
     const bool lds_ok = M * 4 <= 144 * 1024;
-    const int grid = wave ? grid_for(ceil_div(n, kBlock / 64), 2048) : grid_for(n, lds_ok ? 4096 : 1024);
+    const int grid = wave ? grid_for(ceil_div(n, kPBlock / 64), 2048) : grid_for(n, lds_ok ? 4096 : 1024);
     DevArray<uint32_t> scratch;
     if (!wave && !lds_ok && (rc = scratch.alloc(ctx, (size_t)grid * M))) return rc;
-    const size_t lds = wave ? (size_t)((p->S + 7) & ~7) * 2 + (kBlock / 64) * (((M + 3) & ~3) + 120) * 4
+    const size_t lds = wave ? (size_t)((p->S + 7) & ~7) * 2 + (kPBlock / 64) * (((M + 3) & ~3) + 120) * 4
                             : (lds_ok ? M * 4 : 0);
     const int k = p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode;
+    // wave variant: one round of resident blocks, each wave striding over contigs
 #define KARMA_PROFILE_LAUNCH(P56, W, LDS)                                                                        \
-    KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, W, LDS>), grid, kBlock, lds, c->packed.ptr,           \
-                 c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len,            \
-                 p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err.ptr,  \
-                 (int)p->S, p->row_tot.ptr)
+    do {                                                                                                         \
+        const int g_ = W ? resident_grid(ctx, reinterpret_cast<const void*>(&profile_kernel<P56, W, LDS>), kPBlock, \
+                                         lds, ceil_div(n, kPBlock / 64))                                         \
+                         : grid;                                                                                 \
+        KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, W, LDS>), g_, kPBlock, lds, c->packed.ptr,        \
+                     c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len,        \
+                     p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr,   \
+                     err.ptr, (int)p->S, p->row_tot.ptr);                                                        \
+    } while (0)
     if (p->kmode == KARMA_KMER_5P6) {
         if (wave) KARMA_PROFILE_LAUNCH(true, true, true);
         else if (lds_ok) KARMA_PROFILE_LAUNCH(true, false, true);
