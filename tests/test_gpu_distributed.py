@@ -31,7 +31,8 @@ def _worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     ctx = _lib.Context(0)
     blob, offs, key_len, rec = _inputs(rank, world)
-    build = ShardedBuild(ctx, comm, -1, N_LOC * world, rank * N_LOC, N_LOC)
+    # overlap: the local graph build runs concurrently on a second context
+    build = ShardedBuild(ctx, comm, -1, N_LOC * world, rank * N_LOC, N_LOC, overlap=True)
     store = engine.ContigStore(ctx, blob, offs, key_len)
     rec_dev = torch.from_numpy(rec.view(np.int64).reshape(-1)).to(build.ops.dev)
     res = build.run(store, rec_dev.data_ptr(), len(rec), keep=True)
@@ -73,3 +74,28 @@ def test_two_gpu_ranks_match_oracle(tmp_path):
     assert np.array_equal(w.view(np.uint64), o["weight"].view(np.uint64))
     for p in parts:
         assert np.array_equal(p["tot"], o["totals"])
+
+
+def test_overlap_equals_sequential_single_gpu():
+    # the graph build on a second context/stream, concurrent with the profile,
+    # gives the same bytes as the sequential build
+    from karma_amd import _lib, engine
+    from karma_amd.distributed import Comm, ShardedBuild
+    comm = Comm.create(1, 0)
+    ctx = _lib.Context(0)
+    blob, offs, key_len, rec = _inputs(0, 1)
+    store = engine.ContigStore(ctx, blob, offs, key_len)
+    outs = []
+    for overlap in (False, True):
+        build = ShardedBuild(ctx, comm, -1, N_LOC, 0, N_LOC, overlap=overlap)
+        rec_dev = torch.from_numpy(rec.view(np.int64).reshape(-1)).to(build.ops.dev)
+        res = build.run(store, rec_dev.data_ptr(), len(rec), keep=True)
+        e = res["edges"]
+        outs.append([res["profile"].cpu().numpy().copy(), np.array(e.a), np.array(e.b), np.array(e.weight),
+                     np.array(e.totals)])
+        build.close()
+    for x, y in zip(*outs):
+        assert x.shape == y.shape and np.array_equal(x.view(np.uint8), y.view(np.uint8))
+    assert len(outs[0][1]) > 0
+    store.close()
+    ctx.close()

@@ -5,7 +5,7 @@ Input: the per-kernel JSON of profiles/pmc_summary.py (rocprofv3 FETCH_SIZE and
 WRITE_SIZE passes, KiB per dispatch, reported there as MB).  Correction as
 MI355X_MICROARCH.md §HBM prescribes: on gfx950 FETCH_SIZE reports 1/2 of a
 wide (16 B/lane) streaming read, so reads are doubled; WRITE_SIZE is exact for
-16-B stores.  Both graph_partition and kmer_profile read/write 16 B per lane.
+16-B stores.  graph_classify, the partition and kmer_profile move 16 B per lane.
 
 Usage: python tools/pmc_traffic.py pmc_summary.json [out.json]
 """
@@ -14,7 +14,8 @@ import sys
 
 # rocprof kernel name -> bench.py kernel (KARMA_LAUNCH) name
 NAMES = {
-    "partition_kernel": "graph_partition",
+    "classify_kernel": "graph_classify",
+    "partition_kernel<CodeStream>": "graph_code_partition",
     "code_reduce_kernel": "graph_code_reduce",
     "profile_kernel<true, true, true>": "kmer_profile",
     "presence_kernel<true>": "kmer_presence",
