@@ -100,7 +100,6 @@ constexpr int kCW = 256;                // classify threads per block (4 indepen
 constexpr int kCIter = 512;             // records per wave step (8 per lane)
 constexpr int kCPer = kCIter / 128;     // 16-byte units per lane per step
 constexpr int64_t kCChunk = 8192;       // records per wave chunk (16 steps)
-constexpr int kListsPerBlock = 32;      // chunk lists per partition block (<= kMaxListsPerBlock)
 
 struct ClassArgs {
     const uint2* rec;
@@ -110,7 +109,8 @@ struct ClassArgs {
     uint32_t* codes;    // chunk c: [c * kCChunk, +n_codes[c]) codes, general starts from the end down
     uint32_t* n_codes;  // per chunk
     uint32_t* n_gen;    // per chunk
-    unsigned long long* blk_items;  // per partition block (kListsPerBlock chunks): codes
+    unsigned long long* blk_items;  // per partition block (lists_per_block chunks): codes
+    int lists_per_block;
     int64_t* big_list;
     unsigned* big_n;
     int* flags;  // 0 order, 1 contig range (2: general pair list full)
@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
     if (lane == 0) {
         P.n_codes[chunk] = nc;
         P.n_gen[chunk] = ng;
-        if (nc) atomicAdd(P.blk_items + chunk / kListsPerBlock, (unsigned long long)nc);
+        if (nc) atomicAdd(P.blk_items + chunk / P.lists_per_block, (unsigned long long)nc);
     }
     if (bad_order) P.flags[0] = 1;
     if (bad_contig) P.flags[1] = 1;
@@ -308,7 +308,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
                                                        uint64_t* __restrict__ pairs, int64_t pcap,
                                                        uint32_t* __restrict__ n_pairs,
                                                        unsigned long long* __restrict__ blk_items,
-                                                       int* __restrict__ flags) {
+                                                       int lists_per_block, int* __restrict__ flags) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t chunk = (int64_t)blockIdx.x * (kGW / 64) + wave;
     if (chunk >= n_chunks) return;
@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
     }
     if (lane == 0) {
         n_pairs[chunk] = np;
-        if (np) atomicAdd(blk_items + chunk / kListsPerBlock, (unsigned long long)np);
+        if (np) atomicAdd(blk_items + chunk / lists_per_block, (unsigned long long)np);
         if (full) flags[2] = 1;  // the host reruns with room for every pair
     }
 }
@@ -1039,7 +1039,11 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     KARMA_TRY(make_geo(N, &g));
     const int B = g.B;
     const int64_t n_chunks = std::max<int64_t>(1, ceil_div(A, kCChunk));
-    const int64_t n_pblk = ceil_div(n_chunks, kListsPerBlock);
+    // partition: one round of resident blocks, each taking consecutive chunk lists
+    const int resident = resident_grid(ctx, reinterpret_cast<const void*>(&partition_kernel<CodeStream>), kPT, 0,
+                                       int64_t(1) << 30);
+    const int lpb = (int)std::min<int64_t>(kMaxListsPerBlock, ceil_div(n_chunks, resident));
+    const int64_t n_pblk = ceil_div(n_chunks, lpb);
     // per-step scratch
     DevArray<uint32_t> codes, n_codes, n_gen, n_pl;
     DevArray<int64_t> big_list;
@@ -1084,7 +1088,10 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     DevArray<int64_t> pf_base;
     unsigned hc[3] = {0, 0, 0};
     // reduce geometry: grids fixed here, flush ranges from device counters
-    const int n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, ceil_div(512, g.Bc)) : 0;
+    // code reduce: one round (one 128 KB-LDS block per CU), at most ~4 flushes per group
+    const int n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count / g.Bc,
+                                                                              ceil_div(max_cflush, 4)))
+                              : 0;
     const int n_pg = (int)std::max<int64_t>(1, ceil_div(256, B));
     const int64_t nsl = (int64_t)B * n_pg;
     DevArray<uint32_t> part_ch, part_b, part_k, part_c;
@@ -1111,25 +1118,25 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, ctrl_words * 8, ctx->stream));
         KARMA_HIP(hipMemsetAsync(blk_items.ptr, 0, 2 * n_pblk * 8, ctx->stream));
         if (A > 0) {
-            ClassArgs C{rec,      A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
-                        n_gen.ptr, blk_items.ptr, big_list.ptr, counters, flags};
+            ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
+                        n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags};
             KARMA_LAUNCH(ctx, "graph_classify", classify_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         } else {
             KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
             KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
-                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_pblk, flags);
+                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_pblk, lpb, flags);
         const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items.ptr};
         pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items.ptr + n_pblk};
         if (g.Bc > 0) {
             KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr,
-                         kCChunk, n_codes.ptr, n_chunks, kListsPerBlock, g, cent.ptr, cdir);
+                         kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
             KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
                          g.Bc, g.bwc, n_cg, part_ch.ptr);
         }
         KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
-                     n_pl.ptr, n_chunks, kListsPerBlock, g, pent.ptr, pdir);
+                     n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
         KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
                      g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
         KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits, g.bwc,
