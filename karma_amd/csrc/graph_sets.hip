@@ -490,14 +490,20 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
     // items [base, base + kCap) of the range into registers (thread t: t + k * kPT)
     S v[kPer];
     auto load = [&](uint32_t base) {
+        // the thread's items rise with k: one fixed-step search for the first,
+        // then forward steps (lists hold ~2.7K codes, items are kPT apart)
+        int lo = 0;
+        {
+            const uint32_t g0 = base + threadIdx.x;
+#pragma unroll
+            for (int step = kMaxListsPerBlock / 2; step >= 1; step >>= 1)
+                if (lpre[lo + step] <= g0) lo += step;
+        }
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const uint32_t gi = base + threadIdx.x + k * kPT;
             if (gi < items) {
-                int lo = 0;  // list L: lpre[L] <= gi < lpre[L + 1], fixed steps
-#pragma unroll
-                for (int step = kMaxListsPerBlock / 2; step >= 1; step >>= 1)
-                    if (lpre[lo + step] <= gi) lo += step;
+                while (lpre[lo + 1] <= gi) ++lo;  // list L: lpre[L] <= gi < lpre[L + 1]
                 v[k] = lists[(l_lo + lo) * list_cap + (gi - lpre[lo])];
             }
         }
