@@ -18,6 +18,9 @@
  *   karma_pairs_merge / _totals     (new) multi-GPU edge merge, SURVEY.md §8(e)
  *   karma_edges_*                   the normalised weight (s/|A| + s/|B|)/2  read_graph.py:39-42, :128-130
  *   karma_synth_*                   (new) deterministic synthetic inputs, SURVEY.md §8(d)
+ *   karma_fasta_*                   read_fasta_file                      karma/karma.py:40-61
+ *   karma_eq_*                      eq_classes.txt parse                 karma/read_graph.py:75-92
+ *   karma_sam_*                     Contig readsets from SAM lines       karma/contig.py:24,34, hisat2.py:76-81
  *
  * The reference is pure Python and has no FFI; INTEGRATION.md shows the ctypes
  * binding (karma_amd/_lib.py) that the Python classes mirroring the reference
@@ -42,6 +45,7 @@ extern "C" {
 #define KARMA_ERR_ZERO_DIV (-5)  /* non-zero count over a zero normaliser (ZeroDivisionError) */
 #define KARMA_ERR_UNSORTED (-6)  /* records not grouped by read (read ids must not decrease)  */
 #define KARMA_ERR_STATE (-7)     /* call out of order (e.g. profile before finalize)          */
+#define KARMA_ERR_PARSE (-8)     /* input text outside what the C++ parser reproduces exactly */
 
 #define KARMA_KMER_5P6 (-1) /* kmer.py:69 "5p6": all 5-mers + string-palindromic 6-mers */
 
@@ -168,6 +172,43 @@ int karma_synth_read_counts(uint64_t seed, const int64_t* gene_first, const int3
                             int64_t frag_lo, int64_t frag_hi, int paired, int32_t* rec_count);
 int karma_synth_read_records(uint64_t seed, const int64_t* gene_first, const int32_t* gene_size, int64_t n_genes,
                              int64_t frag_lo, int64_t frag_hi, int paired, const int64_t* rec_off, uint32_t* records);
+
+/* ---- host ingestion (C++, std::threads; no device needed) ----------------
+ * Parsers over an in-memory file image, with Python text-mode semantics
+ * (strict UTF-8, universal newlines).  Input the parser cannot reproduce
+ * exactly (a malformed line, a non-ASCII integer, a duplicate eq name, ...)
+ * returns KARMA_ERR_PARSE; the Python front end then raises the reference's
+ * own exception.  threads <= 0: hardware concurrency. */
+typedef struct karma_fasta karma_fasta;
+/* read_fasta_file: records in OrderedDict order, keys with ">" kept.
+ * seq: seq_bytes + 16 zero bytes of padding (the karma_contigs_create layout);
+ * key_len in code points; ascii = 1 when every byte is < 0x80. */
+int karma_fasta_parse(const char* data, size_t len, int threads, karma_fasta** out);
+int karma_fasta_info(karma_fasta* f, int64_t* n, int64_t* seq_bytes, int64_t* key_bytes, int* ascii);
+int karma_fasta_get(karma_fasta* f, uint8_t* seq, int64_t* seq_off, char* keys, int64_t* key_off,
+                    int32_t* key_len);
+int karma_fasta_destroy(karma_fasta* f);
+
+typedef struct karma_eq karma_eq;
+/* eq_classes.txt -> names + the karma_graph_eq arrays (cls_off[C+1], members,
+ * counts, pair_skip = eq_size token == "1"). */
+int karma_eq_parse(const char* data, size_t len, int threads, karma_eq** out);
+int karma_eq_info(karma_eq* q, int64_t* n_contigs, int64_t* n_classes, int64_t* n_members, int64_t* name_bytes);
+int karma_eq_get(karma_eq* q, char* names, int64_t* name_off, int64_t* cls_off, uint32_t* members, int64_t* counts,
+                 uint8_t* pair_skip);
+int karma_eq_destroy(karma_eq* q);
+
+typedef struct karma_sam karma_sam;
+/* SAM lines -> one (read id, contig id) record per line (the karma_graph_records
+ * input, unsorted); contig ids number RNAMEs in order of first appearance, read
+ * ids are an injective numbering of QNAMEs below read_id_bound.  q_start/q_len
+ * locate each line's QNAME in the caller's buffer. */
+int karma_sam_parse(const char* data, size_t len, int skip_headers, int threads, karma_sam** out);
+int karma_sam_info(karma_sam* s, int64_t* n_records, int64_t* n_reads, int64_t* n_contigs, int64_t* rname_bytes,
+                   int64_t* read_id_bound);
+int karma_sam_get(karma_sam* s, uint32_t* records, char* rnames, int64_t* rname_off, int64_t* q_start,
+                  int32_t* q_len);
+int karma_sam_destroy(karma_sam* s);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkarma_hip.so")
+# KARMA_LIB: an alternative build of the same library (tools/build_variant.sh A/B timing)
+LIB_PATH = os.environ.get("KARMA_LIB") or os.path.join(HERE, "libkarma_hip.so")
 
 KARMA_OK = 0
 KARMA_ERR_ARG = -1
@@ -23,6 +24,7 @@ KARMA_ERR_OOM = -4
 KARMA_ERR_ZERO_DIV = -5
 KARMA_ERR_UNSORTED = -6
 KARMA_ERR_STATE = -7
+KARMA_ERR_PARSE = -8
 
 KARMA_KMER_5P6 = -1
 KARMA_REC_SORTED = 0
@@ -86,6 +88,18 @@ _SIGS = {
     "karma_synth_genes": [_u64, _i64, _i32, _c_p, _c_p],
     "karma_synth_read_counts": [_u64, _c_p, _c_p, _i64, _i64, _i64, _i32, _c_p],
     "karma_synth_read_records": [_u64, _c_p, _c_p, _i64, _i64, _i64, _i32, _c_p, _c_p],
+    "karma_fasta_parse": [_c_p, ctypes.c_size_t, _i32, _PP],
+    "karma_fasta_info": [_c_p, _I64P, _I64P, _I64P, ctypes.POINTER(ctypes.c_int)],
+    "karma_fasta_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
+    "karma_fasta_destroy": [_c_p],
+    "karma_eq_parse": [_c_p, ctypes.c_size_t, _i32, _PP],
+    "karma_eq_info": [_c_p, _I64P, _I64P, _I64P, _I64P],
+    "karma_eq_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
+    "karma_eq_destroy": [_c_p],
+    "karma_sam_parse": [_c_p, ctypes.c_size_t, _i32, _i32, _PP],
+    "karma_sam_info": [_c_p, _I64P, _I64P, _I64P, _I64P, _I64P],
+    "karma_sam_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
+    "karma_sam_destroy": [_c_p],
 }
 
 EXPORTED = tuple(_SIGS) + ("karma_last_error",)

@@ -5,8 +5,11 @@ mates of a pair count once (contig.py:11).  `contig_records` turns a list of
 Contig objects into the (read id, contig index) record stream the HIP graph
 kernels consume (karma_amd.engine.graph_from_records).
 """
+import io
+
 import numpy as np
 
+from . import ingest
 from .logs import logger
 
 
@@ -32,6 +35,50 @@ class Contig:
         for line in sam_infos:
             read, _, name, position, *_ = line.split("\t")
             self.add_read(read, position)
+
+
+def _sam_bytes(sam):
+    """SAM input as bytes: a path, str/bytes text, or an iterable of lines."""
+    if isinstance(sam, (bytes, bytearray)):
+        return bytes(sam)
+    if isinstance(sam, str):
+        if "\t" in sam or "\n" in sam:
+            return sam.encode("utf-8")
+        return ingest._read(sam)
+    return "".join(line if line.endswith(("\n", "\r")) else line + "\n" for line in sam).encode("utf-8")
+
+
+def _check_sam_text(data, skip_headers):
+    """The reference's per-line unpack (contig.py:34) over lines the C++ reader
+    declined: raises its ValueError / UnicodeDecodeError."""
+    for line in io.StringIO(data.decode("utf-8"), newline=None):  # text-mode lines
+        if skip_headers and line.startswith("@"):
+            continue
+        read, _, name, position, *_ = line.split("\t")
+
+
+def load_sam_records(sam, skip_headers=True, threads=0):
+    """SAM lines -> ingest.SamRecords: one (read id, contig id) record per line,
+    contig ids numbering RNAMEs (field 3) in order of first appearance
+    (csrc/ingest.cpp, karma_sam_parse).  skip_headers drops "@" lines as the
+    hisat2 generator does (hisat2.py:76-81)."""
+    data = _sam_bytes(sam)
+    try:
+        return ingest.parse_sam(data, skip_headers, threads), data
+    except ingest.ParseDeferred:
+        _check_sam_text(data, skip_headers)
+        raise
+
+
+def contigs_from_sam(sam, skip_headers=True, threads=0):
+    """Contig objects grouped by RNAME (first appearance order), each with the
+    readset contig.py:24,34 builds from its lines."""
+    rec, data = load_sam_records(sam, skip_headers, threads)
+    contigs = [Contig(n) for n in rec.rnames]
+    qs, ql, cid = rec.q_start.tolist(), rec.q_len.tolist(), rec.records[:, 1].tolist()
+    for s0, n, c in zip(qs, ql, cid):
+        contigs[c].readset.add(data[s0:s0 + n].decode("utf-8"))
+    return contigs
 
 
 def contig_records(contigs, start_index=0, read_ids=None):

@@ -116,8 +116,19 @@ struct ClassArgs {
     int* flags;  // 0 order, 1 contig range (2: general pair list full)
 };
 
+// lanes below this one with their bit set in a wave mask
+__device__ __forceinline__ int rank_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // code (m0 | M << 24) of a compact read, or general / big
-__global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
+// 6 waves per SIMD: the LDS slices allow 6 blocks per CU; 80 VGPRs fit them
+// (the compiler's own choice, 82-84, allows 5: 0.714 -> 0.670 ms on config 3)
+#ifndef KARMA_CLS_WAVES
+#define KARMA_CLS_WAVES 6
+#endif
+#define KARMA_CLS_ATTR __attribute__((amdgpu_waves_per_eu(KARMA_CLS_WAVES, KARMA_CLS_WAVES)))
+__global__ void __launch_bounds__(kCW) KARMA_CLS_ATTR classify_kernel(ClassArgs P) {
     __shared__ uint2 srec[kCW / 64][kCIter + kMaxFast];
     __shared__ uint16_t wst[kCW / 64][kCIter + 1];  // read starts (+ the end of the last read)
     __shared__ uint16_t wcl[kCW / 64][kCIter];      // reads by size class
@@ -130,7 +141,6 @@ __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
     uint16_t* ws = wst[wave];
     uint16_t* cl = wcl[wave];
     uint32_t* out = P.codes + c_lo;
-    const unsigned long long lower = (1ull << lane) - 1ull;
 
     // register prefetch of a step: unit u, lane l holds records 128u + 2l, +1;
     // plus the record before the step (read-boundary carry) and the 8 after it
@@ -183,7 +193,7 @@ __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
                 s1 = x0 != x1;
             }
             const unsigned long long b0 = __ballot(s0), b1 = __ballot(s1);
-            const int pos = ns + __popcll(b0 & lower) + __popcll(b1 & lower);
+            const int pos = ns + rank_below(b0) + rank_below(b1);
             if (s0) ws[pos] = (uint16_t)j;
             if (s1) ws[pos + (s0 ? 1 : 0)] = (uint16_t)(j + 1);
             ns += __popcll(b0) + __popcll(b1);
@@ -221,8 +231,8 @@ __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
             const bool sm = k < ns && sz <= 4, lg = k < ns && sz > 4;
             const unsigned long long bs = __ballot(sm), bl = __ballot(lg);
             const uint16_t e = (uint16_t)(j0 | sz << 10);
-            if (sm) cl[n_s + __popcll(bs & lower)] = e;
-            if (lg) cl[kCIter - 1 - (n_l + __popcll(bl & lower))] = e;
+            if (sm) cl[n_s + rank_below(bs)] = e;
+            if (lg) cl[kCIter - 1 - (n_l + rank_below(bl))] = e;
             n_s += __popcll(bs);
             n_l += __popcll(bl);
         }
@@ -255,8 +265,8 @@ __global__ void __launch_bounds__(kCW) classify_kernel(ClassArgs P) {
         };
         auto emit = [&](uint32_t code, bool gen, int j0) {
             const unsigned long long cb = __ballot(code != kEmpty), gb = __ballot(gen);
-            if (code != kEmpty) out[nc + __popcll(cb & lower)] = code;
-            if (gen) out[kCChunk - 1 - (ng + __popcll(gb & lower))] = (uint32_t)(t0 - c_lo + j0);
+            if (code != kEmpty) out[nc + rank_below(cb)] = code;
+            if (gen) out[kCChunk - 1 - (ng + rank_below(gb))] = (uint32_t)(t0 - c_lo + j0);
             nc += __popcll(cb);
             ng += __popcll(gb);
         };

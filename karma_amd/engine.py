@@ -164,7 +164,8 @@ def kmer_profile(sequences, kmer_size, ctx=None):
     Returns (profile float64[N, M], columns list[str], row_totals int64[N])."""
     ctx = ctx or _lib.default_context()
     kmode = kmode_of(kmer_size)
-    blob, offs, key_len = encode_sequences(sequences)
+    packed = getattr(sequences, "karma_packed", None)  # fasta.FastaDict straight from the C++ reader
+    blob, offs, key_len = packed if packed is not None else encode_sequences(sequences)
     store = ContigStore(ctx, blob, offs, key_len)
     try:
         plan = KmerPlan(ctx, store, kmode)

@@ -1,0 +1,153 @@
+"""Host ingestion through the C++ parsers of libkarma_hip.so (csrc/ingest.cpp).
+
+  parse_fasta  read_fasta_file's records (karma/karma.py:40-61)
+  parse_eq     the eq_classes.txt parse (karma/read_graph.py:75-92)
+  parse_sam    per-line (read, contig) records from SAM text (karma/contig.py:24,34)
+
+Each returns plain numpy arrays.  The parsers accept exactly the input whose
+reference result they reproduce and raise ``ParseDeferred`` for anything else.
+The callers in fasta.py, read_graph.py and contig.py then run the reference's
+own Python reading of that file, so a malformed file raises the reference's
+exception (ValueError, KeyError, AssertionError, UnicodeDecodeError).
+"""
+import ctypes
+import locale
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import KARMA_ERR_PARSE, KarmaError, call
+
+
+class ParseDeferred(Exception):
+    """The C++ parser declined; the reference-semantics reader decides."""
+
+
+def _utf8_locale():
+    # text-mode open() decodes with the locale's preferred encoding
+    return locale.getpreferredencoding(False).lower().replace("-", "") in ("utf8",)
+
+
+def _read(path):
+    with open(path, "rb") as fh:
+        return fh.read()
+
+
+def _parse(fn, data, *args):
+    h = ctypes.c_void_p()
+    try:
+        call(fn, ctypes.c_char_p(data), len(data), *args, ctypes.byref(h))
+    except KarmaError as e:
+        if e.code == KARMA_ERR_PARSE:
+            raise ParseDeferred(str(e)) from None
+        raise
+    return h
+
+
+def _buf(n, dtype):
+    return np.empty(max(int(n), 1), dtype)
+
+
+@dataclass
+class FastaRecords:
+    seq: np.ndarray       # uint8, UTF-8 (latin-1 == ASCII when ascii), + 16 bytes padding
+    seq_off: np.ndarray   # int64[N + 1]
+    keys: bytes           # UTF-8 key bytes
+    key_off: np.ndarray   # int64[N + 1]
+    key_len: np.ndarray   # int32[N], code points
+    ascii: bool
+
+    def __len__(self):
+        return len(self.key_len)
+
+    def names(self):
+        k, o = self.keys, self.key_off.tolist()
+        return [k[o[i]:o[i + 1]].decode("utf-8") for i in range(len(self.key_len))]
+
+    def sequences(self):
+        b, o = self.seq.tobytes(), self.seq_off.tolist()
+        return [b[o[i]:o[i + 1]].decode("utf-8") for i in range(len(self.key_len))]
+
+
+def parse_fasta(data: bytes, threads=0) -> FastaRecords:
+    if not _utf8_locale():
+        raise ParseDeferred("locale encoding is not UTF-8")
+    h = _parse("karma_fasta_parse", data, threads)
+    try:
+        n, sb, kb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        asc = ctypes.c_int()
+        call("karma_fasta_info", h, ctypes.byref(n), ctypes.byref(sb), ctypes.byref(kb), ctypes.byref(asc))
+        N = n.value
+        seq = np.empty(sb.value + 16, np.uint8)
+        seq_off = np.empty(N + 1, np.int64)
+        keys = ctypes.create_string_buffer(max(kb.value, 1))
+        key_off = np.empty(N + 1, np.int64)
+        key_len = _buf(N, np.int32)
+        call("karma_fasta_get", h, _lib.ptr(seq), _lib.ptr(seq_off), keys, _lib.ptr(key_off), _lib.ptr(key_len))
+        return FastaRecords(seq, seq_off, keys.raw[:kb.value], key_off, key_len[:N], bool(asc.value))
+    finally:
+        _lib.load().karma_fasta_destroy(h)
+
+
+@dataclass
+class EqClasses:
+    names: list
+    cls_off: np.ndarray   # int64[C + 1]
+    members: np.ndarray   # uint32
+    counts: np.ndarray    # int64[C]
+    pair_skip: np.ndarray  # uint8[C], eq_size token == "1"
+
+
+def parse_eq(data: bytes, threads=0) -> EqClasses:
+    if not _utf8_locale():
+        raise ParseDeferred("locale encoding is not UTF-8")
+    h = _parse("karma_eq_parse", data, threads)
+    try:
+        v = [ctypes.c_int64() for _ in range(4)]
+        call("karma_eq_info", h, *[ctypes.byref(x) for x in v])
+        n, C, nm, nb = (x.value for x in v)
+        names = ctypes.create_string_buffer(max(nb, 1))
+        name_off = np.empty(n + 1, np.int64)
+        cls_off = np.empty(C + 1, np.int64)
+        members = _buf(nm, np.uint32)
+        counts = _buf(C, np.int64)
+        skip = _buf(C, np.uint8)
+        call("karma_eq_get", h, names, _lib.ptr(name_off), _lib.ptr(cls_off), _lib.ptr(members),
+             _lib.ptr(counts), _lib.ptr(skip))
+        raw, o = names.raw[:nb], name_off.tolist()
+        return EqClasses([raw[o[i]:o[i + 1]].decode("utf-8") for i in range(n)], cls_off, members[:nm],
+                         counts[:C], skip[:C])
+    finally:
+        _lib.load().karma_eq_destroy(h)
+
+
+@dataclass
+class SamRecords:
+    records: np.ndarray   # uint32[L, 2]: read id, contig id (file order)
+    rnames: list          # contig id -> RNAME, in order of first appearance
+    q_start: np.ndarray   # int64[L]: QNAME byte range in the parsed buffer
+    q_len: np.ndarray     # int32[L]
+    n_reads: int
+    read_id_bound: int
+
+
+def parse_sam(data: bytes, skip_headers=True, threads=0) -> SamRecords:
+    if not _utf8_locale():
+        raise ParseDeferred("locale encoding is not UTF-8")
+    h = _parse("karma_sam_parse", data, 1 if skip_headers else 0, threads)
+    try:
+        v = [ctypes.c_int64() for _ in range(5)]
+        call("karma_sam_info", h, *[ctypes.byref(x) for x in v])
+        L, nr, nc, rb, bound = (x.value for x in v)
+        rec = np.empty((max(L, 1), 2), np.uint32)
+        rn = ctypes.create_string_buffer(max(rb, 1))
+        rn_off = np.empty(nc + 1, np.int64)
+        qs = _buf(L, np.int64)
+        ql = _buf(L, np.int32)
+        call("karma_sam_get", h, _lib.ptr(rec), rn, _lib.ptr(rn_off), _lib.ptr(qs), _lib.ptr(ql))
+        raw, o = rn.raw[:rb], rn_off.tolist()
+        return SamRecords(rec[:L], [raw[o[i]:o[i + 1]].decode("utf-8") for i in range(nc)], qs[:L], ql[:L], nr,
+                          bound)
+    finally:
+        _lib.load().karma_sam_destroy(h)

@@ -16,9 +16,9 @@ import os
 import networkx as nx
 import numpy as np
 
-from . import engine
+from . import engine, ingest
 from ._lib import KARMA_ERR_ZERO_DIV, KarmaError
-from .contig import contig_records
+from .contig import contig_records, load_sam_records
 from .logs import logger
 
 
@@ -31,10 +31,22 @@ def _edges_or_zero_div(fn, *args, **kw):
         raise
 
 
-def parse_eq_classes(equivalence_class_file):
-    """Parse salmon eq_classes.txt exactly as read_graph.py:75-92 does.
+def parse_eq_classes(equivalence_class_file, threads=0):
+    """Parse salmon eq_classes.txt exactly as read_graph.py:75-92 does, with the
+    C++ parser (csrc/ingest.cpp, karma_eq_parse).  A file it declines goes
+    through the reference's own reading (_parse_eq_text), which raises the
+    reference's exception or, for exotic-but-valid text, returns its result.
 
     Returns (names, cls_off int64[C+1], members uint32, counts int64, pair_skip uint8)."""
+    try:
+        q = ingest.parse_eq(ingest._read(equivalence_class_file), threads)
+    except ingest.ParseDeferred:
+        return _parse_eq_text(equivalence_class_file)
+    return q.names, q.cls_off, q.members, q.counts, q.pair_skip
+
+
+def _parse_eq_text(equivalence_class_file):
+    """read_graph.py:75-92 line by line (int(), str keys, the :93 assert)."""
     with open(equivalence_class_file, "r") as reader:
         no_of_contigs = int(reader.readline())
         _ = reader.readline()
@@ -87,6 +99,21 @@ class ReadGraph(nx.Graph):
             names = [c.name for c in contigs]
             # combinations order: row 0 touches every contig, so nodes appear
             # in list order; edges are added in (i, j) order = sorted order
+            graph.add_nodes_from(names)
+            for a, b, w in zip(e.a.tolist(), e.b.tolist(), e.weight.tolist()):
+                graph.add_edge(names[a], names[b], weight=w)
+        return cls(incoming_graph_data=graph)
+
+    @classmethod
+    def from_sam(cls, sam, skip_headers: bool = True, threads: int = 0) -> "ReadGraph":
+        """from_contigs over the contigs of SAM lines (contig.py:24,34 readsets,
+        grouped by RNAME in order of first appearance) without building Python
+        readsets: the C++ reader's (read, contig) records go straight to the GPU."""
+        rec, _ = load_sam_records(sam, skip_headers, threads)
+        graph = nx.Graph()
+        names = rec.rnames
+        if len(names) >= 2:
+            e = _edges_or_zero_div(engine.graph_from_records, rec.records, len(names), grouped=False)
             graph.add_nodes_from(names)
             for a, b, w in zip(e.a.tolist(), e.b.tolist(), e.weight.tolist()):
                 graph.add_edge(names[a], names[b], weight=w)

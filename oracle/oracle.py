@@ -296,3 +296,37 @@ def graph_dump(g):
 
 def sequences_from_pairs(pairs):
     return OrderedDict(pairs)
+
+
+def read_fasta_file(path):
+    """read_fasta_file (karma/karma.py:40-61): text-mode line loop, key =
+    header.rstrip("\\n").split(" ")[0], sequence = concatenated stripped lines,
+    OrderedDict assignment for repeated keys."""
+    sequences = OrderedDict()
+    with open(path, "r", encoding="utf-8") as reader:
+        name = reader.readline().rstrip("\n").split(" ")[0]
+        seq = ""
+        for line in reader:
+            if line.startswith(">"):
+                sequences[name] = seq
+                name = line.rstrip("\n").split(" ")[0]
+                seq = ""
+            else:
+                seq += line.rstrip("\n")
+        sequences[name] = seq
+    return sequences
+
+
+def sam_groups(text, skip_headers=True):
+    """SAM text -> [(RNAME, set(QNAME))] in order of first RNAME appearance:
+    contig.py:29-35's readset per RNAME group (universal newlines, hisat2.py:76-81
+    header filter)."""
+    import io
+
+    groups = OrderedDict()
+    for line in io.StringIO(text, newline=None):  # text-mode line iteration
+        if skip_headers and line.startswith("@"):
+            continue
+        read, _, name, position, *_ = line.split("\t")
+        groups.setdefault(name, set()).add(read)
+    return list(groups.items())
