@@ -711,6 +711,7 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
         return rc;
     }
     KARMA_HIP(hipMemsetAsync(p->presence.ptr, 0, p->nwords * 4, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(p->row_tot.ptr, 0, (c->n ? c->n : 1) * 8, ctx->stream));
     KARMA_HIP(hipMemsetAsync(exc_cnt.ptr, 0, 8, ctx->stream));
     DevArray<int> full;
     if ((rc = full.alloc(ctx, 1))) {
@@ -907,10 +908,10 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(ld >= p->M, KARMA_ERR_ARG, "ld (%lld) < M (%lld)", (long long)ld, (long long)p->M);
     const int64_t n = c->n, M = p->M;
-    if (n == 0 || M == 0) {
-        if (n && M == 0) return KARMA_OK;
-        return KARMA_OK;
-    }
+    if (n == 0) return KARMA_OK;
+    // row totals first: with M == 0 every row is all-zero (kmer.py:250-258)
+    KARMA_HIP(hipMemsetAsync(p->row_tot.ptr, 0, n * 8, ctx->stream));
+    if (M == 0) return KARMA_OK;
     KARMA_CHECK(out, KARMA_ERR_ARG, "null out");
     KARMA_CHECK(c->zero_key_maxlen < p->kmin, KARMA_ERR_ZERO_DIV,
                 "division by zero: a contig with a zero-length key has k-mers");
@@ -924,7 +925,6 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
     DevArray<int> err;
     if ((rc = err.alloc(ctx, 1))) return rc;
     KARMA_HIP(hipMemsetAsync(err.ptr, 0, 4, ctx->stream));
-    KARMA_HIP(hipMemsetAsync(p->row_tot.ptr, 0, n * 8, ctx->stream));
     bool with_len = p->kmode != 8;
     const bool wave = M <= kWaveMaxM && p->S <= 8192;
     const bool lds_ok = M * 4 <= 144 * 1024;
