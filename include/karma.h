@@ -187,6 +187,9 @@ int karma_fasta_parse(const char* data, size_t len, int threads, karma_fasta** o
 int karma_fasta_info(karma_fasta* f, int64_t* n, int64_t* seq_bytes, int64_t* key_bytes, int* ascii);
 int karma_fasta_get(karma_fasta* f, uint8_t* seq, int64_t* seq_off, char* keys, int64_t* key_off,
                     int32_t* key_len);
+/* Zero-copy view of the parsed arrays (valid until karma_fasta_destroy). */
+int karma_fasta_view(karma_fasta* f, const uint8_t** seq, const int64_t** seq_off, const char** keys,
+                     const int64_t** key_off, const int32_t** key_len);
 int karma_fasta_destroy(karma_fasta* f);
 
 typedef struct karma_eq karma_eq;

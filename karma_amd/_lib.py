@@ -91,6 +91,7 @@ _SIGS = {
     "karma_fasta_parse": [_c_p, ctypes.c_size_t, _i32, _PP],
     "karma_fasta_info": [_c_p, _I64P, _I64P, _I64P, ctypes.POINTER(ctypes.c_int)],
     "karma_fasta_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
+    "karma_fasta_view": [_c_p, _PP, _PP, _PP, _PP, _PP],
     "karma_fasta_destroy": [_c_p],
     "karma_eq_parse": [_c_p, ctypes.c_size_t, _i32, _PP],
     "karma_eq_info": [_c_p, _I64P, _I64P, _I64P, _I64P],

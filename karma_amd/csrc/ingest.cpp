@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -191,13 +192,52 @@ uint64_t hash_bytes(const uint8_t* s, size_t n) {
 //   normalises by len(key)).
 // ============================================================================
 struct karma_fasta {
-    std::vector<uint8_t> seq;
-    std::vector<int64_t> seq_off;  // N + 1
-    std::vector<char> keys;
-    std::vector<int64_t> key_off;  // N + 1
-    std::vector<int32_t> key_len;  // code points
+    std::unique_ptr<uint8_t[]> seq;  // seq_off[N] bytes + 16 zero bytes of padding (karma_contigs_create)
+    std::vector<int64_t> seq_off;    // N + 1
+    std::unique_ptr<char[]> keys;
+    std::vector<int64_t> key_off;    // N + 1
+    std::vector<int32_t> key_len;    // code points
     bool ascii = true;
 };
+
+namespace {
+
+// line terminator bytes in [p, p + n), and the OR of all bytes (high bit: not ASCII)
+inline int64_t count_nl(const uint8_t* p, size_t n, uint8_t* acc) {
+    int64_t c = 0;
+    uint8_t o = 0;
+    for (size_t i = 0; i < n; ++i) {
+        c += (p[i] == '\n') | (p[i] == '\r');
+        o |= p[i];
+    }
+    *acc |= o;
+    return c;
+}
+
+// open-addressing set of byte strings: first index of each distinct key
+struct KeyTable {
+    std::vector<int64_t> slot;  // -1 empty, else an item index
+    size_t mask;
+    explicit KeyTable(size_t n) {
+        size_t cap = 16;
+        while (cap < 2 * n + 16) cap <<= 1;
+        slot.assign(cap, -1);
+        mask = cap - 1;
+    }
+    // returns the index stored for the key (inserting `idx` if new)
+    template <typename Eq>
+    int64_t find_or_insert(uint64_t h, int64_t idx, Eq eq) {
+        for (size_t i = h & mask;; i = (i + 1) & mask) {
+            if (slot[i] < 0) {
+                slot[i] = idx;
+                return idx;
+            }
+            if (eq(slot[i])) return slot[i];
+        }
+    }
+};
+
+}  // namespace
 
 extern "C" int karma_fasta_parse(const char* data_c, size_t len, int threads, karma_fasta** out) {
     if (!out || (!data_c && len)) {
@@ -208,22 +248,36 @@ extern "C" int karma_fasta_parse(const char* data_c, size_t len, int threads, ka
     const uint8_t* s = reinterpret_cast<const uint8_t*>(data_c);
     const int T = clamp_threads(threads, len, 1 << 20);
     const size_t per = (len + T - 1) / (size_t)T;
-    // ---- 1: header line starts (a '>' right after a line terminator) + ASCII check
-    std::vector<std::vector<size_t>> hs(T);
-    std::vector<char> t_ascii(T, 1);
+    // ---- 1 (one pass): header line starts (a '>' right after a line terminator),
+    // terminator counts between them, and the byte OR (ASCII check)
+    struct Chunk {
+        int64_t head_nl = 0;          // terminators before the chunk's first header
+        std::vector<size_t> pos;      // headers found in the chunk
+        std::vector<int64_t> nl;      // terminators from each header to the next / the chunk end
+        uint8_t acc = 0;
+    };
+    std::vector<Chunk> ch(T);
     parallel_for(T, [&](int t) {
+        Chunk& C = ch[t];
         const size_t lo = std::min(len, (size_t)t * per), hi = std::min(len, lo + per);
-        t_ascii[t] = is_ascii(s + lo, hi - lo);
+        size_t seg = lo;
+        int64_t* cur = &C.head_nl;
         for (size_t p = std::max<size_t>(lo, 1); p < hi;) {
             const void* q = memchr(s + p, '>', hi - p);
             if (!q) break;
             const size_t i = (const uint8_t*)q - s;
-            if (is_nl(s[i - 1])) hs[t].push_back(i);
             p = i + 1;
+            if (!is_nl(s[i - 1])) continue;
+            *cur += count_nl(s + seg, i - seg, &C.acc);
+            C.pos.push_back(i);
+            C.nl.push_back(0);
+            cur = &C.nl.back();
+            seg = i;
         }
+        *cur += count_nl(s + seg, hi - seg, &C.acc);
     });
     bool ascii = true;
-    for (int t = 0; t < T; ++t) ascii = ascii && t_ascii[t];
+    for (auto& C : ch) ascii = ascii && C.acc < 0x80;
     if (!ascii) {
         const size_t bad = utf8_invalid_at(s, len);
         if (bad != len) {
@@ -231,14 +285,21 @@ extern "C" int karma_fasta_parse(const char* data_c, size_t len, int threads, ka
             return KARMA_ERR_PARSE;
         }
     }
-    std::vector<size_t> h(1, 0);  // record r: header line at h[r], body up to h[r + 1]
-    for (auto& v : hs) h.insert(h.end(), v.begin(), v.end());
+    // record r: header line at h[r], up to h[r + 1]; nl[r] terminators inside
+    std::vector<size_t> h(1, 0);
+    std::vector<int64_t> nl(1, 0);
+    for (auto& C : ch) {
+        nl.back() += C.head_nl;
+        h.insert(h.end(), C.pos.begin(), C.pos.end());
+        nl.insert(nl.end(), C.nl.begin(), C.nl.end());
+    }
     const int64_t R = (int64_t)h.size();
     h.push_back(len);
-    // ---- 2: per record key range and sequence size (bytes that are not terminators)
+    // ---- 2: per record key range, body start, sequence size, key hash
     std::vector<size_t> kend(R), body(R);
     std::vector<int64_t> slen(R);
-    const int TR = clamp_threads(threads, (size_t)R, 256);
+    std::vector<uint64_t> kh(R);
+    const int TR = clamp_threads(threads, (size_t)R, 1024);
     parallel_for(TR, [&](int t) {
         const int64_t lo = R * t / TR, hi = R * (t + 1) / TR;
         for (int64_t r = lo; r < hi; ++r) {
@@ -246,23 +307,31 @@ extern "C" int karma_fasta_parse(const char* data_c, size_t len, int threads, ka
             const void* sp = memchr(s + h[r], ' ', e - h[r]);
             kend[r] = sp ? (size_t)((const uint8_t*)sp - s) : e;
             body[r] = next_line(s, len, e);
-            int64_t n = 0;
-            for (size_t p = body[r]; p < h[r + 1]; ++p) n += !is_nl(s[p]);
-            slen[r] = n;
+            slen[r] = (int64_t)(h[r + 1] - e) - nl[r];  // the header line holds no terminator
+            kh[r] = hash_bytes(s + h[r], kend[r] - h[r]);
         }
     });
     // ---- 3: OrderedDict assignment: first position, last value
     std::vector<int64_t> slot(R);  // output slot of record r
     std::vector<int64_t> src;      // output slot -> record providing the value
+    std::vector<int64_t> first_rec;
+    src.reserve(R);
+    first_rec.reserve(R);
     {
-        std::unordered_map<std::string_view, int64_t, SVHash> seen;
-        seen.reserve((size_t)R * 2);
+        KeyTable tab((size_t)R);
         for (int64_t r = 0; r < R; ++r) {
-            std::string_view k(reinterpret_cast<const char*>(s + h[r]), kend[r] - h[r]);
-            auto it = seen.emplace(k, (int64_t)src.size());
-            if (it.second) src.push_back(r);
-            else src[it.first->second] = r;
-            slot[r] = it.first->second;
+            const size_t kl = kend[r] - h[r];
+            const int64_t f0 = tab.find_or_insert(kh[r], r, [&](int64_t o) {
+                return kh[o] == kh[r] && kend[o] - h[o] == kl && memcmp(s + h[o], s + h[r], kl) == 0;
+            });
+            if (f0 == r) {
+                slot[r] = (int64_t)src.size();
+                src.push_back(r);
+                first_rec.push_back(r);
+            } else {
+                slot[r] = slot[f0];
+                src[slot[r]] = r;
+            }
         }
     }
     const int64_t N = (int64_t)src.size();
@@ -271,33 +340,35 @@ extern "C" int karma_fasta_parse(const char* data_c, size_t len, int threads, ka
     f->seq_off.assign(N + 1, 0);
     f->key_off.assign(N + 1, 0);
     f->key_len.assign(N, 0);
-    std::vector<int64_t> first_rec(N, -1);
-    for (int64_t r = 0; r < R; ++r)
-        if (first_rec[slot[r]] < 0) first_rec[slot[r]] = r;
     for (int64_t i = 0; i < N; ++i) {
         const int64_t kr = first_rec[i], vr = src[i];
         f->seq_off[i + 1] = f->seq_off[i] + slen[vr];
         f->key_off[i + 1] = f->key_off[i] + (int64_t)(kend[kr] - h[kr]);
     }
     try {
-        f->seq.resize((size_t)f->seq_off[N] + 16, 0);  // 16 zero bytes of padding (karma_contigs_create)
-        f->keys.resize((size_t)f->key_off[N]);
+        f->seq.reset(new uint8_t[(size_t)f->seq_off[N] + 16]);
+        f->keys.reset(new char[(size_t)f->key_off[N] + 1]);
     } catch (...) {
         delete f;
         set_error("fasta: out of host memory");
         return KARMA_ERR_OOM;
     }
-    const int TN = clamp_threads(threads, (size_t)N, 256);
+    memset(f->seq.get() + f->seq_off[N], 0, 16);
+    // ---- 4: copy keys and sequences (terminators dropped)
+    const int TN = clamp_threads(threads, (size_t)N, 1024);
     parallel_for(TN, [&](int t) {
         const int64_t lo = N * t / TN, hi = N * (t + 1) / TN;
         for (int64_t i = lo; i < hi; ++i) {
             const int64_t kr = first_rec[i], vr = src[i];
             const size_t kl = kend[kr] - h[kr];
-            memcpy(f->keys.data() + f->key_off[i], s + h[kr], kl);
+            memcpy(f->keys.get() + f->key_off[i], s + h[kr], kl);
             f->key_len[i] = (int32_t)(ascii ? (int64_t)kl : code_points(s + h[kr], kl));
-            uint8_t* d = f->seq.data() + f->seq_off[i];
+            uint8_t* d = f->seq.get() + f->seq_off[i];
             for (size_t p = body[vr]; p < h[vr + 1];) {
-                const size_t e = line_end(s, h[vr + 1], p);
+                const void* q = memchr(s + p, '\n', h[vr + 1] - p);
+                size_t e = q ? (size_t)((const uint8_t*)q - s) : h[vr + 1];
+                const void* r = memchr(s + p, '\r', e - p);  // a '\r' ends the line first
+                if (r) e = (size_t)((const uint8_t*)r - s);
                 memcpy(d, s + p, e - p);
                 d += e - p;
                 p = next_line(s, h[vr + 1], e);
@@ -328,11 +399,25 @@ extern "C" int karma_fasta_get(karma_fasta* f, uint8_t* seq, int64_t* seq_off, c
         return KARMA_ERR_ARG;
     }
     const int64_t N = (int64_t)f->key_len.size();
-    if (seq) memcpy(seq, f->seq.data(), (size_t)f->seq_off[N] + 16);
+    if (seq) memcpy(seq, f->seq.get(), (size_t)f->seq_off[N] + 16);
     if (seq_off) memcpy(seq_off, f->seq_off.data(), sizeof(int64_t) * (N + 1));
-    if (keys) memcpy(keys, f->keys.data(), (size_t)f->key_off[N]);
+    if (keys) memcpy(keys, f->keys.get(), (size_t)f->key_off[N]);
     if (key_off) memcpy(key_off, f->key_off.data(), sizeof(int64_t) * (N + 1));
     if (key_len) memcpy(key_len, f->key_len.data(), sizeof(int32_t) * N);
+    return KARMA_OK;
+}
+
+extern "C" int karma_fasta_view(karma_fasta* f, const uint8_t** seq, const int64_t** seq_off, const char** keys,
+                                const int64_t** key_off, const int32_t** key_len) {
+    if (!f) {
+        set_error("karma_fasta_view: null handle");
+        return KARMA_ERR_ARG;
+    }
+    if (seq) *seq = f->seq.get();
+    if (seq_off) *seq_off = f->seq_off.data();
+    if (keys) *keys = f->keys.get();
+    if (key_off) *key_off = f->key_off.data();
+    if (key_len) *key_len = f->key_len.data();
     return KARMA_OK;
 }
 
@@ -547,6 +632,7 @@ struct karma_sam {
     std::vector<int64_t> q_start;     // per record: QNAME byte range in the caller's buffer
     std::vector<int32_t> q_len;
     int64_t n_reads = 0;
+    int64_t id_bound = 0;  // read ids < id_bound
 };
 
 namespace {
@@ -557,6 +643,7 @@ struct SamPart {
     std::vector<uint64_t> qh;
     std::vector<size_t> r0;   // RNAME start
     std::vector<uint32_t> rl;
+    std::vector<uint64_t> rh;
     int64_t bad_line = -1;
     int64_t lines = 0;        // parsed data lines
     int64_t all_lines = 0;    // including headers
@@ -593,6 +680,7 @@ void parse_sam_lines(const uint8_t* s, size_t lo, size_t hi, bool skip_headers, 
             P.qh.push_back(hash_bytes(s + f[0], ql));
             P.r0.push_back(f[2]);
             P.rl.push_back((uint32_t)rl);
+            P.rh.push_back(hash_bytes(s + f[2], rl));
             ++P.lines;
         }
         p = next_line(s, hi, e);
@@ -640,45 +728,89 @@ extern "C" int karma_sam_parse(const char* data_c, size_t len, int skip_headers,
         set_error("sam: out of host memory");
         return KARMA_ERR_OOM;
     }
-    // ---- RNAME ids in order of first appearance (sequential over few names)
+    // ---- RNAME ids in order of first appearance: distinct names per part
+    // (parallel), numbered part by part, then every line mapped (parallel)
+    std::vector<std::vector<int64_t>> local_first(T);  // part-local distinct -> first local line
+    std::vector<std::vector<uint32_t>> local_id(T);    // local line -> part-local distinct id
+    parallel_for(T, [&](int t) {
+        const SamPart& P = parts[t];
+        KeyTable tab((size_t)P.lines);
+        local_id[t].resize(P.lines);
+        std::vector<int64_t>& lf = local_first[t];
+        for (int64_t i = 0; i < P.lines; ++i) {
+            const int64_t f0 = tab.find_or_insert(P.rh[i], i, [&](int64_t o) {
+                return P.rh[o] == P.rh[i] && P.rl[o] == P.rl[i] && memcmp(s + P.r0[o], s + P.r0[i], P.rl[i]) == 0;
+            });
+            if (f0 == i) {
+                local_id[t][i] = (uint32_t)lf.size();
+                lf.push_back(i);
+            } else {
+                local_id[t][i] = local_id[t][f0];
+            }
+        }
+    });
+    std::vector<std::vector<uint32_t>> global_of_local(T);
     {
-        std::unordered_map<std::string_view, uint32_t, SVHash> rid;
+        size_t total = 0;
+        for (auto& v : local_first) total += v.size();
+        KeyTable tab(total);
+        std::vector<std::pair<int, int64_t>> owner;  // global id -> (part, local line)
         S->rname_off.push_back(0);
         for (int t = 0; t < T; ++t) {
             const SamPart& P = parts[t];
-            for (int64_t i = 0; i < P.lines; ++i) {
-                std::string_view v(reinterpret_cast<const char*>(s + P.r0[i]), P.rl[i]);
-                auto it = rid.find(v);
-                uint32_t id;
-                if (it == rid.end()) {
-                    id = (uint32_t)rid.size();
-                    rid.emplace(v, id);
-                    S->rnames.insert(S->rnames.end(), v.begin(), v.end());
+            for (int64_t i : local_first[t]) {
+                const int64_t idx = (int64_t)owner.size();
+                const int64_t g = tab.find_or_insert(P.rh[i], idx, [&](int64_t o) {
+                    const SamPart& Q = parts[owner[o].first];
+                    const int64_t j = owner[o].second;
+                    return Q.rh[j] == P.rh[i] && Q.rl[j] == P.rl[i] && memcmp(s + Q.r0[j], s + P.r0[i], P.rl[i]) == 0;
+                });
+                if (g == idx) {
+                    owner.emplace_back(t, i);
+                    S->rnames.insert(S->rnames.end(), s + P.r0[i], s + P.r0[i] + P.rl[i]);
                     S->rname_off.push_back((int64_t)S->rnames.size());
-                } else {
-                    id = it->second;
                 }
-                const int64_t g = first[t] + i;
-                S->records[2 * g + 1] = id;
-                S->q_start[g] = (int64_t)P.q0[i];
-                S->q_len[g] = (int32_t)P.ql[i];
+                global_of_local[t].push_back((uint32_t)g);
             }
         }
     }
+    parallel_for(T, [&](int t) {
+        const SamPart& P = parts[t];
+        for (int64_t i = 0; i < P.lines; ++i) {
+            const int64_t g = first[t] + i;
+            S->records[2 * g + 1] = global_of_local[t][local_id[t][i]];
+            S->q_start[g] = (int64_t)P.q0[i];
+            S->q_len[g] = (int32_t)P.ql[i];
+        }
+    });
     // ---- QNAME ids: shard by hash, one thread per shard; id = local * T + shard
     std::vector<uint64_t> n_local(T, 0);
     parallel_for(T, [&](int sh) {
-        std::unordered_map<std::string_view, uint64_t, SVHash> qid;
+        KeyTable tab((size_t)(L / T + 16) * 2);
+        std::vector<std::pair<int, int64_t>> own;  // shard-local id -> (part, line)
         for (int t = 0; t < T; ++t) {
             const SamPart& P = parts[t];
             for (int64_t i = 0; i < P.lines; ++i) {
-                if ((int)(P.qh[i] % (uint64_t)T) != sh) continue;
-                std::string_view v(reinterpret_cast<const char*>(s + P.q0[i]), P.ql[i]);
-                auto it = qid.emplace(v, (uint64_t)qid.size());
-                S->records[2 * (first[t] + i)] = (uint32_t)(it.first->second * (uint64_t)T + (uint64_t)sh);
+                if ((int)((P.qh[i] >> 40) % (uint64_t)T) != sh) continue;
+                const int64_t idx = (int64_t)own.size();
+                if (own.size() * 2 + 16 > tab.slot.size()) {  // grow: rehash the shard
+                    KeyTable big(tab.slot.size());
+                    for (int64_t o = 0; o < idx; ++o) {
+                        const SamPart& Q = parts[own[o].first];
+                        big.find_or_insert(Q.qh[own[o].second], o, [](int64_t) { return false; });
+                    }
+                    tab = std::move(big);
+                }
+                const int64_t id = tab.find_or_insert(P.qh[i], idx, [&](int64_t o) {
+                    const SamPart& Q = parts[own[o].first];
+                    const int64_t j = own[o].second;
+                    return Q.qh[j] == P.qh[i] && Q.ql[j] == P.ql[i] && memcmp(s + Q.q0[j], s + P.q0[i], P.ql[i]) == 0;
+                });
+                if (id == idx) own.emplace_back(t, i);
+                S->records[2 * (first[t] + i)] = (uint32_t)((uint64_t)id * (uint64_t)T + (uint64_t)sh);
             }
         }
-        n_local[sh] = qid.size();
+        n_local[sh] = own.size();
     });
     uint64_t nreads = 0, maxid = 0;
     for (int t = 0; t < T; ++t) {
@@ -691,6 +823,7 @@ extern "C" int karma_sam_parse(const char* data_c, size_t len, int skip_headers,
         return KARMA_ERR_ARG;
     }
     S->n_reads = (int64_t)nreads;
+    S->id_bound = nreads ? (int64_t)maxid + 1 : 0;
     *out = S;
     return KARMA_OK;
 }
@@ -705,11 +838,7 @@ extern "C" int karma_sam_info(karma_sam* S, int64_t* n_records, int64_t* n_reads
     if (n_reads) *n_reads = S->n_reads;
     if (n_contigs) *n_contigs = (int64_t)S->rname_off.size() - 1;
     if (rname_bytes) *rname_bytes = (int64_t)S->rnames.size();
-    if (read_id_bound) {
-        uint64_t m = 0;
-        for (size_t i = 0; i < S->q_len.size(); ++i) m = std::max<uint64_t>(m, S->records[2 * i] + 1ull);
-        *read_id_bound = (int64_t)m;
-    }
+    if (read_id_bound) *read_id_bound = S->id_bound;
     return KARMA_OK;
 }
 

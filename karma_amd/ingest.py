@@ -62,32 +62,54 @@ class FastaRecords:
         return len(self.key_len)
 
     def names(self):
-        k, o = self.keys, self.key_off.tolist()
-        return [k[o[i]:o[i + 1]].decode("utf-8") for i in range(len(self.key_len))]
+        return self._strs(memoryview(self.keys), self.key_off)
 
     def sequences(self):
-        b, o = self.seq.tobytes(), self.seq_off.tolist()
-        return [b[o[i]:o[i + 1]].decode("utf-8") for i in range(len(self.key_len))]
+        return self._strs(memoryview(self.seq), self.seq_off)
+
+    def _strs(self, mv, off):
+        o = off.tolist()
+        if self.ascii:  # one decode, then str slices (code point offsets == byte offsets)
+            whole = str(mv[:o[-1]], "ascii")
+            return [whole[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+        return [str(mv[o[i]:o[i + 1]], "utf-8") for i in range(len(o) - 1)]
+
+
+class _Handle:
+    """Owns a parser handle; numpy views of its arrays keep it alive."""
+
+    def __init__(self, h, destroy):
+        self.h, self._destroy = h, destroy
+
+    def __del__(self):
+        if self.h:
+            getattr(_lib.load(), self._destroy)(self.h)
+            self.h = None
+
+
+def _view(owner, addr, n, dtype):
+    """numpy array over n items at addr; its base keeps `owner` alive."""
+    if n == 0 or not addr:
+        return np.zeros(0, dtype)
+    raw = (ctypes.c_uint8 * (n * np.dtype(dtype).itemsize)).from_address(addr)
+    raw._owner = owner
+    return np.frombuffer(raw, dtype)
 
 
 def parse_fasta(data: bytes, threads=0) -> FastaRecords:
     if not _utf8_locale():
         raise ParseDeferred("locale encoding is not UTF-8")
-    h = _parse("karma_fasta_parse", data, threads)
-    try:
-        n, sb, kb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        asc = ctypes.c_int()
-        call("karma_fasta_info", h, ctypes.byref(n), ctypes.byref(sb), ctypes.byref(kb), ctypes.byref(asc))
-        N = n.value
-        seq = np.empty(sb.value + 16, np.uint8)
-        seq_off = np.empty(N + 1, np.int64)
-        keys = ctypes.create_string_buffer(max(kb.value, 1))
-        key_off = np.empty(N + 1, np.int64)
-        key_len = _buf(N, np.int32)
-        call("karma_fasta_get", h, _lib.ptr(seq), _lib.ptr(seq_off), keys, _lib.ptr(key_off), _lib.ptr(key_len))
-        return FastaRecords(seq, seq_off, keys.raw[:kb.value], key_off, key_len[:N], bool(asc.value))
-    finally:
-        _lib.load().karma_fasta_destroy(h)
+    own = _Handle(_parse("karma_fasta_parse", data, threads), "karma_fasta_destroy")
+    n, sb, kb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    asc = ctypes.c_int()
+    call("karma_fasta_info", own.h, ctypes.byref(n), ctypes.byref(sb), ctypes.byref(kb), ctypes.byref(asc))
+    p = [ctypes.c_void_p() for _ in range(5)]
+    call("karma_fasta_view", own.h, *[ctypes.byref(x) for x in p])
+    N = n.value
+    seq = _view(own, p[0].value, sb.value + 16, np.uint8)
+    keys = ctypes.string_at(p[2].value, kb.value) if kb.value else b""
+    return FastaRecords(seq, _view(own, p[1].value, N + 1, np.int64), keys, _view(own, p[3].value, N + 1, np.int64),
+                        _view(own, p[4].value, N, np.int32), bool(asc.value))
 
 
 @dataclass
