@@ -38,6 +38,10 @@ CONFIGS = {
     "config2": (2, 50_000, 10_000_000, True, "5p6"),
     "config1": (1, 1_000, 100_000, False, 5),
     "tiny": (7, 5_000, 500_000, True, "5p6"),
+    # configs[4] (1M contigs, 500M paired fragments, k=7) as its per-GPU share on 8 GPUs,
+    # and the whole problem on one GPU (a 131 GB profile + 1.5e9 records fit in 288 GB HBM)
+    "config5": (5, 125_000, 62_500_000, True, 7),
+    "config5_1gpu": (5, 1_000_000, 500_000_000, True, 7),
 }
 
 

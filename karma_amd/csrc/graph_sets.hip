@@ -49,8 +49,11 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kMaxB = 512;            // pair buckets
-constexpr int kMaxBc = 128;           // code buckets
+constexpr int kMaxB = 1024;           // pair buckets (n_contigs <= 2^20 keeps the compact path)
+constexpr int kMaxBc = 256;           // code buckets
+// partition LDS is sized by the bucket count: the narrow variants (<= 512 pair
+// and <= 128 code buckets, n_contigs <= 2^19) keep 3 code-partition blocks per CU
+constexpr int kNarrowB = 512, kNarrowBc = 128;
 constexpr int kMaxBwCompact = 10;     // compact reads need 2^(bw+3) band counters <= kBand
 
 struct Geo {
@@ -380,12 +383,13 @@ constexpr int kPT = 512;                 // partition threads (several blocks pe
 constexpr int kMaxListsPerBlock = 64;    // chunk lists per partition block, at most (a power of 2)
 
 // compact-read codes: u32 (m0 | M << 24) -> u16 (m0_local << 3 | M) per code bucket
-struct CodeStream {
+template <int NB>
+struct CodeStreamT {
     using S = uint32_t;
     using D = uint16_t;
     static constexpr int kCap = 8192;   // codes per flush (32 KB of LDS)
     static constexpr int kPad = 8;      // 16 B of u16
-    static constexpr int kMaxNb = kMaxBc;
+    static constexpr int kMaxNb = NB;
     static constexpr D kPadV = 0xFFFF;  // codes are < 2^15
     __device__ static int nb(const Geo& g) { return g.Bc; }
     __device__ static uint32_t bucket(S s, const Geo& g) { return (s & 0xFFFFFFu) >> g.bwc; }
@@ -395,12 +399,13 @@ struct CodeStream {
 };
 
 // general pairs: u64 (a << 32 | b) -> u32 (a_local << bbits | b) per pair bucket
-struct PairStream {
+template <int NB>
+struct PairStreamT {
     using S = uint64_t;
     using D = uint32_t;
     static constexpr int kCap = 4096;
     static constexpr int kPad = 4;
-    static constexpr int kMaxNb = kMaxB;
+    static constexpr int kMaxNb = NB;
     static constexpr D kPadV = kEmpty;  // pair keys are < 2^31
     __device__ static int nb(const Geo& g) { return g.B; }
     __device__ static uint32_t bucket(S s, const Geo& g) { return (uint32_t)(s >> 32) >> g.bw; }
@@ -408,6 +413,11 @@ struct PairStream {
         return (((uint32_t)(s >> 32) & ((1u << g.bw) - 1u)) << g.bbits) | (uint32_t)s;
     }
 };
+
+using CodeStream = CodeStreamT<kNarrowBc>;
+using CodeStreamWide = CodeStreamT<kMaxBc>;
+using PairStream = PairStreamT<kNarrowB>;
+using PairStreamWide = PairStreamT<kMaxB>;
 
 struct RunDir {
     int64_t* base;                        // per flush: start of its runs in the stream
@@ -1049,15 +1059,146 @@ int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
 
 namespace karma {
 
+// The sorted unique list (mk, mc, U) plus the pairs of reads with > 8 records
+// (big_list) -> out.
+int finish_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, const int64_t* big_list, unsigned n_big,
+                 DevArray<uint64_t>& mk, DevArray<int64_t>& mc, int64_t U, karma_pairs* out) {
+    out->n_contigs = N;
+    if (n_big == 0) {
+        out->keys.swap(mk);
+        out->counts.swap(mc);
+        out->n = U;
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        return KARMA_OK;
+    }
+    DevArray<unsigned long long> np;
+    KARMA_TRY(np.alloc(ctx, 1));
+    KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
+    KARMA_LAUNCH(ctx, "graph_big_count", big_pairs_kernel, grid_n(n_big, 64), 64, 0, rec, A, big_list,
+                 (int64_t)n_big, (uint32_t)N, (uint64_t*)nullptr, np.ptr, 1);
+    unsigned long long hp = 0;
+    KARMA_HIP(hipMemcpyAsync(&hp, np.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    DevArray<uint64_t> allk;
+    DevArray<int64_t> allc;
+    KARMA_TRY(allk.alloc(ctx, U + hp));
+    KARMA_TRY(allc.alloc(ctx, U + hp));
+    if (U) {
+        KARMA_HIP(hipMemcpyAsync(allk.ptr, mk.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(allc.ptr, mc.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
+    KARMA_LAUNCH(ctx, "graph_big_pairs", big_pairs_kernel, grid_n(n_big, 64), 64, 0, rec, A, big_list,
+                 (int64_t)n_big, (uint32_t)N, allk.ptr + U, np.ptr, 0);
+    KARMA_LAUNCH(ctx, "fill_ones", fill_ones_i64_kernel, grid_n(hp), 256, 0, allc.ptr + U, (int64_t)hp);
+    KARMA_TRY(sort_reduce_pairs(ctx, allk.ptr, allc.ptr, nullptr, U + (int64_t)hp, 64, out->keys, out->counts,
+                                nullptr, &out->n));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    return KARMA_OK;
+}
+
+// per-chunk pair lists -> one contiguous list of ones-counted keys
+__global__ void widen_counts_kernel(const uint32_t* __restrict__ n, int64_t m, int64_t* __restrict__ w) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= m) w[i] = i < m ? (int64_t)n[i] : 0;
+}
+
+__global__ void gather_lists_kernel(const uint64_t* __restrict__ lists, int64_t cap, const uint32_t* __restrict__ n,
+                                    const int64_t* __restrict__ off, uint64_t* __restrict__ keys,
+                                    int64_t* __restrict__ ones) {
+    const int64_t c = blockIdx.x;
+    const uint64_t* src = lists + c * cap;
+    const int64_t d = off[c];
+    for (uint32_t t = threadIdx.x; t < n[c]; t += blockDim.x) {
+        keys[d + t] = src[t];
+        ones[d + t] = 1;
+    }
+}
+
+// n_contigs > 2^20: bucket-local 32-bit pair keys (a_local << bbits | b) no
+// longer fit, so every read takes the general path (sorted distinct contigs,
+// per-chunk u64 pair lists, no atomics) and one 64-bit sort-reduce follows;
+// reads of > 8 records are merged as in the main path.
+int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
+    KARMA_CHECK(N >= 1 && N <= (int64_t(1) << 24), KARMA_ERR_ARG, "n_contigs %lld out of range [1, 2^24]",
+                (long long)N);
+    int bbits = 1;
+    while ((int64_t(1) << bbits) < N) ++bbits;
+    const int64_t n_chunks = std::max<int64_t>(1, ceil_div(A, kCChunk));
+    DevArray<uint32_t> codes, n_codes, n_gen, n_pl;
+    DevArray<int64_t> big_list, ctrl, widths, off;
+    DevArray<unsigned long long> blk_items;
+    KARMA_TRY(codes.alloc(ctx, n_chunks * kCChunk));
+    KARMA_TRY(n_codes.alloc(ctx, n_chunks));
+    KARMA_TRY(n_gen.alloc(ctx, n_chunks));
+    KARMA_TRY(n_pl.alloc(ctx, n_chunks));
+    KARMA_TRY(big_list.alloc(ctx, A / (kMaxFast + 1) + 1));
+    KARMA_TRY(blk_items.alloc(ctx, 2 * n_chunks));
+    KARMA_TRY(widths.alloc(ctx, n_chunks + 1));
+    KARMA_TRY(off.alloc(ctx, n_chunks + 1));
+    KARMA_TRY(ctrl.alloc(ctx, 4));  // flags[4] | counters[3] (big reads) | spare
+    int* const flags = reinterpret_cast<int*>(ctrl.ptr);
+    unsigned* const counters = reinterpret_cast<unsigned*>(ctrl.ptr + 2);
+    void* hpin = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, 5 * 8, &hpin));
+    int64_t* const h = static_cast<int64_t*>(hpin);
+    int64_t pcap = kCChunk / 8;
+    DevArray<uint64_t> plist;
+    int64_t P = 0;
+    unsigned n_big = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        KARMA_TRY(plist.alloc(ctx, n_chunks * pcap));
+        KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, 4 * 8, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(blk_items.ptr, 0, 2 * n_chunks * 8, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
+        if (A > 0) {
+            ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
+                        n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags};
+            KARMA_LAUNCH(ctx, "graph_classify", classify_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+        }
+        KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
+                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags);
+        KARMA_LAUNCH(ctx, "widen_counts", widen_counts_kernel, grid_n(n_chunks + 1), 256, 0, n_pl.ptr, n_chunks,
+                     widths.ptr);
+        KARMA_TRY(scan_excl_i64(ctx, widths.ptr, off.ptr, n_chunks + 1));
+        KARMA_HIP(hipMemcpyAsync(h, ctrl.ptr, 4 * 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(h + 4, off.ptr + n_chunks, 8, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        const int* hf = reinterpret_cast<const int*>(h);
+        KARMA_CHECK(!hf[0], KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
+        KARMA_CHECK(!hf[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
+        n_big = reinterpret_cast<const unsigned*>(h + 2)[0];
+        P = h[4];
+        if (!hf[2]) break;
+        KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "pair list capacity exceeded twice");
+        pcap = kCChunk * 9 / 2;  // every read with <= 8 records fits
+    }
+    DevArray<uint64_t> keys;
+    DevArray<int64_t> ones;
+    KARMA_TRY(keys.alloc(ctx, P));
+    KARMA_TRY(ones.alloc(ctx, P));
+    if (P) KARMA_LAUNCH(ctx, "gather_lists", gather_lists_kernel, n_chunks, 256, 0, plist.ptr, pcap, n_pl.ptr,
+                        off.ptr, keys.ptr, ones.ptr);
+    DevArray<uint64_t> mk;
+    DevArray<int64_t> mc;
+    int64_t U = 0;
+    KARMA_TRY(sort_reduce_pairs(ctx, keys.ptr, ones.ptr, nullptr, P, 32 + bbits, mk, mc, nullptr, &U));
+    return finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out);
+}
+
 // Records (grouped by read, 16-byte aligned) -> sorted unique (a<<32|b, count).
 int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
+    if (N > (int64_t(1) << 20)) return records_to_pairs_wide(ctx, rec, A, N, out);
     Geo g;
     KARMA_TRY(make_geo(N, &g));
     const int B = g.B;
     const int64_t n_chunks = std::max<int64_t>(1, ceil_div(A, kCChunk));
     // partition: one round of resident blocks, each taking consecutive chunk lists
-    const int resident = resident_grid(ctx, reinterpret_cast<const void*>(&partition_kernel<CodeStream>), kPT, 0,
-                                       int64_t(1) << 30);
+    const bool wide_c = g.Bc > kNarrowBc, wide_p = B > kNarrowB;
+    const int resident = resident_grid(ctx,
+                                       wide_c ? reinterpret_cast<const void*>(&partition_kernel<CodeStreamWide>)
+                                              : reinterpret_cast<const void*>(&partition_kernel<CodeStream>),
+                                       kPT, 0, int64_t(1) << 30);
     const int lpb = (int)std::min<int64_t>(kMaxListsPerBlock, ceil_div(n_chunks, resident));
     const int64_t n_pblk = ceil_div(n_chunks, lpb);
     // per-step scratch
@@ -1146,13 +1287,21 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items.ptr};
         pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items.ptr + n_pblk};
         if (g.Bc > 0) {
-            KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr,
-                         kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
+            if (wide_c)
+                KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStreamWide>, n_pblk, kPT, 0, codes.ptr,
+                             kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
+            else
+                KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr,
+                             kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
             KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
                          g.Bc, g.bwc, n_cg, part_ch.ptr);
         }
-        KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
-                     n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
+        if (wide_p)
+            KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStreamWide>, n_pblk, kPT, 0, plist.ptr,
+                         pcap, n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
+        else
+            KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
+                         n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
         KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
                      g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
         KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits, g.bwc,
@@ -1221,40 +1370,10 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     }
     DevArray<uint64_t> mk;
     DevArray<int64_t> mc;
-    const bool merge_big = n_big > 0;
-    KARMA_TRY((merge_big ? mk : out->keys).alloc(ctx, U));
-    KARMA_TRY((merge_big ? mc : out->counts).alloc(ctx, U));
-    KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, pk.ptr, pc.ptr, n_per, dst,
-                 (merge_big ? mk : out->keys).ptr, (merge_big ? mc : out->counts).ptr);
-    out->n = U;
-    out->n_contigs = N;
-    if (merge_big) {
-        // pairs of reads with > 8 records, merged with the main list
-        DevArray<unsigned long long> np;
-        KARMA_TRY(np.alloc(ctx, 1));
-        KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
-        KARMA_LAUNCH(ctx, "graph_big_count", big_pairs_kernel, grid_n(n_big, 64), 64, 0, rec, A, big_list.ptr,
-                     (int64_t)n_big, (uint32_t)N, (uint64_t*)nullptr, np.ptr, 1);
-        unsigned long long hp = 0;
-        KARMA_HIP(hipMemcpyAsync(&hp, np.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipStreamSynchronize(ctx->stream));
-        DevArray<uint64_t> allk;
-        DevArray<int64_t> allc;
-        KARMA_TRY(allk.alloc(ctx, U + hp));
-        KARMA_TRY(allc.alloc(ctx, U + hp));
-        if (U) {
-            KARMA_HIP(hipMemcpyAsync(allk.ptr, mk.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
-            KARMA_HIP(hipMemcpyAsync(allc.ptr, mc.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        }
-        KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
-        KARMA_LAUNCH(ctx, "graph_big_pairs", big_pairs_kernel, grid_n(n_big, 64), 64, 0, rec, A, big_list.ptr,
-                     (int64_t)n_big, (uint32_t)N, allk.ptr + U, np.ptr, 0);
-        KARMA_LAUNCH(ctx, "fill_ones", fill_ones_i64_kernel, grid_n(hp), 256, 0, allc.ptr + U, (int64_t)hp);
-        KARMA_TRY(sort_reduce_pairs(ctx, allk.ptr, allc.ptr, nullptr, U + (int64_t)hp, 64, out->keys, out->counts,
-                                    nullptr, &out->n));
-    }
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    return KARMA_OK;
+    KARMA_TRY(mk.alloc(ctx, U));
+    KARMA_TRY(mc.alloc(ctx, U));
+    KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, pk.ptr, pc.ptr, n_per, dst, mk.ptr, mc.ptr);
+    return finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out);
 }
 
 }  // namespace karma

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/karma.h"
@@ -99,6 +100,11 @@ struct DevArray {
         if (ptr) ctx_free(ctx, ptr);
         ptr = nullptr;
         n = 0;
+    }
+    void swap(DevArray& o) {
+        std::swap(ctx, o.ctx);
+        std::swap(ptr, o.ptr);
+        std::swap(n, o.n);
     }
 };
 

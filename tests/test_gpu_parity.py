@@ -194,7 +194,11 @@ def check_records(rec, n, grouped=True):
 
 
 @pytest.mark.parametrize("seed,n,nf,paired", [(2, 20_000, 400_000, True), (5, 3_000, 200_000, False),
-                                              (9, 777, 50_000, True), (4, 1, 1000, True)])
+                                              (9, 777, 50_000, True), (4, 1, 1000, True),
+                                              # wide partition variants (> 512 pair / > 128 code buckets),
+                                              # config 5's 1M contigs, and past 2^20 (no compact path)
+                                              (10, 600_000, 1_000_000, True), (11, 1_000_000, 2_000_000, True),
+                                              (12, 1_100_000, 1_000_000, True)])
 def test_records_graph_vs_oracle(seed, n, nf, paired):
     rec = engine.synth_records(seed, n, 0, nf, paired)
     check_records(rec, n)
@@ -251,16 +255,18 @@ def test_records_compact_spans_and_bucket_edges():
     check_records(np.array(rows, np.uint32), 300)
 
 
-def test_records_big_reads_and_duplicates():
+@pytest.mark.parametrize("n", [200, 1_200_000])  # 1.2M: the 64-bit-key path (n_contigs > 2^20)
+def test_records_big_reads_and_duplicates(n):
     rng = np.random.default_rng(2)
     rows = []
     for r in range(3000):
         m = int(rng.choice([1, 2, 3, 9, 17, 40]))
-        for c in rng.integers(0, 200, m):
+        lo = int(rng.integers(0, n - 200)) if n > 200 else 0
+        for c in rng.integers(lo, lo + 200, m):
             rows.append((r, int(c)))
             if rng.random() < 0.3:
                 rows.append((r, int(c)))  # mate on the same contig
-    check_records(np.array(rows, np.uint32), 200)
+    check_records(np.array(rows, np.uint32), n)
 
 
 def test_records_empty_and_bad_contig():
