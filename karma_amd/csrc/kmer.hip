@@ -30,6 +30,7 @@ struct karma_contigs {
     karma_ctx* ctx = nullptr;
     int64_t n = 0, total = 0, words = 0, exc_bases = 0;
     int64_t zero_key_maxlen = -1;  // longest contig with an empty FASTA key (-1: none)
+    int64_t max_len = 0;           // longest contig (bases)
     DevArray<uint8_t> raw_own;
     DevArray<int64_t> off_own;
     DevArray<int32_t> keylen_own;
@@ -403,12 +404,12 @@ __global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* __re
 }
 
 // -------------------------------------------------------------- profile ------
-// WAVE=true : one wave per contig, its own LDS histogram (M <= kWaveMaxM),
-//             no block barriers; WAVE=false: one block per contig (large M,
-//             histogram in LDS or, past the LDS budget, in a global scratch row).
-// The dense row count / len(key) (kmer.py:120, :231-233) streams out with
-// 16-byte non-temporal stores when the row start is 16-byte aligned.
+// profile_wave_kernel: one wave per contig (M <= kWaveMaxM); profile_kernel:
+// one block per contig (large M).
 constexpr int kWaveMaxM = 4096;
+#ifndef KARMA_PROF_C16
+#define KARMA_PROF_C16 1
+#endif
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 template <bool P56, typename Add>
@@ -466,7 +467,252 @@ __device__ __forceinline__ void write_row(double* __restrict__ row, const uint32
     }
 }
 
-template <bool P56, bool WAVE, bool LDS_COUNTS>
+// ---- wave-per-contig profile (M <= kWaveMaxM) -------------------------------
+// One wave per contig, its own LDS histogram, no block barriers after the
+// table fill.  Blocks of 8 waves share one LDS column table:
+//   5p6: 1024 entries by 5-mer code, then 64 by the first three bases of a
+//        palindromic 6-mer (they determine it);  k: 4^k entries by code.
+// C16: counters are u16, two per u32 (used when every contig is shorter than
+// 2^16 bases, so no count can carry into its neighbour); this halves the
+// histogram and lets 4 blocks share a CU.
+// Per wave LDS: [counts][window region 128 u32] -- the window region holds the
+// staged words (+ mask) while counting and the count/len table while writing.
+constexpr int kProfWin = 128;  // u32 per wave past the counts
+
+__device__ __forceinline__ uint32_t rev3(uint32_t l3) { return ((l3 & 3u) << 4) | (l3 & 12u) | (l3 >> 4); }
+
+template <bool C16>
+__device__ __forceinline__ void hist_add(uint32_t* counts, uint32_t col) {
+    if (C16) atomicAdd(&counts[col >> 1], 1u << ((col & 1u) << 4));
+    else atomicAdd(&counts[col], 1u);
+}
+
+// Counting for a contig without exception bases (every base A/C/G/T): lane l
+// takes positions 64t + l of each 1024-position stage, so its offset inside a
+// word (l mod 16) is fixed and its 16-base window is one alignbit of the word
+// pair staged in LDS as a u64 (one 8-byte read per position).  The k-mer code
+// is the window's top 2k bits; for 5p6 the 5-mer is the 6-mer's top 10 bits.
+template <bool P56, bool C16>
+__device__ __forceinline__ void count_clean(const Stage& first, const uint32_t* __restrict__ packed, int64_t w0,
+                                            int64_t L, int kmin, int k, const uint16_t* __restrict__ tab,
+                                            uint32_t* __restrict__ counts, uint32_t* __restrict__ win, int lane,
+                                            unsigned& my) {
+    uint64_t* pairs = reinterpret_cast<uint64_t*>(win);
+    const int64_t npos = L - kmin + 1;
+    const int o = lane & 15;
+    const uint32_t sh = 32u - 2u * (uint32_t)o;
+    for (int64_t b0 = 0; b0 < npos; b0 += 1024) {
+        Stage st;
+        if (b0 == 0) st = first;
+        else st.load(packed, nullptr, false, w0 + (b0 >> 4), lane);
+        // lane l: words l and l + 1 of the stage (DPP wave_shl:1; lane 63 takes word 64)
+        const uint32_t w64s = (uint32_t)__builtin_amdgcn_readlane((int)st.w64, 0);
+        const uint32_t wn = (uint32_t)__builtin_amdgcn_update_dpp((int)w64s, (int)st.w, 0x130, 0xF, 0xF, false);
+        pairs[lane] = ((uint64_t)st.w << 32) | wn;
+        wave_lds_sync();
+        const uint64_t* pw = pairs + (lane >> 4);
+        const int64_t lim = npos - b0 - lane;  // position 64t + lane is valid iff 64t < lim
+        const int nt = (int)min<int64_t>(16, (npos - b0 + 63) >> 6);
+#pragma unroll 2
+        for (int t = 0; t < nt; ++t) {
+            if (64 * t < lim) {
+                const uint64_t x = pw[4 * t];
+                const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
+                const uint32_t W = o ? __builtin_amdgcn_alignbit(hi, lo, sh) : hi;
+                if (P56) {
+                    hist_add<C16>(counts, tab[W >> 22]);  // kmer.py:72-73
+                    ++my;
+                    const uint32_t c6 = W >> 20;
+                    // palindromic 6-mers that fit in the contig, kmer.py:76-80
+                    if ((c6 >> 6) == rev3(c6 & 63u) && 64 * t + 1 < lim) {
+                        hist_add<C16>(counts, tab[1024u + (c6 >> 6)]);
+                        ++my;
+                    }
+                } else {
+                    hist_add<C16>(counts, tab[W >> (32 - 2 * k)]);
+                    ++my;
+                }
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// The dense row count / len(key) (kmer.py:120, :231-233).  Counts below 64
+// come from a per-row table the wave fills with the same IEEE division (lane c
+// holds c / len), so a value costs one LDS read instead of one f64 division;
+// larger counts still divide.  The histogram is cleared as it is read, so the
+// next contig starts from zero.  16-byte non-temporal stores when the row
+// start is 16-byte aligned.
+template <bool C16>
+__device__ __forceinline__ void write_row_wave(double* __restrict__ row, uint32_t* __restrict__ counts, int64_t M,
+                                               int32_t klen, int* __restrict__ err, double* __restrict__ lut,
+                                               int lane) {
+    const double len = (double)klen;
+    lut[lane] = lane ? (double)lane / len : 0.0;  // IEEE correctly rounded (kmer.py:120)
+    wave_lds_sync();
+    auto val = [&](uint32_t a) {
+        double v = lut[min(a, 63u)];
+        if (a >= 64u) v = (double)a / len;
+        return v;
+    };
+    if ((reinterpret_cast<uintptr_t>(row) & 15) == 0) {
+        const int64_t M2 = M >> 1;
+        for (int64_t j = lane; j < M2; j += 64) {
+            uint32_t a, b;
+            if (C16) {
+                const uint32_t ab = counts[j];
+                counts[j] = 0;
+                a = ab & 0xFFFFu;
+                b = ab >> 16;
+            } else {
+                const uint2 ab = reinterpret_cast<uint2*>(counts)[j];
+                reinterpret_cast<uint2*>(counts)[j] = make_uint2(0u, 0u);
+                a = ab.x;
+                b = ab.y;
+            }
+            if ((a | b) && klen == 0) *err = 1;
+            d2 v;
+            v.x = val(a);
+            v.y = val(b);
+            __builtin_nontemporal_store(v, reinterpret_cast<d2*>(row) + j);
+        }
+        if ((M & 1) && lane == 0) {
+            const uint32_t a = C16 ? counts[M >> 1] & 0xFFFFu : counts[M - 1];
+            counts[C16 ? M >> 1 : M - 1] = 0;
+            if (a && klen == 0) *err = 1;
+            __builtin_nontemporal_store(val(a), row + M - 1);
+        }
+    } else {
+        uint16_t* c16 = reinterpret_cast<uint16_t*>(counts);
+        for (int64_t j = lane; j < M; j += 64) {
+            const uint32_t a = C16 ? c16[j] : counts[j];
+            if (C16) c16[j] = 0;
+            else counts[j] = 0;
+            if (a && klen == 0) *err = 1;
+            __builtin_nontemporal_store(val(a), row + j);
+        }
+    }
+}
+
+// u32 slots of a wave's histogram
+__host__ __device__ constexpr int64_t hist_words(int64_t M, bool c16) {
+    return c16 ? (((M + 1) >> 1) + 3) & ~int64_t(3) : (M + 3) & ~int64_t(3);
+}
+// column-table entries (u16) in LDS
+__host__ __device__ constexpr int64_t tab_entries(bool p56, uint32_t S) { return p56 ? 1088 : (int64_t)S; }
+
+template <bool P56, bool C16>
+// 8 waves per SIMD (4 blocks per CU with u16 counters)
+#ifndef KARMA_PROF_WAVES
+#define KARMA_PROF_WAVES 8
+#endif
+__global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(KARMA_PROF_WAVES, KARMA_PROF_WAVES)))
+profile_wave_kernel(
+    const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
+    const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
+    const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
+    const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
+    double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    // wave index in an SGPR: contig offsets and lengths load with scalar loads
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+    uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
+    const int t_pad = (int)((tab_entries(P56, S) + 7) & ~7);
+    const int h_words = (int)hist_words(M, C16);
+    uint32_t* counts = lds + t_pad / 2 + wave * (h_words + kProfWin);
+    uint32_t* win = counts + h_words;
+    uint16_t* mbuf = reinterpret_cast<uint16_t*>(win + 80);
+    double* lut = reinterpret_cast<double*>(win);
+    if (P56) {
+        for (int o = threadIdx.x; o < 1088; o += blockDim.x) {
+            uint32_t ord;
+            if (o < 1024) {
+                ord = 5u * o;
+            } else {
+                const uint32_t h3 = o - 1024, c6 = h3 << 6 | rev3(h3);
+                ord = (c6 >> 2) * 5u + 1u + (c6 & 3u);
+            }
+            tab[o] = (uint16_t)col_of_ord[ord];
+        }
+    } else {
+        for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
+    }
+    for (int j = lane; j < h_words; j += 64) counts[j] = 0;  // write_row_wave clears it after each row
+    __syncthreads();
+    const int kmin = P56 ? 5 : k;
+    // software pipeline over this wave's contigs: the next contig's offsets
+    // load at the top of the current one, and its first stage of packed
+    // words before the current row is written
+    struct Meta {
+        int64_t s = 0, L = 0, w0 = 0;
+        int32_t klen = 0;
+        bool exc = false;
+    };
+    auto meta = [&](int64_t cc, Meta& m) {
+        if (cc < n) {
+            m.s = off[cc];
+            m.L = off[cc + 1] - m.s;
+            m.w0 = woff[cc];
+            m.klen = keylen[cc];
+            m.exc = has_exc[cc] != 0;
+        }
+    };
+    const int64_t stride = (int64_t)gridDim.x * wpb;
+    int64_t c = (int64_t)blockIdx.x * wpb + wave;
+    Meta cur, nxt;
+    Stage st0;
+    meta(c, cur);
+    if (c < n) st0.load(packed, mask, cur.exc, cur.w0, lane);
+    for (; c < n; c += stride) {
+        meta(c + stride, nxt);
+        const int64_t L = cur.L;
+        unsigned my = 0;
+        if (!cur.exc) {
+            count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
+        } else {
+            // a contig with exception bases: windows that touch one are keyed by
+            // their bytes and looked up among the sorted exception keys
+            const uint8_t* craw = raw + cur.s;
+            auto add = [&](uint32_t cl) {
+                hist_add<C16>(counts, cl);
+                ++my;
+            };
+            for_each_window(packed, mask, true, cur.w0, L - kmin + 1, win, mbuf, lane,
+                            [&](int64_t i, const Window& v) {
+                if (P56) {
+                    if (v.clean(5)) add(tab[v.code(5)]);
+                    else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 5, true))]);
+                    if (i + 6 <= L) {
+                        if (v.clean(6)) {
+                            const uint32_t c6 = v.code(6);
+                            if (pal6_code(c6)) add(tab[1024u + (c6 >> 6)]);
+                        } else if (pal_bytes(craw + i, 6)) {
+                            add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 6, true))]);
+                        }
+                    }
+                } else {
+                    if (v.clean(k)) add(tab[v.code(k)]);
+                    else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
+                }
+            }, &st0);
+        }
+        if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
+        // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) my += __shfl_xor(my, d);
+        if (lane == 0) row_tot[c] = (int64_t)my;
+        write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        cur = nxt;
+    }
+}
+
+// ---- block-per-contig profile (large M) --------------------------------------
+// One block per contig: histogram in LDS or, past the LDS budget, in a global
+// scratch row.
+template <bool P56, bool LDS_COUNTS>
 __global__ void __launch_bounds__(kPBlock) profile_kernel(
     const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
     const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
@@ -475,82 +721,7 @@ __global__ void __launch_bounds__(kPBlock) profile_kernel(
     double* __restrict__ out, int64_t ld, uint32_t* __restrict__ scratch, int* __restrict__ err, int S,
     int64_t* __restrict__ row_tot) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_counts[];
-    if (WAVE) {
-        // LDS: [col table u16, S rounded to 8][per wave: counts M (even) | words 80 | mask 80 u16]
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
-        uint16_t* col = reinterpret_cast<uint16_t*>(lds_counts);
-        const int s_pad = (S + 7) & ~7;
-        const int m_pad = (int)((M + 3) & ~3);
-        uint32_t* base = lds_counts + s_pad / 2 + wave * (m_pad + 80 + 40);
-        uint32_t* counts = base;
-        uint32_t* wbuf = base + m_pad;
-        uint16_t* mbuf = reinterpret_cast<uint16_t*>(base + m_pad + 80);
-        for (int o = threadIdx.x; o < S; o += blockDim.x) col[o] = (uint16_t)col_of_ord[o];
-        __syncthreads();
-        const int kmin = P56 ? 5 : k;
-        // software pipeline over this wave's contigs: the next contig's offsets
-        // load at the top of the current one, and its first stage of packed
-        // words before the current row is written
-        struct Meta {
-            int64_t s = 0, L = 0, w0 = 0;
-            int32_t klen = 0;
-            bool exc = false;
-        };
-        auto meta = [&](int64_t cc, Meta& m) {
-            if (cc < n) {
-                m.s = off[cc];
-                m.L = off[cc + 1] - m.s;
-                m.w0 = woff[cc];
-                m.klen = keylen[cc];
-                m.exc = has_exc[cc] != 0;
-            }
-        };
-        const int64_t stride = (int64_t)gridDim.x * wpb;
-        int64_t c = (int64_t)blockIdx.x * wpb + wave;
-        Meta cur, nxt;
-        Stage st0;
-        meta(c, cur);
-        if (c < n) st0.load(packed, mask, cur.exc, cur.w0, lane);
-        for (; c < n; c += stride) {
-            meta(c + stride, nxt);
-            for (int64_t j = lane; j < M; j += 64) counts[j] = 0;
-            wave_lds_sync();
-            const int64_t L = cur.L;
-            const uint8_t* craw = raw + cur.s;
-            unsigned my = 0;
-            auto add = [&](uint32_t cl) {
-                atomicAdd(&counts[cl], 1u);
-                ++my;
-            };
-            for_each_window(packed, mask, cur.exc, cur.w0, L - kmin + 1, wbuf, mbuf, lane,
-                            [&](int64_t i, const Window& v) {
-                if (P56) {
-                    if (v.clean(5)) add(col[v.code(5) * 5u]);
-                    else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 5, true))]);
-                    if (i + 6 <= L) {
-                        if (v.clean(6)) {
-                            const uint32_t c6 = v.code(6);
-                            if (pal6_code(c6)) add(col[(c6 >> 2) * 5u + 1u + (c6 & 3u)]);
-                        } else if (pal_bytes(craw + i, 6)) {
-                            add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 6, true))]);
-                        }
-                    }
-                } else {
-                    if (v.clean(k)) add(col[v.code(k)]);
-                    else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
-                }
-            }, &st0);
-            if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
-            // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
-#pragma unroll
-            for (int d = 32; d > 0; d >>= 1) my += __shfl_xor(my, d);
-            if (lane == 0) row_tot[c] = (int64_t)my;
-            write_row(out + c * ld, counts, M, cur.klen, err, lane, 64);
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            cur = nxt;
-        }
-    } else {
+    {
         uint32_t* counts = LDS_COUNTS ? lds_counts : scratch + (int64_t)blockIdx.x * M;
         for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
             for (int64_t j = threadIdx.x; j < M; j += blockDim.x) counts[j] = 0;
@@ -572,10 +743,21 @@ int grid_for(int64_t n, int64_t cap) { return (int)std::max<int64_t>(1, std::min
 
 // longest contig whose key is empty: it divides by zero iff it has k-mers
 // (kmer.py:213), so karma_kmer_profile can refuse before launching
+// (also the longest contig overall, which sizes the profile's counters)
 __global__ void zero_key_kernel(const int64_t* __restrict__ off, const int32_t* __restrict__ keylen, int64_t n,
-                                unsigned long long* __restrict__ maxlen_plus1) {
+                                unsigned long long* __restrict__ maxlen_plus1, unsigned long long* __restrict__ maxlen) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && keylen[i] == 0) atomicMax(maxlen_plus1, (unsigned long long)(off[i + 1] - off[i] + 1));
+    if (i >= n) return;
+    const unsigned long long L = (unsigned long long)(off[i + 1] - off[i]);
+    if (keylen[i] == 0) atomicMax(maxlen_plus1, L + 1);
+    // wave maximum first: one atomic per wave
+    unsigned long long m = L;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        const unsigned long long y = __shfl_xor(m, d);
+        m = y > m ? y : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(maxlen, m);
 }
 
 int kmer_shape(int kmode, int* kmin, int* kmax, uint32_t* S, bool* with_len) {
@@ -650,22 +832,24 @@ int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offs
     }
     KARMA_HIP(hipMemsetAsync(c->packed.ptr + c->words, 0, kPadWords * sizeof(uint32_t), ctx->stream));
     KARMA_HIP(hipMemsetAsync(c->mask.ptr + c->words, 0, kPadWords * sizeof(uint16_t), ctx->stream));
-    DevArray<unsigned long long> stat;  // 0 exception bases, 1 zero-key max length + 1
-    if ((rc = stat.alloc(ctx, 2))) {
+    DevArray<unsigned long long> stat;  // 0 exception bases, 1 zero-key max length + 1, 2 max length
+    if ((rc = stat.alloc(ctx, 3))) {
         delete c;
         return rc;
     }
-    KARMA_HIP(hipMemsetAsync(stat.ptr, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    KARMA_HIP(hipMemsetAsync(stat.ptr, 0, 3 * sizeof(unsigned long long), ctx->stream));
     if (n) {
         KARMA_LAUNCH(ctx, "pack_2bit", pack_kernel, grid_for(n, 8192), kBlock, 0, c->raw, c->off, c->woff.ptr, n,
                      c->packed.ptr, c->mask.ptr, c->has_exc.ptr, stat.ptr);
-        KARMA_LAUNCH(ctx, "zero_key", zero_key_kernel, ceil_div(n, 256), 256, 0, c->off, c->keylen, n, stat.ptr + 1);
+        KARMA_LAUNCH(ctx, "zero_key", zero_key_kernel, ceil_div(n, 256), 256, 0, c->off, c->keylen, n, stat.ptr + 1,
+                     stat.ptr + 2);
     }
-    unsigned long long hs[2] = {0, 0};
+    unsigned long long hs[3] = {0, 0, 0};
     KARMA_HIP(hipMemcpyAsync(hs, stat.ptr, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
     c->exc_bases = (int64_t)hs[0];
     c->zero_key_maxlen = (int64_t)hs[1] - 1;
+    c->max_len = (int64_t)hs[2];
     *out = c;
     return KARMA_OK;
 }
@@ -927,34 +1111,51 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
     KARMA_HIP(hipMemsetAsync(err.ptr, 0, 4, ctx->stream));
     bool with_len = p->kmode != 8;
     const bool wave = M <= kWaveMaxM && p->S <= 8192;
-    const bool lds_ok = M * 4 <= 144 * 1024;
-    const int grid = wave ? grid_for(ceil_div(n, kPBlock / 64), 2048) : grid_for(n, lds_ok ? 4096 : 1024);
-    DevArray<uint32_t> scratch;
-    if (!wave && !lds_ok && (rc = scratch.alloc(ctx, (size_t)grid * M))) return rc;
-    const size_t lds = wave ? (size_t)((p->S + 7) & ~7) * 2 + (kPBlock / 64) * (((M + 3) & ~3) + 120) * 4
-                            : (lds_ok ? M * 4 : 0);
     const int k = p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode;
-    // wave variant: one round of resident blocks, each wave striding over contigs
-#define KARMA_PROFILE_LAUNCH(P56, W, LDS)                                                                        \
+    if (wave) {
+        // one round of resident blocks, each wave striding over contigs; u16
+        // counters when no contig reaches 2^16 bases (a count is <= L)
+        const bool p56 = p->kmode == KARMA_KMER_5P6;
+        const bool c16 = KARMA_PROF_C16 && c->max_len < 65536;
+        const size_t lds = (size_t)((tab_entries(p56, p->S) + 7) & ~7) * 2 +
+                           (kPBlock / 64) * (size_t)(hist_words(M, c16) + kProfWin) * 4;
+#define KARMA_WAVE_LAUNCH(P56, C16)                                                                              \
     do {                                                                                                         \
-        const int g_ = W ? resident_grid(ctx, reinterpret_cast<const void*>(&profile_kernel<P56, W, LDS>), kPBlock, \
-                                         lds, ceil_div(n, kPBlock / 64))                                         \
-                         : grid;                                                                                 \
-        KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, W, LDS>), g_, kPBlock, lds, c->packed.ptr,        \
+        const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_wave_kernel<P56, C16>), kPBlock, \
+                                     lds, ceil_div(n, kPBlock / 64));                                            \
+        KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16>), g_, kPBlock, lds, c->packed.ptr,      \
                      c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len,        \
-                     p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr,   \
-                     err.ptr, (int)p->S, p->row_tot.ptr);                                                        \
+                     p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err.ptr,       \
+                     (int)p->S, p->row_tot.ptr);                                                                 \
     } while (0)
-    if (p->kmode == KARMA_KMER_5P6) {
-        if (wave) KARMA_PROFILE_LAUNCH(true, true, true);
-        else if (lds_ok) KARMA_PROFILE_LAUNCH(true, false, true);
-        else KARMA_PROFILE_LAUNCH(true, false, false);
+        if (p56) {
+            if (c16) KARMA_WAVE_LAUNCH(true, true);
+            else KARMA_WAVE_LAUNCH(true, false);
+        } else {
+            if (c16) KARMA_WAVE_LAUNCH(false, true);
+            else KARMA_WAVE_LAUNCH(false, false);
+        }
+#undef KARMA_WAVE_LAUNCH
     } else {
-        if (wave) KARMA_PROFILE_LAUNCH(false, true, true);
-        else if (lds_ok) KARMA_PROFILE_LAUNCH(false, false, true);
-        else KARMA_PROFILE_LAUNCH(false, false, false);
-    }
+        const bool lds_ok = M * 4 <= 144 * 1024;
+        const int grid = grid_for(n, lds_ok ? 4096 : 1024);
+        DevArray<uint32_t> scratch;
+        if (!lds_ok && (rc = scratch.alloc(ctx, (size_t)grid * M))) return rc;
+        const size_t lds = lds_ok ? M * 4 : 0;
+#define KARMA_PROFILE_LAUNCH(P56, LDS)                                                                           \
+    KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, LDS>), grid, kPBlock, lds, c->packed.ptr, c->mask.ptr, \
+                 c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len, p->col_of_ord.ptr,      \
+                 p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err.ptr, (int)p->S,      \
+                 p->row_tot.ptr)
+        if (p->kmode == KARMA_KMER_5P6) {
+            if (lds_ok) KARMA_PROFILE_LAUNCH(true, true);
+            else KARMA_PROFILE_LAUNCH(true, false);
+        } else {
+            if (lds_ok) KARMA_PROFILE_LAUNCH(false, true);
+            else KARMA_PROFILE_LAUNCH(false, false);
+        }
 #undef KARMA_PROFILE_LAUNCH
+    }
     if (!out_is_device) {
         KARMA_HIP(hipMemcpyAsync(out, dst, (size_t)n * ld * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
