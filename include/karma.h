@@ -63,6 +63,9 @@ int karma_ctx_set_stream(karma_ctx* ctx, void* hip_stream);
 int karma_ctx_sync(karma_ctx* ctx);
 /* Per-kernel HIP-event timing on the launch stream (for bench.py's roofline). */
 int karma_timing_enable(karma_ctx* ctx, int on);
+/* Restrict timing to launches of one kernel name (NULL or "": every kernel), so a
+ * timed region carries two events per launch of that kernel only. */
+int karma_timing_only(karma_ctx* ctx, const char* name);
 int karma_timing_reset(karma_ctx* ctx);
 /* Fills up to cap entries: name (NUL-separated into names[cap*64]), total ms, launches.
  * Returns number of distinct kernels in *n. Synchronises the stream. */

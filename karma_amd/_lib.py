@@ -48,6 +48,7 @@ _SIGS = {
     "karma_ctx_set_stream": [_c_p, _c_p],
     "karma_ctx_sync": [_c_p],
     "karma_timing_enable": [_c_p, _i32],
+    "karma_timing_only": [_c_p, ctypes.c_char_p],
     "karma_timing_reset": [_c_p],
     "karma_timing_read": [_c_p, ctypes.c_char_p, _c_p, _c_p, _i32, ctypes.POINTER(ctypes.c_int)],
     "karma_dev_alloc": [_c_p, ctypes.c_size_t, _PP],
@@ -174,7 +175,9 @@ class Context:
     def sync(self):
         call("karma_ctx_sync", self.h)
 
-    def timing(self, on=True):
+    def timing(self, on=True, only=None):
+        """Per-kernel HIP-event timing; `only` restricts it to one kernel name."""
+        call("karma_timing_only", self.h, (only or "").encode())
         call("karma_timing_enable", self.h, 1 if on else 0)
 
     def timing_reset(self):

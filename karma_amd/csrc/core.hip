@@ -67,6 +67,7 @@ void ctx_free(karma_ctx* ctx, void* p) {
 void timing_start(karma_ctx* ctx, const char* name, hipEvent_t* ev_stop) {
     *ev_stop = nullptr;
     if (!ctx->timing) return;
+    if (!ctx->timing_only.empty() && ctx->timing_only != name) return;
     hipEvent_t a, b;
     if (ctx->event_pool.size() >= 2) {
         a = ctx->event_pool.back();
@@ -185,6 +186,12 @@ int karma_ctx_sync(karma_ctx* ctx) {
 int karma_timing_enable(karma_ctx* ctx, int on) {
     KARMA_CHECK(ctx, KARMA_ERR_ARG, "null ctx");
     ctx->timing = on != 0;
+    return KARMA_OK;
+}
+
+int karma_timing_only(karma_ctx* ctx, const char* name) {
+    KARMA_CHECK(ctx, KARMA_ERR_ARG, "null ctx");
+    ctx->timing_only = name ? name : "";
     return KARMA_OK;
 }
 

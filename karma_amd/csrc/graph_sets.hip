@@ -127,6 +127,17 @@ __device__ __forceinline__ int rank_below(unsigned long long m) {
 // code (m0 | M << 24) of a compact read, or general / big
 // 6 waves per SIMD: the LDS slices allow 6 blocks per CU; 80 VGPRs fit them
 // (the compiler's own choice, 82-84, allows 5: 0.714 -> 0.670 ms on config 3)
+#ifndef KARMA_CLS_V2
+#define KARMA_CLS_V2 1
+#endif
+#if KARMA_CLS_V2
+#define KARMA_CLS_KERNEL classify2_kernel
+#else
+#define KARMA_CLS_KERNEL classify_kernel
+#endif
+#ifndef KARMA_CLS_ABL
+#define KARMA_CLS_ABL 0  // ablation builds only: 1 loads alone, 2 loads + read starts
+#endif
 #ifndef KARMA_CLS_WAVES
 #define KARMA_CLS_WAVES 6
 #endif
@@ -171,6 +182,21 @@ __global__ void __launch_bounds__(kCW) KARMA_CLS_ATTR classify_kernel(ClassArgs 
     prefetch(c_lo);
     uint32_t nc = 0, ng = 0;
     int bad_order = 0, bad_contig = 0;
+#if KARMA_CLS_ABL == 1
+    uint32_t acc = 0;
+    for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) {
+#pragma unroll
+        for (int u = 0; u < kCPer; ++u) acc ^= nxt[u].x ^ nxt[u].y ^ nxt[u].z ^ nxt[u].w;
+        acc ^= nxc.x ^ nxh.y;
+        prefetch(t0 + kCIter);
+    }
+    if (lane == 0) {
+        P.n_codes[chunk] = 0;
+        P.n_gen[chunk] = 0;
+    }
+    if (acc == 0x9E3779B9u) P.flags[3] = 1;
+    return;
+#endif
     for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) {
         const int tn = (int)min<int64_t>(kCIter, c_hi - t0);
         // ---- read starts (records past tn are the following ones) ----
@@ -211,6 +237,10 @@ __global__ void __launch_bounds__(kCW) KARMA_CLS_ATTR classify_kernel(ClassArgs 
         if (lane < kMaxFast) sr[kCIter + lane] = nxh;
         prefetch(t0 + kCIter);
         wave_sync();
+#if KARMA_CLS_ABL == 2
+        nc += ns;
+        continue;
+#endif
         // ---- read sizes: the gap to the next read start (the last read's end
         // is found in the slice + halo; 9 means more than 8 records) ----
         if (lane == 0 && ns > 0) {
@@ -300,6 +330,274 @@ __global__ void __launch_bounds__(kCW) KARMA_CLS_ATTR classify_kernel(ClassArgs 
             emit(code, gen, j0);
         }
         wave_sync();  // every lane is done with the slice
+    }
+#if KARMA_CLS_ABL == 2
+    if (lane == 0) {
+        P.n_codes[chunk] = 0;
+        P.n_gen[chunk] = 0;
+    }
+    if (nc == 0x9E3779B9u) P.flags[3] = 1;
+    return;
+#endif
+    if (lane == 0) {
+        P.n_codes[chunk] = nc;
+        P.n_gen[chunk] = ng;
+        if (nc) atomicAdd(P.blk_items + chunk / P.lists_per_block, (unsigned long long)nc);
+    }
+    if (bad_order) P.flags[0] = 1;
+    if (bad_contig) P.flags[1] = 1;
+}
+
+// ---- classify, register-resident variant ---------------------------------------
+// The same outputs as classify_kernel, without LDS: lane l of a 512-record step
+// holds records 8l .. 8l + 7 (four 16-byte loads) and walks them in order.
+//   * a read that starts and ends inside the lane is emitted at its end;
+//   * the lane's last read (its "tail") continues into the next lane's
+//     "head" (the records before that lane's first read start): the next lane
+//     receives the tail (DPP) and emits the merged read; lane 63's tail is
+//     carried into the next step's lane 0, and after the chunk's last step
+//     into a tail-only pass over the next 8 records;
+//   * a read longer than 8 records (a tail plus a head of > 8 records, or a
+//     lane without any read start) goes to the big-read list from the lane
+//     that merges its tail.
+// A read's contigs are tracked as min, max and a bit window relative to its
+// first contig - 3; a compact read (max - min < 4) becomes (m0 | M << 24).
+struct RState {
+    uint32_t fm3, win, mn, mx;  // first contig - 3, bits (c - fm3), min, max
+};
+
+__device__ __forceinline__ void rs_reset(RState& s, uint32_t c) {
+    s.fm3 = c - 3u;
+    s.win = 8u;
+    s.mn = c;
+    s.mx = c;
+}
+__device__ __forceinline__ void rs_add(RState& s, uint32_t c) {
+    s.win |= 1u << ((c - s.fm3) & 31u);
+    s.mn = min(s.mn, c);
+    s.mx = max(s.mx, c);
+}
+// compact code, or kEmpty when the read is general
+__device__ __forceinline__ uint32_t rs_code(const RState& s, uint32_t N, int compact) {
+    const uint32_t rel = s.win >> ((s.mn - s.fm3) & 31u);
+    return compact && s.mx - s.mn < 4u && s.mx < N ? (s.mn | (rel >> 1) << 24) : kEmpty;
+}
+__device__ __forceinline__ uint32_t rs_code2(const RState& a, const RState& b, uint32_t N, int compact) {
+    const uint32_t m0 = min(a.mn, b.mn), mx = max(a.mx, b.mx);
+    const uint32_t ra = (a.win >> ((a.mn - a.fm3) & 31u)) << ((a.mn - m0) & 31u);
+    const uint32_t rb = (b.win >> ((b.mn - b.fm3) & 31u)) << ((b.mn - m0) & 31u);
+    return compact && mx - m0 < 4u && mx < N ? (m0 | ((ra | rb) >> 1) << 24) : kEmpty;
+}
+
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lane l <- lane l - 1; lane 0 <- old
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+#ifndef KARMA_CLS2_LDS
+#define KARMA_CLS2_LDS 1  // coalesced loads transposed through LDS (0: per-lane 64-byte loads)
+#endif
+#ifndef KARMA_CLS2_WAVES
+#define KARMA_CLS2_WAVES 6
+#endif
+__global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
+classify2_kernel(ClassArgs P) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t chunk = (int64_t)blockIdx.x * (kCW / 64) + wave;
+    const int64_t c_lo = chunk * kCChunk;
+    if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
+    const int64_t c_hi = min(P.A, c_lo + kCChunk);
+    uint32_t* out = P.codes + c_lo;
+#if KARMA_CLS2_LDS
+    // transpose buffer: lane l's 8 records at byte 80l (16 bytes of padding per
+    // lane make both the 16-byte stores and the lane-sequential reads conflict-free)
+    __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][64 * 5];
+    u32x4* tb = tbuf[wave];
+#endif
+
+    u32x4 nxt[kCPer];
+    // records [t0, hi) of a step; lane l ends up with records t0 + 8l .. + 7
+    auto prefetch = [&](int64_t t0, int64_t hi) {
+#if KARMA_CLS2_LDS
+        // coalesced: unit u of lane l = records t0 + 128u + 2l, + 1
+        const int64_t gb = t0 + 2 * lane;
+#else
+        const int64_t gb = t0 + 8 * lane;
+#endif
+        if (t0 + kCIter <= hi) {
+#pragma unroll
+            for (int u = 0; u < kCPer; ++u) {
+#if KARMA_CLS2_LDS
+                const int64_t gi = gb + 128 * u;
+#else
+                const int64_t gi = gb + 2 * u;
+#endif
+                nxt[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.rec + gi));
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kCPer; ++u) {
+#if KARMA_CLS2_LDS
+                const int64_t gi = gb + 128 * u;
+#else
+                const int64_t gi = gb + 2 * u;
+#endif
+                const uint2 r0 = gi < hi ? P.rec[gi] : make_uint2(kEmpty, kEmpty);
+                const uint2 r1 = gi + 1 < hi ? P.rec[gi + 1] : make_uint2(kEmpty, kEmpty);
+                nxt[u] = u32x4{r0.x, r0.y, r1.x, r1.y};
+            }
+        }
+    };
+    prefetch(c_lo, c_hi);
+    // carry from the previous lane 63: its last read id, and its tail read
+    bool have_prev = c_lo > 0;
+    uint32_t prev_rid = have_prev ? P.rec[c_lo - 1].x : kEmpty;
+    bool ct_ok = false;  // a tail read (started in this chunk) is carried
+    RState ct{};
+    uint32_t ct_len = 0, ct_pos = 0;
+    uint32_t nc = 0, ng = 0;
+    int bad_order = 0, bad_contig = 0;
+    for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) {
+        uint32_t rid[8], ctg[8];
+#if KARMA_CLS2_LDS
+        {
+            // loader lane L, unit u -> lane 16u + L/4, unit L & 3
+#pragma unroll
+            for (int u = 0; u < kCPer; ++u) tb[5 * (16 * u + (lane >> 2)) + (lane & 3)] = nxt[u];
+            wave_sync();
+#pragma unroll
+            for (int u = 0; u < kCPer; ++u) {
+                const u32x4 q = tb[5 * lane + u];
+                rid[2 * u] = q.x;
+                ctg[2 * u] = q.y;
+                rid[2 * u + 1] = q.z;
+                ctg[2 * u + 1] = q.w;
+            }
+            wave_sync();
+        }
+#else
+#pragma unroll
+        for (int u = 0; u < kCPer; ++u) {
+            rid[2 * u] = nxt[u].x;
+            ctg[2 * u] = nxt[u].y;
+            rid[2 * u + 1] = nxt[u].z;
+            ctg[2 * u + 1] = nxt[u].w;
+        }
+#endif
+        if (t0 + kCIter < c_hi) prefetch(t0 + kCIter, c_hi);
+        // valid records of this lane (own reads start at a valid record)
+        const int nval = (int)max<int64_t>(0, min<int64_t>(8, c_hi - (t0 + 8 * lane)));
+        const bool first_any = have_prev || lane > 0;
+        const uint32_t prev_last = dpp_shr1(prev_rid, rid[7]);
+        uint32_t sm = (!first_any || rid[0] != prev_last) ? 1u : 0u;  // bit i: a read starts at record i
+        int bo = (nval > 0 && first_any && prev_last > rid[0]) ? 1 : 0;
+        int bc = (nval > 0 && ctg[0] >= P.N) ? 1 : 0;
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+            sm |= (rid[i] != rid[i - 1] ? 1u : 0u) << i;
+            bo |= (i < nval && rid[i - 1] > rid[i]) ? 1 : 0;
+            bc |= (i < nval && ctg[i] >= P.N) ? 1 : 0;
+        }
+        bad_order |= bo;
+        bad_contig |= bc;
+        // emission: codes from the front of the chunk's region, general read
+        // starts (chunk-relative) from the back, big reads to the big list
+        auto emit = [&](bool e, uint32_t code, uint32_t pos, bool big) {
+            const bool ec = e && !big && code != kEmpty;
+            const unsigned long long b = __ballot(ec);
+            if (ec) out[nc + rank_below(b)] = code;
+            nc += __popcll(b);
+            const bool eg = e && !big && code == kEmpty;
+            const unsigned long long g = __ballot(eg);
+            if (g) {  // rare
+                if (eg) out[kCChunk - 1 - (ng + rank_below(g))] = pos;
+                ng += __popcll(g);
+            }
+            if (__ballot(e && big)) {
+                if (e && big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + pos;
+            }
+        };
+        // walk the lane (branch-free state updates): an own read ending at
+        // record i < 7 is emitted there
+        RState st, hd;
+        rs_reset(st, ctg[0]);
+        hd = st;
+        // head = records before the first read start (8: no start in the lane)
+        const uint32_t hlen = (sm & 1u) ? 0u : (sm ? (uint32_t)__builtin_ctz(sm) : 8u);
+        uint32_t spos = 0;
+        const uint32_t ubase = (uint32_t)(t0 - c_lo) + 8u * lane;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i > 0) {
+                const bool si = (sm >> i) & 1u;
+                const bool cap = (uint32_t)i == hlen;  // first start: the head ends here
+                hd.fm3 = cap ? st.fm3 : hd.fm3;
+                hd.win = cap ? st.win : hd.win;
+                hd.mn = cap ? st.mn : hd.mn;
+                hd.mx = cap ? st.mx : hd.mx;
+                spos = si ? (uint32_t)i : spos;
+                const uint32_t c = ctg[i];
+                const uint32_t fm3 = si ? c - 3u : st.fm3;
+                const uint32_t bit = 1u << ((c - fm3) & 31u);
+                st.win = si ? bit : (st.win | bit);
+                st.fm3 = fm3;
+                st.mn = si ? c : min(st.mn, c);
+                st.mx = si ? c : max(st.mx, c);
+            }
+            if (i < 7) {
+                const bool e = ((sm >> (i + 1)) & 1u) && hlen <= (uint32_t)i && (int)spos < nval;
+                emit(e, rs_code(st, P.N, P.compact), ubase + spos, false);
+            }
+        }
+        if (hlen == 8u) hd = st;  // no read starts here: the whole lane is a head
+        // this lane's tail (an own read reaching record 7) -> the next lane
+        const bool t_ok = hlen < 8u && (int)spos < nval;
+        const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
+        RState in;
+        in.fm3 = dpp_shr1(ct.fm3, st.fm3);
+        in.win = dpp_shr1(ct.win, st.win);
+        in.mn = dpp_shr1(ct.mn, st.mn);
+        in.mx = dpp_shr1(ct.mx, st.mx);
+        const uint32_t in_pk = dpp_shr1(ct_ok ? (ct_len | ct_pos << 8) : kEmpty, t_ok ? (t_len | t_pos << 8) : kEmpty);
+        // the incoming tail, merged with this lane's head when the read continues
+        {
+            const bool have = in_pk != kEmpty;
+            const uint32_t in_len = in_pk & 255u, in_pos = in_pk >> 8;
+            const bool cont = !(sm & 1u);
+            const bool big = cont && in_len + hlen > (uint32_t)kMaxFast;
+            emit(have, cont ? rs_code2(in, hd, P.N, P.compact) : rs_code(in, P.N, P.compact), in_pos, big);
+        }
+        // carry lane 63 into the next step
+        ct_ok = __builtin_amdgcn_readlane((int)t_ok, 63) != 0;
+        ct.fm3 = (uint32_t)__builtin_amdgcn_readlane((int)st.fm3, 63);
+        ct.win = (uint32_t)__builtin_amdgcn_readlane((int)st.win, 63);
+        ct.mn = (uint32_t)__builtin_amdgcn_readlane((int)st.mn, 63);
+        ct.mx = (uint32_t)__builtin_amdgcn_readlane((int)st.mx, 63);
+        ct_len = (uint32_t)__builtin_amdgcn_readlane((int)t_len, 63);
+        ct_pos = (uint32_t)__builtin_amdgcn_readlane((int)t_pos, 63);
+        prev_rid = (uint32_t)__builtin_amdgcn_readlane((int)rid[7], 63);
+        have_prev = true;
+    }
+    // the chunk's last tail read continues into the next chunk's first records
+    // (at most 8 of them matter): uniform scalar walk
+    if (ct_ok) {
+        RState h{};
+        uint32_t hl = 0;
+        for (; hl < (uint32_t)kMaxFast && c_hi + hl < P.A; ++hl) {
+            const uint2 r = P.rec[c_hi + hl];
+            if (r.x != prev_rid) break;
+            if (hl == 0) rs_reset(h, r.y);
+            else rs_add(h, r.y);
+        }
+        const bool big = ct_len + hl > (uint32_t)kMaxFast;
+        const uint32_t code = big ? kEmpty : hl ? rs_code2(ct, h, P.N, P.compact) : rs_code(ct, P.N, P.compact);
+        if (lane == 0) {
+            if (big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + ct_pos;
+            else if (code != kEmpty) out[nc] = code;
+            else out[kCChunk - 1 - ng] = ct_pos;
+        }
+        nc += !big && code != kEmpty ? 1u : 0u;
+        ng += !big && code == kEmpty ? 1u : 0u;
     }
     if (lane == 0) {
         P.n_codes[chunk] = nc;
@@ -1154,7 +1452,7 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         if (A > 0) {
             ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags};
-            KARMA_LAUNCH(ctx, "graph_classify", classify_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", KARMA_CLS_KERNEL, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags);
@@ -1277,7 +1575,7 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         if (A > 0) {
             ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags};
-            KARMA_LAUNCH(ctx, "graph_classify", classify_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", KARMA_CLS_KERNEL, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         } else {
             KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
             KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));

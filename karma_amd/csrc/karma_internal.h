@@ -57,6 +57,7 @@ struct karma_ctx {
     size_t cached_bytes = 0;
     // per-kernel event timing
     bool timing = false;
+    std::string timing_only;  // empty: time every kernel
     std::vector<karma::TimedLaunch> launches;
     std::vector<hipEvent_t> event_pool;
     // pinned host scratch for small status readbacks (one async copy + one sync)

@@ -15,9 +15,11 @@ import sys
 # rocprof kernel name -> bench.py kernel (KARMA_LAUNCH) name
 NAMES = {
     "classify_kernel": "graph_classify",
+    "classify2_kernel": "graph_classify",
     "partition_kernel<CodeStream>": "graph_code_partition",
     "code_reduce_kernel": "graph_code_reduce",
     "profile_kernel<true, true, true>": "kmer_profile",
+    "profile_wave_kernel<true, true>": "kmer_profile",
     "presence_kernel<true>": "kmer_presence",
 }
 
