@@ -6,7 +6,7 @@ set -e
 NAME=$1; shift
 EXTRA="$*"
 REPO=$(cd "$(dirname "$0")/.." && pwd)
-SRC=$REPO/karma_amd/csrc
+SRC=${SRC:-$REPO/karma_amd/csrc}
 OUT=$REPO/karma_amd/variants
 B=$OUT/build_$NAME
 mkdir -p $B

@@ -17,6 +17,7 @@ NAMES = {
     "classify_kernel": "graph_classify",
     "classify2_kernel": "graph_classify",
     "partition_kernel<CodeStream>": "graph_code_partition",
+    "partition_kernel<CodeStreamT<128> >": "graph_code_partition",
     "code_reduce_kernel": "graph_code_reduce",
     "profile_kernel<true, true, true>": "kmer_profile",
     "profile_wave_kernel<true, true>": "kmer_profile",
