@@ -21,6 +21,8 @@
  *   karma_fasta_*                   read_fasta_file                      karma/karma.py:40-61
  *   karma_eq_*                      eq_classes.txt parse                 karma/read_graph.py:75-92
  *   karma_sam_*                     Contig readsets from SAM lines       karma/contig.py:24,34, hisat2.py:76-81
+ *   karma_adj_*                     graph consumers: unconnected nodes, node weights, edge_list
+ *                                   karma/read_graph.py:150-190, :315-357
  *
  * The reference is pure Python and has no FFI; INTEGRATION.md shows the ctypes
  * binding (karma_amd/_lib.py) that the Python classes mirroring the reference
@@ -215,6 +217,43 @@ int karma_sam_info(karma_sam* s, int64_t* n_records, int64_t* n_reads, int64_t* 
 int karma_sam_get(karma_sam* s, uint32_t* records, char* rnames, int64_t* rname_off, int64_t* q_start,
                   int32_t* q_len);
 int karma_sam_destroy(karma_sam* s);
+
+/* ---- graph consumers --------------------------------
+ * read_graph.py:150-172 (get_unconnected_nodes / get_connected_nodes),
+ * :174-190 + :315-344 (node weights, representative sequences) and :350-357
+ * (edge_list, MCL stdin), as karma.py:255-395 uses them on
+ * ReadGraph(full_graph.subgraph(cluster)).  A karma_adj is a graph laid out as
+ * networkx iterates it: nodes in iteration order (positions 0..n-1, each with an
+ * id into the caller's name table) and per node its neighbours (positions) and
+ * weights in adjacency-dict order. */
+typedef struct karma_adj karma_adj;
+/* add_edge(a[e], b[e], weight=w[e]) for e = 0..n_edges-1 on a graph whose n
+ * nodes were added first (positions = ids order when ids == NULL). */
+int karma_adj_from_edges(karma_ctx* ctx, int64_t n, const uint32_t* ids, const uint32_t* a, const uint32_t* b,
+                         const double* w, int64_t n_edges, int is_device, karma_adj** out);
+/* An exported adjacency: off[n+1] into nbr (positions) / w, in dict order. */
+int karma_adj_from_lists(karma_ctx* ctx, int64_t n, const uint32_t* ids, const int64_t* off, const uint32_t* nbr,
+                         const double* w, int is_device, karma_adj** out);
+/* nx.Graph(G.subgraph(nodes)) of G = src: order[k] = src positions in the
+ * view's node order (host).  Adjacency rebuilt as from_dict_of_dicts does. */
+int karma_adj_view(karma_adj* src, const int64_t* order, int64_t k, karma_adj** out);
+/* G.remove_nodes_from: keep[n] (host, 1 = stays); remaining orders unchanged. */
+int karma_adj_keep(karma_adj* src, const uint8_t* keep, karma_adj** out);
+int karma_adj_info(karma_adj* g, int64_t* n, int64_t* n_entries);
+/* Host copies of the layout (any pointer may be NULL). */
+int karma_adj_get(karma_adj* g, uint32_t* ids, int64_t* off, uint32_t* nbr, double* w);
+/* len(G.adj[u]) per position (nx.all_neighbors, a self-loop once). */
+int karma_adj_degrees(karma_adj* g, int64_t* deg_host);
+/* 0 + w_1 + w_2 + ... over G.adj[u] in order, f64 left to right (read_graph.py:183-187). */
+int karma_adj_node_weights(karma_adj* g, double* w_host);
+/* "\n".join(f"{A} {B} {w}" for A, B, w in G.edges(data="weight")) as UTF-8:
+ * names[name_off[i]:name_off[i+1]] is the UTF-8 name of id i; w is written as
+ * Python repr(float).  out == NULL: only *len (the text is kept for the next call). */
+int karma_adj_edge_list(karma_adj* g, const uint8_t* names, const int64_t* name_off, int64_t n_names,
+                        int names_on_device, uint8_t* out, int64_t cap, int64_t* len);
+int karma_adj_destroy(karma_adj* g);
+/* Host build of the device's repr(float) formatter, for tests: one line per value. */
+int karma_repr_f64_host(const double* x, int64_t n, char* out, int64_t cap, int64_t* len);
 
 #ifdef __cplusplus
 }

@@ -102,6 +102,17 @@ _SIGS = {
     "karma_sam_info": [_c_p, _I64P, _I64P, _I64P, _I64P, _I64P],
     "karma_sam_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
     "karma_sam_destroy": [_c_p],
+    "karma_adj_from_edges": [_c_p, _i64, _c_p, _c_p, _c_p, _c_p, _i64, _i32, _PP],
+    "karma_adj_from_lists": [_c_p, _i64, _c_p, _c_p, _c_p, _c_p, _i32, _PP],
+    "karma_adj_view": [_c_p, _c_p, _i64, _PP],
+    "karma_adj_keep": [_c_p, _c_p, _PP],
+    "karma_adj_info": [_c_p, _I64P, _I64P],
+    "karma_adj_get": [_c_p, _c_p, _c_p, _c_p, _c_p],
+    "karma_adj_degrees": [_c_p, _c_p],
+    "karma_adj_node_weights": [_c_p, _c_p],
+    "karma_adj_edge_list": [_c_p, _c_p, _c_p, _i64, _i32, _c_p, _i64, _I64P],
+    "karma_adj_destroy": [_c_p],
+    "karma_repr_f64_host": [_c_p, _i64, _c_p, _i64, _I64P],
 }
 
 EXPORTED = tuple(_SIGS) + ("karma_last_error",)

@@ -1,0 +1,591 @@
+// consumers.hip — the read graph's consumers on the device.
+//
+// Reference (lmfaber/karma, networkx + Python) being replaced:
+//   ReadGraph.get_unconnected_nodes / get_connected_nodes  karma/read_graph.py:150-172
+//   ReadGraph.__calculate_node_weights                     karma/read_graph.py:174-190
+//   ReadGraph.calculate_representative_sequences (weights) karma/read_graph.py:315-344
+//   ReadGraph.edge_list (MCL stdin text)                   karma/read_graph.py:350-357
+// as karma.py:255-395 uses them on ReadGraph(full_graph.subgraph(cluster)).
+//
+// A karma_adj holds a graph the way networkx iterates it: nodes in iteration
+// order (position 0..n-1, each with an id into the caller's name table) and,
+// per node, its neighbours (positions) and weights in adjacency-dict order.
+// Every consumer is a function of that layout:
+//   degree(u)        = len(G.adj[u])                     (all_neighbors, self-loop once)
+//   node_weight(u)   = 0 + w_1 + w_2 + ... in G.adj[u] order   (f64, left to right)
+//   edge_list        = for u in order: for v in G.adj[u] with pos(v) >= pos(u):
+//                      "name(u) name(v) repr(w)", joined by '\n'
+// The layouts networkx produces are rebuilt here:
+//   karma_adj_from_edges  add_edge calls in a known order on pre-added nodes
+//                         (adj[u] = incident edges in call order);
+//   karma_adj_view        nx.Graph(G.subgraph(nodes)) — from_dict_of_dicts over the
+//                         view: nodes in view order (the caller's: networkx walks
+//                         the smaller of the filter set and G's nodes); each u's
+//                         view neighbours L(u) in G.adj[u] order (FilterAdjacency
+//                         filters a node's dict in place); the copy's adj[u] =
+//                         neighbours before u by position, then the L(u) entries
+//                         at or after u in L order;
+//   karma_adj_keep        G.remove_nodes_from (orders kept).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "karma_internal.h"
+#include "repr.h"
+
+using namespace karma;
+
+struct karma_adj {
+    karma_ctx* ctx = nullptr;
+    int64_t n = 0, m = 0;        // nodes, adjacency entries
+    DevArray<uint32_t> ids;      // n: name id per position
+    DevArray<int64_t> off;       // n + 1
+    DevArray<uint32_t> nbr;      // m: neighbour positions
+    DevArray<double> w;          // m
+    DevArray<uint8_t> text;      // cached edge_list bytes (+1 trailing newline)
+    int64_t text_len = -1;
+    const void* text_names = nullptr;
+};
+
+namespace {
+
+__global__ void iota_u32_kernel(uint32_t* p, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = (uint32_t)i;
+}
+
+int grid_of(int64_t n, int b = 256) { return (int)std::max<int64_t>(1, ceil_div(n, b)); }
+
+// ---- from edges: entries (u, edge) sorted by u then edge --------------------
+__global__ void edge_entries_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, int64_t E,
+                                    const int64_t* __restrict__ slot, uint64_t* __restrict__ key,
+                                    uint32_t* __restrict__ val, int* __restrict__ bad, uint32_t n) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const uint32_t x = a[e], y = b[e];
+    if (x >= n || y >= n) {
+        *bad = 1;
+        return;
+    }
+    const int64_t s = slot[e];  // 2 entries, or 1 for a self-loop
+    key[s] = (uint64_t)x << 32 | (uint64_t)e;
+    val[s] = (uint32_t)e;
+    if (x != y) {
+        key[s + 1] = (uint64_t)y << 32 | (uint64_t)e;
+        val[s + 1] = (uint32_t)e;
+    }
+}
+
+__global__ void edge_slots_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, int64_t E,
+                                  int64_t* __restrict__ width) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e <= E) width[e] = e < E ? (a[e] != b[e] ? 2 : 1) : 0;
+}
+
+__global__ void entries_fill_kernel(const uint64_t* __restrict__ key, const uint32_t* __restrict__ eidx, int64_t m,
+                                    const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                    const double* __restrict__ w, uint32_t* __restrict__ nbr,
+                                    double* __restrict__ wo, int64_t* __restrict__ cnt) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t u = (uint32_t)(key[j] >> 32), e = eidx[j];
+    nbr[j] = a[e] == u ? b[e] : a[e];
+    wo[j] = w[e];
+    atomicAdd(reinterpret_cast<unsigned long long*>(cnt + u), 1ull);
+}
+
+// ---- view -----------------------------------------------------------------
+__global__ void posmap_kernel(const int64_t* __restrict__ order, int64_t k, int64_t n_src,
+                              int32_t* __restrict__ pos, int* __restrict__ bad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const int64_t u = order[i];
+    if (u < 0 || u >= n_src) {
+        *bad = 1;
+        return;
+    }
+    if (atomicExch(pos + u, (int32_t)i) != -1) *bad = 2;  // a node twice
+}
+
+__global__ void view_count_kernel(const int64_t* __restrict__ order, int64_t k, const int64_t* __restrict__ off,
+                                  const uint32_t* __restrict__ nbr, const int32_t* __restrict__ pos,
+                                  int64_t* __restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > k) return;
+    int64_t c = 0;
+    if (i < k) {
+        const int64_t u = order[i];
+        for (int64_t j = off[u]; j < off[u + 1]; ++j) c += pos[nbr[j]] >= 0;
+    }
+    cnt[i] = c;
+}
+
+// key (node << 32 | rank) orders the copy's adjacency: neighbours before the
+// node by position, then the rest in list order
+__global__ void view_fill_kernel(const int64_t* __restrict__ order, int64_t k, const int64_t* __restrict__ off,
+                                 const uint32_t* __restrict__ nbr, const double* __restrict__ w,
+                                 const int32_t* __restrict__ pos, const int64_t* __restrict__ noff,
+                                 uint64_t* __restrict__ key, uint32_t* __restrict__ x_out,
+                                 double* __restrict__ w_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const int64_t u = order[i];
+    int64_t d = noff[i];
+    uint32_t r = 0;
+    for (int64_t j = off[u]; j < off[u + 1]; ++j) {
+        const int32_t x = pos[nbr[j]];
+        if (x < 0) continue;
+        const uint32_t rank = (int64_t)x < i ? (uint32_t)x : (uint32_t)(k + r);
+        key[d] = (uint64_t)i << 32 | rank;
+        x_out[d] = (uint32_t)x;
+        w_out[d] = w[j];
+        ++d;
+        ++r;
+    }
+}
+
+__global__ void gather_entries_kernel(const uint32_t* __restrict__ idx, int64_t m, const uint32_t* __restrict__ x_in,
+                                      const double* __restrict__ w_in, uint32_t* __restrict__ x_out,
+                                      double* __restrict__ w_out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    x_out[j] = x_in[idx[j]];
+    w_out[j] = w_in[idx[j]];
+}
+
+__global__ void gather_ids_kernel(const int64_t* __restrict__ order, int64_t k, const uint32_t* __restrict__ ids_src,
+                                  uint32_t* __restrict__ ids) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) ids[i] = ids_src[order[i]];
+}
+
+// ---- keep -------------------------------------------------------------------
+__global__ void keep_count_kernel(const uint8_t* __restrict__ keep, int64_t n, const int64_t* __restrict__ off,
+                                  const uint32_t* __restrict__ nbr, int64_t* __restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    int64_t c = 0;
+    if (i < n && keep[i])
+        for (int64_t j = off[i]; j < off[i + 1]; ++j) c += keep[nbr[j]] != 0;
+    cnt[i] = c;
+}
+
+__global__ void keep_fill_kernel(const uint8_t* __restrict__ keep, int64_t n, const int64_t* __restrict__ off,
+                                 const uint32_t* __restrict__ nbr, const double* __restrict__ w,
+                                 const int64_t* __restrict__ npos, const int64_t* __restrict__ ooff,
+                                 const uint32_t* __restrict__ ids, uint32_t* __restrict__ nbr_out,
+                                 double* __restrict__ w_out, uint32_t* __restrict__ ids_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !keep[i]) return;
+    ids_out[npos[i]] = ids[i];
+    int64_t d = ooff[i];  // entries of dropped nodes count 0, so the old-index scan is the new start
+    for (int64_t j = off[i]; j < off[i + 1]; ++j) {
+        const uint32_t v = nbr[j];
+        if (!keep[v]) continue;
+        nbr_out[d] = (uint32_t)npos[v];
+        w_out[d] = w[j];
+        ++d;
+    }
+}
+
+__global__ void keep_off_kernel(const uint8_t* __restrict__ keep, int64_t n, const int64_t* __restrict__ npos,
+                                const int64_t* __restrict__ ooff, int64_t* __restrict__ off) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) off[npos[n]] = ooff[n];
+    else if (keep[i]) off[npos[i]] = ooff[i];
+}
+
+__global__ void u8_to_i64_kernel(const uint8_t* __restrict__ in, int64_t n, int64_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) out[i] = i < n ? (in[i] != 0) : 0;
+}
+
+// ---- consumers ----------------------------------------------------------------
+__global__ void node_weights_kernel(const int64_t* __restrict__ off, const double* __restrict__ w, int64_t n,
+                                    double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s = 0.0;  // read_graph.py:183-187: 0 + w_1 + w_2 + ..., left to right
+    for (int64_t j = off[i]; j < off[i + 1]; ++j) s = __dadd_rn(s, w[j]);
+    out[i] = s;
+}
+
+// bytes of node i's lines, each with its '\n'
+__global__ void edge_list_len_kernel(const int64_t* __restrict__ off, const uint32_t* __restrict__ nbr,
+                                     const double* __restrict__ w, const uint32_t* __restrict__ ids, int64_t n,
+                                     const int64_t* __restrict__ name_off, int64_t* __restrict__ len) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    int64_t s = 0;
+    if (i < n) {
+        const uint32_t a = ids[i];
+        const int64_t la = name_off[a + 1] - name_off[a];
+        for (int64_t j = off[i]; j < off[i + 1]; ++j) {
+            const uint32_t v = nbr[j];
+            if ((int64_t)v < i) continue;  // G.edges(): each edge from its earlier end
+            const uint32_t b = ids[v];
+            s += la + 1 + (name_off[b + 1] - name_off[b]) + 1 + karma_repr::repr_f64(w[j], nullptr) + 1;
+        }
+    }
+    len[i] = s;
+}
+
+__global__ void edge_list_write_kernel(const int64_t* __restrict__ off, const uint32_t* __restrict__ nbr,
+                                       const double* __restrict__ w, const uint32_t* __restrict__ ids, int64_t n,
+                                       const uint8_t* __restrict__ names, const int64_t* __restrict__ name_off,
+                                       const int64_t* __restrict__ start, uint8_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t* p = out + start[i];
+    const uint32_t a = ids[i];
+    for (int64_t j = off[i]; j < off[i + 1]; ++j) {
+        const uint32_t v = nbr[j];
+        if ((int64_t)v < i) continue;
+        const uint32_t b = ids[v];
+        for (int64_t t = name_off[a]; t < name_off[a + 1]; ++t) *p++ = names[t];
+        *p++ = ' ';
+        for (int64_t t = name_off[b]; t < name_off[b + 1]; ++t) *p++ = names[t];
+        *p++ = ' ';
+        char buf[karma_repr::kMaxRepr];
+        const int r = karma_repr::repr_f64(w[j], buf);
+        for (int t = 0; t < r; ++t) *p++ = (uint8_t)buf[t];
+        *p++ = '\n';
+    }
+}
+
+int scan_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
+    size_t tb = 0;
+    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, ctx->stream));
+    DevArray<uint8_t> tmp;
+    KARMA_TRY(tmp.alloc(ctx, tb ? tb : 1));
+    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.ptr, tb, in, out, n, ctx->stream));
+    return KARMA_OK;
+}
+
+int read_i64(karma_ctx* ctx, const int64_t* dev, int64_t* host) {
+    KARMA_HIP(hipMemcpyAsync(host, dev, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    return KARMA_OK;
+}
+
+int check_flag(karma_ctx* ctx, const int* dev, const char* what) {
+    int h = 0;
+    KARMA_HIP(hipMemcpyAsync(&h, dev, 4, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_CHECK(h == 0, KARMA_ERR_ARG, "%s (code %d)", what, h);
+    return KARMA_OK;
+}
+
+// copy n elements from host or device into a new device array
+template <typename T>
+int upload(karma_ctx* ctx, const T* src, int64_t n, int is_device, DevArray<T>& dst) {
+    KARMA_TRY(dst.alloc(ctx, n ? n : 1));
+    if (n)
+        KARMA_HIP(hipMemcpyAsync(dst.ptr, src, n * sizeof(T), is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                 ctx->stream));
+    return KARMA_OK;
+}
+
+int ids_or_iota(karma_ctx* ctx, const uint32_t* ids, int64_t n, int is_device, DevArray<uint32_t>& dst) {
+    if (ids) return upload(ctx, ids, n, is_device, dst);
+    KARMA_TRY(dst.alloc(ctx, n ? n : 1));
+    KARMA_LAUNCH(ctx, "adj_iota", iota_u32_kernel, grid_of(n), 256, 0, dst.ptr, n);
+    return KARMA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int karma_adj_from_edges(karma_ctx* ctx, int64_t n, const uint32_t* ids, const uint32_t* a, const uint32_t* b,
+                         const double* w, int64_t n_edges, int is_device, karma_adj** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && n >= 0 && n < (int64_t(1) << 32) && n_edges >= 0 && n_edges < (int64_t(1) << 32) &&
+                    (n_edges == 0 || (a && b && w)),
+                KARMA_ERR_ARG, "karma_adj_from_edges: bad arguments");
+    auto g = std::make_unique<karma_adj>();
+    g->ctx = ctx;
+    g->n = n;
+    KARMA_TRY(ids_or_iota(ctx, ids, n, is_device, g->ids));
+    DevArray<uint32_t> da, db;
+    DevArray<double> dw;
+    KARMA_TRY(upload(ctx, a, n_edges, is_device, da));
+    KARMA_TRY(upload(ctx, b, n_edges, is_device, db));
+    KARMA_TRY(upload(ctx, w, n_edges, is_device, dw));
+    DevArray<int64_t> width, slot, cnt;
+    KARMA_TRY(width.alloc(ctx, n_edges + 1));
+    KARMA_TRY(slot.alloc(ctx, n_edges + 1));
+    KARMA_LAUNCH(ctx, "adj_edge_slots", edge_slots_kernel, grid_of(n_edges + 1), 256, 0, da.ptr, db.ptr, n_edges,
+                 width.ptr);
+    KARMA_TRY(scan_i64(ctx, width.ptr, slot.ptr, n_edges + 1));
+    KARMA_TRY(read_i64(ctx, slot.ptr + n_edges, &g->m));
+    const int64_t m = g->m;
+    DevArray<uint64_t> key, key2;
+    DevArray<uint32_t> val, val2;
+    DevArray<int> bad;
+    KARMA_TRY(key.alloc(ctx, m ? m : 1));
+    KARMA_TRY(key2.alloc(ctx, m ? m : 1));
+    KARMA_TRY(val.alloc(ctx, m ? m : 1));
+    KARMA_TRY(val2.alloc(ctx, m ? m : 1));
+    KARMA_TRY(bad.alloc(ctx, 1));
+    KARMA_HIP(hipMemsetAsync(bad.ptr, 0, 4, ctx->stream));
+    if (n_edges)
+        KARMA_LAUNCH(ctx, "adj_edge_entries", edge_entries_kernel, grid_of(n_edges), 256, 0, da.ptr, db.ptr, n_edges,
+                     slot.ptr, key.ptr, val.ptr, bad.ptr, (uint32_t)n);
+    KARMA_TRY(check_flag(ctx, bad.ptr, "edge endpoint >= n"));
+    if (m) {
+        size_t tb = 0;
+        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.ptr, key2.ptr, val.ptr, val2.ptr, (int)m, 0, 64,
+                                                     ctx->stream));
+        DevArray<uint8_t> tmp;
+        KARMA_TRY(tmp.alloc(ctx, tb ? tb : 1));
+        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, key.ptr, key2.ptr, val.ptr, val2.ptr, (int)m, 0, 64,
+                                                     ctx->stream));
+    }
+    KARMA_TRY(cnt.alloc(ctx, n + 1));
+    KARMA_HIP(hipMemsetAsync(cnt.ptr, 0, (n + 1) * 8, ctx->stream));
+    KARMA_TRY(g->nbr.alloc(ctx, m ? m : 1));
+    KARMA_TRY(g->w.alloc(ctx, m ? m : 1));
+    if (m)
+        KARMA_LAUNCH(ctx, "adj_fill", entries_fill_kernel, grid_of(m), 256, 0, key2.ptr, val2.ptr, m, da.ptr, db.ptr,
+                     dw.ptr, g->nbr.ptr, g->w.ptr, cnt.ptr);
+    KARMA_TRY(g->off.alloc(ctx, n + 1));
+    KARMA_TRY(scan_i64(ctx, cnt.ptr, g->off.ptr, n + 1));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    *out = g.release();
+    return KARMA_OK;
+}
+
+int karma_adj_from_lists(karma_ctx* ctx, int64_t n, const uint32_t* ids, const int64_t* off, const uint32_t* nbr,
+                         const double* w, int is_device, karma_adj** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && off && n >= 0 && n < (int64_t(1) << 32), KARMA_ERR_ARG, "karma_adj_from_lists: bad arguments");
+    auto g = std::make_unique<karma_adj>();
+    g->ctx = ctx;
+    g->n = n;
+    KARMA_TRY(upload(ctx, off, n + 1, is_device, g->off));
+    KARMA_TRY(read_i64(ctx, g->off.ptr + n, &g->m));
+    KARMA_CHECK(g->m >= 0, KARMA_ERR_ARG, "bad offsets");
+    KARMA_TRY(ids_or_iota(ctx, ids, n, is_device, g->ids));
+    KARMA_TRY(upload(ctx, nbr, g->m, is_device, g->nbr));
+    KARMA_TRY(upload(ctx, w, g->m, is_device, g->w));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    *out = g.release();
+    return KARMA_OK;
+}
+
+int karma_adj_view(karma_adj* src, const int64_t* order, int64_t k, karma_adj** out) {
+    KARMA_CHECK(src && out && k >= 0 && k <= src->n && (k == 0 || order), KARMA_ERR_ARG, "karma_adj_view: bad arguments");
+    karma_ctx* ctx = src->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    auto g = std::make_unique<karma_adj>();
+    g->ctx = ctx;
+    g->n = k;
+    DevArray<int64_t> dorder, cnt;
+    DevArray<int32_t> pos;
+    DevArray<int> bad;
+    KARMA_TRY(upload(ctx, order, k, 0, dorder));
+    KARMA_TRY(pos.alloc(ctx, src->n ? src->n : 1));
+    KARMA_HIP(hipMemsetAsync(pos.ptr, 0xFF, src->n * 4, ctx->stream));
+    KARMA_TRY(bad.alloc(ctx, 1));
+    KARMA_HIP(hipMemsetAsync(bad.ptr, 0, 4, ctx->stream));
+    if (k) KARMA_LAUNCH(ctx, "adj_posmap", posmap_kernel, grid_of(k), 256, 0, dorder.ptr, k, src->n, pos.ptr, bad.ptr);
+    KARMA_TRY(check_flag(ctx, bad.ptr, "view order: a position out of range or listed twice"));
+    KARMA_TRY(cnt.alloc(ctx, k + 1));
+    KARMA_LAUNCH(ctx, "adj_view_count", view_count_kernel, grid_of(k + 1), 256, 0, dorder.ptr, k, src->off.ptr,
+                 src->nbr.ptr, pos.ptr, cnt.ptr);
+    KARMA_TRY(g->off.alloc(ctx, k + 1));
+    KARMA_TRY(scan_i64(ctx, cnt.ptr, g->off.ptr, k + 1));
+    KARMA_TRY(read_i64(ctx, g->off.ptr + k, &g->m));
+    const int64_t m = g->m;
+    DevArray<uint64_t> key, key2;
+    DevArray<uint32_t> x, idx, idx2;
+    DevArray<double> wv;
+    KARMA_TRY(key.alloc(ctx, m ? m : 1));
+    KARMA_TRY(key2.alloc(ctx, m ? m : 1));
+    KARMA_TRY(x.alloc(ctx, m ? m : 1));
+    KARMA_TRY(idx.alloc(ctx, m ? m : 1));
+    KARMA_TRY(idx2.alloc(ctx, m ? m : 1));
+    KARMA_TRY(wv.alloc(ctx, m ? m : 1));
+    if (k)
+        KARMA_LAUNCH(ctx, "adj_view_fill", view_fill_kernel, grid_of(k), 256, 0, dorder.ptr, k, src->off.ptr,
+                     src->nbr.ptr, src->w.ptr, pos.ptr, g->off.ptr, key.ptr, x.ptr, wv.ptr);
+    KARMA_TRY(g->nbr.alloc(ctx, m ? m : 1));
+    KARMA_TRY(g->w.alloc(ctx, m ? m : 1));
+    if (m) {
+        KARMA_LAUNCH(ctx, "adj_iota", iota_u32_kernel, grid_of(m), 256, 0, idx.ptr, m);
+        size_t tb = 0;
+        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.ptr, key2.ptr, idx.ptr, idx2.ptr, (int)m, 0, 64,
+                                                     ctx->stream));
+        DevArray<uint8_t> tmp;
+        KARMA_TRY(tmp.alloc(ctx, tb ? tb : 1));
+        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, key.ptr, key2.ptr, idx.ptr, idx2.ptr, (int)m, 0, 64,
+                                                     ctx->stream));
+        KARMA_LAUNCH(ctx, "adj_gather", gather_entries_kernel, grid_of(m), 256, 0, idx2.ptr, m, x.ptr, wv.ptr,
+                     g->nbr.ptr, g->w.ptr);
+    }
+    KARMA_TRY(g->ids.alloc(ctx, k ? k : 1));
+    if (k) KARMA_LAUNCH(ctx, "adj_ids", gather_ids_kernel, grid_of(k), 256, 0, dorder.ptr, k, src->ids.ptr, g->ids.ptr);
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    *out = g.release();
+    return KARMA_OK;
+}
+
+int karma_adj_keep(karma_adj* src, const uint8_t* keep, karma_adj** out) {
+    KARMA_CHECK(src && out && (src->n == 0 || keep), KARMA_ERR_ARG, "karma_adj_keep: bad arguments");
+    karma_ctx* ctx = src->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    const int64_t n = src->n;
+    DevArray<uint8_t> dkeep;
+    DevArray<int64_t> flag, npos, cnt;
+    KARMA_TRY(upload(ctx, keep, n, 0, dkeep));
+    KARMA_TRY(flag.alloc(ctx, n + 1));
+    KARMA_TRY(npos.alloc(ctx, n + 1));
+    KARMA_LAUNCH(ctx, "adj_keep_flags", u8_to_i64_kernel, grid_of(n + 1), 256, 0, dkeep.ptr, n, flag.ptr);
+    KARMA_TRY(scan_i64(ctx, flag.ptr, npos.ptr, n + 1));
+    auto g = std::make_unique<karma_adj>();
+    g->ctx = ctx;
+    KARMA_TRY(read_i64(ctx, npos.ptr + n, &g->n));
+    const int64_t k = g->n;
+    KARMA_TRY(cnt.alloc(ctx, n + 1));
+    KARMA_LAUNCH(ctx, "adj_keep_count", keep_count_kernel, grid_of(n + 1), 256, 0, dkeep.ptr, n, src->off.ptr,
+                 src->nbr.ptr, cnt.ptr);
+    // counts of dropped nodes are 0, so the scan over old positions gives the
+    // new offsets at each kept node's old index; compact them
+    DevArray<int64_t> ooff;
+    KARMA_TRY(ooff.alloc(ctx, n + 1));
+    KARMA_TRY(scan_i64(ctx, cnt.ptr, ooff.ptr, n + 1));
+    KARMA_TRY(read_i64(ctx, ooff.ptr + n, &g->m));
+    const int64_t m = g->m;
+    KARMA_TRY(g->off.alloc(ctx, k + 1));
+    KARMA_TRY(g->nbr.alloc(ctx, m ? m : 1));
+    KARMA_TRY(g->w.alloc(ctx, m ? m : 1));
+    KARMA_TRY(g->ids.alloc(ctx, k ? k : 1));
+    // new offsets: off_new[npos[i]] = ooff[i] for kept i, off_new[k] = m
+    KARMA_LAUNCH(ctx, "adj_keep_off", keep_off_kernel, grid_of(n + 1), 256, 0, dkeep.ptr, n, npos.ptr, ooff.ptr,
+                 g->off.ptr);
+    if (n)
+        KARMA_LAUNCH(ctx, "adj_keep_fill", keep_fill_kernel, grid_of(n), 256, 0, dkeep.ptr, n, src->off.ptr,
+                     src->nbr.ptr, src->w.ptr, npos.ptr, ooff.ptr, src->ids.ptr, g->nbr.ptr, g->w.ptr, g->ids.ptr);
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    *out = g.release();
+    return KARMA_OK;
+}
+
+int karma_adj_info(karma_adj* g, int64_t* n, int64_t* n_entries) {
+    KARMA_CHECK(g, KARMA_ERR_ARG, "null graph");
+    if (n) *n = g->n;
+    if (n_entries) *n_entries = g->m;
+    return KARMA_OK;
+}
+
+int karma_adj_get(karma_adj* g, uint32_t* ids, int64_t* off, uint32_t* nbr, double* w) {
+    KARMA_CHECK(g, KARMA_ERR_ARG, "null graph");
+    karma_ctx* ctx = g->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    if (ids && g->n) KARMA_HIP(hipMemcpyAsync(ids, g->ids.ptr, g->n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (off) KARMA_HIP(hipMemcpyAsync(off, g->off.ptr, (g->n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (nbr && g->m) KARMA_HIP(hipMemcpyAsync(nbr, g->nbr.ptr, g->m * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (w && g->m) KARMA_HIP(hipMemcpyAsync(w, g->w.ptr, g->m * 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    return KARMA_OK;
+}
+
+int karma_adj_degrees(karma_adj* g, int64_t* deg) {
+    KARMA_CHECK(g && (g->n == 0 || deg), KARMA_ERR_ARG, "karma_adj_degrees: bad arguments");
+    karma_ctx* ctx = g->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    std::vector<int64_t> off(g->n + 1);
+    KARMA_HIP(hipMemcpyAsync(off.data(), g->off.ptr, (g->n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    for (int64_t i = 0; i < g->n; ++i) deg[i] = off[i + 1] - off[i];
+    return KARMA_OK;
+}
+
+int karma_adj_node_weights(karma_adj* g, double* out) {
+    KARMA_CHECK(g && (g->n == 0 || out), KARMA_ERR_ARG, "karma_adj_node_weights: bad arguments");
+    karma_ctx* ctx = g->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    if (!g->n) return KARMA_OK;
+    DevArray<double> dw;
+    KARMA_TRY(dw.alloc(ctx, g->n));
+    KARMA_LAUNCH(ctx, "adj_node_weights", node_weights_kernel, grid_of(g->n), 256, 0, g->off.ptr, g->w.ptr, g->n,
+                 dw.ptr);
+    KARMA_HIP(hipMemcpyAsync(out, dw.ptr, g->n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    return KARMA_OK;
+}
+
+int karma_adj_edge_list(karma_adj* g, const uint8_t* names, const int64_t* name_off, int64_t n_names,
+                        int names_on_device, uint8_t* out, int64_t cap, int64_t* len) {
+    KARMA_CHECK(g && names && name_off && len, KARMA_ERR_ARG, "karma_adj_edge_list: bad arguments");
+    karma_ctx* ctx = g->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    if (g->text_len < 0 || g->text_names != names) {
+        DevArray<uint8_t> hnames;
+        DevArray<int64_t> hoff;
+        const uint8_t* dnames = names;
+        const int64_t* doff = name_off;
+        if (!names_on_device) {
+            const int64_t nb = name_off[n_names];
+            KARMA_TRY(upload(ctx, names, nb, 0, hnames));
+            KARMA_TRY(upload(ctx, name_off, n_names + 1, 0, hoff));
+            dnames = hnames.ptr;
+            doff = hoff.ptr;
+        }
+        const int64_t n = g->n;
+        DevArray<int64_t> lens, start;
+        KARMA_TRY(lens.alloc(ctx, n + 1));
+        KARMA_TRY(start.alloc(ctx, n + 1));
+        KARMA_LAUNCH(ctx, "adj_edge_list_len", edge_list_len_kernel, grid_of(n + 1), 256, 0, g->off.ptr, g->nbr.ptr,
+                     g->w.ptr, g->ids.ptr, n, doff, lens.ptr);
+        KARMA_TRY(scan_i64(ctx, lens.ptr, start.ptr, n + 1));
+        int64_t total = 0;
+        KARMA_TRY(read_i64(ctx, start.ptr + n, &total));
+        KARMA_TRY(g->text.alloc(ctx, total ? total : 1));
+        if (n)
+            KARMA_LAUNCH(ctx, "adj_edge_list_write", edge_list_write_kernel, grid_of(n), 256, 0, g->off.ptr,
+                         g->nbr.ptr, g->w.ptr, g->ids.ptr, n, dnames, doff, start.ptr, g->text.ptr);
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        g->text_len = total ? total - 1 : 0;  // "\n".join: no newline after the last line
+        g->text_names = names;
+    }
+    *len = g->text_len;
+    if (out) {
+        KARMA_CHECK(cap >= g->text_len, KARMA_ERR_ARG, "edge list buffer too small (%lld < %lld)", (long long)cap,
+                    (long long)g->text_len);
+        if (g->text_len)
+            KARMA_HIP(hipMemcpyAsync(out, g->text.ptr, g->text_len, hipMemcpyDeviceToHost, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    return KARMA_OK;
+}
+
+int karma_adj_destroy(karma_adj* g) {
+    if (!g) return KARMA_OK;
+    if (g->ctx) (void)ctx_begin(g->ctx);
+    delete g;
+    return KARMA_OK;
+}
+
+int karma_repr_f64_host(const double* x, int64_t n, char* out, int64_t cap, int64_t* len) {
+    KARMA_CHECK(len && (n == 0 || x), KARMA_ERR_ARG, "karma_repr_f64_host: bad arguments");
+    int64_t p = 0;
+    char buf[karma_repr::kMaxRepr];
+    for (int64_t i = 0; i < n; ++i) {
+        const int r = karma_repr::repr_f64(x[i], buf);
+        if (out && p + r + 1 <= cap) {
+            std::memcpy(out + p, buf, r);
+            out[p + r] = '\n';
+        }
+        p += r + 1;
+    }
+    *len = p;
+    return KARMA_OK;
+}
+
+}  // extern "C"

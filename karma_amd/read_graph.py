@@ -6,17 +6,27 @@ Graph construction (the hot path) runs on the MI355X through libkarma_hip.so:
   from_equivalence_classes     -> eq-class pair emission + sort/reduce
 The resulting networkx graph has the reference's nodes, edges, weights (bit
 for bit) and insertion order (tests/test_gpu_parity.py compares
-G.edges(data=True) lists with the reference's own output).  The query helpers
-below are small pure-graph utilities kept for API completeness.
+G.edges(data=True) lists with the reference's own output).
+
+The consumers karma.py runs on cluster graphs -- get_unconnected_nodes /
+get_connected_nodes, the node weights behind calculate_representative_sequences
+and edge_list (MCL's input) -- run on the device too (consumers.py,
+csrc/consumers.hip): a graph keeps a device mirror of its networkx layout (node
+order, adjacency-dict order, weights).  The constructors and
+ReadGraph(G.subgraph(...)) copies of a mirrored graph get one without a Python
+walk; node removals are applied to it; any other mutation drops it and the next
+consumer call exports the graph's dicts (in-place edits of edge attribute dicts
+are not seen: change weights through add_edge).
 """
 
 import itertools
+import logging
 import os
 
 import networkx as nx
 import numpy as np
 
-from . import engine, ingest
+from . import consumers, engine, ingest
 from ._lib import KARMA_ERR_ZERO_DIV, KarmaError
 from .contig import contig_records, load_sam_records
 from .logs import logger
@@ -76,6 +86,31 @@ def _parse_eq_text(equivalence_class_file):
     return names, off, np.array(members, np.uint32), counts, skip
 
 
+def _invalidating(name):
+    base = getattr(nx.Graph, name)
+
+    def method(self, *args, **kw):
+        self._mirror = None
+        self._mirror_spec = None
+        return base(self, *args, **kw)
+
+    method.__name__ = name
+    method.__doc__ = base.__doc__
+    return method
+
+
+def _removing(name):
+    base = getattr(nx.Graph, name)
+
+    def method(self, *args, **kw):
+        self._mirror_dirty = True
+        return base(self, *args, **kw)
+
+    method.__name__ = name
+    method.__doc__ = base.__doc__
+    return method
+
+
 class ReadGraph(nx.Graph):
     """Read graph to find clusters (read_graph.py:10)."""
 
@@ -83,6 +118,51 @@ class ReadGraph(nx.Graph):
         super().__init__(incoming_graph_data, **attr)
         self.original_contigs = []
         self.mcl_cluster = []
+        self._mirror = None        # consumers.Mirror of this graph's layout
+        self._mirror_spec = None   # or how to build it on first use
+        self._mirror_dirty = False  # nodes removed since the mirror was taken
+        src = incoming_graph_data
+        # nx.Graph(G.subgraph(nodes)) / nx.Graph(G) of a mirrored ReadGraph: the
+        # copy's layout is derived from G's on the device
+        if isinstance(src, ReadGraph):
+            base = src
+            if hasattr(src, "_NODE_OK"):
+                base = getattr(src, "_graph", None)
+                if getattr(src, "_EDGE_OK", None) is not nx.filters.no_filter:
+                    base = None
+            if isinstance(base, ReadGraph) and (base._mirror is not None or base._mirror_spec is not None):
+                self._mirror_spec = ("view", base._device_mirror(), list(self))
+
+    for _name in ("add_node", "add_nodes_from", "add_edge", "add_edges_from", "add_weighted_edges_from",
+                  "remove_edge", "remove_edges_from", "update", "clear", "clear_edges"):
+        locals()[_name] = _invalidating(_name)
+    for _name in ("remove_node", "remove_nodes_from"):
+        locals()[_name] = _removing(_name)
+    del _name
+
+    def _device_mirror(self) -> consumers.Mirror:
+        """The device mirror of this graph's current layout (built, synced or exported)."""
+        m = self._mirror
+        if m is None:
+            spec = self._mirror_spec
+            if spec is None:
+                m = consumers.export(self)
+            elif spec[0] == "edges":
+                _, nodes, a, b, w = spec
+                adj = consumers.DeviceAdj.from_edges(len(nodes), a, b, w)
+                # cls(incoming_graph_data=graph) rebuilt the adjacency (from_dict_of_dicts)
+                rebuilt = adj.view(np.arange(len(nodes), dtype=np.int64))
+                m = consumers.Mirror(rebuilt, consumers.NameTable(nodes), nodes)
+            else:  # ("view", base mirror, node order)
+                m = spec[1].view(spec[2])
+            self._mirror, self._mirror_spec = m, None
+            self._mirror_dirty = False
+        if self._mirror_dirty:
+            cur = list(self)
+            synced = m.sync(cur)
+            m = synced if synced is not None else consumers.export(self)
+            self._mirror, self._mirror_dirty = m, False
+        return m
 
     # ------------------------------------------------------------ build ----
     @classmethod
@@ -102,7 +182,10 @@ class ReadGraph(nx.Graph):
             graph.add_nodes_from(names)
             for a, b, w in zip(e.a.tolist(), e.b.tolist(), e.weight.tolist()):
                 graph.add_edge(names[a], names[b], weight=w)
-        return cls(incoming_graph_data=graph)
+        out = cls(incoming_graph_data=graph)
+        if n >= 2 and len(out) == n:  # distinct names: positions = list indices
+            out._mirror_spec = ("edges", names, e.a, e.b, e.weight)
+        return out
 
     @classmethod
     def from_sam(cls, sam, skip_headers: bool = True, threads: int = 0) -> "ReadGraph":
@@ -117,7 +200,10 @@ class ReadGraph(nx.Graph):
             graph.add_nodes_from(names)
             for a, b, w in zip(e.a.tolist(), e.b.tolist(), e.weight.tolist()):
                 graph.add_edge(names[a], names[b], weight=w)
-        return cls(incoming_graph_data=graph)
+        out = cls(incoming_graph_data=graph)
+        if len(names) >= 2:
+            out._mirror_spec = ("edges", list(names), e.a, e.b, e.weight)
+        return out
 
     def set_original_contigs(self, original_contigs: list) -> None:
         self.original_contigs = original_contigs
@@ -133,12 +219,13 @@ class ReadGraph(nx.Graph):
             e = _edges_or_zero_div(engine.graph_from_eq, off, members, counts, skip, n)
         weighted_graph = nx.Graph()
         weighted_graph.add_nodes_from(names)
+        ea = eb = ew = np.zeros(0, np.uint32)
         if e is not None and len(e.a):
             # the reference's intermediate graph yields edge (u, v) from its
             # lower-index endpoint u, in first-insertion order (read_graph.py:120)
             order = np.lexsort((e.first, e.a))
-            a, b, w = e.a[order].tolist(), e.b[order].tolist(), e.weight[order].tolist()
-            for x, y, wt in zip(a, b, w):
+            ea, eb, ew = e.a[order], e.b[order], e.weight[order]
+            for x, y, wt in zip(ea.tolist(), eb.tolist(), ew.tolist()):
                 weighted_graph.add_edge(names[x], names[y], weight=wt)
         assert len(weighted_graph.nodes()) == n
         original_sequence_names = set([name.lstrip(">") for name in sequences_from_fasta.keys()])
@@ -146,7 +233,10 @@ class ReadGraph(nx.Graph):
             weighted_graph.add_node(missing_node)
         assert len(weighted_graph.nodes()) == len(sequences_from_fasta), (
             "The read graph has not enough nodes. Maybe Salmon could couldn't add all contigs to a equivalence class")
-        return cls(incoming_graph_data=weighted_graph)
+        out = cls(incoming_graph_data=weighted_graph)
+        # node order: the eq names (positions 0..n-1), then the FASTA-only nodes
+        out._mirror_spec = ("edges", list(out), ea, eb, np.asarray(ew, np.float64))
+        return out
 
     def update_graph(self, contigs: list) -> None:
         """read_graph.py:192-221: weights between every (original, new) pair,
@@ -180,22 +270,28 @@ class ReadGraph(nx.Graph):
 
     # ---------------------------------------------------------- queries ----
     def get_unconnected_nodes(self) -> list:
-        """Nodes without any neighbour (read_graph.py:150-160)."""
-        return [n for n in self.nodes() if len(self._adj[n]) == 0]
+        """Nodes without any neighbour, in node order (read_graph.py:150-160); degrees on the device."""
+        m = self._device_mirror()
+        deg = m.adj.degrees()
+        return [m.nodes[i] for i in np.flatnonzero(deg == 0).tolist()]
 
     def get_connected_nodes(self) -> list:
-        """Nodes with at least one neighbour (read_graph.py:162-172)."""
-        return [n for n in self.nodes() if len(self._adj[n]) != 0]
+        """Nodes with at least one neighbour (read_graph.py:162-172); degrees on the device."""
+        m = self._device_mirror()
+        deg = m.adj.degrees()
+        return [m.nodes[i] for i in np.flatnonzero(deg != 0).tolist()]
 
     def __calculate_node_weights(self) -> dict:
-        """Sum of incident edge weights in adjacency order (read_graph.py:174-190)."""
-        weights = {}
-        for node in self.nodes():
-            total = 0
-            for _, _, d in self.edges(node, data=True):
-                total += d["weight"]
-            weights[node] = total
-        logger.debug(f"Node weights: {weights}")
+        """Sum of incident edge weights in adjacency order (read_graph.py:174-190):
+        0 + w_1 + w_2 + ... in f64 on the device; a node without edges keeps the int 0."""
+        m = self._device_mirror()
+        w = m.adj.node_weights().tolist()
+        deg = m.adj.degrees()
+        for i in np.flatnonzero(deg == 0).tolist():
+            w[i] = 0
+        weights = dict(zip(m.nodes, w))
+        if logger.isEnabledFor(logging.DEBUG):
+            logger.debug(f"Node weights: {weights}")
         return weights
 
     def save_graph(self, filename: str) -> None:
@@ -252,8 +348,10 @@ class ReadGraph(nx.Graph):
         return list(self.nodes())
 
     def edge_list(self) -> str:
-        """MCL stdin text "A B w" per edge (read_graph.py:350-357)."""
-        return "\n".join(f"{a} {b} {d['weight']}" for a, b, d in self.edges(data=True)).encode("utf-8")
+        """MCL stdin text "A B w" per edge, UTF-8 (read_graph.py:350-357): names and
+        repr(weight) written on the device, edges in G.edges() order."""
+        m = self._device_mirror()
+        return m.adj.edge_list(m.names)
 
     def calc_distance_between_subgraphs(self, nodes_a: list, nodes_b: list) -> int:
         """Sum of weights between two node sets (read_graph.py:359-373)."""

@@ -11,7 +11,7 @@ OUT=$REPO/karma_amd/variants
 B=$OUT/build_$NAME
 mkdir -p $B
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result -Wno-unused-value"
-for f in core kmer graph graph_sets; do
+for f in core kmer graph graph_sets consumers; do
   /opt/rocm/bin/hipcc $FLAGS $EXTRA -c $SRC/$f.hip -o $B/$f.o &
 done
 wait
