@@ -234,11 +234,13 @@ int karma_adj_from_edges(karma_ctx* ctx, int64_t n, const uint32_t* ids, const u
 /* An exported adjacency: off[n+1] into nbr (positions) / w, in dict order. */
 int karma_adj_from_lists(karma_ctx* ctx, int64_t n, const uint32_t* ids, const int64_t* off, const uint32_t* nbr,
                          const double* w, int is_device, karma_adj** out);
-/* nx.Graph(G.subgraph(nodes)) of G = src: order[k] = src positions in the
- * view's node order (host).  Adjacency rebuilt as from_dict_of_dicts does. */
+/* nx.Graph(G.subgraph(nodes)) of G = src: order[k] = distinct src positions in
+ * the view's node order (host).  Adjacency rebuilt as from_dict_of_dicts does.
+ * Stream-ordered: no host synchronisation. */
 int karma_adj_view(karma_adj* src, const int64_t* order, int64_t k, karma_adj** out);
-/* G.remove_nodes_from: keep[n] (host, 1 = stays); remaining orders unchanged. */
-int karma_adj_keep(karma_adj* src, const uint8_t* keep, karma_adj** out);
+/* G.remove_nodes_from: keep[n] (host, 1 = stays), n_keep = ones in keep;
+ * remaining orders unchanged.  No host synchronisation. */
+int karma_adj_keep(karma_adj* src, const uint8_t* keep, int64_t n_keep, karma_adj** out);
 int karma_adj_info(karma_adj* g, int64_t* n, int64_t* n_entries);
 /* Host copies of the layout (any pointer may be NULL). */
 int karma_adj_get(karma_adj* g, uint32_t* ids, int64_t* off, uint32_t* nbr, double* w);
@@ -246,9 +248,11 @@ int karma_adj_get(karma_adj* g, uint32_t* ids, int64_t* off, uint32_t* nbr, doub
 int karma_adj_degrees(karma_adj* g, int64_t* deg_host);
 /* 0 + w_1 + w_2 + ... over G.adj[u] in order, f64 left to right (read_graph.py:183-187). */
 int karma_adj_node_weights(karma_adj* g, double* w_host);
+/* Both of the above in one pass (either pointer may be NULL). */
+int karma_adj_node_stats(karma_adj* g, int64_t* deg_host, double* w_host);
 /* "\n".join(f"{A} {B} {w}" for A, B, w in G.edges(data="weight")) as UTF-8:
  * names[name_off[i]:name_off[i+1]] is the UTF-8 name of id i; w is written as
- * Python repr(float).  out == NULL: only *len (the text is kept for the next call). */
+ * Python repr(float).  out == NULL: only *len (the text is kept for the copying call). */
 int karma_adj_edge_list(karma_adj* g, const uint8_t* names, const int64_t* name_off, int64_t n_names,
                         int names_on_device, uint8_t* out, int64_t cap, int64_t* len);
 int karma_adj_destroy(karma_adj* g);

@@ -67,11 +67,15 @@ class NameTable:
 class DeviceAdj:
     """A karma_adj: graph layout in networkx iteration order on the device."""
 
-    def __init__(self, ctx, h):
-        self.ctx, self.h = ctx, h
-        n, m = _lib._i64(0), _lib._i64(0)
-        call("karma_adj_info", h, ctypes.byref(n), ctypes.byref(m))
-        self.n, self.m = n.value, m.value
+    def __init__(self, ctx, h, n):
+        self.ctx, self.h, self.n = ctx, h, n
+
+    @property
+    def m(self):
+        """Adjacency entries (reads the device-side count)."""
+        m = _lib._i64(0)
+        call("karma_adj_info", self.h, None, ctypes.byref(m))
+        return m.value
 
     @classmethod
     def from_edges(cls, n, a, b, w, ids=None, ctx=None):
@@ -83,7 +87,7 @@ class DeviceAdj:
         ids = None if ids is None else np.ascontiguousarray(ids, np.uint32)
         h = ctypes.c_void_p()
         call("karma_adj_from_edges", ctx.h, n, ptr(ids), ptr(a), ptr(b), ptr(w), len(a), 0, ctypes.byref(h))
-        return cls(ctx, h)
+        return cls(ctx, h, n)
 
     @classmethod
     def from_lists(cls, off, nbr, w, ids=None, ctx=None):
@@ -94,27 +98,31 @@ class DeviceAdj:
         ids = None if ids is None else np.ascontiguousarray(ids, np.uint32)
         h = ctypes.c_void_p()
         call("karma_adj_from_lists", ctx.h, len(off) - 1, ptr(ids), ptr(off), ptr(nbr), ptr(w), 0, ctypes.byref(h))
-        return cls(ctx, h)
+        return cls(ctx, h, len(off) - 1)
 
     def view(self, order):
         """nx.Graph(G.subgraph(nodes)): order = positions in the view's node order."""
         order = np.ascontiguousarray(order, np.int64)
         h = ctypes.c_void_p()
+        if len(order) and (order.min() < 0 or order.max() >= self.n or len(np.unique(order)) != len(order)):
+            raise ValueError("view order: positions must be distinct and in range")
         call("karma_adj_view", self.h, ptr(order), len(order), ctypes.byref(h))
-        return DeviceAdj(self.ctx, h)
+        return DeviceAdj(self.ctx, h, len(order))
 
     def keep(self, mask):
         """G.remove_nodes_from(nodes at positions where mask == 0)."""
         mask = np.ascontiguousarray(mask, np.uint8)
+        k = int(np.count_nonzero(mask))
         h = ctypes.c_void_p()
-        call("karma_adj_keep", self.h, ptr(mask), ctypes.byref(h))
-        return DeviceAdj(self.ctx, h)
+        call("karma_adj_keep", self.h, ptr(mask), k, ctypes.byref(h))
+        return DeviceAdj(self.ctx, h, k)
 
     def layout(self):
+        m = self.m
         ids = np.zeros(self.n, np.uint32)
         off = np.zeros(self.n + 1, np.int64)
-        nbr = np.zeros(self.m, np.uint32)
-        w = np.zeros(self.m, np.float64)
+        nbr = np.zeros(m, np.uint32)
+        w = np.zeros(m, np.float64)
         call("karma_adj_get", self.h, ptr(ids), ptr(off), ptr(nbr), ptr(w))
         return ids, off, nbr, w
 
@@ -127,6 +135,13 @@ class DeviceAdj:
         out = np.zeros(self.n, np.float64)
         call("karma_adj_node_weights", self.h, ptr(out))
         return out
+
+    def node_stats(self):
+        """(degrees, node weights) in one device pass."""
+        d = np.zeros(self.n, np.int64)
+        w = np.zeros(self.n, np.float64)
+        call("karma_adj_node_stats", self.h, ptr(d), ptr(w))
+        return d, w
 
     def edge_list(self, names: NameTable) -> bytes:
         dn, do = names.device()

@@ -40,12 +40,14 @@ using namespace karma;
 
 struct karma_adj {
     karma_ctx* ctx = nullptr;
-    int64_t n = 0, m = 0;        // nodes, adjacency entries
+    int64_t n = 0;               // nodes
+    int64_t m = -1;              // adjacency entries (off[n]); -1 until read back
+    int64_t m_cap = 0;           // entry capacity of nbr / w (an upper bound of m)
     DevArray<uint32_t> ids;      // n: name id per position
     DevArray<int64_t> off;       // n + 1
     DevArray<uint32_t> nbr;      // m: neighbour positions
     DevArray<double> w;          // m
-    DevArray<uint8_t> text;      // cached edge_list bytes (+1 trailing newline)
+    DevArray<uint8_t> text;      // edge_list bytes between the length query and the copy
     int64_t text_len = -1;
     const void* text_names = nullptr;
 };
@@ -147,13 +149,21 @@ __global__ void view_fill_kernel(const int64_t* __restrict__ order, int64_t k, c
     }
 }
 
-__global__ void gather_entries_kernel(const uint32_t* __restrict__ idx, int64_t m, const uint32_t* __restrict__ x_in,
-                                      const double* __restrict__ w_in, uint32_t* __restrict__ x_out,
-                                      double* __restrict__ w_out) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    x_out[j] = x_in[idx[j]];
-    w_out[j] = w_in[idx[j]];
+// Within each node's segment the rank keys are distinct: an entry's place is
+// the number of smaller keys in its segment (one thread per entry, grid-stride
+// over the device-side entry count; O(d^2) per node of degree d).
+__global__ void rank_scatter_kernel(const uint64_t* __restrict__ key, const int64_t* __restrict__ off, int64_t k,
+                                    const uint32_t* __restrict__ x_in, const double* __restrict__ w_in,
+                                    uint32_t* __restrict__ x_out, double* __restrict__ w_out) {
+    const int64_t m = off[k];
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t kj = key[j];
+        const int64_t i = (int64_t)(kj >> 32);
+        int64_t r = 0;
+        for (int64_t t = off[i]; t < off[i + 1]; ++t) r += key[t] < kj;
+        x_out[off[i] + r] = x_in[j];
+        w_out[off[i] + r] = w_in[j];
+    }
 }
 
 __global__ void gather_ids_kernel(const int64_t* __restrict__ order, int64_t k, const uint32_t* __restrict__ ids_src,
@@ -205,13 +215,14 @@ __global__ void u8_to_i64_kernel(const uint8_t* __restrict__ in, int64_t n, int6
 }
 
 // ---- consumers ----------------------------------------------------------------
-__global__ void node_weights_kernel(const int64_t* __restrict__ off, const double* __restrict__ w, int64_t n,
-                                    double* __restrict__ out) {
+__global__ void node_stats_kernel(const int64_t* __restrict__ off, const double* __restrict__ w, int64_t n,
+                                  int64_t* __restrict__ deg, double* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     double s = 0.0;  // read_graph.py:183-187: 0 + w_1 + w_2 + ..., left to right
     for (int64_t j = off[i]; j < off[i + 1]; ++j) s = __dadd_rn(s, w[j]);
     out[i] = s;
+    deg[i] = off[i + 1] - off[i];
 }
 
 // bytes of node i's lines, each with its '\n'
@@ -324,6 +335,7 @@ int karma_adj_from_edges(karma_ctx* ctx, int64_t n, const uint32_t* ids, const u
     KARMA_TRY(scan_i64(ctx, width.ptr, slot.ptr, n_edges + 1));
     KARMA_TRY(read_i64(ctx, slot.ptr + n_edges, &g->m));
     const int64_t m = g->m;
+    g->m_cap = m;
     DevArray<uint64_t> key, key2;
     DevArray<uint32_t> val, val2;
     DevArray<int> bad;
@@ -370,6 +382,7 @@ int karma_adj_from_lists(karma_ctx* ctx, int64_t n, const uint32_t* ids, const i
     KARMA_TRY(upload(ctx, off, n + 1, is_device, g->off));
     KARMA_TRY(read_i64(ctx, g->off.ptr + n, &g->m));
     KARMA_CHECK(g->m >= 0, KARMA_ERR_ARG, "bad offsets");
+    g->m_cap = g->m;
     KARMA_TRY(ids_or_iota(ctx, ids, n, is_device, g->ids));
     KARMA_TRY(upload(ctx, nbr, g->m, is_device, g->nbr));
     KARMA_TRY(upload(ctx, w, g->m, is_device, g->w));
@@ -379,12 +392,15 @@ int karma_adj_from_lists(karma_ctx* ctx, int64_t n, const uint32_t* ids, const i
 }
 
 int karma_adj_view(karma_adj* src, const int64_t* order, int64_t k, karma_adj** out) {
+    // order: distinct positions of src (checked by the caller); no host sync
     KARMA_CHECK(src && out && k >= 0 && k <= src->n && (k == 0 || order), KARMA_ERR_ARG, "karma_adj_view: bad arguments");
     karma_ctx* ctx = src->ctx;
     KARMA_TRY(ctx_begin(ctx));
     auto g = std::make_unique<karma_adj>();
     g->ctx = ctx;
     g->n = k;
+    g->m_cap = src->m_cap;  // a view has at most its source's entries
+    const int64_t cap = std::max<int64_t>(1, g->m_cap);
     DevArray<int64_t> dorder, cnt;
     DevArray<int32_t> pos;
     DevArray<int> bad;
@@ -392,56 +408,41 @@ int karma_adj_view(karma_adj* src, const int64_t* order, int64_t k, karma_adj** 
     KARMA_TRY(pos.alloc(ctx, src->n ? src->n : 1));
     KARMA_HIP(hipMemsetAsync(pos.ptr, 0xFF, src->n * 4, ctx->stream));
     KARMA_TRY(bad.alloc(ctx, 1));
-    KARMA_HIP(hipMemsetAsync(bad.ptr, 0, 4, ctx->stream));
     if (k) KARMA_LAUNCH(ctx, "adj_posmap", posmap_kernel, grid_of(k), 256, 0, dorder.ptr, k, src->n, pos.ptr, bad.ptr);
-    KARMA_TRY(check_flag(ctx, bad.ptr, "view order: a position out of range or listed twice"));
     KARMA_TRY(cnt.alloc(ctx, k + 1));
     KARMA_LAUNCH(ctx, "adj_view_count", view_count_kernel, grid_of(k + 1), 256, 0, dorder.ptr, k, src->off.ptr,
                  src->nbr.ptr, pos.ptr, cnt.ptr);
     KARMA_TRY(g->off.alloc(ctx, k + 1));
     KARMA_TRY(scan_i64(ctx, cnt.ptr, g->off.ptr, k + 1));
-    KARMA_TRY(read_i64(ctx, g->off.ptr + k, &g->m));
-    const int64_t m = g->m;
-    DevArray<uint64_t> key, key2;
-    DevArray<uint32_t> x, idx, idx2;
+    DevArray<uint64_t> key;
+    DevArray<uint32_t> x;
     DevArray<double> wv;
-    KARMA_TRY(key.alloc(ctx, m ? m : 1));
-    KARMA_TRY(key2.alloc(ctx, m ? m : 1));
-    KARMA_TRY(x.alloc(ctx, m ? m : 1));
-    KARMA_TRY(idx.alloc(ctx, m ? m : 1));
-    KARMA_TRY(idx2.alloc(ctx, m ? m : 1));
-    KARMA_TRY(wv.alloc(ctx, m ? m : 1));
-    if (k)
+    KARMA_TRY(key.alloc(ctx, cap));
+    KARMA_TRY(x.alloc(ctx, cap));
+    KARMA_TRY(wv.alloc(ctx, cap));
+    KARMA_TRY(g->nbr.alloc(ctx, cap));
+    KARMA_TRY(g->w.alloc(ctx, cap));
+    if (k) {
         KARMA_LAUNCH(ctx, "adj_view_fill", view_fill_kernel, grid_of(k), 256, 0, dorder.ptr, k, src->off.ptr,
                      src->nbr.ptr, src->w.ptr, pos.ptr, g->off.ptr, key.ptr, x.ptr, wv.ptr);
-    KARMA_TRY(g->nbr.alloc(ctx, m ? m : 1));
-    KARMA_TRY(g->w.alloc(ctx, m ? m : 1));
-    if (m) {
-        KARMA_LAUNCH(ctx, "adj_iota", iota_u32_kernel, grid_of(m), 256, 0, idx.ptr, m);
-        size_t tb = 0;
-        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.ptr, key2.ptr, idx.ptr, idx2.ptr, (int)m, 0, 64,
-                                                     ctx->stream));
-        DevArray<uint8_t> tmp;
-        KARMA_TRY(tmp.alloc(ctx, tb ? tb : 1));
-        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, key.ptr, key2.ptr, idx.ptr, idx2.ptr, (int)m, 0, 64,
-                                                     ctx->stream));
-        KARMA_LAUNCH(ctx, "adj_gather", gather_entries_kernel, grid_of(m), 256, 0, idx2.ptr, m, x.ptr, wv.ptr,
-                     g->nbr.ptr, g->w.ptr);
+        KARMA_LAUNCH(ctx, "adj_view_sort", rank_scatter_kernel, (int)std::min<int64_t>(grid_of(cap), 2048), 256, 0,
+                     key.ptr, g->off.ptr, k, x.ptr, wv.ptr, g->nbr.ptr, g->w.ptr);
     }
     KARMA_TRY(g->ids.alloc(ctx, k ? k : 1));
     if (k) KARMA_LAUNCH(ctx, "adj_ids", gather_ids_kernel, grid_of(k), 256, 0, dorder.ptr, k, src->ids.ptr, g->ids.ptr);
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
     *out = g.release();
     return KARMA_OK;
 }
 
-int karma_adj_keep(karma_adj* src, const uint8_t* keep, karma_adj** out) {
-    KARMA_CHECK(src && out && (src->n == 0 || keep), KARMA_ERR_ARG, "karma_adj_keep: bad arguments");
+int karma_adj_keep(karma_adj* src, const uint8_t* keep, int64_t n_keep, karma_adj** out) {
+    // n_keep = number of ones in keep (checked by the caller); no host sync
+    KARMA_CHECK(src && out && (src->n == 0 || keep) && n_keep >= 0 && n_keep <= src->n, KARMA_ERR_ARG,
+                "karma_adj_keep: bad arguments");
     karma_ctx* ctx = src->ctx;
     KARMA_TRY(ctx_begin(ctx));
     const int64_t n = src->n;
     DevArray<uint8_t> dkeep;
-    DevArray<int64_t> flag, npos, cnt;
+    DevArray<int64_t> flag, npos, cnt, ooff;
     KARMA_TRY(upload(ctx, keep, n, 0, dkeep));
     KARMA_TRY(flag.alloc(ctx, n + 1));
     KARMA_TRY(npos.alloc(ctx, n + 1));
@@ -449,44 +450,63 @@ int karma_adj_keep(karma_adj* src, const uint8_t* keep, karma_adj** out) {
     KARMA_TRY(scan_i64(ctx, flag.ptr, npos.ptr, n + 1));
     auto g = std::make_unique<karma_adj>();
     g->ctx = ctx;
-    KARMA_TRY(read_i64(ctx, npos.ptr + n, &g->n));
-    const int64_t k = g->n;
+    g->n = n_keep;
+    g->m_cap = src->m_cap;
+    const int64_t cap = std::max<int64_t>(1, g->m_cap);
     KARMA_TRY(cnt.alloc(ctx, n + 1));
     KARMA_LAUNCH(ctx, "adj_keep_count", keep_count_kernel, grid_of(n + 1), 256, 0, dkeep.ptr, n, src->off.ptr,
                  src->nbr.ptr, cnt.ptr);
-    // counts of dropped nodes are 0, so the scan over old positions gives the
-    // new offsets at each kept node's old index; compact them
-    DevArray<int64_t> ooff;
+    // counts of dropped nodes are 0, so the scan over old positions is each
+    // kept node's new start
     KARMA_TRY(ooff.alloc(ctx, n + 1));
     KARMA_TRY(scan_i64(ctx, cnt.ptr, ooff.ptr, n + 1));
-    KARMA_TRY(read_i64(ctx, ooff.ptr + n, &g->m));
-    const int64_t m = g->m;
-    KARMA_TRY(g->off.alloc(ctx, k + 1));
-    KARMA_TRY(g->nbr.alloc(ctx, m ? m : 1));
-    KARMA_TRY(g->w.alloc(ctx, m ? m : 1));
-    KARMA_TRY(g->ids.alloc(ctx, k ? k : 1));
-    // new offsets: off_new[npos[i]] = ooff[i] for kept i, off_new[k] = m
+    KARMA_TRY(g->off.alloc(ctx, n_keep + 1));
+    KARMA_TRY(g->nbr.alloc(ctx, cap));
+    KARMA_TRY(g->w.alloc(ctx, cap));
+    KARMA_TRY(g->ids.alloc(ctx, n_keep ? n_keep : 1));
     KARMA_LAUNCH(ctx, "adj_keep_off", keep_off_kernel, grid_of(n + 1), 256, 0, dkeep.ptr, n, npos.ptr, ooff.ptr,
                  g->off.ptr);
     if (n)
         KARMA_LAUNCH(ctx, "adj_keep_fill", keep_fill_kernel, grid_of(n), 256, 0, dkeep.ptr, n, src->off.ptr,
                      src->nbr.ptr, src->w.ptr, npos.ptr, ooff.ptr, src->ids.ptr, g->nbr.ptr, g->w.ptr, g->ids.ptr);
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
     *out = g.release();
+    return KARMA_OK;
+}
+
+int karma_adj_node_stats(karma_adj* g, int64_t* deg, double* w) {
+    KARMA_CHECK(g, KARMA_ERR_ARG, "null graph");
+    karma_ctx* ctx = g->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    if (!g->n) return KARMA_OK;
+    DevArray<int64_t> dd;
+    DevArray<double> dw;
+    KARMA_TRY(dd.alloc(ctx, g->n));
+    KARMA_TRY(dw.alloc(ctx, g->n));
+    KARMA_LAUNCH(ctx, "adj_node_stats", node_stats_kernel, grid_of(g->n), 256, 0, g->off.ptr, g->w.ptr, g->n,
+                 dd.ptr, dw.ptr);
+    if (deg) KARMA_HIP(hipMemcpyAsync(deg, dd.ptr, g->n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (w) KARMA_HIP(hipMemcpyAsync(w, dw.ptr, g->n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
     return KARMA_OK;
 }
 
 int karma_adj_info(karma_adj* g, int64_t* n, int64_t* n_entries) {
     KARMA_CHECK(g, KARMA_ERR_ARG, "null graph");
     if (n) *n = g->n;
-    if (n_entries) *n_entries = g->m;
+    if (n_entries) {
+        if (g->m < 0) {
+            KARMA_TRY(ctx_begin(g->ctx));
+            KARMA_TRY(read_i64(g->ctx, g->off.ptr + g->n, &g->m));
+        }
+        *n_entries = g->m;
+    }
     return KARMA_OK;
 }
 
 int karma_adj_get(karma_adj* g, uint32_t* ids, int64_t* off, uint32_t* nbr, double* w) {
     KARMA_CHECK(g, KARMA_ERR_ARG, "null graph");
     karma_ctx* ctx = g->ctx;
-    KARMA_TRY(ctx_begin(ctx));
+    KARMA_TRY(karma_adj_info(g, nullptr, &g->m));
     if (ids && g->n) KARMA_HIP(hipMemcpyAsync(ids, g->ids.ptr, g->n * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (off) KARMA_HIP(hipMemcpyAsync(off, g->off.ptr, (g->n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
     if (nbr && g->m) KARMA_HIP(hipMemcpyAsync(nbr, g->nbr.ptr, g->m * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -497,27 +517,12 @@ int karma_adj_get(karma_adj* g, uint32_t* ids, int64_t* off, uint32_t* nbr, doub
 
 int karma_adj_degrees(karma_adj* g, int64_t* deg) {
     KARMA_CHECK(g && (g->n == 0 || deg), KARMA_ERR_ARG, "karma_adj_degrees: bad arguments");
-    karma_ctx* ctx = g->ctx;
-    KARMA_TRY(ctx_begin(ctx));
-    std::vector<int64_t> off(g->n + 1);
-    KARMA_HIP(hipMemcpyAsync(off.data(), g->off.ptr, (g->n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    for (int64_t i = 0; i < g->n; ++i) deg[i] = off[i + 1] - off[i];
-    return KARMA_OK;
+    return karma_adj_node_stats(g, deg, nullptr);
 }
 
 int karma_adj_node_weights(karma_adj* g, double* out) {
     KARMA_CHECK(g && (g->n == 0 || out), KARMA_ERR_ARG, "karma_adj_node_weights: bad arguments");
-    karma_ctx* ctx = g->ctx;
-    KARMA_TRY(ctx_begin(ctx));
-    if (!g->n) return KARMA_OK;
-    DevArray<double> dw;
-    KARMA_TRY(dw.alloc(ctx, g->n));
-    KARMA_LAUNCH(ctx, "adj_node_weights", node_weights_kernel, grid_of(g->n), 256, 0, g->off.ptr, g->w.ptr, g->n,
-                 dw.ptr);
-    KARMA_HIP(hipMemcpyAsync(out, dw.ptr, g->n * 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    return KARMA_OK;
+    return karma_adj_node_stats(g, nullptr, out);
 }
 
 int karma_adj_edge_list(karma_adj* g, const uint8_t* names, const int64_t* name_off, int64_t n_names,
@@ -561,6 +566,9 @@ int karma_adj_edge_list(karma_adj* g, const uint8_t* names, const int64_t* name_
         if (g->text_len)
             KARMA_HIP(hipMemcpyAsync(out, g->text.ptr, g->text_len, hipMemcpyDeviceToHost, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        g->text.release();  // kept only between the length query and the copy
+        g->text_len = -1;
+        g->text_names = nullptr;
     }
     return KARMA_OK;
 }

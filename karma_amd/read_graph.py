@@ -285,8 +285,8 @@ class ReadGraph(nx.Graph):
         """Sum of incident edge weights in adjacency order (read_graph.py:174-190):
         0 + w_1 + w_2 + ... in f64 on the device; a node without edges keeps the int 0."""
         m = self._device_mirror()
-        w = m.adj.node_weights().tolist()
-        deg = m.adj.degrees()
+        deg, w = m.adj.node_stats()
+        w = w.tolist()
         for i in np.flatnonzero(deg == 0).tolist():
             w[i] = 0
         weights = dict(zip(m.nodes, w))
