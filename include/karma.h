@@ -23,6 +23,7 @@
  *   karma_sam_*                     Contig readsets from SAM lines       karma/contig.py:24,34, hisat2.py:76-81
  *   karma_adj_*                     graph consumers: unconnected nodes, node weights, edge_list
  *                                   karma/read_graph.py:150-190, :315-357
+ *   karma_adj_cross_sums            --rearrange subcluster connections  karma/karma.py:103-118
  *
  * The reference is pure Python and has no FFI; INTEGRATION.md shows the ctypes
  * binding (karma_amd/_lib.py) that the Python classes mirroring the reference
@@ -255,6 +256,15 @@ int karma_adj_node_stats(karma_adj* g, int64_t* deg_host, double* w_host);
  * Python repr(float).  out == NULL: only *len (the text is kept for the copying call). */
 int karma_adj_edge_list(karma_adj* g, const uint8_t* names, const int64_t* name_off, int64_t n_names,
                         int names_on_device, uint8_t* out, int64_t cap, int64_t* len);
+/* --rearrange (karma.py:103-118): sub[u] = subcluster
+ * index of position u (-1: none; each node in at most one), rank[u] = its index
+ * in that subcluster's node list.  For every pair A < B joined by an edge:
+ * pair = A << 32 | B, sum = 0 + w_1 + w_2 + ... over the edges between them in
+ * itertools.product(nodes_A, nodes_B) order, n_edges = their count, n_over = how
+ * many of the partial sums exceed cutoff (the reference appends [A, B] once per
+ * such edge); sorted by (A, B).  All outputs NULL: only *n_pairs. */
+int karma_adj_cross_sums(karma_adj* g, const int32_t* sub, const int32_t* rank, double cutoff, uint64_t* pair,
+                         double* sum, int64_t* n_edges, int64_t* n_over, int64_t cap, int64_t* n_pairs);
 int karma_adj_destroy(karma_adj* g);
 /* Host build of the device's repr(float) formatter, for tests: one line per value. */
 int karma_repr_f64_host(const double* x, int64_t n, char* out, int64_t cap, int64_t* len);

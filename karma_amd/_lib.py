@@ -112,6 +112,7 @@ _SIGS = {
     "karma_adj_degrees": [_c_p, _c_p],
     "karma_adj_node_weights": [_c_p, _c_p],
     "karma_adj_edge_list": [_c_p, _c_p, _c_p, _i64, _i32, _c_p, _i64, _I64P],
+    "karma_adj_cross_sums": [_c_p, _c_p, _c_p, ctypes.c_double, _c_p, _c_p, _c_p, _c_p, _i64, _I64P],
     "karma_adj_destroy": [_c_p],
     "karma_repr_f64_host": [_c_p, _i64, _c_p, _i64, _I64P],
 }

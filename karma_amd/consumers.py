@@ -143,6 +143,24 @@ class DeviceAdj:
         call("karma_adj_node_stats", self.h, ptr(d), ptr(w))
         return d, w
 
+    def cross_sums(self, sub, rank, cutoff):
+        """karma_adj_cross_sums: (A, B, sum, n_edges, n_over) arrays of the
+        subcluster pairs joined by edges, sorted by (A, B)."""
+        sub = np.ascontiguousarray(sub, np.int32)
+        rank = np.ascontiguousarray(rank, np.int32)
+        P = _lib._i64(0)
+        call("karma_adj_cross_sums", self.h, ptr(sub), ptr(rank), float(cutoff), None, None, None, None, 0,
+             ctypes.byref(P))
+        p = P.value
+        pair = np.zeros(p, np.uint64)
+        s = np.zeros(p, np.float64)
+        ne = np.zeros(p, np.int64)
+        no = np.zeros(p, np.int64)
+        if p:
+            call("karma_adj_cross_sums", self.h, ptr(sub), ptr(rank), float(cutoff), ptr(pair), ptr(s), ptr(ne),
+                 ptr(no), p, ctypes.byref(P))
+        return (pair >> np.uint64(32)).astype(np.int64), (pair & np.uint64(0xFFFFFFFF)).astype(np.int64), s, ne, no
+
     def edge_list(self, names: NameTable) -> bytes:
         dn, do = names.device()
         n = _lib._i64(0)

@@ -26,6 +26,9 @@
 //                         neighbours before u by position, then the L(u) entries
 //                         at or after u in L order;
 //   karma_adj_keep        G.remove_nodes_from (orders kept).
+// and the --rearrange aggregation (karma.py:103-118):
+//   karma_adj_cross_sums  per subcluster pair (A, B), A < B, the edge weights
+//                         between them summed in product(nodes_A, nodes_B) order.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -266,6 +269,75 @@ __global__ void edge_list_write_kernel(const int64_t* __restrict__ off, const ui
         for (int t = 0; t < r; ++t) *p++ = (uint8_t)buf[t];
         *p++ = '\n';
     }
+}
+
+// ---- --rearrange: cross-subcluster weight sums (karma.py:103-118) ------------
+// Entries u -> v with sub[u] < sub[v] (each undirected edge once, from the side
+// in the earlier subcluster).  Keys: (A, B) and, inside a pair, (rank of u in
+// A's list, rank of v in B's list) = itertools.product(nodes_A, nodes_B) order.
+__global__ void cross_count_kernel(const int64_t* __restrict__ off, const uint32_t* __restrict__ nbr, int64_t n,
+                                   const int32_t* __restrict__ sub, int64_t* __restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    int64_t c = 0;
+    if (i < n && sub[i] >= 0)
+        for (int64_t j = off[i]; j < off[i + 1]; ++j) {
+            const int32_t sv = sub[nbr[j]];
+            c += sv > sub[i];
+        }
+    cnt[i] = c;
+}
+
+__global__ void cross_fill_kernel(const int64_t* __restrict__ off, const uint32_t* __restrict__ nbr,
+                                  const double* __restrict__ w, int64_t n, const int32_t* __restrict__ sub,
+                                  const int32_t* __restrict__ rank, const int64_t* __restrict__ start,
+                                  uint64_t* __restrict__ pair_key, uint64_t* __restrict__ in_key,
+                                  double* __restrict__ ew) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || sub[i] < 0) return;
+    int64_t d = start[i];
+    for (int64_t j = off[i]; j < off[i + 1]; ++j) {
+        const uint32_t v = nbr[j];
+        if (sub[v] <= sub[i]) continue;
+        pair_key[d] = (uint64_t)(uint32_t)sub[i] << 32 | (uint32_t)sub[v];
+        in_key[d] = (uint64_t)(uint32_t)rank[i] << 32 | (uint32_t)rank[v];
+        ew[d] = w[j];
+        ++d;
+    }
+}
+
+__global__ void gather_u64_kernel(const uint32_t* __restrict__ idx, int64_t m, const uint64_t* __restrict__ in,
+                                  uint64_t* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) out[j] = in[idx[j]];
+}
+
+__global__ void segment_heads_kernel(const uint64_t* __restrict__ key, int64_t m, int64_t* __restrict__ head) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j <= m) head[j] = j < m ? (j == 0 || key[j] != key[j - 1]) : 0;
+}
+
+// one thread per (A, B): 0 + w_1 + w_2 + ... in product order (karma.py:111-117)
+// (and how many of those partial sums exceed the cutoff: the reference appends
+// [A, B] once for each)
+__global__ void cross_sum_kernel(const uint64_t* __restrict__ key, const uint32_t* __restrict__ idx,
+                                 const double* __restrict__ ew, int64_t m, const int64_t* __restrict__ head,
+                                 const int64_t* __restrict__ seg, double cutoff, uint64_t* __restrict__ out_key,
+                                 double* __restrict__ out_sum, int64_t* __restrict__ out_n,
+                                 int64_t* __restrict__ out_over) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m || !head[j]) return;
+    double s = 0.0;
+    int64_t t = j, over = 0;
+    for (; t < m && key[t] == key[j]; ++t) {
+        s = __dadd_rn(s, ew[idx[t]]);
+        over += s > cutoff;
+    }
+    const int64_t o = seg[j];
+    out_key[o] = key[j];
+    out_sum[o] = s;
+    out_n[o] = t - j;
+    out_over[o] = over;
 }
 
 int scan_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
@@ -570,6 +642,82 @@ int karma_adj_edge_list(karma_adj* g, const uint8_t* names, const int64_t* name_
         g->text_len = -1;
         g->text_names = nullptr;
     }
+    return KARMA_OK;
+}
+
+int karma_adj_cross_sums(karma_adj* g, const int32_t* sub, const int32_t* rank, double cutoff, uint64_t* pair,
+                         double* sum, int64_t* n_edges, int64_t* n_over, int64_t cap, int64_t* n_pairs) {
+    KARMA_CHECK(g && sub && rank && n_pairs, KARMA_ERR_ARG, "karma_adj_cross_sums: bad arguments");
+    karma_ctx* ctx = g->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    const int64_t n = g->n;
+    DevArray<int32_t> dsub, drank;
+    DevArray<int64_t> cnt, start;
+    KARMA_TRY(upload(ctx, sub, n, 0, dsub));
+    KARMA_TRY(upload(ctx, rank, n, 0, drank));
+    KARMA_TRY(cnt.alloc(ctx, n + 1));
+    KARMA_TRY(start.alloc(ctx, n + 1));
+    KARMA_LAUNCH(ctx, "adj_cross_count", cross_count_kernel, grid_of(n + 1), 256, 0, g->off.ptr, g->nbr.ptr, n,
+                 dsub.ptr, cnt.ptr);
+    KARMA_TRY(scan_i64(ctx, cnt.ptr, start.ptr, n + 1));
+    int64_t m = 0;
+    KARMA_TRY(read_i64(ctx, start.ptr + n, &m));
+    if (m == 0) {
+        *n_pairs = 0;
+        return KARMA_OK;
+    }
+    KARMA_CHECK(m < (int64_t(1) << 31), KARMA_ERR_ARG, "too many cross-subcluster edges");
+    DevArray<uint64_t> pk, ik, k1, k2;
+    DevArray<double> ew;
+    DevArray<uint32_t> idx, idx2, idx3;
+    KARMA_TRY(pk.alloc(ctx, m));
+    KARMA_TRY(ik.alloc(ctx, m));
+    KARMA_TRY(k1.alloc(ctx, m));
+    KARMA_TRY(k2.alloc(ctx, m));
+    KARMA_TRY(ew.alloc(ctx, m));
+    KARMA_TRY(idx.alloc(ctx, m));
+    KARMA_TRY(idx2.alloc(ctx, m));
+    KARMA_TRY(idx3.alloc(ctx, m));
+    KARMA_LAUNCH(ctx, "adj_cross_fill", cross_fill_kernel, grid_of(n), 256, 0, g->off.ptr, g->nbr.ptr, g->w.ptr, n,
+                 dsub.ptr, drank.ptr, start.ptr, pk.ptr, ik.ptr, ew.ptr);
+    KARMA_LAUNCH(ctx, "adj_iota", iota_u32_kernel, grid_of(m), 256, 0, idx.ptr, m);
+    // LSD: by the in-pair key, then stably by (A, B)
+    size_t tb = 0, tb2 = 0;
+    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ik.ptr, k1.ptr, idx.ptr, idx2.ptr, (int)m, 0, 64,
+                                                 ctx->stream));
+    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, k2.ptr, k1.ptr, idx2.ptr, idx3.ptr, (int)m, 0, 64,
+                                                 ctx->stream));
+    DevArray<uint8_t> tmp;
+    KARMA_TRY(tmp.alloc(ctx, std::max<size_t>(1, std::max(tb, tb2))));
+    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, ik.ptr, k1.ptr, idx.ptr, idx2.ptr, (int)m, 0, 64,
+                                                 ctx->stream));
+    KARMA_LAUNCH(ctx, "adj_cross_gather", gather_u64_kernel, grid_of(m), 256, 0, idx2.ptr, m, pk.ptr, k2.ptr);
+    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb2, k2.ptr, k1.ptr, idx2.ptr, idx3.ptr, (int)m, 0, 64,
+                                                 ctx->stream));
+    DevArray<int64_t> head, seg;
+    KARMA_TRY(head.alloc(ctx, m + 1));
+    KARMA_TRY(seg.alloc(ctx, m + 1));
+    KARMA_LAUNCH(ctx, "adj_cross_heads", segment_heads_kernel, grid_of(m + 1), 256, 0, k1.ptr, m, head.ptr);
+    KARMA_TRY(scan_i64(ctx, head.ptr, seg.ptr, m + 1));
+    int64_t P = 0;
+    KARMA_TRY(read_i64(ctx, seg.ptr + m, &P));
+    *n_pairs = P;
+    if (!pair && !sum && !n_edges && !n_over) return KARMA_OK;
+    KARMA_CHECK(cap >= P, KARMA_ERR_ARG, "cross-sum buffers too small (%lld < %lld)", (long long)cap, (long long)P);
+    DevArray<uint64_t> okey;
+    DevArray<double> osum;
+    DevArray<int64_t> on, oo;
+    KARMA_TRY(okey.alloc(ctx, P));
+    KARMA_TRY(osum.alloc(ctx, P));
+    KARMA_TRY(on.alloc(ctx, P));
+    KARMA_TRY(oo.alloc(ctx, P));
+    KARMA_LAUNCH(ctx, "adj_cross_sum", cross_sum_kernel, grid_of(m), 256, 0, k1.ptr, idx3.ptr, ew.ptr, m, head.ptr,
+                 seg.ptr, cutoff, okey.ptr, osum.ptr, on.ptr, oo.ptr);
+    if (pair) KARMA_HIP(hipMemcpyAsync(pair, okey.ptr, P * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (sum) KARMA_HIP(hipMemcpyAsync(sum, osum.ptr, P * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (n_edges) KARMA_HIP(hipMemcpyAsync(n_edges, on.ptr, P * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (n_over) KARMA_HIP(hipMemcpyAsync(n_over, oo.ptr, P * 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
     return KARMA_OK;
 }
 

@@ -1,0 +1,116 @@
+"""GPU parity of --rearrange (karma/karma.py:409-437).
+
+* tests/golden/rearrange.json: the reference's own helpers (taken from
+  karma.py's syntax tree, tests/golden/make_golden_rearrange.py) on graphs the
+  reference built, at four weight cutoffs -- the connection list (with its
+  duplicates) and the rearranged nesting must match exactly;
+* in process: the reference's O(N^2) has_edge walk (karma.py:103-118, restated
+  below) on larger seeded graphs, including nodes outside the graph, FASTA-only
+  nodes and a graph built by hand (export path).
+"""
+import itertools
+import json
+import os
+import random
+from collections import OrderedDict
+
+import pytest
+
+from karma_amd import rearrange, synth
+from karma_amd.read_graph import ReadGraph
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def ref_calc_connections(mcl_subclusters, full_graph, weight_cutoff=0):
+    """karma.py:103-118 with full_graph passed in (the reference reads a global)."""
+    mcl_groups_to_combine = []
+    for index_A, index_B in itertools.combinations(mcl_subclusters, 2):
+        nodes_A = mcl_subclusters[index_A]["mcl_subcluster"]
+        nodes_B = mcl_subclusters[index_B]["mcl_subcluster"]
+        weight = 0
+        for A, B in itertools.product(nodes_A, nodes_B):
+            if full_graph.has_edge(A, B):
+                weight += full_graph[A][B]["weight"]
+                if weight > weight_cutoff:
+                    mcl_groups_to_combine.append([index_A, index_B])
+    return mcl_groups_to_combine
+
+
+def eq_graph(tmp_path, seed, n, nf, paired, extra=()):
+    classes = synth.eq_classes(seed, n, nf, paired)
+    names = [f"ctg{i}" for i in range(n)]
+    p = tmp_path / f"eq{seed}.txt"
+    p.write_text(synth.eq_file_text(names, classes))
+    return ReadGraph.from_equivalence_classes(str(p), OrderedDict((">" + x, "") for x in names + list(extra))), names
+
+
+def test_rearrange_golden(tmp_path):
+    with open(os.path.join(HERE, "golden", "rearrange.json")) as f:
+        gold = json.load(f)
+    for name, case in gold["cases"].items():
+        g, names = eq_graph(tmp_path, case["seed"], case["n"], case["n_frags"], case["paired"])
+        for run in case["runs"]:
+            subs = rearrange.create_lookup_dict(case["nesting"], names)
+            groups = rearrange.calc_connections_between_mcl_subclusters(subs, weight_cutoff=run["cutoff"],
+                                                                        full_graph=g)
+            assert groups == run["groups"], (name, run["cutoff"])
+            new = rearrange.rearrange(case["nesting"], names, g, weight_cutoff=run["cutoff"])
+            assert new == run["new_cluster_subcluster"], (name, run["cutoff"])
+
+
+def nesting(nodes, rng, max_cluster=10):
+    out, i = [], 0
+    while i < len(nodes):
+        k = rng.randint(1, max_cluster)
+        cl = nodes[i:i + k]
+        i += k
+        cuts = sorted(rng.sample(range(1, len(cl)), min(len(cl) - 1, rng.randint(0, 3)))) if len(cl) > 1 else []
+        parts, s = [], 0
+        for c in cuts + [len(cl)]:
+            parts.append(cl[s:c])
+            s = c
+        out.append(parts)
+    return out
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_rearrange_vs_reference_walk(tmp_path, seed):
+    g, names = eq_graph(tmp_path, seed, 1500, 60_000, True, extra=("iso_x",))
+    rng = random.Random(seed)
+    nodes = names + ["iso_x", "not_in_graph"]
+    rng.shuffle(nodes)  # subclusters that mix genes: many cross pairs
+    nest = nesting(nodes, rng)
+    for cutoff in (0, 0.01, 0.3, 2.0):
+        subs = rearrange.create_lookup_dict(nest, nodes)
+        assert rearrange.calc_connections_between_mcl_subclusters(subs, cutoff, full_graph=g) == \
+            ref_calc_connections(subs, g, cutoff)
+    # the module global the reference reads, and the NameError without it
+    subs = rearrange.create_lookup_dict(nest, nodes)
+    with pytest.raises(NameError):
+        rearrange.calc_connections_between_mcl_subclusters(subs, 0)
+    rearrange.full_graph = g
+    try:
+        assert rearrange.calc_connections_between_mcl_subclusters(subs, 0.1) == ref_calc_connections(subs, g, 0.1)
+    finally:
+        rearrange.full_graph = None
+
+
+def test_rearrange_hand_graph_and_partition_check():
+    h = ReadGraph()
+    h.add_edge("a", "b", weight=0.25)
+    h.add_edge("b", "c", weight=0.5)
+    h.add_edge("c", "d", weight=0.125)
+    h.add_edge("a", "d", weight=0.0625)
+    h.add_node("e")
+    nest = [[["a"], ["b"]], [["c", "d"]], [["e"]]]
+    seqs = ["a", "b", "c", "d", "e"]
+    for cutoff in (0, 0.1, 0.3, 0.6):
+        subs = rearrange.create_lookup_dict(nest, seqs)
+        assert rearrange.calc_connections_between_mcl_subclusters(subs, cutoff, full_graph=h) == \
+            ref_calc_connections(subs, h, cutoff)
+    with pytest.raises(ValueError):
+        subs = rearrange.create_lookup_dict([[["a", "b"], ["b"]]], ["a", "b", "c"])
+        rearrange.calc_connections_between_mcl_subclusters(subs, 0, full_graph=h)
