@@ -27,6 +27,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from karma_amd import _lib, engine, synth  # noqa: E402
+from karma_amd import rearrange  # noqa: E402
 from karma_amd.read_graph import ReadGraph  # noqa: E402
 
 
@@ -176,6 +177,51 @@ def main():
                                       "subgraph_copy_s": round(t_copy, 3), "gpu_s": round(t_gpu, 3),
                                       "ref_s": round(t_ref, 3), "speedup": round(t_ref / max(t_gpu, 1e-9), 2),
                                       "edge_list_bytes": nbytes}
+    # ---- --rearrange (karma.py:409-437) -------------------------------------------
+    import itertools
+    import random
+
+    def ref_calc(subs, graph, cutoff):  # karma.py:103-118
+        out = []
+        for ia, ib in itertools.combinations(subs, 2):
+            weight = 0
+            for A, B in itertools.product(subs[ia]["mcl_subcluster"], subs[ib]["mcl_subcluster"]):
+                if graph.has_edge(A, B):
+                    weight += graph[A][B]["weight"]
+                    if weight > cutoff:
+                        out.append([ia, ib])
+        return out
+
+    rng = random.Random(9)
+    nest, i = [], 0
+    while i < len(nodes):  # k-mer clusters of 1..12 consecutive contigs, 1..3 MCL subclusters each
+        k = rng.randint(1, 12)
+        cl = nodes[i:i + k]
+        i += k
+        cuts = sorted(rng.sample(range(1, len(cl)), min(len(cl) - 1, rng.randint(0, 2)))) if len(cl) > 1 else []
+        parts, s0 = [], 0
+        for c in cuts + [len(cl)]:
+            parts.append(cl[s0:c])
+            s0 = c
+        nest.append(parts)
+    subs = rearrange.create_lookup_dict(nest, nodes)
+    rearrange.calc_connections_between_mcl_subclusters(subs, 0.05, full_graph=g)  # warm
+    t = time.perf_counter()
+    groups = rearrange.calc_connections_between_mcl_subclusters(subs, 0.05, full_graph=g)
+    t_gpu = time.perf_counter() - t
+    # the reference's walk is O(S^2): time it on the first clusters and scale by (S / s)^2
+    small = nest[: max(1, len(nest) // 25)]
+    small_nodes = [x for c in small for sc in c for x in sc]
+    ssubs = rearrange.create_lookup_dict(small, small_nodes)
+    t = time.perf_counter()
+    ref_small = ref_calc(ssubs, g, 0.05)
+    t_ref_small = time.perf_counter() - t
+    assert ref_small == rearrange.calc_connections_between_mcl_subclusters(ssubs, 0.05, full_graph=g)
+    S, s_small = len(subs), len(ssubs)
+    res["rearrange"] = {"subclusters": S, "groups": len(groups), "gpu_s": round(t_gpu, 4),
+                        "ref_sample_subclusters": s_small, "ref_sample_s": round(t_ref_small, 3),
+                        "ref_extrapolated_s": round(t_ref_small * (S / s_small) ** 2, 1),
+                        "speedup_extrapolated": round(t_ref_small * (S / s_small) ** 2 / t_gpu, 1)}
     print(json.dumps(res), flush=True)
 
 
