@@ -397,7 +397,7 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 #define KARMA_CLS2_LDS 1  // coalesced loads transposed through LDS (0: per-lane 64-byte loads)
 #endif
 #ifndef KARMA_CLS2_WAVES
-#define KARMA_CLS2_WAVES 6
+#define KARMA_CLS2_WAVES 5  // 5: no spills at 96 VGPRs (0.504 vs 0.518 ms at 6 with 80)
 #endif
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
 classify2_kernel(ClassArgs P) {
