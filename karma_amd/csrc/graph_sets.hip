@@ -12,11 +12,12 @@
 // marking contig m0 + i: dedup and order come for free.  Other reads (wider
 // spans) take the general path: sort network, dedup, every pair (p <= q).
 //
-//   classify    one wave per chunk of 8192 records, no block barriers: stages
-//               512 records at a time in its own LDS slice, finds read starts
-//               with DPP, and writes one u32 code per compact read (coalesced,
-//               into the chunk's own region); general reads' starts go to the
-//               region's tail, reads of > 8 records to the big-read list.
+//   classify    one wave per chunk of 8192 records, no block barriers: lane l
+//               walks records 8l..8l+7 of each 512-record step in registers
+//               (reads crossing lanes merge by DPP) and writes one u32 code per
+//               compact read (ballot-compacted, into the chunk's own region);
+//               general reads' starts go to the region's tail, reads of > 8
+//               records to the big-read list.
 //   general     one wave per chunk with general reads: pairs as u64 keys into
 //               the chunk's pair list.
 //   partition   (codes, pairs) consecutive chunk lists fill a 64 KB LDS buffer;
@@ -124,233 +125,10 @@ __device__ __forceinline__ int rank_below(unsigned long long m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// code (m0 | M << 24) of a compact read, or general / big
-// 6 waves per SIMD: the LDS slices allow 6 blocks per CU; 80 VGPRs fit them
-// (the compiler's own choice, 82-84, allows 5: 0.714 -> 0.670 ms on config 3)
-#ifndef KARMA_CLS_V2
-#define KARMA_CLS_V2 1
-#endif
-#if KARMA_CLS_V2
-#define KARMA_CLS_KERNEL classify2_kernel
-#else
-#define KARMA_CLS_KERNEL classify_kernel
-#endif
-#ifndef KARMA_CLS_ABL
-#define KARMA_CLS_ABL 0  // ablation builds only: 1 loads alone, 2 loads + read starts
-#endif
-#ifndef KARMA_CLS_WAVES
-#define KARMA_CLS_WAVES 6
-#endif
-#define KARMA_CLS_ATTR __attribute__((amdgpu_waves_per_eu(KARMA_CLS_WAVES, KARMA_CLS_WAVES)))
-__global__ void __launch_bounds__(kCW) KARMA_CLS_ATTR classify_kernel(ClassArgs P) {
-    __shared__ uint2 srec[kCW / 64][kCIter + kMaxFast];
-    __shared__ uint16_t wst[kCW / 64][kCIter + 1];  // read starts (+ the end of the last read)
-    __shared__ uint16_t wcl[kCW / 64][kCIter];      // reads by size class
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t chunk = (int64_t)blockIdx.x * (kCW / 64) + wave;
-    const int64_t c_lo = chunk * kCChunk;
-    if (c_lo >= P.A) return;  // this kernel has no block barrier: waves are independent
-    const int64_t c_hi = min(P.A, c_lo + kCChunk);
-    uint2* sr = srec[wave];
-    uint16_t* ws = wst[wave];
-    uint16_t* cl = wcl[wave];
-    uint32_t* out = P.codes + c_lo;
-
-    // register prefetch of a step: unit u, lane l holds records 128u + 2l, +1;
-    // plus the record before the step (read-boundary carry) and the 8 after it
-    u32x4 nxt[kCPer];
-    uint2 nxc = make_uint2(kEmpty, kEmpty), nxh = make_uint2(kEmpty, kEmpty);
-    auto prefetch = [&](int64_t t0) {
-#pragma unroll
-        for (int u = 0; u < kCPer; ++u) {
-            const int64_t gi = t0 + 128 * u + 2 * lane;
-            u32x4 v = {kEmpty, kEmpty, kEmpty, kEmpty};
-            if (t0 < c_hi) {
-                if (gi + 1 < P.A) {
-                    v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.rec + gi));
-                } else if (gi < P.A) {
-                    const uint2 r = P.rec[gi];
-                    v = u32x4{r.x, r.y, kEmpty, kEmpty};
-                }
-            }
-            nxt[u] = v;
-        }
-        nxc = t0 < c_hi && t0 > 0 ? P.rec[t0 - 1] : make_uint2(kEmpty, kEmpty);
-        const int64_t gh = t0 + kCIter + lane;
-        nxh = t0 < c_hi && lane < kMaxFast && gh < P.A ? P.rec[gh] : make_uint2(kEmpty, kEmpty);
-    };
-    prefetch(c_lo);
-    uint32_t nc = 0, ng = 0;
-    int bad_order = 0, bad_contig = 0;
-#if KARMA_CLS_ABL == 1
-    uint32_t acc = 0;
-    for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) {
-#pragma unroll
-        for (int u = 0; u < kCPer; ++u) acc ^= nxt[u].x ^ nxt[u].y ^ nxt[u].z ^ nxt[u].w;
-        acc ^= nxc.x ^ nxh.y;
-        prefetch(t0 + kCIter);
-    }
-    if (lane == 0) {
-        P.n_codes[chunk] = 0;
-        P.n_gen[chunk] = 0;
-    }
-    if (acc == 0x9E3779B9u) P.flags[3] = 1;
-    return;
-#endif
-    for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) {
-        const int tn = (int)min<int64_t>(kCIter, c_hi - t0);
-        // ---- read starts (records past tn are the following ones) ----
-        uint32_t carry = nxc.x;
-        const bool carry_valid = t0 > 0;
-        int ns = 0;
-#pragma unroll
-        for (int u = 0; u < kCPer; ++u) {
-            const int j = 128 * u + 2 * lane;
-            const uint32_t x0 = nxt[u].x, x1 = nxt[u].z;
-            uint32_t p = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)x1, 0x138, 0xF, 0xF, false);
-            if (lane == 0) p = carry;  // lane 0 takes the previous unit's last record
-            bool s0 = false, s1 = false;
-            if (j < tn) {
-                const bool hp = j > 0 || carry_valid;
-                if (hp && p > x0) bad_order = 1;
-                if (nxt[u].y >= P.N) bad_contig = 1;
-                s0 = !hp || p != x0;
-            }
-            if (j + 1 < tn) {
-                if (x0 > x1) bad_order = 1;
-                if (nxt[u].w >= P.N) bad_contig = 1;
-                s1 = x0 != x1;
-            }
-            const unsigned long long b0 = __ballot(s0), b1 = __ballot(s1);
-            const int pos = ns + rank_below(b0) + rank_below(b1);
-            if (s0) ws[pos] = (uint16_t)j;
-            if (s1) ws[pos + (s0 ? 1 : 0)] = (uint16_t)(j + 1);
-            ns += __popcll(b0) + __popcll(b1);
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)x1, 63);
-        }
-#pragma unroll
-        for (int u = 0; u < kCPer; ++u) {
-            const int j = 128 * u + 2 * lane;
-            sr[j] = make_uint2(nxt[u].x, nxt[u].y);
-            sr[j + 1] = make_uint2(nxt[u].z, nxt[u].w);
-        }
-        if (lane < kMaxFast) sr[kCIter + lane] = nxh;
-        prefetch(t0 + kCIter);
-        wave_sync();
-#if KARMA_CLS_ABL == 2
-        nc += ns;
-        continue;
-#endif
-        // ---- read sizes: the gap to the next read start (the last read's end
-        // is found in the slice + halo; 9 means more than 8 records) ----
-        if (lane == 0 && ns > 0) {
-            const int jl = ws[ns - 1];
-            const uint32_t rid = sr[jl].x;
-            int j = jl + 1;
-            while (j < jl + kMaxFast + 1 && sr[j].x == rid) ++j;
-            ws[ns] = (uint16_t)j;
-        }
-        wave_sync();
-        // split: small reads (<= 4 records) from the front of cl, large ones
-        // (5..9) from the back; an entry is j0 | size << 10
-        int n_s = 0, n_l = 0;
-        for (int kb = 0; kb < ns; kb += 64) {
-            const int k = kb + lane;
-            int j0 = 0, sz = 0;
-            if (k < ns) {
-                j0 = ws[k];
-                sz = min((int)ws[k + 1] - j0, kMaxFast + 1);
-            }
-            const bool sm = k < ns && sz <= 4, lg = k < ns && sz > 4;
-            const unsigned long long bs = __ballot(sm), bl = __ballot(lg);
-            const uint16_t e = (uint16_t)(j0 | sz << 10);
-            if (sm) cl[n_s + rank_below(bs)] = e;
-            if (lg) cl[kCIter - 1 - (n_l + rank_below(bl))] = e;
-            n_s += __popcll(bs);
-            n_l += __popcll(bl);
-        }
-        wave_sync();
-        // a read's code, or general: min/max of its contigs (ids only, the
-        // records past its size are replaced by its first contig)
-        auto classify = [&](auto width, int j0, int sz, uint32_t* code, bool* gen) {
-            constexpr int W = decltype(width)::value;
-            uint32_t y[W];
-            y[0] = sr[j0].y;
-#pragma unroll
-            for (int t = 1; t < W; ++t) {
-                const uint32_t v = sr[j0 + t].y;
-                y[t] = t < sz ? v : y[0];
-            }
-            uint32_t mn = y[0], mx = y[0];
-#pragma unroll
-            for (int t = 1; t < W; ++t) {
-                mn = min(mn, y[t]);
-                mx = max(mx, y[t]);
-            }
-            if (P.compact && mx - mn < 4u && mx < P.N) {
-                uint32_t M = 0;
-#pragma unroll
-                for (int t = 0; t < W; ++t) M |= 1u << (y[t] - mn);
-                *code = (M >> 1) << 24 | mn;
-            } else {
-                *gen = true;
-            }
-        };
-        auto emit = [&](uint32_t code, bool gen, int j0) {
-            const unsigned long long cb = __ballot(code != kEmpty), gb = __ballot(gen);
-            if (code != kEmpty) out[nc + rank_below(cb)] = code;
-            if (gen) out[kCChunk - 1 - (ng + rank_below(gb))] = (uint32_t)(t0 - c_lo + j0);
-            nc += __popcll(cb);
-            ng += __popcll(gb);
-        };
-        for (int kb = 0; kb < n_s; kb += 64) {
-            const int k = kb + lane;
-            uint32_t code = kEmpty;
-            bool gen = false;
-            int j0 = 0;
-            if (k < n_s) {
-                const uint32_t e = cl[k];
-                j0 = e & 1023;
-                classify(std::integral_constant<int, 4>{}, j0, (int)(e >> 10), &code, &gen);
-            }
-            emit(code, gen, j0);
-        }
-        for (int kb = 0; kb < n_l; kb += 64) {
-            const int k = kb + lane;
-            uint32_t code = kEmpty;
-            bool gen = false;
-            int j0 = 0;
-            if (k < n_l) {
-                const uint32_t e = cl[kCIter - 1 - k];
-                j0 = e & 1023;
-                const int sz = (int)(e >> 10);
-                if (sz > kMaxFast) P.big_list[atomicAdd(P.big_n, 1u)] = t0 + j0;  // > 8 records: generic path
-                else classify(std::integral_constant<int, kMaxFast>{}, j0, sz, &code, &gen);
-            }
-            emit(code, gen, j0);
-        }
-        wave_sync();  // every lane is done with the slice
-    }
-#if KARMA_CLS_ABL == 2
-    if (lane == 0) {
-        P.n_codes[chunk] = 0;
-        P.n_gen[chunk] = 0;
-    }
-    if (nc == 0x9E3779B9u) P.flags[3] = 1;
-    return;
-#endif
-    if (lane == 0) {
-        P.n_codes[chunk] = nc;
-        P.n_gen[chunk] = ng;
-        if (nc) atomicAdd(P.blk_items + chunk / P.lists_per_block, (unsigned long long)nc);
-    }
-    if (bad_order) P.flags[0] = 1;
-    if (bad_contig) P.flags[1] = 1;
-}
-
-// ---- classify, register-resident variant ---------------------------------------
-// The same outputs as classify_kernel, without LDS: lane l of a 512-record step
-// holds records 8l .. 8l + 7 (four 16-byte loads) and walks them in order.
+// ---- classify ---------------------------------------------------------------------
+// One wave per chunk of 8192 records, no block barriers.  Lane l of a 512-record
+// step holds records 8l .. 8l + 7 (coalesced 16-byte loads, transposed through
+// the wave's LDS slice) and walks them in order.
 //   * a read that starts and ends inside the lane is emitted at its end;
 //   * the lane's last read (its "tail") continues into the next lane's
 //     "head" (the records before that lane's first read start): the next lane
@@ -393,9 +171,6 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-#ifndef KARMA_CLS2_LDS
-#define KARMA_CLS2_LDS 1  // coalesced loads transposed through LDS (0: per-lane 64-byte loads)
-#endif
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 5  // 5: no spills at 96 VGPRs (0.504 vs 0.518 ms at 6 with 80)
 #endif
@@ -408,47 +183,28 @@ classify2_kernel(ClassArgs P) {
     if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
     const int64_t c_hi = min(P.A, c_lo + kCChunk);
     uint32_t* out = P.codes + c_lo;
-#if KARMA_CLS2_LDS
     // transpose buffer: lane l's 8 records at byte 80l (16 bytes of padding per
     // lane make both the 16-byte stores and the lane-sequential reads conflict-free)
     __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][64 * 5];
     u32x4* tb = tbuf[wave];
-#endif
 
-    u32x4 nxt[kCPer];
-    // records [t0, hi) of a step; lane l ends up with records t0 + 8l .. + 7
-    auto prefetch = [&](int64_t t0, int64_t hi) {
-#if KARMA_CLS2_LDS
-        // coalesced: unit u of lane l = records t0 + 128u + 2l, + 1
+    // records [t0, hi) of a step, coalesced: unit u of lane l = records t0 + 128u + 2l, + 1
+    auto prefetch = [&](u32x4 (&dst)[kCPer], int64_t t0, int64_t hi) {
         const int64_t gb = t0 + 2 * lane;
-#else
-        const int64_t gb = t0 + 8 * lane;
-#endif
         if (t0 + kCIter <= hi) {
 #pragma unroll
-            for (int u = 0; u < kCPer; ++u) {
-#if KARMA_CLS2_LDS
-                const int64_t gi = gb + 128 * u;
-#else
-                const int64_t gi = gb + 2 * u;
-#endif
-                nxt[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.rec + gi));
-            }
+            for (int u = 0; u < kCPer; ++u)
+                dst[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.rec + gb + 128 * u));
         } else {
 #pragma unroll
             for (int u = 0; u < kCPer; ++u) {
-#if KARMA_CLS2_LDS
                 const int64_t gi = gb + 128 * u;
-#else
-                const int64_t gi = gb + 2 * u;
-#endif
                 const uint2 r0 = gi < hi ? P.rec[gi] : make_uint2(kEmpty, kEmpty);
                 const uint2 r1 = gi + 1 < hi ? P.rec[gi + 1] : make_uint2(kEmpty, kEmpty);
-                nxt[u] = u32x4{r0.x, r0.y, r1.x, r1.y};
+                dst[u] = u32x4{r0.x, r0.y, r1.x, r1.y};
             }
         }
     };
-    prefetch(c_lo, c_hi);
     // carry from the previous lane 63: its last read id, and its tail read
     bool have_prev = c_lo > 0;
     uint32_t prev_rid = have_prev ? P.rec[c_lo - 1].x : kEmpty;
@@ -457,34 +213,25 @@ classify2_kernel(ClassArgs P) {
     uint32_t ct_len = 0, ct_pos = 0;
     uint32_t nc = 0, ng = 0;
     int bad_order = 0, bad_contig = 0;
-    for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) {
+    // one 512-record step from `buf`, which then takes the next step's loads
+    // (two steps in flight -- a second register set at 4 waves/SIMD -- measured
+    // the same: the walk already runs at ~5.7 TB/s of records + codes)
+    auto step = [&](u32x4 (&buf)[kCPer], int64_t t0) {
         uint32_t rid[8], ctg[8];
-#if KARMA_CLS2_LDS
-        {
-            // loader lane L, unit u -> lane 16u + L/4, unit L & 3
+        // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
 #pragma unroll
-            for (int u = 0; u < kCPer; ++u) tb[5 * (16 * u + (lane >> 2)) + (lane & 3)] = nxt[u];
-            wave_sync();
-#pragma unroll
-            for (int u = 0; u < kCPer; ++u) {
-                const u32x4 q = tb[5 * lane + u];
-                rid[2 * u] = q.x;
-                ctg[2 * u] = q.y;
-                rid[2 * u + 1] = q.z;
-                ctg[2 * u + 1] = q.w;
-            }
-            wave_sync();
-        }
-#else
+        for (int u = 0; u < kCPer; ++u) tb[5 * (16 * u + (lane >> 2)) + (lane & 3)] = buf[u];
+        wave_sync();
 #pragma unroll
         for (int u = 0; u < kCPer; ++u) {
-            rid[2 * u] = nxt[u].x;
-            ctg[2 * u] = nxt[u].y;
-            rid[2 * u + 1] = nxt[u].z;
-            ctg[2 * u + 1] = nxt[u].w;
+            const u32x4 q = tb[5 * lane + u];
+            rid[2 * u] = q.x;
+            ctg[2 * u] = q.y;
+            rid[2 * u + 1] = q.z;
+            ctg[2 * u + 1] = q.w;
         }
-#endif
-        if (t0 + kCIter < c_hi) prefetch(t0 + kCIter, c_hi);
+        wave_sync();
+        if (t0 + kCIter < c_hi) prefetch(buf, t0 + kCIter, c_hi);
         // valid records of this lane (own reads start at a valid record)
         const int nval = (int)max<int64_t>(0, min<int64_t>(8, c_hi - (t0 + 8 * lane)));
         const bool first_any = have_prev || lane > 0;
@@ -577,7 +324,10 @@ classify2_kernel(ClassArgs P) {
         ct_pos = (uint32_t)__builtin_amdgcn_readlane((int)t_pos, 63);
         prev_rid = (uint32_t)__builtin_amdgcn_readlane((int)rid[7], 63);
         have_prev = true;
-    }
+    };
+    u32x4 buf[kCPer];
+    prefetch(buf, c_lo, c_hi);
+    for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) step(buf, t0);
     // the chunk's last tail read continues into the next chunk's first records
     // (at most 8 of them matter): uniform scalar walk
     if (ct_ok) {
@@ -1452,7 +1202,7 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         if (A > 0) {
             ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags};
-            KARMA_LAUNCH(ctx, "graph_classify", KARMA_CLS_KERNEL, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags);
@@ -1575,7 +1325,7 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         if (A > 0) {
             ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags};
-            KARMA_LAUNCH(ctx, "graph_classify", KARMA_CLS_KERNEL, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         } else {
             KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
             KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
