@@ -11,9 +11,10 @@ those use collectives (RCCL over xGMI through torch.distributed "nccl"):
                  own rows.
   shared graph   each rank reduces its fragments' pairs locally (HIP bucket
                  reduce), routes the pre-reduced (key, count) list to the owner
-                 of contig a (all-to-all-v), the owner merges, the readset
-                 sizes (diagonal counts) are SUM-allreduced so every owner can
-                 weight edges to contigs it does not own.
+                 of contig a (all-to-all-v), the owner merges; its merged
+                 diagonal counts are the readset sizes of the contigs it owns,
+                 and those slices are all-gathered so every owner can weight
+                 edges to contigs it does not own.
 All arithmetic is integer until the one weight formula, so the result is
 bit-identical to the single-GPU (and the reference) result.
 
@@ -121,6 +122,27 @@ class Comm:
         outs = [torch.empty_like(pad) for _ in range(self.world)]
         self.dist.all_gather(outs, pad)
         return torch.cat([o[:s] for o, s in zip(outs, sizes)]).to(dev)
+
+    def allgather_slices_(self, t, bounds):
+        """t[bounds[r]:bounds[r+1]] of rank r into every rank's t (in place):
+        each rank contributes only its own slice (bounds are known everywhere,
+        so no size exchange; slices padded to the largest)."""
+        if not self.dist:
+            return t
+        import torch
+
+        lo, hi = int(bounds[self.rank]), int(bounds[self.rank + 1])
+        sizes = [int(bounds[r + 1] - bounds[r]) for r in range(self.world)]
+        mx = max(sizes)
+        h = self._h(t)
+        mine = torch.zeros(mx, dtype=h.dtype, device=h.device)
+        mine[: hi - lo] = h[lo:hi]
+        outs = [torch.empty_like(mine) for _ in range(self.world)]
+        self.dist.all_gather(outs, mine)
+        for r in range(self.world):
+            h[int(bounds[r]):int(bounds[r + 1])] = outs[r][: sizes[r]]
+        self._back(h, t)
+        return t
 
     def alltoallv(self, t, send_counts):
         """1-D all-to-all-v: send_counts[r] consecutive elements go to rank r."""
@@ -342,7 +364,9 @@ class ShardedBuild:
             rk = comm.alltoallv(keys, send)
             rc = comm.alltoallv(counts, send)
             merged = ops.merge(rk, rc)
-            tot = comm.allreduce_sum_(ops.totals(merged, self.n_glob))
+            # the owner's merged list holds the diagonal (a, a) of every a it owns:
+            # complete readset sizes for its slice, gathered to every rank
+            tot = comm.allgather_slices_(ops.totals(merged, self.n_glob), self.bounds)
             edges = ops.edges(merged, self.n_glob, tot)
             ops.close(local)
             final_pairs = merged

@@ -5,7 +5,7 @@ backend is an oracle-backed CPU implementation of the same ops interface
 (presence bytes in the HIP ordinal layout, exception keys in the karma.h key
 encoding, sorted (a << 32 | b, count) pair lists), so what is under test is the
 sharding, the presence MAX-allreduce, the exception all-gather, the pair
-all-to-all-v to contig owners, the totals SUM-allreduce and the owner-side
+all-to-all-v to contig owners, the owned-totals all-gather and the owner-side
 weights.  The result must equal a single-process oracle run bit for bit.
 """
 import os
