@@ -361,9 +361,10 @@ class ShardedBuild:
         if comm.world > 1:
             keys, counts, starts = ops.pairs_split(local, self.bounds)
             send = np.diff(starts)
-            rk = comm.alltoallv(keys, send)
-            rc = comm.alltoallv(counts, send)
-            merged = ops.merge(rk, rc)
+            # one all-to-all-v of interleaved (key, count) int64 pairs
+            import torch
+            kc = comm.alltoallv(torch.stack([keys, counts], 1).reshape(-1), 2 * send).reshape(-1, 2)
+            merged = ops.merge(kc[:, 0].contiguous(), kc[:, 1].contiguous())
             # the owner's merged list holds the diagonal (a, a) of every a it owns:
             # complete readset sizes for its slice, gathered to every rank
             tot = comm.allgather_slices_(ops.totals(merged, self.n_glob), self.bounds)
