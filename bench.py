@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=float, default=0.1,
                     help="fraction of the per-GPU workload the CPU baseline processes (0 disables)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
+    ap.add_argument("--emulate-ranks", type=int, default=1,
+                    help="diagnostic: one process runs rank 0's compute of a W-rank weak-scaled problem "
+                         "(global contig ids over W x the per-GPU contigs, no exchange); not the metric")
     return ap.parse_args()
 
 
@@ -86,7 +89,8 @@ def main():
 
     # ---------------- synthetic input (host), then resident in HBM ----------------
     t_gen = time.time()
-    n_glob, f_glob = n_loc * world, f_loc * world
+    emu = max(1, args.emulate_ranks) if world == 1 else 1
+    n_glob, f_glob = n_loc * world * emu, f_loc * world * emu
     c_lo = rank * n_loc
     blob, offs, key_len = engine.synth_contigs(seed, n_loc, 400, 800, 0, first=c_lo)
     genes = engine.synth_genes(seed, n_glob)
@@ -202,7 +206,8 @@ def main():
             "config": {"workload": f"{args.config}: {n_loc} contigs (mean 800 bp) + {f_loc} "
                                    f"{'paired' if paired else 'single-end'} fragments per GPU, k={kmer}",
                        "contigs_per_gpu": n_loc, "fragments_per_gpu": f_loc, "records_per_gpu": A,
-                       "columns_M": M, "edges": E, "parallelism": f"contig+fragment shards x{world}"},
+                       "columns_M": M, "edges": E, "parallelism": f"contig+fragment shards x{world}",
+                       **({"emulated_ranks": emu, "global_contigs": n_glob} if emu > 1 else {})},
             "roofline": roof,
             "step_hbm_bytes_per_gpu": step_bytes,
             "step_achieved_GBs_per_gpu": round(step_bytes / (dt / args.steps) / 1e9, 1),

@@ -50,12 +50,15 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kMaxB = 1024;           // pair buckets (n_contigs <= 2^20 keeps the compact path)
-constexpr int kMaxBc = 256;           // code buckets
+constexpr int kMaxB = 2048;           // pair buckets (n_contigs <= 2^21 keeps the compact path)
+constexpr int kMaxBc = 512;           // code buckets
 // partition LDS is sized by the bucket count: the narrow variants (<= 512 pair
 // and <= 128 code buckets, n_contigs <= 2^19) keep 3 code-partition blocks per CU
 constexpr int kNarrowB = 512, kNarrowBc = 128;
 constexpr int kMaxBwCompact = 10;     // compact reads need 2^(bw+3) band counters <= kBand
+// the compact path: kMaxB pair buckets of 2^kMaxBwCompact contigs (8 GPUs x 200k
+// contigs of a weak-scaled config 3 = 1.6M stay on it)
+constexpr int64_t kMaxCompactN = int64_t(kMaxB) << kMaxBwCompact;
 
 struct Geo {
     int bw, bbits, B;  // pair buckets of 2^bw contigs; pair keys a_local << bbits | b
@@ -1163,7 +1166,7 @@ __global__ void gather_lists_kernel(const uint64_t* __restrict__ lists, int64_t 
     }
 }
 
-// n_contigs > 2^20: bucket-local 32-bit pair keys (a_local << bbits | b) no
+// n_contigs > 2^21: bucket-local 32-bit pair keys (a_local << bbits | b) no
 // longer fit, so every read takes the general path (sorted distinct contigs,
 // per-chunk u64 pair lists, no atomics) and one 64-bit sort-reduce follows;
 // reads of > 8 records are merged as in the main path.
@@ -1236,7 +1239,7 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
 
 // Records (grouped by read, 16-byte aligned) -> sorted unique (a<<32|b, count).
 int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
-    if (N > (int64_t(1) << 20)) return records_to_pairs_wide(ctx, rec, A, N, out);
+    if (N > kMaxCompactN) return records_to_pairs_wide(ctx, rec, A, N, out);
     Geo g;
     KARMA_TRY(make_geo(N, &g));
     const int B = g.B;

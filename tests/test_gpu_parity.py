@@ -196,9 +196,11 @@ def check_records(rec, n, grouped=True):
 @pytest.mark.parametrize("seed,n,nf,paired", [(2, 20_000, 400_000, True), (5, 3_000, 200_000, False),
                                               (9, 777, 50_000, True), (4, 1, 1000, True),
                                               # wide partition variants (> 512 pair / > 128 code buckets),
-                                              # config 5's 1M contigs, and past 2^20 (no compact path)
+                                              # config 5's 1M contigs, 8 x 200k (weak-scaled config 3), and
+                                              # past 2^21 (no compact path)
                                               (10, 600_000, 1_000_000, True), (11, 1_000_000, 2_000_000, True),
-                                              (12, 1_100_000, 1_000_000, True)])
+                                              (12, 1_100_000, 1_000_000, True), (13, 1_600_000, 1_500_000, True),
+                                              (14, 2_200_000, 1_000_000, True)])
 def test_records_graph_vs_oracle(seed, n, nf, paired):
     rec = engine.synth_records(seed, n, 0, nf, paired)
     check_records(rec, n)
@@ -255,7 +257,7 @@ def test_records_compact_spans_and_bucket_edges():
     check_records(np.array(rows, np.uint32), 300)
 
 
-@pytest.mark.parametrize("n", [200, 1_200_000])  # 1.2M: the 64-bit-key path (n_contigs > 2^20)
+@pytest.mark.parametrize("n", [200, 1_200_000, 2_500_000])  # 2.5M: the 64-bit-key path (n_contigs > 2^21)
 def test_records_big_reads_and_duplicates(n):
     rng = np.random.default_rng(2)
     rows = []
