@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--emulate-ranks", type=int, default=1,
                     help="diagnostic: one process runs rank 0's compute of a W-rank weak-scaled problem "
-                         "(global contig ids over W x the per-GPU contigs, no exchange); not the metric")
+                         "(global contig ids over W x the per-GPU contigs; the exchange's local work - device split, "
+                         "merge of W sorted slices, totals - without its collectives); not the metric")
     return ap.parse_args()
 
 
@@ -99,7 +100,8 @@ def main():
     log(f"[rank {rank}] generated {n_loc} contigs ({int(offs[-1])} bases), {f_loc} fragments, {A} records "
         f"in {time.time() - t_gen:.1f}s")
 
-    build = ShardedBuild(ctx, comm, engine.kmode_of(kmer), n_glob, c_lo, n_loc)  # sets the shared stream
+    build = ShardedBuild(ctx, comm, engine.kmode_of(kmer), n_glob, c_lo, n_loc,
+                         emulate_ranks=emu)  # sets the shared stream
     store = engine.ContigStore(ctx, blob, offs, key_len)
     rec_dev = torch.from_numpy(rec.view(np.int64).reshape(-1)).to(build.ops.dev)
     torch.cuda.synchronize()

@@ -138,6 +138,13 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
 /* Merge (key, count) lists in any order into one sorted unique list (exchange merge). */
 int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, int64_t n, int is_device,
                       karma_pairs** out);
+/* Merge runs [run_off[r], run_off[r + 1]) of (key, count), each sorted by key
+ * (the slices an exchange owner receives, one per sender), into one sorted
+ * unique list: a pairwise merge tree, then equal keys summed.
+ * KARMA_ERR_UNSORTED when a run is not sorted.  run_off is a host array of
+ * n_runs + 1 offsets starting at 0. */
+int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, const int64_t* run_off,
+                           int n_runs, int is_device, karma_pairs** out);
 int karma_pairs_destroy(karma_pairs* p);
 /* Later kernels on p run on ctx's stream (after p's current stream is drained);
  * p's memory stays with the allocator that made it.  Lets a list built on a
@@ -147,7 +154,7 @@ int karma_pairs_count(karma_pairs* p, int64_t* n);
 /* Device pointers of the list (valid until destroy): keys u64[n], counts i64[n]. */
 int karma_pairs_device(karma_pairs* p, const uint64_t** keys, const int64_t** counts);
 int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* first, int is_device);
-/* Index of the first key with a >= bounds[r] for r = 0..nranks (host out). */
+/* Index of the first key with a >= bounds[r] for r = 0..nranks (host out; searched on the device). */
 int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts);
 /* totals[c] = count of the diagonal pair (c, c) (readset sizes) for c in [0, n_contigs). */
 int karma_pairs_totals(karma_pairs* p, int64_t* totals_dev, int64_t n_contigs);

@@ -12,6 +12,7 @@
 // list counts |readset(a)| (the normaliser), so one mechanism yields both the
 // shared counts and the totals.
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_merge.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -177,6 +178,37 @@ __global__ void deinterleave_kernel(const uint2* __restrict__ in, int64_t n, uin
     if (i < n) {
         rid[i] = in[i].x;
         cid[i] = in[i].y;
+    }
+}
+
+// rank boundaries of a sorted pair list: first key with a >= bounds[r]
+__global__ void split_kernel(const uint64_t* __restrict__ keys, int64_t n, const int64_t* __restrict__ bounds, int nb,
+                             int64_t* __restrict__ starts) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nb) return;
+    const uint64_t lim = (uint64_t)bounds[r] << 32;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < lim) lo = mid + 1;
+        else hi = mid;
+    }
+    starts[r] = lo;
+}
+
+// keys sorted within each run [off[r], off[r + 1]): a descent is allowed only
+// where a run starts
+__global__ void runs_check_kernel(const uint64_t* __restrict__ k, int64_t n, const int64_t* __restrict__ off, int nr,
+                                  int64_t* __restrict__ bad) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (k[i] <= k[i + 1]) continue;
+        int lo = 0, hi = nr;  // off[lo] <= i + 1 < off[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (off[mid] <= i + 1) lo = mid;
+            else hi = mid;
+        }
+        if (off[lo] != i + 1) *bad = 1;
     }
 }
 
@@ -409,6 +441,114 @@ int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* count
     return KARMA_OK;
 }
 
+int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, const int64_t* run_off,
+                           int n_runs, int is_device, karma_pairs** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && run_off && n_runs >= 1, KARMA_ERR_ARG, "karma_pairs_merge_runs: bad arguments");
+    std::vector<int64_t> off(run_off, run_off + n_runs + 1);
+    KARMA_CHECK(off[0] == 0, KARMA_ERR_ARG, "karma_pairs_merge_runs: run_off[0] must be 0");
+    for (int r = 0; r < n_runs; ++r)
+        KARMA_CHECK(off[r] <= off[r + 1], KARMA_ERR_ARG, "karma_pairs_merge_runs: run offsets decrease");
+    const int64_t n = off[n_runs];
+    KARMA_CHECK(n == 0 || (keys && counts), KARMA_ERR_ARG, "karma_pairs_merge_runs: null keys or counts");
+    KARMA_CHECK(n < (int64_t(1) << 31), KARMA_ERR_ARG, "karma_pairs_merge_runs: %lld items exceed 2^31", (long long)n);
+    auto* p = new karma_pairs();
+    p->ctx = ctx;
+    std::unique_ptr<karma_pairs> guard(p);
+    DevArray<uint64_t> kb[2];
+    DevArray<int64_t> cb[2];
+    const uint64_t* sk = keys;
+    const int64_t* sc = counts;
+    if (!is_device && n) {
+        KARMA_TRY(kb[1].alloc(ctx, n));
+        KARMA_TRY(cb[1].alloc(ctx, n));
+        KARMA_HIP(hipMemcpyAsync(kb[1].ptr, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(cb[1].ptr, counts, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        sk = kb[1].ptr;
+        sc = cb[1].ptr;
+    }
+    // st: [0] unique keys (ReduceByKey's run count), [1] order violation
+    DevArray<int64_t> st, doff;
+    KARMA_TRY(st.alloc(ctx, 2));
+    KARMA_TRY(doff.alloc(ctx, n_runs + 1));
+    KARMA_HIP(hipMemsetAsync(st.ptr, 0, 16, ctx->stream));
+    void* hpin = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, std::max<size_t>(16, (n_runs + 1) * 8), &hpin));
+    std::memcpy(hpin, off.data(), (n_runs + 1) * 8);
+    KARMA_HIP(hipMemcpyAsync(doff.ptr, hpin, (n_runs + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (n > 1)
+        KARMA_LAUNCH(ctx, "runs_check", runs_check_kernel, std::min<int64_t>(grid1(n), 4096), 256, 0, sk, n, doff.ptr,
+                     n_runs, st.ptr + 1);
+    // pairwise merge tree over the runs (rocprim merge path), ping-pong buffers
+    if (n_runs > 1 && n) {
+        size_t need = 0;
+        for (std::vector<int64_t> o = off; o.size() > 2;) {  // plan: the largest temporary
+            std::vector<int64_t> next{0};
+            for (size_t j = 0; j + 1 < o.size(); j += 2) {
+                if (j + 2 < o.size()) {
+                    size_t tb = 0;
+                    KARMA_HIP(rocprim::merge(nullptr, tb, sk, sk, (uint64_t*)nullptr, sc, sc, (int64_t*)nullptr,
+                                             (size_t)(o[j + 1] - o[j]), (size_t)(o[j + 2] - o[j + 1]),
+                                             rocprim::less<uint64_t>(), ctx->stream));
+                    need = std::max(need, tb);
+                }
+                next.push_back(o[std::min(j + 2, o.size() - 1)]);
+            }
+            o.swap(next);
+        }
+        DevArray<uint8_t> tmp;
+        KARMA_TRY(tmp.alloc(ctx, std::max<size_t>(need, 1)));
+        KARMA_TRY(kb[0].alloc(ctx, n));
+        KARMA_TRY(cb[0].alloc(ctx, n));
+        if (!kb[1].ptr) {
+            KARMA_TRY(kb[1].alloc(ctx, n));
+            KARMA_TRY(cb[1].alloc(ctx, n));
+        }
+        int dst = 0;
+        for (std::vector<int64_t> o = off; o.size() > 2; dst ^= 1) {
+            std::vector<int64_t> next{0};
+            for (size_t j = 0; j + 1 < o.size(); j += 2) {
+                const int64_t a0 = o[j], a1 = o[j + 1];
+                if (j + 2 < o.size()) {
+                    const int64_t a2 = o[j + 2];
+                    size_t tb = need;
+                    KARMA_HIP(rocprim::merge(tmp.ptr, tb, sk + a0, sk + a1, kb[dst].ptr + a0, sc + a0, sc + a1,
+                                             cb[dst].ptr + a0, (size_t)(a1 - a0), (size_t)(a2 - a1),
+                                             rocprim::less<uint64_t>(), ctx->stream));
+                } else if (a1 > a0) {  // odd run out: carried to the next level
+                    KARMA_HIP(hipMemcpyAsync(kb[dst].ptr + a0, sk + a0, (a1 - a0) * 8, hipMemcpyDeviceToDevice,
+                                             ctx->stream));
+                    KARMA_HIP(hipMemcpyAsync(cb[dst].ptr + a0, sc + a0, (a1 - a0) * 8, hipMemcpyDeviceToDevice,
+                                             ctx->stream));
+                }
+                next.push_back(o[std::min(j + 2, o.size() - 1)]);
+            }
+            o.swap(next);
+            sk = kb[dst].ptr;
+            sc = cb[dst].ptr;
+        }
+    }
+    // equal keys (from different runs, or repeated in one) are now adjacent
+    KARMA_TRY(p->keys.alloc(ctx, n));
+    KARMA_TRY(p->counts.alloc(ctx, n));
+    if (n) {
+        size_t tb = 0;
+        KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, sk, p->keys.ptr, sc, p->counts.ptr, st.ptr,
+                                                    hipcub::Sum(), (int)n, ctx->stream));
+        DevArray<uint8_t> tmp;
+        KARMA_TRY(tmp.alloc(ctx, tb));
+        KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(tmp.ptr, tb, sk, p->keys.ptr, sc, p->counts.ptr, st.ptr,
+                                                    hipcub::Sum(), (int)n, ctx->stream));
+    }
+    KARMA_HIP(hipMemcpyAsync(hpin, st.ptr, 16, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    const int64_t* h = static_cast<const int64_t*>(hpin);
+    KARMA_CHECK(!h[1], KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
+    p->n = h[0];
+    *out = guard.release();
+    return KARMA_OK;
+}
+
 int karma_pairs_destroy(karma_pairs* p) {
     if (!p) return KARMA_OK;
     hipSetDevice(p->ctx->device);
@@ -453,16 +593,21 @@ int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* f
 
 int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts) {
     KARMA_CHECK(p && bounds && starts && nranks >= 1, KARMA_ERR_ARG, "bad arguments");
-    KARMA_TRY(ctx_begin(p->ctx));
-    std::vector<uint64_t> hk(p->n);
-    if (p->n) {
-        KARMA_HIP(hipMemcpyAsync(hk.data(), p->keys.ptr, p->n * 8, hipMemcpyDeviceToHost, p->ctx->stream));
-        KARMA_HIP(hipStreamSynchronize(p->ctx->stream));
-    }
-    for (int r = 0; r <= nranks; ++r) {
-        const uint64_t lim = (uint64_t)bounds[r] << 32;
-        starts[r] = std::lower_bound(hk.begin(), hk.end(), lim) - hk.begin();
-    }
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    // binary searches on the device: only the nranks + 1 starts cross PCIe
+    const int nb = nranks + 1;
+    DevArray<int64_t> d;
+    KARMA_TRY(d.alloc(ctx, 2 * nb));
+    void* hpin = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, 2 * nb * 8, &hpin));
+    int64_t* h = static_cast<int64_t*>(hpin);
+    std::memcpy(h, bounds, nb * 8);
+    KARMA_HIP(hipMemcpyAsync(d.ptr, h, nb * 8, hipMemcpyHostToDevice, ctx->stream));
+    KARMA_LAUNCH(ctx, "pairs_split", split_kernel, grid1(nb, 64), 64, 0, p->keys.ptr, p->n, d.ptr, nb, d.ptr + nb);
+    KARMA_HIP(hipMemcpyAsync(h + nb, d.ptr + nb, nb * 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    std::memcpy(starts, h + nb, nb * 8);
     return KARMA_OK;
 }
 

@@ -55,6 +55,9 @@ constexpr int kMaxBc = 512;           // code buckets
 // partition LDS is sized by the bucket count: the narrow variants (<= 512 pair
 // and <= 128 code buckets, n_contigs <= 2^19) keep 3 code-partition blocks per CU
 constexpr int kNarrowB = 512, kNarrowBc = 128;
+#ifndef KARMA_APPEND_MIN_BC
+#define KARMA_APPEND_MIN_BC 129  // code_append_kernel from this many code buckets on (n_contigs > 2^19)
+#endif
 constexpr int kMaxBwCompact = 10;     // compact reads need 2^(bw+3) band counters <= kBand
 // the compact path: kMaxB pair buckets of 2^kMaxBwCompact contigs (8 GPUs x 200k
 // contigs of a weak-scaled config 3 = 1.6M stay on it)
@@ -96,6 +99,20 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Inclusive sum over lanes 0..l of a wave, in DPP steps (row shifts within
+// 16-lane rows, then row broadcasts of lanes 15 and 31) instead of ds_bpermute
+// round trips through the LDS crossbar.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return x;
+}
+__device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
@@ -121,6 +138,8 @@ struct ClassArgs {
     int64_t* big_list;
     unsigned* big_n;
     int* flags;  // 0 order, 1 contig range (2: general pair list full)
+    uint32_t* blk_hist;  // per partition block: codes per code bucket (null: no compact path)
+    int bwc, Bc;
 };
 
 // lanes below this one with their bit set in a wave mask
@@ -190,6 +209,14 @@ classify2_kernel(ClassArgs P) {
     // lane make both the 16-byte stores and the lane-sequential reads conflict-free)
     __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][64 * 5];
     u32x4* tb = tbuf[wave];
+    // the chunk's codes per code bucket, added to its partition block's row at the end
+    __shared__ uint32_t whist[kCW / 64][kMaxBc];
+    uint32_t* wh = whist[wave];
+    const bool hist_on = P.blk_hist != nullptr;
+    if (hist_on) {
+        for (int b = lane; b < P.Bc; b += 64) wh[b] = 0;
+        wave_sync();
+    }
 
     // records [t0, hi) of a step, coalesced: unit u of lane l = records t0 + 128u + 2l, + 1
     auto prefetch = [&](u32x4 (&dst)[kCPer], int64_t t0, int64_t hi) {
@@ -255,7 +282,10 @@ classify2_kernel(ClassArgs P) {
         auto emit = [&](bool e, uint32_t code, uint32_t pos, bool big) {
             const bool ec = e && !big && code != kEmpty;
             const unsigned long long b = __ballot(ec);
-            if (ec) out[nc + rank_below(b)] = code;
+            if (ec) {
+                out[nc + rank_below(b)] = code;
+                if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
+            }
             nc += __popcll(b);
             const bool eg = e && !big && code == kEmpty;
             const unsigned long long g = __ballot(eg);
@@ -346,8 +376,10 @@ classify2_kernel(ClassArgs P) {
         const uint32_t code = big ? kEmpty : hl ? rs_code2(ct, h, P.N, P.compact) : rs_code(ct, P.N, P.compact);
         if (lane == 0) {
             if (big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + ct_pos;
-            else if (code != kEmpty) out[nc] = code;
-            else out[kCChunk - 1 - ng] = ct_pos;
+            else if (code != kEmpty) {
+                out[nc] = code;
+                if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
+            } else out[kCChunk - 1 - ng] = ct_pos;
         }
         nc += !big && code != kEmpty ? 1u : 0u;
         ng += !big && code == kEmpty ? 1u : 0u;
@@ -356,6 +388,14 @@ classify2_kernel(ClassArgs P) {
         P.n_codes[chunk] = nc;
         P.n_gen[chunk] = ng;
         if (nc) atomicAdd(P.blk_items + chunk / P.lists_per_block, (unsigned long long)nc);
+    }
+    if (hist_on && nc) {
+        wave_sync();
+        uint32_t* gh = P.blk_hist + (chunk / P.lists_per_block) * P.Bc;
+        for (int b = lane; b < P.Bc; b += 64) {
+            const uint32_t k = wh[b];
+            if (k) atomicAdd(gh + b, k);
+        }
     }
     if (bad_order) P.flags[0] = 1;
     if (bad_contig) P.flags[1] = 1;
@@ -401,12 +441,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
             sort_dedup(rs);
         }
         const uint32_t cnt = rs.u * (rs.u + 1) / 2;
-        uint32_t x = cnt;  // wave inclusive scan of the pair counts
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d);
-            if (lane >= d) x += y;
-        }
+        const uint32_t x = wave_scan_incl(cnt);  // wave inclusive scan of the pair counts
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
         if ((int64_t)np + total > pcap) {
             full = true;
@@ -431,7 +466,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
 
 // ---- partition: chunk lists -> bucket-major padded runs ---------------------------
 constexpr int kPT = 512;                 // partition threads (several blocks per CU overlap their phases)
-constexpr int kMaxListsPerBlock = 64;    // chunk lists per partition block, at most (a power of 2)
+constexpr int kMaxListsPerBlock = 128;   // chunk lists per partition block, at most (a power of 2)
 
 // compact-read codes: u32 (m0 | M << 24) -> u16 (m0_local << 3 | M) per code bucket
 template <int NB>
@@ -545,14 +580,9 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
         uint32_t carry = 0;
         for (int base = 0; base < nl; base += 64) {
             const uint32_t v = base + lane < nl ? list_n[l_lo + base + lane] : 0u;
-            uint32_t x = v;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(x, d);
-                if (lane >= d) x += y;
-            }
+            const uint32_t x = wave_scan_incl(v);
             if (base + lane < nl) lpre[base + lane] = carry + x - v;
-            carry += __shfl(x, 63);
+            carry += lane63(x);
         }
         for (int i = nl + lane; i <= kMaxListsPerBlock; i += 64) lpre[i] = carry;  // pad: fixed-step search
     }
@@ -601,14 +631,9 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
             for (int b0 = 0; b0 < nb; b0 += 64) {
                 const uint32_t val =
                     b0 + lane < nb ? (h[b0 + lane] + (T::kPad - 1)) & ~(uint32_t)(T::kPad - 1) : 0u;
-                uint32_t x = val;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(x, d);
-                    if (lane >= d) x += y;
-                }
+                const uint32_t x = wave_scan_incl(val);
                 if (b0 + lane < nb) toff[b0 + lane] = c2 + x - val;
-                c2 += __shfl(x, 63);
+                c2 += lane63(x);
             }
             if (lane == 0) toff[nb] = c2;
         }
@@ -640,6 +665,204 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
     }
 }
 
+// ---- code partition: one run per (block, code bucket) ------------------------------
+// The general partition above pads every bucket's run of every flush: with
+// hundreds of code buckets (n_contigs > 2^19, the 8-rank weak-scaled config 3)
+// a flush's runs hold ~20 codes and the reduce spends its time on run tables.
+// Here the classify kernel has already counted each partition block's codes
+// per bucket (blk_hist), so a block knows its final run for every bucket up
+// front and appends each flush's sorted segment to it: one directory row per
+// block, runs of items / Bc codes, padded once.
+__device__ __forceinline__ int64_t append_need(uint64_t items, int nb) {
+    return ((int64_t)items + (int64_t)nb * 7 + 7) / 8 * 8;
+}
+
+// Block barrier for LDS hand-offs only: outstanding global stores and loads are
+// not waited for (__syncthreads' release fence would drain vmcnt every flush).
+__device__ __forceinline__ void lds_barrier() {
+#ifdef KARMA_APPEND_FENCE
+    __syncthreads();
+#else
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+}
+
+template <int NB>
+__global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __restrict__ lists, int64_t list_cap,
+                                                           const uint32_t* __restrict__ list_n, int64_t n_lists,
+                                                           int per_block, Geo g, const uint32_t* __restrict__ blk_hist,
+                                                           uint16_t* __restrict__ out, uint16_t* trash, RunDir dir,
+                                                           int* err) {
+    using T = CodeStreamT<NB>;
+    // codes per flush: 34 KB (narrow) / 62 KB (wide) of LDS, 4 / 2 blocks per CU
+#ifndef KARMA_APPEND_WIDE_CAP
+#define KARMA_APPEND_WIDE_CAP 4096
+#endif
+    constexpr int kCap = NB > 128 ? KARMA_APPEND_WIDE_CAP : 4096;
+    constexpr int kPer = kCap / kPT;
+    constexpr int kVMax = kCap / 8 + NB;               // 16-byte vectors of one flush, at most
+    constexpr int kVPer = (kVMax + kPT - 1) / kPT;
+    __shared__ uint32_t buf[kCap];
+    // a flush's codes by bucket: bucket b's pending tail (< 8 codes from earlier
+    // flushes) then its new codes, from an 8-aligned start toff[b]
+    __shared__ __attribute__((aligned(16))) uint16_t s16[kCap + 8 * NB];
+    __shared__ __attribute__((aligned(16))) uint16_t pend[8 * NB];
+    __shared__ uint32_t hist[2][NB + 1];
+    __shared__ uint32_t toff[NB + 1];  // 8-aligned region starts in s16
+    __shared__ uint32_t qoff[NB + 1];  // full vectors before bucket b
+    __shared__ uint32_t cur[NB];
+    __shared__ uint32_t rb[NB + 1];    // the block's run starts in its slice (multiples of 8)
+    __shared__ uint32_t wr[NB];        // codes written to run b (multiple of 8)
+    __shared__ uint32_t pc[NB];        // pending codes of run b (< 8)
+    __shared__ uint32_t dlt[NB];       // slice position of s16[i] (bucket b) = dlt[b] + i
+    __shared__ uint16_t vb[kVMax];     // bucket of each full vector of the flush
+    __shared__ uint32_t lpre[kMaxListsPerBlock + 1];
+    __shared__ int64_t red_s[kPT / 64];
+    const int nb = g.Bc;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    {
+        int64_t so = 0;
+        for (int64_t b = threadIdx.x; b < (int64_t)blockIdx.x; b += kPT) so += append_need(dir.blk_items[b], nb);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) so += __shfl_xor(so, d);
+        if (lane == 0) red_s[wave] = so;
+        if (blockIdx.x == 0 && threadIdx.x == 0) *dir.n = gridDim.x;
+    }
+    const uint32_t* bh = blk_hist + (int64_t)blockIdx.x * nb;
+    for (int b = threadIdx.x; b <= nb; b += kPT) hist[0][b] = hist[1][b] = 0;
+    for (int b = threadIdx.x; b < nb; b += kPT) wr[b] = pc[b] = 0;
+    const int64_t l_lo = (int64_t)blockIdx.x * per_block;
+    const int nl = (int)min<int64_t>(per_block, n_lists - l_lo);
+    if (wave == 0) {
+        // run starts: exclusive scan of the padded per-bucket counts
+        uint32_t c2 = 0;
+        for (int b0 = 0; b0 < nb; b0 += 64) {
+            const uint32_t val = b0 + lane < nb ? (bh[b0 + lane] + 7u) & ~7u : 0u;
+            const uint32_t x = wave_scan_incl(val);
+            if (b0 + lane < nb) rb[b0 + lane] = c2 + x - val;
+            c2 += lane63(x);
+        }
+        if (lane == 0) rb[nb] = c2;
+    } else if (wave == 1) {
+        uint32_t carry = 0;
+        for (int base = 0; base < nl; base += 64) {
+            const uint32_t v = base + lane < nl ? list_n[l_lo + base + lane] : 0u;
+            const uint32_t x = wave_scan_incl(v);
+            if (base + lane < nl) lpre[base + lane] = carry + x - v;
+            carry += lane63(x);
+        }
+        for (int i = nl + lane; i <= kMaxListsPerBlock; i += 64) lpre[i] = carry;
+    }
+    __syncthreads();
+    int64_t out0 = 0;
+    for (int w = 0; w < kPT / 64; ++w) out0 += red_s[w];
+    if (threadIdx.x == 0) dir.base[blockIdx.x] = out0;
+    for (int b = threadIdx.x; b <= nb; b += kPT) dir.off[(int64_t)blockIdx.x * (nb + 1) + b] = rb[b];
+    const uint32_t items = lpre[nl];
+    u32x4* const vout = reinterpret_cast<u32x4*>(out + out0);  // out0 is a multiple of 8
+    u32x4* const vtrash = reinterpret_cast<u32x4*>(trash);
+    uint32_t v[kPer];
+    // Loads and stores of the flush loop are unconditional (clamped loads, stores
+    // past the end go to `trash`): the compiler then counts them exactly and the
+    // next fill waits for its loads only, not for the stores issued after them.
+    auto load = [&](uint32_t base) {
+        int lo = 0;
+        {
+            const uint32_t g0 = min(base + threadIdx.x, items - 1);
+#pragma unroll
+            for (int step = kMaxListsPerBlock / 2; step >= 1; step >>= 1)
+                if (lpre[lo + step] <= g0) lo += step;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t gi = min(base + threadIdx.x + k * kPT, items - 1);
+            while (lpre[lo + 1] <= gi) ++lo;
+            v[k] = lists[(l_lo + lo) * list_cap + (gi - lpre[lo])];
+        }
+    };
+    if (items > 0) load(0);
+    int parity = 0;
+    for (uint32_t base = 0; base < items; base += kCap, parity ^= 1) {
+        const uint32_t n = min(items - base, (uint32_t)kCap);
+        uint32_t* h = hist[parity];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kPT;
+            if (i < n) {
+                buf[i] = v[k];
+                atomicAdd(&h[T::bucket(v[k], g)], 1u);
+            }
+        }
+        load(base + kCap);
+        lds_barrier();
+        // bucket regions (pending + new, 8-aligned) and full-vector counts
+        for (int b = threadIdx.x; b < nb; b += kPT) cur[b] = 0;
+        if (wave == 0) {
+            uint32_t c8 = 0, cq = 0;
+            for (int b0 = 0; b0 < nb; b0 += 64) {
+                const uint32_t tot = b0 + lane < nb ? pc[b0 + lane] + h[b0 + lane] : 0u;
+                const uint32_t r8 = (tot + 7u) & ~7u, q = tot >> 3;
+                const uint32_t x = wave_scan_incl(r8), y = wave_scan_incl(q);
+                if (b0 + lane < nb) {
+                    toff[b0 + lane] = c8 + x - r8;
+                    qoff[b0 + lane] = cq + y - q;
+                }
+                c8 += lane63(x);
+                cq += lane63(y);
+            }
+            if (lane == 0) toff[nb] = c8, qoff[nb] = cq;
+        }
+        lds_barrier();
+        for (int b = threadIdx.x; b < nb; b += kPT) {
+            const uint32_t t = toff[b], p = pc[b];
+            // the pending tail: one 16-byte read, then only its p codes (new codes
+            // of this bucket land right behind them, concurrently)
+            if (p) {
+                const u32x4 pv = *reinterpret_cast<const u32x4*>(pend + 8 * b);
+                const uint32_t w[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 7; ++j)
+                    if (j < p) s16[t + j] = (uint16_t)(w[j >> 1] >> (16 * (j & 1)));
+            }
+            for (uint32_t q = qoff[b]; q < qoff[b + 1]; ++q) vb[q] = (uint16_t)b;
+            dlt[b] = rb[b] + wr[b] - t;
+        }
+        for (uint32_t i = threadIdx.x; i < n; i += kPT) {
+            const uint32_t x = buf[i];
+            const uint32_t b = T::bucket(x, g);
+            s16[toff[b] + pc[b] + atomicAdd(&cur[b], 1u)] = T::value(x, g);
+        }
+        lds_barrier();
+        // full vectors to the runs; the rest of each bucket becomes its pending tail
+        const uint32_t nv = qoff[nb];
+#pragma unroll
+        for (int k = 0; k < kVPer; ++k) {
+            const uint32_t t = threadIdx.x + k * kPT;
+            const uint32_t b = t < nv ? vb[t] : 0u;
+            const uint32_t si = t < nv ? toff[b] + 8u * (t - qoff[b]) : 0u;
+            const u32x4 val = *reinterpret_cast<const u32x4*>(s16 + si);
+            *(t < nv ? vout + ((dlt[b] + si) >> 3) : vtrash) = val;
+        }
+        for (int b = threadIdx.x; b < nb; b += kPT) {
+            const uint32_t tot = pc[b] + h[b], full = tot & ~7u, r = tot & 7u;
+            if (r) *reinterpret_cast<u32x4*>(pend + 8 * b) = *reinterpret_cast<const u32x4*>(s16 + toff[b] + full);
+            pc[b] = r;
+            wr[b] += full;
+            h[b] = 0;
+        }
+    }
+    lds_barrier();
+    // the runs' last vectors, padded; the counts must agree with the classify's
+    for (int b = threadIdx.x; b < nb; b += kPT) {
+        const uint32_t p = pc[b];
+        if (wr[b] + p != bh[b]) *err = 1;
+        if (p) {
+            for (uint32_t j = p; j < 8; ++j) pend[8 * b + j] = T::kPadV;
+            vout[(rb[b] + wr[b]) >> 3] = *reinterpret_cast<const u32x4*>(pend + 8 * b);
+        }
+    }
+}
+
 // ---- run streams ------------------------------------------------------------------
 // A reduce block reads the runs of one bucket from a range of flushes.  Each
 // wave takes batches of 64 runs (lane i holds run i) and reads them as one
@@ -657,12 +880,7 @@ __device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int6
         int64_t beg = 0;
         uint32_t len = 0;
         if (r < r_hi) bounds(r, &beg, &len);
-        uint32_t incl = len;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d);
-            if (lane >= d) incl += y;
-        }
+        const uint32_t incl = wave_scan_incl(len);
         const uint32_t excl = incl - len;
         const int64_t roff = beg - (int64_t)excl;  // vector j of run r: data[roff + j]
         const uint32_t Tn = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -714,16 +932,24 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
     __syncthreads();
     int64_t f_lo, f_hi;
     group_range(dir.n, n_cg, grp, &f_lo, &f_hi);
+    // rows hold one long run per bucket (code_append_kernel): split each into S
+    // pieces so that every wave has runs to stream
+    const int64_t R = f_hi - f_lo;
+    const int S = R > 0 ? (int)min<int64_t>(64, (2 * kCRT + R - 1) / R) : 1;
     bool stop = false;
     auto add = [&](uint32_t c) {
         if (c != CodeStream::kPadV) __hip_atomic_fetch_add(&h[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     stream_runs(
-        reinterpret_cast<const u32x4*>(cent), f_lo, f_hi, kCRT,
-        [&](int64_t f, int64_t* beg, uint32_t* len) {
+        reinterpret_cast<const u32x4*>(cent), f_lo * S, f_hi * S, kCRT,
+        [&](int64_t v, int64_t* beg, uint32_t* len) {
+            const int64_t f = v / S;
+            const uint32_t s = (uint32_t)(v - f * S);
             const uint32_t* o = dir.off + f * (Bc + 1) + bucket;
-            *beg = (dir.base[f] + o[0]) >> 3;
-            *len = (o[1] - o[0]) >> 3;
+            const uint32_t L = (o[1] - o[0]) >> 3, seg = (L + S - 1) / S;
+            const uint32_t lo = min(L, s * seg), hi = min(L, lo + seg);
+            *beg = ((dir.base[f] + o[0]) >> 3) + lo;
+            *len = hi - lo;
         },
         [&](const u32x4 v) {
             add(v.x & 0xFFFFu), add(v.x >> 16), add(v.y & 0xFFFFu), add(v.y >> 16);
@@ -884,20 +1110,24 @@ __device__ __forceinline__ uint32_t code_count(const uint32_t* __restrict__ part
 // Band pairs and hash pairs are disjoint (b - a < D vs >= D); a pair's output
 // position is its rank in its own sorted list plus the number of smaller keys
 // in the other one.
+// HF hash slots: one group's list (n_pg = 1, < kHashR keys) fits 4096, and the
+// block then takes 68 KB of LDS (2 blocks per CU for the many small buckets of
+// a large n_contigs); several groups' lists are merged in 8192.
+template <int HF>
 __global__ void __launch_bounds__(kFT) final_kernel(
     int n_pg, int n_cg, int bw, int bbits, int dbits, int bwc, const uint32_t* __restrict__ part_band,
     const uint32_t* __restrict__ part_ch, const uint32_t* __restrict__ part_keys,
     const uint32_t* __restrict__ part_cnt, const int* __restrict__ part_n, uint64_t* __restrict__ out_keys,
     int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n, uint8_t* __restrict__ overflow) {
     __shared__ uint32_t bsum[kBand];
-    __shared__ uint32_t bpos[kBand + 1];
-    __shared__ uint32_t hkeys[kHashF];
-    __shared__ uint32_t hvals[kHashF];
+    __shared__ uint32_t rowpos[(kBand >> 3) + 1];  // nonzero band slots before row a_local (D = 8 on this path)
+    __shared__ uint32_t hkeys[HF];
+    __shared__ uint32_t hvals[HF];
     __shared__ uint32_t wsum[kFT / 64];
     __shared__ int nuniq, cnt;
     const int bucket = blockIdx.x;
     if (overflow[bucket]) return;  // generic path
-    HTab<kHashF, kFT> t{hkeys, hvals, &nuniq};
+    HTab<HF, kFT> t{hkeys, hvals, &nuniq};
     const int band_n = dbits >= 0 ? (1 << (bw + dbits)) : 0;
     t.init();
     for (int i = threadIdx.x; i < band_n; i += kFT) {
@@ -949,51 +1179,54 @@ __global__ void __launch_bounds__(kFT) final_kernel(
     }
     __syncthreads();
     if (nh > 1) lds_bitonic(hkeys, hvals, p2);
-    // exclusive scan of the band's nonzero flags (consecutive slots per thread)
-    const int per = (band_n + kFT - 1) / kFT;
-    const int i0 = threadIdx.x * per;
-    uint32_t mine = 0;
-    for (int i = i0; i < min(band_n, i0 + per); ++i) mine += bsum[i] != 0;
+    // band output positions: wave w takes a segment of the band, lane l the
+    // slots seg + l + 64k (coalesced stores); a slot's rank among the nonzero
+    // slots comes from ballots, the segments' bases from their totals
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t x = mine;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
+    const int seg_len = max(64, band_n / (kFT / 64));
+    const int seg0 = wave * seg_len, seg1 = min(band_n, seg0 + seg_len);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    {
+        uint32_t nz = 0;
+        for (int e0 = seg0; e0 < seg1; e0 += 64) nz += (uint32_t)__popcll(__ballot(bsum[e0 + lane] != 0));
+        if (lane == 0) wsum[wave] = nz;
     }
-    if (lane == 63) wsum[wave] = x;
     __syncthreads();
-    uint32_t wb = 0;
-    for (int w = 0; w < wave; ++w) wb += wsum[w];
-    uint32_t run = wb + x - mine;
-    for (int i = i0; i < min(band_n, i0 + per); ++i) {
-        bpos[i] = run;
-        run += bsum[i] != 0;
+    uint32_t run = 0, nb = 0;
+    for (int w = 0; w < kFT / 64; ++w) {
+        const uint32_t c = wsum[w];
+        run += w < wave ? c : 0u;
+        nb += c;
     }
-    if (threadIdx.x == kFT - 1) bpos[band_n] = run;
-    __syncthreads();
-    const uint32_t nb = bpos[band_n];
     const uint32_t bmask = (1u << bbits) - 1u;
     const uint64_t abase = (uint64_t)bucket << bw;
     uint64_t* ok = out_keys + (int64_t)bucket * kSlotCap;
     int64_t* oc = out_counts + (int64_t)bucket * kSlotCap;
-    for (int i = threadIdx.x; i < band_n; i += kFT) {
-        if (!bsum[i]) continue;
-        const uint32_t al = (uint32_t)i >> dbits, b = (uint32_t)abase + al + ((uint32_t)i & ((1u << dbits) - 1u));
-        const uint32_t key = (al << bbits) | b;
-        int lo = 0, hi = nh;  // hash keys below key
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (hkeys[mid] < key) lo = mid + 1;
-            else hi = mid;
+    for (int e0 = seg0; e0 < seg1; e0 += 64) {
+        const int i = e0 + lane;
+        const uint32_t c = bsum[i];
+        const unsigned long long m = __ballot(c != 0);
+        const uint32_t at = run + (uint32_t)__popcll(m & lt);  // nonzero slots before i
+        if ((i & ((1 << dbits) - 1)) == 0) rowpos[i >> dbits] = at;
+        if (c) {
+            const uint32_t al = (uint32_t)i >> dbits, b = (uint32_t)abase + al + ((uint32_t)i & ((1u << dbits) - 1u));
+            const uint32_t key = (al << bbits) | b;
+            int lo = 0, hi = nh;  // hash keys below key
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (hkeys[mid] < key) lo = mid + 1;
+                else hi = mid;
+            }
+            ok[at + lo] = ((abase + al) << 32) | b;
+            oc[at + lo] = c;
         }
-        const uint32_t pos = bpos[i] + lo;
-        ok[pos] = ((abase + al) << 32) | b;
-        oc[pos] = bsum[i];
+        run += (uint32_t)__popcll(m);
     }
+    if (threadIdx.x == 0 && band_n) rowpos[band_n >> dbits] = nb;
+    __syncthreads();
     for (int j = threadIdx.x; j < nh; j += kFT) {
         const uint32_t k = hkeys[j], al = k >> bbits;
-        const uint32_t below = band_n ? bpos[min((int)((al + 1) << dbits), band_n)] : 0u;
+        const uint32_t below = band_n ? rowpos[min((int)(al + 1), band_n >> dbits)] : 0u;
         const uint32_t pos = j + below;
         ok[pos] = ((abase + al) << 32) | (k & bmask);
         oc[pos] = hvals[j];
@@ -1204,7 +1437,8 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
         if (A > 0) {
             ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
-                        n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags};
+                        n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags,
+                        nullptr,   0,         0};
             KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
@@ -1246,10 +1480,14 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     const int64_t n_chunks = std::max<int64_t>(1, ceil_div(A, kCChunk));
     // partition: one round of resident blocks, each taking consecutive chunk lists
     const bool wide_c = g.Bc > kNarrowBc, wide_p = B > kNarrowB;
-    const int resident = resident_grid(ctx,
-                                       wide_c ? reinterpret_cast<const void*>(&partition_kernel<CodeStreamWide>)
-                                              : reinterpret_cast<const void*>(&partition_kernel<CodeStream>),
-                                       kPT, 0, int64_t(1) << 30);
+    // code partition: per-flush padded runs while a flush's runs are long (few
+    // code buckets); one appended run per (block, bucket) beyond that
+    const bool append = g.Bc >= KARMA_APPEND_MIN_BC;
+    const void* code_part = append ? (wide_c ? reinterpret_cast<const void*>(&code_append_kernel<kMaxBc>)
+                                             : reinterpret_cast<const void*>(&code_append_kernel<kNarrowBc>))
+                                   : (wide_c ? reinterpret_cast<const void*>(&partition_kernel<CodeStreamWide>)
+                                             : reinterpret_cast<const void*>(&partition_kernel<CodeStream>));
+    const int resident = resident_grid(ctx, code_part, kPT, 0, int64_t(1) << 30);
     const int lpb = (int)std::min<int64_t>(kMaxListsPerBlock, ceil_div(n_chunks, resident));
     const int64_t n_pblk = ceil_div(n_chunks, lpb);
     // per-step scratch
@@ -1283,6 +1521,8 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     DevArray<uint32_t> cf_off;
     DevArray<unsigned long long> blk_items;       // per partition block: codes, pairs
     KARMA_TRY(blk_items.alloc(ctx, 2 * n_pblk));
+    DevArray<uint32_t> blk_hist;                  // per partition block: codes per code bucket (append)
+    if (append) KARMA_TRY(blk_hist.alloc(ctx, n_pblk * g.Bc));
     if (g.Bc > 0) {
         KARMA_TRY(cent.alloc(ctx, ccap + 16));
         KARMA_TRY(cf_base.alloc(ctx, max_cflush));
@@ -1325,9 +1565,11 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
         KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, ctrl_words * 8, ctx->stream));
         KARMA_HIP(hipMemsetAsync(blk_items.ptr, 0, 2 * n_pblk * 8, ctx->stream));
+        if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
         if (A > 0) {
             ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
-                        n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags};
+                        n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags,
+                        append ? blk_hist.ptr : nullptr, g.bwc, g.Bc};
             KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         } else {
             KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
@@ -1338,7 +1580,14 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items.ptr};
         pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items.ptr + n_pblk};
         if (g.Bc > 0) {
-            if (wide_c)
+            uint16_t* const trash = cent.ptr + (ccap + 7) / 8 * 8;
+            if (append && wide_c)
+                KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kMaxBc>, n_pblk, kPT, 0, codes.ptr,
+                             kCChunk, n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
+            else if (append)
+                KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kNarrowBc>, n_pblk, kPT, 0, codes.ptr,
+                             kCChunk, n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
+            else if (wide_c)
                 KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStreamWide>, n_pblk, kPT, 0, codes.ptr,
                              kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
             else
@@ -1355,9 +1604,14 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
                          n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
         KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
                      g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
-        KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits, g.bwc,
-                     part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
-                     ovf);
+        if (n_pg == 1)
+            KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashR>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits,
+                         g.dbits, g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr,
+                         slot_c.ptr, n_per, ovf);
+        else
+            KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashF>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits,
+                         g.dbits, g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr,
+                         slot_c.ptr, n_per, ovf);
         KARMA_TRY(scan_excl_i64(ctx, n_per, dst, B + 1));
         // the one synchronisation of the common path
         KARMA_HIP(hipMemcpyAsync(hpin, ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1368,6 +1622,7 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         U = hctrl[6 + (B + 1) + B];
         KARMA_CHECK(!hf[0], KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
         KARMA_CHECK(!hf[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
+        KARMA_CHECK(!hf[3], KARMA_ERR_STATE, "code partition: block counts disagree with the classify histogram");
         if (!hf[2]) break;
         KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "pair list capacity exceeded twice");
         pcap = kCChunk * 9 / 2;  // every read with <= 8 records fits

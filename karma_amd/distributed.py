@@ -145,9 +145,10 @@ class Comm:
         return t
 
     def alltoallv(self, t, send_counts):
-        """1-D all-to-all-v: send_counts[r] consecutive elements go to rank r."""
+        """1-D all-to-all-v: send_counts[r] consecutive elements go to rank r.
+        Returns (received, recv_counts): recv_counts[r] elements came from rank r."""
         if not self.dist:
-            return t
+            return t, [int(x) for x in send_counts]
         import torch
 
         dev = t.device
@@ -159,7 +160,7 @@ class Comm:
         out = torch.empty(sum(recv_counts), dtype=t.dtype, device=t.device)
         self.dist.all_to_all_single(out, t, output_split_sizes=recv_counts,
                                     input_split_sizes=[int(x) for x in send_counts])
-        return out.to(dev)
+        return out.to(dev), recv_counts
 
     def close(self):
         if self.dist and self.dist.is_initialized():
@@ -257,9 +258,11 @@ class HipOps:
                  None, 1)
         return keys[:n], counts[:n], starts
 
-    def merge(self, keys, counts):
+    def merge(self, keys, counts, runs):
+        """The owner's list from the senders' slices (runs: their lengths, each sorted)."""
         return self.engine.Pairs.merge(self.ctx, keys.data_ptr() if keys.numel() else None,
-                                       counts.data_ptr() if counts.numel() else None, device=True, n=keys.numel())
+                                       counts.data_ptr() if counts.numel() else None, device=True, n=keys.numel(),
+                                       runs=runs)
 
     def totals(self, pairs, n_contigs):
         tot = self.torch.zeros(n_contigs, dtype=self.torch.int64, device=self.dev)
@@ -292,8 +295,12 @@ class HipOps:
 class ShardedBuild:
     """k-mer profile + shared-read graph over contig/fragment shards."""
 
-    def __init__(self, ctx, comm: Comm, kmode, n_glob, c_lo, n_loc, ops=None, overlap=None):
+    def __init__(self, ctx, comm: Comm, kmode, n_glob, c_lo, n_loc, ops=None, overlap=None, emulate_ranks=1):
         self.comm, self.kmode, self.n_glob, self.c_lo, self.n_loc = comm, kmode, n_glob, c_lo, n_loc
+        # one process standing in for a rank of a W-rank job (bench.py
+        # --emulate-ranks W): the exchange's local work runs -- split at the W
+        # owners' bounds, merge of W sorted slices, totals -- its collectives do not
+        self.emulate = emulate_ranks if comm.world == 1 and emulate_ranks > 1 else 0
         self.ops = ops if ops is not None else HipOps(ctx)
         self._prof = None
         # The local graph build (records -> pair list) shares nothing with the
@@ -358,13 +365,19 @@ class ShardedBuild:
         if keep:
             stats["entries"] = ops.entries(local)
             stats["pairs_local"] = ops.pair_count(local)
-        if comm.world > 1:
-            keys, counts, starts = ops.pairs_split(local, self.bounds)
-            send = np.diff(starts)
-            # one all-to-all-v of interleaved (key, count) int64 pairs
-            import torch
-            kc = comm.alltoallv(torch.stack([keys, counts], 1).reshape(-1), 2 * send).reshape(-1, 2)
-            merged = ops.merge(kc[:, 0].contiguous(), kc[:, 1].contiguous())
+        if comm.world > 1 or self.emulate:
+            if comm.world > 1:
+                keys, counts, starts = ops.pairs_split(local, self.bounds)
+                # one all-to-all-v of interleaved (key, count) int64 pairs; the
+                # owner receives one sorted slice per sender and merges them
+                import torch
+                kc, recv = comm.alltoallv(torch.stack([keys, counts], 1).reshape(-1), 2 * np.diff(starts))
+                kc = kc.reshape(-1, 2)
+                merged = ops.merge(kc[:, 0].contiguous(), kc[:, 1].contiguous(), [r // 2 for r in recv])
+            else:  # emulation: this rank's own W slices stand in for the W received ones
+                keys, counts, starts = ops.pairs_split(local, np.linspace(0, self.n_glob, self.emulate + 1)
+                                                       .astype(np.int64))
+                merged = ops.merge(keys, counts, np.diff(starts).tolist())
             # the owner's merged list holds the diagonal (a, a) of every a it owns:
             # complete readset sizes for its slice, gathered to every rank
             tot = comm.allgather_slices_(ops.totals(merged, self.n_glob), self.bounds)

@@ -217,8 +217,24 @@ class Pairs:
         return cls(ctx, h)
 
     @classmethod
-    def merge(cls, ctx, keys, counts, device=False, n=None):
+    def merge(cls, ctx, keys, counts, device=False, n=None, runs=None):
+        """Sorted unique (key, count) list.  runs = lengths of consecutive runs that
+        are each sorted by key (an exchange owner's received slices): merged by a
+        merge tree instead of a full sort."""
         h = ctypes.c_void_p()
+        if runs is not None:
+            off = np.zeros(len(runs) + 1, np.int64)
+            np.cumsum(np.asarray(runs, np.int64), out=off[1:])
+            if device:
+                assert n is None or n == off[-1], "run lengths do not add up to n"
+                call("karma_pairs_merge_runs", ctx.h, ctypes.c_void_p(keys) if keys else None,
+                     ctypes.c_void_p(counts) if counts else None, ptr(off), len(runs), 1, ctypes.byref(h))
+            else:
+                keys = np.ascontiguousarray(keys, np.uint64)
+                counts = np.ascontiguousarray(counts, np.int64)
+                call("karma_pairs_merge_runs", ctx.h, ptr(keys) if len(keys) else None,
+                     ptr(counts) if len(counts) else None, ptr(off), len(runs), 0, ctypes.byref(h))
+            return cls(ctx, h)
         if device:
             call("karma_pairs_merge", ctx.h, ctypes.c_void_p(keys) if keys else None,
                  ctypes.c_void_p(counts) if counts else None, n, 1, ctypes.byref(h))

@@ -140,8 +140,12 @@ class OracleOps:
         return (torch.from_numpy(pairs["keys"].view(np.int64).copy()), torch.from_numpy(pairs["counts"].copy()),
                 starts)
 
-    def merge(self, keys, counts):
+    def merge(self, keys, counts, runs):
         k = keys.numpy().view(np.uint64)
+        # the contract of karma_pairs_merge_runs: one sorted slice per sender
+        off = np.r_[0, np.cumsum(runs)]
+        assert off[-1] == len(k) and all(np.all(k[off[r] + 1:off[r + 1]] >= k[off[r]:off[r + 1] - 1])
+                                         for r in range(len(runs)))
         u, inv = np.unique(k, return_inverse=True)
         c = np.zeros(len(u), np.int64)
         np.add.at(c, inv, counts.numpy())

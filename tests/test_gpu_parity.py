@@ -321,3 +321,40 @@ def test_profile_presence_two_phase(kmer, n_rate):
     assert cols == ocols
     assert np.array_equal(prof.view(np.uint64), oprof.view(np.uint64))
     assert np.array_equal(tot, ocounts.sum(axis=1))
+
+
+@pytest.mark.parametrize("seed,n_runs,n", [(61, 8, 2_000_000), (62, 3, 5000), (63, 1, 17), (64, 5, 0),
+                                           (65, 2, 1)])
+def test_merge_runs_and_split(seed, n_runs, n):
+    # the exchange owner's merge of sorted per-sender slices
+    # (karma_pairs_merge_runs: merge tree + sum of equal keys) equals numpy and
+    # the generic sort-reduce; split finds rank boundaries on the device
+    rng = np.random.default_rng(seed)
+    n_contigs = 1_600_000
+    cuts = np.sort(rng.integers(0, n + 1, n_runs - 1))
+    lens = np.diff(np.r_[0, cuts, n]).astype(np.int64)
+    a = rng.integers(200_000, 400_000, n, dtype=np.uint64)
+    b = rng.integers(0, n_contigs, n, dtype=np.uint64)
+    keys = (a << np.uint64(32)) | b
+    keys[: n // 4] = keys[n // 2: n // 2 + n // 4]  # equal keys, in several runs
+    off = np.r_[0, np.cumsum(lens)]
+    for r in range(n_runs):  # each sender's slice is sorted; it may repeat a key
+        keys[off[r]:off[r + 1]] = np.sort(keys[off[r]:off[r + 1]])
+    counts = rng.integers(1, 1 << 40, n, dtype=np.int64)
+    ctx = _lib.default_context()
+    u, inv = np.unique(keys, return_inverse=True)
+    c = np.zeros(len(u), np.int64)
+    np.add.at(c, inv, counts)
+    for runs in (lens.tolist(), None):
+        p = engine.Pairs.merge(ctx, keys, counts, runs=runs)
+        k2, c2, _ = p.get()
+        assert np.array_equal(k2, u) and np.array_equal(c2, c)
+        bounds = [0, 200_000, 300_000, 400_000, n_contigs]
+        assert np.array_equal(p.split(bounds), np.searchsorted(u, np.array(bounds, np.uint64) << np.uint64(32)))
+        p.close()
+    if n > 1 and lens.max() > 1:
+        r = int(np.argmax(lens))
+        bad = keys.copy()
+        bad[off[r]], bad[off[r] + 1] = keys[off[r] + 1] + np.uint64(1), keys[off[r]]  # a descent inside a run
+        with pytest.raises(_lib.KarmaError):
+            engine.Pairs.merge(ctx, bad, counts, runs=lens.tolist())
