@@ -611,16 +611,19 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
     };
     load(0);
     int parity = 0;
+    // a thread scatters the items it counted (its own slots of the fill),
+    // staged in LDS across the flush's barriers while v takes the next
+    // fill's loads (held in registers instead: 104 VGPRs, 2 blocks per CU,
+    // measured slower)
+#define PART_ITEM(k) buf[threadIdx.x + (k) * kPT]
     for (uint32_t base = 0; base < items; base += T::kCap, parity ^= 1) {
         const uint32_t n = min(items - base, (uint32_t)T::kCap);
         uint32_t* h = hist[parity];
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const uint32_t i = threadIdx.x + k * kPT;
-            if (i < n) {
-                buf[i] = v[k];
-                atomicAdd(&h[T::bucket(v[k], g)], 1u);
-            }
+            PART_ITEM(k) = v[k];
+            if (i < n) atomicAdd(&h[T::bucket(v[k], g)], 1u);
         }
         load(base + T::kCap);  // the next fill's loads overlap this flush
         // ---- flush: counting sort of buf by bucket into padded runs ----
@@ -648,14 +651,18 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
             for (int b = threadIdx.x; b <= nb; b += kPT) dir.off[(int64_t)f * (nb + 1) + b] = toff[b];
             for (int b = threadIdx.x; b < nb; b += kPT)
                 for (uint32_t i = toff[b] + h[b]; i < toff[b + 1]; ++i) sorted[i] = T::kPadV;
-            for (uint32_t i = threadIdx.x; i < n; i += kPT) {
-                const S x = buf[i];
-                const uint32_t b = T::bucket(x, g);
-                sorted[toff[b] + atomicAdd(&cur[b], 1u)] = T::value(x, g);
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                if (threadIdx.x + k * kPT < n) {
+                    const S it = PART_ITEM(k);
+                    const uint32_t b = T::bucket(it, g);
+                    sorted[toff[b] + atomicAdd(&cur[b], 1u)] = T::value(it, g);
+                }
             }
+#undef PART_ITEM
         }
         __syncthreads();
-        // buf, h and cur are free: the next fill may start once this block's
+        // h and cur are free: the next fill may start once this block's
         // 16-byte stores are issued (their completion is never waited for)
         for (int b = threadIdx.x; b < nb; b += kPT) h[b] = 0;
         u32x4* dst = reinterpret_cast<u32x4*>(out + at);
@@ -702,7 +709,6 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
     constexpr int kPer = kCap / kPT;
     constexpr int kVMax = kCap / 8 + NB;               // 16-byte vectors of one flush, at most
     constexpr int kVPer = (kVMax + kPT - 1) / kPT;
-    __shared__ uint32_t buf[kCap];
     // a flush's codes by bucket: bucket b's pending tail (< 8 codes from earlier
     // flushes) then its new codes, from an 8-aligned start toff[b]
     __shared__ __attribute__((aligned(16))) uint16_t s16[kCap + 8 * NB];
@@ -782,16 +788,15 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
     };
     if (items > 0) load(0);
     int parity = 0;
+    uint32_t x[kPer];  // this thread's items of the flush (it scatters what it counted)
     for (uint32_t base = 0; base < items; base += kCap, parity ^= 1) {
         const uint32_t n = min(items - base, (uint32_t)kCap);
         uint32_t* h = hist[parity];
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const uint32_t i = threadIdx.x + k * kPT;
-            if (i < n) {
-                buf[i] = v[k];
-                atomicAdd(&h[T::bucket(v[k], g)], 1u);
-            }
+            x[k] = v[k];
+            if (i < n) atomicAdd(&h[T::bucket(x[k], g)], 1u);
         }
         load(base + kCap);
         lds_barrier();
@@ -802,13 +807,13 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
             for (int b0 = 0; b0 < nb; b0 += 64) {
                 const uint32_t tot = b0 + lane < nb ? pc[b0 + lane] + h[b0 + lane] : 0u;
                 const uint32_t r8 = (tot + 7u) & ~7u, q = tot >> 3;
-                const uint32_t x = wave_scan_incl(r8), y = wave_scan_incl(q);
+                const uint32_t sx = wave_scan_incl(r8), sy = wave_scan_incl(q);
                 if (b0 + lane < nb) {
-                    toff[b0 + lane] = c8 + x - r8;
-                    qoff[b0 + lane] = cq + y - q;
+                    toff[b0 + lane] = c8 + sx - r8;
+                    qoff[b0 + lane] = cq + sy - q;
                 }
-                c8 += lane63(x);
-                cq += lane63(y);
+                c8 += lane63(sx);
+                cq += lane63(sy);
             }
             if (lane == 0) toff[nb] = c8, qoff[nb] = cq;
         }
@@ -827,10 +832,12 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
             for (uint32_t q = qoff[b]; q < qoff[b + 1]; ++q) vb[q] = (uint16_t)b;
             dlt[b] = rb[b] + wr[b] - t;
         }
-        for (uint32_t i = threadIdx.x; i < n; i += kPT) {
-            const uint32_t x = buf[i];
-            const uint32_t b = T::bucket(x, g);
-            s16[toff[b] + pc[b] + atomicAdd(&cur[b], 1u)] = T::value(x, g);
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            if (threadIdx.x + k * kPT < n) {
+                const uint32_t b = T::bucket(x[k], g);
+                s16[toff[b] + pc[b] + atomicAdd(&cur[b], 1u)] = T::value(x[k], g);
+            }
         }
         lds_barrier();
         // full vectors to the runs; the rest of each bucket becomes its pending tail
