@@ -15,7 +15,8 @@
  *                                   + Contig readsets                    karma/contig.py:4-35
  *                                   and ReadGraph.update_graph           karma/read_graph.py:192-221
  *   karma_graph_eq                  ReadGraph.from_equivalence_classes   karma/read_graph.py:61-148
- *   karma_pairs_merge / _totals     (new) multi-GPU edge merge, SURVEY.md §8(e)
+ *   karma_pairs_merge{,_runs} /     (new) multi-GPU edge merge, SURVEY.md §8(e)
+ *   _split / _totals
  *   karma_edges_*                   the normalised weight (s/|A| + s/|B|)/2  read_graph.py:39-42, :128-130
  *   karma_synth_*                   (new) deterministic synthetic inputs, SURVEY.md §8(d)
  *   karma_fasta_*                   read_fasta_file                      karma/karma.py:40-61
