@@ -115,6 +115,14 @@ int karma_kmer_columns(karma_kmer_plan* p, uint64_t* keys_host);
 /* Dense float64 profile, row r = contig r of the store, stride ld >= M:
  * out[r*ld + col] = count / key_len[r] (kmer.py:120, :231-233), zeros written. */
 int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_device);
+/* karma_kmer_profile into device memory, launched on `side` (a hipStream_t)
+ * after everything already enqueued on the context's stream, so it overlaps
+ * whatever the caller enqueues next on that stream.  Call karma_ctx_join
+ * before the plan or the output are used or destroyed.  side = NULL: the
+ * context's stream. */
+int karma_kmer_profile_side(karma_kmer_plan* plan, double* out_dev, int64_t ld, void* side);
+/* The context's stream waits (on the device) for the work enqueued on `side`. */
+int karma_ctx_join(karma_ctx* ctx, void* side);
 /* Number of k-mer occurrences per contig (0 => the all-zero row of kmer.py:250-258). */
 int karma_kmer_row_totals(karma_kmer_plan* p, int64_t* dst_host);
 
@@ -130,6 +138,15 @@ typedef struct karma_pairs karma_pairs;
  * (a, b) counts |R_a ∩ R_b| (read_graph.py:34). */
 int karma_graph_records(karma_ctx* ctx, const uint32_t* records, int64_t n_records, int64_t n_contigs, int flags,
                         int is_device, karma_pairs** out);
+/* karma_graph_records in two halves.  _begin enqueues the pipeline up to its
+ * one host synchronisation and returns; the caller may enqueue other work (on
+ * another stream) before _end waits, checks and assembles the list.  Device
+ * records must stay valid until _end.  One open job per context; _end always
+ * consumes the job (also on error). */
+typedef struct karma_graph_job karma_graph_job;
+int karma_graph_records_begin(karma_ctx* ctx, const uint32_t* records, int64_t n_records, int64_t n_contigs,
+                              int flags, int is_device, karma_graph_job** job);
+int karma_graph_records_end(karma_graph_job* job, karma_pairs** out);
 /* Salmon eq classes (read_graph.py:75-114): cls_off[n_classes+1] into members
  * (contig indices as listed, duplicates kept), counts[n_classes], pair_skip[c]=1
  * when the eq_size token is "1" (read_graph.py:102).  Totals (read_graph.py:86-92)
@@ -154,6 +171,8 @@ int karma_pairs_rebind(karma_pairs* p, karma_ctx* ctx);
 int karma_pairs_count(karma_pairs* p, int64_t* n);
 /* Device pointers of the list (valid until destroy): keys u64[n], counts i64[n]. */
 int karma_pairs_device(karma_pairs* p, const uint64_t** keys, const int64_t** counts);
+/* Copy the list out.  Host copies (is_device = 0) have completed on return;
+ * device copies (is_device = 1) are ordered on p's stream and not waited for. */
 int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* first, int is_device);
 /* Index of the first key with a >= bounds[r] for r = 0..nranks (host out; searched on the device). */
 int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts);

@@ -68,8 +68,12 @@ _SIGS = {
     "karma_kmer_plan_finalize": [_c_p, _I64P],
     "karma_kmer_columns": [_c_p, _c_p],
     "karma_kmer_profile": [_c_p, _c_p, _i64, _i32],
+    "karma_kmer_profile_side": [_c_p, _c_p, _i64, _c_p],
+    "karma_ctx_join": [_c_p, _c_p],
     "karma_kmer_row_totals": [_c_p, _c_p],
     "karma_graph_records": [_c_p, _c_p, _i64, _i64, _i32, _i32, _PP],
+    "karma_graph_records_begin": [_c_p, _c_p, _i64, _i64, _i32, _i32, _PP],
+    "karma_graph_records_end": [_c_p, _PP],
     "karma_graph_eq": [_c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i64, _i32, _PP],
     "karma_pairs_merge": [_c_p, _c_p, _c_p, _i64, _i32, _PP],
     "karma_pairs_merge_runs": [_c_p, _c_p, _c_p, _c_p, _i32, _i32, _PP],
@@ -188,6 +192,10 @@ class Context:
 
     def sync(self):
         call("karma_ctx_sync", self.h)
+
+    def join(self, side_stream_ptr):
+        """This context's stream waits (on the device) for work on a side stream."""
+        call("karma_ctx_join", self.h, ctypes.c_void_p(side_stream_ptr))
 
     def timing(self, on=True, only=None):
         """Per-kernel HIP-event timing; `only` restricts it to one kernel name."""

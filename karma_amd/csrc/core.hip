@@ -87,10 +87,24 @@ void timing_stop(karma_ctx* ctx, hipEvent_t ev_stop) {
     if (ev_stop) hipEventRecord(ev_stop, ctx->stream);
 }
 
+int ctx_job_pinned(karma_ctx* ctx, size_t bytes, void** out) {
+    if (ctx->job_pinned_bytes < bytes) {
+        if (ctx->job_pinned) KARMA_HIP(hipHostFree(ctx->job_pinned));
+        ctx->job_pinned = nullptr;
+        ctx->job_pinned_bytes = 0;
+        const size_t want = std::max<size_t>(bytes, 64 * 1024);
+        KARMA_HIP(hipHostMalloc(&ctx->job_pinned, want, hipHostMallocDefault));
+        ctx->job_pinned_bytes = want;
+    }
+    *out = ctx->job_pinned;
+    return KARMA_OK;
+}
+
 int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int64_t work) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
+    per_cu = std::max(1, per_cu - ctx->grid_headroom);
     return (int)std::max<int64_t>(1, std::min<int64_t>(work, (int64_t)per_cu * ctx->cu_count));
 }
 
@@ -167,6 +181,8 @@ int karma_ctx_destroy(karma_ctx* ctx) {
     for (auto e : ctx->event_pool) hipEventDestroy(e);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
     if (ctx->pinned) hipHostFree(ctx->pinned);
+    if (ctx->job_pinned) hipHostFree(ctx->job_pinned);
+    if (ctx->side_ev) hipEventDestroy(ctx->side_ev);
     delete ctx;
     return KARMA_OK;
 }

@@ -281,17 +281,26 @@ int sort_reduce_pairs(karma_ctx* ctx, const uint64_t* keys_in, const int64_t* co
         KARMA_TRY(first_out->alloc(ctx, U));
         KARMA_HIP(hipMemcpyAsync(first_out->ptr, uf.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
     }
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    *n_out = U;
+    *n_out = U;  // the copies are stream-ordered; temporaries return to the stream's free list
     return KARMA_OK;
 }
 
 }  // namespace karma
 
+struct karma_graph_job {
+    karma_pairs* p = nullptr;
+    karma::DevArray<uint2> own;      // copied / read-sorted records, read by the kernels until _end
+    karma::SetsJob* sets = nullptr;  // open compact-path call (null: p already complete)
+    ~karma_graph_job() {
+        if (sets) karma::sets_free(sets);
+        delete p;
+    }
+};
+
 extern "C" {
 
-int karma_graph_records(karma_ctx* ctx, const uint32_t* records, int64_t A, int64_t N, int flags, int is_device,
-                        karma_pairs** out) {
+int karma_graph_records_begin(karma_ctx* ctx, const uint32_t* records, int64_t A, int64_t N, int flags, int is_device,
+                              karma_graph_job** out) {
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(out && (records || A == 0) && A >= 0, KARMA_ERR_ARG, "karma_graph_records: bad arguments");
     KARMA_CHECK(A < (int64_t(1) << 40), KARMA_ERR_ARG, "too many records");
@@ -342,13 +351,46 @@ int karma_graph_records(karma_ctx* ctx, const uint32_t* records, int64_t A, int6
             rec = own.ptr;
         }
     }
-    rc = records_to_pairs_sets(ctx, rec, A, N, p);
+    auto* job = new karma_graph_job();
+    job->p = p;
+    job->own.swap(own);
+    if (N > sets_max_contigs()) {  // wide path: runs to completion here
+        rc = records_to_pairs_sets(ctx, rec, A, N, p);
+    } else {
+        rc = sets_begin(ctx, rec, A, N, &job->sets);
+    }
     if (rc) {
-        delete p;
+        delete job;
         return rc;
     }
-    *out = p;
+    *out = job;
     return KARMA_OK;
+}
+
+int karma_graph_records_end(karma_graph_job* job, karma_pairs** out) {
+    KARMA_CHECK(job && out, KARMA_ERR_ARG, "karma_graph_records_end: null argument");
+    KARMA_TRY(ctx_begin(job->p->ctx));
+    int rc = KARMA_OK;
+    if (job->sets) {
+        SetsJob* sj = job->sets;
+        job->sets = nullptr;
+        rc = sets_end(sj, job->p);
+    }
+    if (rc) {
+        delete job;
+        return rc;
+    }
+    *out = job->p;
+    job->p = nullptr;
+    delete job;
+    return KARMA_OK;
+}
+
+int karma_graph_records(karma_ctx* ctx, const uint32_t* records, int64_t A, int64_t N, int flags, int is_device,
+                        karma_pairs** out) {
+    karma_graph_job* job = nullptr;
+    KARMA_TRY(karma_graph_records_begin(ctx, records, A, N, flags, is_device, &job));
+    return karma_graph_records_end(job, out);
 }
 
 int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
@@ -587,7 +629,7 @@ int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* f
         if (counts) KARMA_HIP(hipMemcpyAsync(counts, p->counts.ptr, p->n * 8, kind, p->ctx->stream));
         if (first && p->has_first) KARMA_HIP(hipMemcpyAsync(first, p->first.ptr, p->n * 8, kind, p->ctx->stream));
     }
-    KARMA_HIP(hipStreamSynchronize(p->ctx->stream));
+    if (!is_device) KARMA_HIP(hipStreamSynchronize(p->ctx->stream));  // device copies stay stream-ordered
     return KARMA_OK;
 }
 

@@ -1356,10 +1356,12 @@ int finish_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, const i
                  DevArray<uint64_t>& mk, DevArray<int64_t>& mc, int64_t U, karma_pairs* out) {
     out->n_contigs = N;
     if (n_big == 0) {
+        // no synchronisation: later work on this stream is ordered after the
+        // assemble kernel, host reads synchronise, and the records were last
+        // read before the control-block read
         out->keys.swap(mk);
         out->counts.swap(mc);
         out->n = U;
-        KARMA_HIP(hipStreamSynchronize(ctx->stream));
         return KARMA_OK;
     }
     DevArray<unsigned long long> np;
@@ -1479,80 +1481,107 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
 }
 
 // Records (grouped by read, 16-byte aligned) -> sorted unique (a<<32|b, count).
-int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
-    if (N > kMaxCompactN) return records_to_pairs_wide(ctx, rec, A, N, out);
-    Geo g;
+// One compact-path graph call, split at its only common-path synchronisation:
+// begin() sizes the scratch and enqueues classify .. final plus the control
+// block readback; end() waits, checks, reruns on a full pair list, and
+// assembles.  Between the two the host may enqueue unrelated work (the k-mer
+// profile on a side stream).
+struct SetsJob {
+    karma_ctx* ctx = nullptr;
+    const uint2* rec = nullptr;
+    int64_t A = 0, N = 0;
+    Geo g{};
+    int B = 0;
+    int64_t n_chunks = 0;
+    bool wide_c = false, wide_p = false, append = false;
+    int lpb = 0;
+    int64_t n_pblk = 0;
+    DevArray<uint32_t> codes, n_codes, n_gen, n_pl;
+    DevArray<int64_t> big_list;
+    // control block, cleared by one memset and read back by one copy:
+    // flags[4] | counters[3] (big reads, code flushes, pair flushes) | spare[2]
+    // | pairs per bucket[B+1] | their exclusive scan[B+1] | overflow[B]
+    int64_t ctrl_words = 0;
+    DevArray<int64_t> ctrl;
+    int* flags = nullptr;
+    unsigned* counters = nullptr;
+    int64_t* n_per = nullptr;
+    int64_t* dst = nullptr;
+    uint8_t* ovf = nullptr;
+    const int64_t* hctrl = nullptr;  // pinned copy of the control block
+    int64_t max_cflush = 0, ccap = 0;
+    DevArray<uint16_t> cent;
+    DevArray<int64_t> cf_base;
+    DevArray<uint32_t> cf_off;
+    DevArray<unsigned long long> blk_items;  // per partition block: codes, pairs
+    DevArray<uint32_t> blk_hist;             // per partition block: codes per code bucket (append)
+    int64_t pcap = kCChunk / 8;
+    DevArray<uint64_t> plist;
+    DevArray<uint32_t> pent, pf_off;
+    DevArray<int64_t> pf_base;
+    int n_cg = 0, n_pg = 0;
+    int64_t nsl = 0;
+    DevArray<uint32_t> part_ch, part_b, part_k, part_c;
+    DevArray<int> part_n;
+    DevArray<uint64_t> slot_k;
+    DevArray<int64_t> slot_c;
+    RunDir pdir{};
+    int attempt = 0;
+
+    int setup();
+    int launch();
+    int finish(karma_pairs* out);
+};
+
+int SetsJob::setup() {
     KARMA_TRY(make_geo(N, &g));
-    const int B = g.B;
-    const int64_t n_chunks = std::max<int64_t>(1, ceil_div(A, kCChunk));
+    B = g.B;
+    n_chunks = std::max<int64_t>(1, ceil_div(A, kCChunk));
     // partition: one round of resident blocks, each taking consecutive chunk lists
-    const bool wide_c = g.Bc > kNarrowBc, wide_p = B > kNarrowB;
+    wide_c = g.Bc > kNarrowBc;
+    wide_p = B > kNarrowB;
     // code partition: per-flush padded runs while a flush's runs are long (few
     // code buckets); one appended run per (block, bucket) beyond that
-    const bool append = g.Bc >= KARMA_APPEND_MIN_BC;
+    append = g.Bc >= KARMA_APPEND_MIN_BC;
     const void* code_part = append ? (wide_c ? reinterpret_cast<const void*>(&code_append_kernel<kMaxBc>)
                                              : reinterpret_cast<const void*>(&code_append_kernel<kNarrowBc>))
                                    : (wide_c ? reinterpret_cast<const void*>(&partition_kernel<CodeStreamWide>)
                                              : reinterpret_cast<const void*>(&partition_kernel<CodeStream>));
     const int resident = resident_grid(ctx, code_part, kPT, 0, int64_t(1) << 30);
-    const int lpb = (int)std::min<int64_t>(kMaxListsPerBlock, ceil_div(n_chunks, resident));
-    const int64_t n_pblk = ceil_div(n_chunks, lpb);
-    // per-step scratch
-    DevArray<uint32_t> codes, n_codes, n_gen, n_pl;
-    DevArray<int64_t> big_list;
+    lpb = (int)std::min<int64_t>(kMaxListsPerBlock, ceil_div(n_chunks, resident));
+    n_pblk = ceil_div(n_chunks, lpb);
     KARMA_TRY(codes.alloc(ctx, n_chunks * kCChunk));
     KARMA_TRY(n_codes.alloc(ctx, n_chunks));
     KARMA_TRY(n_gen.alloc(ctx, n_chunks));
     KARMA_TRY(n_pl.alloc(ctx, n_chunks));
     KARMA_TRY(big_list.alloc(ctx, A / (kMaxFast + 1) + 1));
-    // control block, cleared by one memset and read back by one copy:
-    // flags[4] | counters[3] (big reads, code flushes, pair flushes) | spare[2]
-    // | pairs per bucket[B+1] | their exclusive scan[B+1] | overflow[B]
-    const int64_t ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8);
-    DevArray<int64_t> ctrl;
+    ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8);
     KARMA_TRY(ctrl.alloc(ctx, ctrl_words));
-    int* const flags = reinterpret_cast<int*>(ctrl.ptr);
-    unsigned* const counters = reinterpret_cast<unsigned*>(ctrl.ptr + 2);
-    int64_t* const n_per = ctrl.ptr + 6;
-    int64_t* const dst = n_per + (B + 1);
-    uint8_t* const ovf = reinterpret_cast<uint8_t*>(dst + (B + 1));
+    flags = reinterpret_cast<int*>(ctrl.ptr);
+    counters = reinterpret_cast<unsigned*>(ctrl.ptr + 2);
+    n_per = ctrl.ptr + 6;
+    dst = n_per + (B + 1);
+    ovf = reinterpret_cast<uint8_t*>(dst + (B + 1));
     void* hpin = nullptr;
-    KARMA_TRY(ctx_pinned(ctx, ctrl_words * 8, &hpin));
-    const int64_t* const hctrl = static_cast<const int64_t*>(hpin);
+    KARMA_TRY(ctx_job_pinned(ctx, ctrl_words * 8, &hpin));
+    hctrl = static_cast<const int64_t*>(hpin);
     // code stream: <= one code per record + < 8 padding codes per run; a block
     // flushes only a full buffer, and once at its end
-    const int64_t max_cflush = n_pblk + ceil_div(A, CodeStream::kCap) + 1;
-    const int64_t ccap = A + max_cflush * (8 * (int64_t)g.Bc + 8);
-    DevArray<uint16_t> cent;
-    DevArray<int64_t> cf_base;
-    DevArray<uint32_t> cf_off;
-    DevArray<unsigned long long> blk_items;       // per partition block: codes, pairs
+    max_cflush = n_pblk + ceil_div(A, CodeStream::kCap) + 1;
+    ccap = A + max_cflush * (8 * (int64_t)g.Bc + 8);
     KARMA_TRY(blk_items.alloc(ctx, 2 * n_pblk));
-    DevArray<uint32_t> blk_hist;                  // per partition block: codes per code bucket (append)
     if (append) KARMA_TRY(blk_hist.alloc(ctx, n_pblk * g.Bc));
     if (g.Bc > 0) {
         KARMA_TRY(cent.alloc(ctx, ccap + 16));
         KARMA_TRY(cf_base.alloc(ctx, max_cflush));
         KARMA_TRY(cf_off.alloc(ctx, max_cflush * (g.Bc + 1)));
     }
-    // pair lists: general reads' pairs per chunk; start with room for 1/8 pair
-    // per record and rerun with the bound (4.5 per record) when short
-    int64_t pcap = kCChunk / 8;
-    DevArray<uint64_t> plist;
-    DevArray<uint32_t> pent, pf_off;
-    DevArray<int64_t> pf_base;
-    unsigned hc[3] = {0, 0, 0};
     // reduce geometry: grids fixed here, flush ranges from device counters
     // code reduce: one round (one 128 KB-LDS block per CU), at most ~4 flushes per group
-    const int n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count / g.Bc,
-                                                                              ceil_div(max_cflush, 4)))
-                              : 0;
-    const int n_pg = (int)std::max<int64_t>(1, ceil_div(256, B));
-    const int64_t nsl = (int64_t)B * n_pg;
-    DevArray<uint32_t> part_ch, part_b, part_k, part_c;
-    DevArray<int> part_n;
-    DevArray<uint64_t> slot_k;
-    DevArray<int64_t> slot_c;
+    n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count / g.Bc, ceil_div(max_cflush, 4)))
+                    : 0;
+    n_pg = (int)std::max<int64_t>(1, ceil_div(256, B));
+    nsl = (int64_t)B * n_pg;
     if (n_cg) KARMA_TRY(part_ch.alloc(ctx, (int64_t)g.Bc * n_cg * (int64_t(8) << g.bwc)));
     KARMA_TRY(part_b.alloc(ctx, nsl * (int64_t)kBand));
     KARMA_TRY(part_k.alloc(ctx, nsl * (int64_t)kHashR));
@@ -1560,68 +1589,80 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     KARMA_TRY(part_n.alloc(ctx, nsl));
     KARMA_TRY(slot_k.alloc(ctx, (int64_t)B * kSlotCap));
     KARMA_TRY(slot_c.alloc(ctx, (int64_t)B * kSlotCap));
-    RunDir pdir{};
+    return KARMA_OK;
+}
+
+// One attempt: every kernel up to the control block readback (no host wait).
+int SetsJob::launch() {
+    // pair lists: general reads' pairs per chunk; room for 1/8 pair per record
+    // first, the bound (4.5 per record) on a rerun
+    const int64_t max_pflush = n_pblk + ceil_div(n_chunks * pcap, PairStream::kCap) + 1;
+    const int64_t pscap = n_chunks * pcap + max_pflush * (4 * (int64_t)B + 4);
+    KARMA_TRY(plist.alloc(ctx, n_chunks * pcap));
+    KARMA_TRY(pent.alloc(ctx, pscap + 8));
+    KARMA_TRY(pf_base.alloc(ctx, max_pflush));
+    KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
+    KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, ctrl_words * 8, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(blk_items.ptr, 0, 2 * n_pblk * 8, ctx->stream));
+    if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
+    if (A > 0) {
+        ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
+                    n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags,
+                    append ? blk_hist.ptr : nullptr, g.bwc, g.Bc};
+        KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+    } else {
+        KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
+        KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
+    }
+    KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
+                 codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_pblk, lpb, flags);
+    const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items.ptr};
+    pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items.ptr + n_pblk};
+    if (g.Bc > 0) {
+        uint16_t* const trash = cent.ptr + (ccap + 7) / 8 * 8;
+        if (append && wide_c)
+            KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kMaxBc>, n_pblk, kPT, 0, codes.ptr, kCChunk,
+                         n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
+        else if (append)
+            KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kNarrowBc>, n_pblk, kPT, 0, codes.ptr,
+                         kCChunk, n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
+        else if (wide_c)
+            KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStreamWide>, n_pblk, kPT, 0, codes.ptr,
+                         kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
+        else
+            KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr, kCChunk,
+                         n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
+        KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
+                     g.Bc, g.bwc, n_cg, part_ch.ptr);
+    }
+    if (wide_p)
+        KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStreamWide>, n_pblk, kPT, 0, plist.ptr, pcap,
+                     n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
+    else
+        KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
+                     n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
+    KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
+                 g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
+    if (n_pg == 1)
+        KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashR>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits,
+                     g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
+                     ovf);
+    else
+        KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashF>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits,
+                     g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
+                     ovf);
+    KARMA_TRY(scan_excl_i64(ctx, n_per, dst, B + 1));
+    KARMA_HIP(hipMemcpyAsync(const_cast<int64_t*>(hctrl), ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost,
+                             ctx->stream));
+    return KARMA_OK;
+}
+
+int SetsJob::finish(karma_pairs* out) {
+    unsigned hc[3] = {0, 0, 0};
     std::vector<uint8_t> hovf(B);
     int64_t U = 0;
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        const int64_t max_pflush = n_pblk + ceil_div(n_chunks * pcap, PairStream::kCap) + 1;
-        const int64_t pscap = n_chunks * pcap + max_pflush * (4 * (int64_t)B + 4);
-        KARMA_TRY(plist.alloc(ctx, n_chunks * pcap));
-        KARMA_TRY(pent.alloc(ctx, pscap + 8));
-        KARMA_TRY(pf_base.alloc(ctx, max_pflush));
-        KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
-        KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, ctrl_words * 8, ctx->stream));
-        KARMA_HIP(hipMemsetAsync(blk_items.ptr, 0, 2 * n_pblk * 8, ctx->stream));
-        if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
-        if (A > 0) {
-            ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
-                        n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags,
-                        append ? blk_hist.ptr : nullptr, g.bwc, g.Bc};
-            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
-        } else {
-            KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
-            KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
-        }
-        KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
-                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_pblk, lpb, flags);
-        const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items.ptr};
-        pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items.ptr + n_pblk};
-        if (g.Bc > 0) {
-            uint16_t* const trash = cent.ptr + (ccap + 7) / 8 * 8;
-            if (append && wide_c)
-                KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kMaxBc>, n_pblk, kPT, 0, codes.ptr,
-                             kCChunk, n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
-            else if (append)
-                KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kNarrowBc>, n_pblk, kPT, 0, codes.ptr,
-                             kCChunk, n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
-            else if (wide_c)
-                KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStreamWide>, n_pblk, kPT, 0, codes.ptr,
-                             kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
-            else
-                KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr,
-                             kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
-            KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
-                         g.Bc, g.bwc, n_cg, part_ch.ptr);
-        }
-        if (wide_p)
-            KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStreamWide>, n_pblk, kPT, 0, plist.ptr,
-                         pcap, n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
-        else
-            KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
-                         n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
-        KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
-                     g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
-        if (n_pg == 1)
-            KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashR>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits,
-                         g.dbits, g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr,
-                         slot_c.ptr, n_per, ovf);
-        else
-            KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashF>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits,
-                         g.dbits, g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr,
-                         slot_c.ptr, n_per, ovf);
-        KARMA_TRY(scan_excl_i64(ctx, n_per, dst, B + 1));
+    for (;;) {
         // the one synchronisation of the common path
-        KARMA_HIP(hipMemcpyAsync(hpin, ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
         const int* hf = reinterpret_cast<const int*>(hctrl);
         std::memcpy(hc, hctrl + 2, sizeof hc);
@@ -1632,7 +1673,9 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         KARMA_CHECK(!hf[3], KARMA_ERR_STATE, "code partition: block counts disagree with the classify histogram");
         if (!hf[2]) break;
         KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "pair list capacity exceeded twice");
+        attempt = 1;
         pcap = kCChunk * 9 / 2;  // every read with <= 8 records fits
+        KARMA_TRY(launch());
     }
     const unsigned n_big = hc[0];
     DevArray<const uint64_t*> pk;
@@ -1667,8 +1710,8 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         keep_k.emplace_back(new DevArray<uint64_t>());
         keep_c.emplace_back(new DevArray<int64_t>());
         int64_t nu = 0;
-        KARMA_TRY(sort_reduce_pairs(ctx, wide.ptr, wc.ptr, nullptr, (int64_t)hp, 64, *keep_k.back(),
-                                    *keep_c.back(), nullptr, &nu));
+        KARMA_TRY(sort_reduce_pairs(ctx, wide.ptr, wc.ptr, nullptr, (int64_t)hp, 64, *keep_k.back(), *keep_c.back(),
+                                    nullptr, &nu));
         const uint64_t* kp = keep_k.back()->ptr;
         const int64_t* cp = keep_c.back()->ptr;
         KARMA_HIP(hipMemcpyAsync(pk.ptr + b, &kp, sizeof kp, hipMemcpyHostToDevice, ctx->stream));
@@ -1687,6 +1730,43 @@ int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     KARMA_TRY(mc.alloc(ctx, U));
     KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, pk.ptr, pc.ptr, n_per, dst, mk.ptr, mc.ptr);
     return finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out);
+}
+
+int64_t sets_max_contigs() { return kMaxCompactN; }
+
+int sets_begin(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job) {
+    KARMA_CHECK(N <= kMaxCompactN, KARMA_ERR_ARG, "sets_begin: n_contigs above the compact path");
+    KARMA_CHECK(!ctx->job_open, KARMA_ERR_STATE, "a split graph call is already open on this context");
+    std::unique_ptr<SetsJob> j(new SetsJob());
+    j->ctx = ctx;
+    j->rec = rec;
+    j->A = A;
+    j->N = N;
+    KARMA_TRY(j->setup());
+    KARMA_TRY(j->launch());
+    ctx->job_open = true;
+    *job = j.release();
+    return KARMA_OK;
+}
+
+int sets_end(SetsJob* job, karma_pairs* out) {
+    std::unique_ptr<SetsJob> j(job);
+    j->ctx->job_open = false;
+    return j->finish(out);
+}
+
+void sets_free(SetsJob* job) {
+    if (!job) return;
+    job->ctx->job_open = false;
+    hipStreamSynchronize(job->ctx->stream);  // its kernels may still use the scratch
+    delete job;
+}
+
+int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
+    if (N > kMaxCompactN) return records_to_pairs_wide(ctx, rec, A, N, out);
+    SetsJob* job = nullptr;
+    KARMA_TRY(sets_begin(ctx, rec, A, N, &job));
+    return sets_end(job, out);
 }
 
 }  // namespace karma

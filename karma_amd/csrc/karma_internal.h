@@ -63,6 +63,13 @@ struct karma_ctx {
     // pinned host scratch for small status readbacks (one async copy + one sync)
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
+    // a split graph call (karma_graph_records_begin/_end) keeps its control-block
+    // readback here until _end, so calls in between may use `pinned`
+    void* job_pinned = nullptr;
+    size_t job_pinned_bytes = 0;
+    bool job_open = false;
+    hipEvent_t side_ev = nullptr;  // main -> side stream ordering (karma_kmer_profile_side)
+    int grid_headroom = 0;         // blocks per CU resident_grid leaves free (a side-stream launch)
 };
 
 namespace karma {
@@ -75,6 +82,8 @@ int ctx_begin(karma_ctx* ctx);  // hipSetDevice
 int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int64_t work);
 // Pinned host scratch of >= bytes (valid until the next call on this ctx).
 int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out);
+// Pinned scratch owned by the open split graph call (valid until its _end).
+int ctx_job_pinned(karma_ctx* ctx, size_t bytes, void** out);
 // Wrap a launch with HIP events when timing is on.
 void timing_start(karma_ctx* ctx, const char* name, hipEvent_t* ev_stop);
 void timing_stop(karma_ctx* ctx, hipEvent_t ev_stop);
@@ -143,4 +152,13 @@ struct karma_pairs {
 namespace karma {
 // set-partition records pipeline (graph_sets.hip)
 int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out);
+// The same in two halves: sets_begin enqueues every kernel up to the control
+// block readback and returns; sets_end synchronises and assembles the list.
+// Only for N <= sets_max_contigs() (the compact path); `rec` must stay valid
+// until sets_end.
+struct SetsJob;
+int64_t sets_max_contigs();
+int sets_begin(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job);
+int sets_end(SetsJob* job, karma_pairs* out);  // frees the job
+void sets_free(SetsJob* job);
 }  // namespace karma

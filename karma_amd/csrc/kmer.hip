@@ -57,6 +57,7 @@ struct karma_kmer_plan {
     DevArray<int32_t> col_of_exc;
     DevArray<uint64_t> col_keys;
     DevArray<int64_t> row_tot;
+    DevArray<int> err;  // zero-length-key guard flag of the profile kernels (the host checks first)
     int64_t M = -1;
 };
 
@@ -890,7 +891,7 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
     DevArray<uint64_t> exc_buf;
     DevArray<unsigned long long> exc_cnt;
     if ((rc = p->presence.alloc(ctx, p->nwords)) || (rc = p->row_tot.alloc(ctx, c->n ? c->n : 1)) ||
-        (rc = exc_buf.alloc(ctx, exc_cap)) || (rc = exc_cnt.alloc(ctx, 1))) {
+        (rc = p->err.alloc(ctx, 1)) || (rc = exc_buf.alloc(ctx, exc_cap)) || (rc = exc_cnt.alloc(ctx, 1))) {
         delete p;
         return rc;
     }
@@ -1106,9 +1107,8 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
         if ((rc = dev_out.alloc(ctx, (size_t)n * ld))) return rc;
         dst = dev_out.ptr;
     }
-    DevArray<int> err;
-    if ((rc = err.alloc(ctx, 1))) return rc;
-    KARMA_HIP(hipMemsetAsync(err.ptr, 0, 4, ctx->stream));
+    int* const err = p->err.ptr;  // no temporaries: the launch may run on a side stream
+    KARMA_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
     bool with_len = p->kmode != 8;
     const bool wave = M <= kWaveMaxM && p->S <= 8192;
     const int k = p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode;
@@ -1125,7 +1125,7 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
                                      lds, ceil_div(n, kPBlock / 64));                                            \
         KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16>), g_, kPBlock, lds, c->packed.ptr,      \
                      c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len,        \
-                     p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err.ptr,       \
+                     p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err,       \
                      (int)p->S, p->row_tot.ptr);                                                                 \
     } while (0)
         if (p56) {
@@ -1145,7 +1145,7 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
 #define KARMA_PROFILE_LAUNCH(P56, LDS)                                                                           \
     KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, LDS>), grid, kPBlock, lds, c->packed.ptr, c->mask.ptr, \
                  c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len, p->col_of_ord.ptr,      \
-                 p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err.ptr, (int)p->S,      \
+                 p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err, (int)p->S,      \
                  p->row_tot.ptr)
         if (p->kmode == KARMA_KMER_5P6) {
             if (lds_ok) KARMA_PROFILE_LAUNCH(true, true);
@@ -1160,6 +1160,40 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
         KARMA_HIP(hipMemcpyAsync(out, dst, (size_t)n * ld * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
     }
+    return KARMA_OK;
+}
+
+#ifndef KARMA_SIDE_HEADROOM
+#define KARMA_SIDE_HEADROOM 1
+#endif
+int karma_kmer_profile_side(karma_kmer_plan* p, double* out_dev, int64_t ld, void* side) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null plan");
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    // the general kernel past 36,864 columns allocates scratch: main stream
+    if (!side || (p->M > kWaveMaxM && p->M * 4 > 144 * 1024)) return karma_kmer_profile(p, out_dev, ld, 1);
+    if (!ctx->side_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming));
+    hipStream_t s = static_cast<hipStream_t>(side);
+    KARMA_HIP(hipEventRecord(ctx->side_ev, ctx->stream));  // after everything enqueued on the main stream
+    KARMA_HIP(hipStreamWaitEvent(s, ctx->side_ev, 0));
+    hipStream_t main_stream = ctx->stream;
+    ctx->stream = s;  // launches and timing events go to the side stream
+    // its one-round grid leaves a block slot per CU, so the main stream's
+    // short kernels find room beside it instead of queueing behind it
+    ctx->grid_headroom = KARMA_SIDE_HEADROOM;
+    const int rc = karma_kmer_profile(p, out_dev, ld, 1);
+    ctx->grid_headroom = 0;
+    ctx->stream = main_stream;
+    return rc;
+}
+
+int karma_ctx_join(karma_ctx* ctx, void* side) {
+    KARMA_CHECK(ctx, KARMA_ERR_ARG, "null ctx");
+    if (!side) return KARMA_OK;
+    KARMA_TRY(ctx_begin(ctx));
+    if (!ctx->side_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming));
+    KARMA_HIP(hipEventRecord(ctx->side_ev, static_cast<hipStream_t>(side)));
+    KARMA_HIP(hipStreamWaitEvent(ctx->stream, ctx->side_ev, 0));
     return KARMA_OK;
 }
 

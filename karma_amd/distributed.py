@@ -188,6 +188,9 @@ class HipOps:
             torch.cuda.set_stream(self.stream)
         ctx.set_stream(self.stream.cuda_stream)
         self.ctx = ctx
+        # the k-mer profile runs here, beside the graph's tail and exchange
+        # (ShardedBuild.run); the main stream keeps the higher priority
+        self.side = torch.cuda.Stream(device=self.dev, priority=0)
 
     # -- k-mer --
     def kmer_plan(self, store, kmode):
@@ -232,6 +235,15 @@ class HipOps:
         if out.numel():
             plan.profile_device(out.data_ptr(), out.shape[1])
 
+    def profile_side(self, plan, out):
+        """The profile on the side stream, after everything enqueued so far."""
+        if out.numel():
+            plan.profile_side(out.data_ptr(), self.side.cuda_stream, out.shape[1])
+
+    def join(self):
+        """The main stream waits for the side stream (before the plan or profile are used)."""
+        self.ctx.join(self.side.cuda_stream)
+
     def profile_buffer(self, n, M):
         return self.torch.empty((n, M), dtype=self.torch.float64, device=self.dev)
 
@@ -240,6 +252,12 @@ class HipOps:
         """Continue work on a pair list built by another HipOps on this stream."""
         pairs.rebind(self.ctx)
         return pairs
+
+    def graph_begin(self, records, n_records, n_contigs):
+        return self.engine.Pairs.from_records_begin(self.ctx, n_contigs, records, n_records)
+
+    def graph_end(self, job):
+        return job.end()
 
     def graph_local(self, records, n_records, n_contigs):
         return self.engine.Pairs.from_records(self.ctx, None, n_contigs, grouped=True, device_ptr=records,
@@ -340,10 +358,25 @@ class ShardedBuild:
         return [c for c in (self.ops.ctx if hasattr(self.ops, "ctx") else None, self.gctx) if c is not None]
 
     def run(self, store, records, n_records, keep=False):
+        ops = self.ops
+        # Default order (one stream pair): k-mer columns, then the graph's big
+        # kernels alone on the chip, then the profile on the side stream while
+        # the graph's host-synchronised tail (assembly, exchange, weights) runs
+        # on the main stream.  The side stream is joined before anything uses
+        # the plan or the profile.
+        side = self._pool is None and hasattr(ops, "graph_begin")
+        try:
+            return self._run(store, records, n_records, keep, side)
+        finally:
+            if side:
+                ops.join()
+
+    def _run(self, store, records, n_records, keep, side):
         ops, comm = self.ops, self.comm
         fut = None
         if self._pool is not None:  # ---- shared-read graph, concurrent (read_graph.py:19-50) ----
             fut = self._pool.submit(self.gops.graph_local, records, n_records, self.n_glob)
+        local = None
         try:
             # ---- k-mer profile (kmer.py:199-233) ----
             plan = ops.kmer_plan(store, self.kmode)
@@ -354,13 +387,21 @@ class ShardedBuild:
             M = ops.finalize(plan)
             if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
                 self._prof = ops.profile_buffer(self.n_loc, M)
-            ops.profile(plan, self._prof)
+            if side:  # ---- shared-read graph (read_graph.py:19-50), then the profile beside its tail ----
+                job = ops.graph_begin(records, n_records, self.n_glob)
+                try:
+                    ops.profile_side(plan, self._prof)
+                finally:
+                    local = ops.graph_end(job)
+            else:
+                ops.profile(plan, self._prof)
         finally:
-            local = fut.result() if fut is not None else None  # joined on every path
-        if local is None:  # ---- shared-read graph (read_graph.py:19-50) ----
-            local = ops.graph_local(records, n_records, self.n_glob)
-        else:
+            if fut is not None:
+                local = fut.result()  # joined on every path
+        if fut is not None:
             local = ops.adopt(local)
+        elif local is None:  # ---- shared-read graph (read_graph.py:19-50) ----
+            local = ops.graph_local(records, n_records, self.n_glob)
         stats = {"M": M}
         if keep:
             stats["entries"] = ops.entries(local)

@@ -149,6 +149,12 @@ class KmerPlan:
     def profile_device(self, dst_dev_ptr, ld=None):
         call("karma_kmer_profile", self.h, ctypes.c_void_p(dst_dev_ptr), ld or self.M, 1)
 
+    def profile_side(self, dst_dev_ptr, side_stream_ptr, ld=None):
+        """profile_device on a side stream, after the work already enqueued on the
+        context's stream; the context joins it with Context.join(side)."""
+        call("karma_kmer_profile_side", self.h, ctypes.c_void_p(dst_dev_ptr), ld or self.M,
+             ctypes.c_void_p(side_stream_ptr))
+
     def close(self):
         if getattr(self, "h", None):
             _lib.load().karma_kmer_plan_destroy(self.h)
@@ -185,6 +191,26 @@ def kmer_profile(sequences, kmer_size, ctx=None):
 # Graph
 # ---------------------------------------------------------------------------
 
+class GraphJob:
+    """An open karma_graph_records_begin call (one per context)."""
+
+    def __init__(self, pairs_cls, ctx, h):
+        self.pairs_cls, self.ctx, self.h = pairs_cls, ctx, h
+
+    def end(self):
+        h, self.h = self.h, None
+        out = ctypes.c_void_p()
+        call("karma_graph_records_end", h, ctypes.byref(out))
+        return self.pairs_cls(self.ctx, out)
+
+    def __del__(self):
+        if getattr(self, "h", None):  # never ended: end it (frees the job and its list)
+            try:
+                self.end().close()
+            except Exception:
+                pass
+
+
 class Pairs:
     """Sorted unique (a << 32 | b, count) list (karma_pairs)."""
 
@@ -203,6 +229,16 @@ class Pairs:
             call("karma_graph_records", ctx.h, ptr(rec) if len(rec) else None, len(rec), n_contigs, flags, 0,
                  ctypes.byref(h))
         return cls(ctx, h)
+
+    @classmethod
+    def from_records_begin(cls, ctx, n_contigs, device_ptr, n_records, grouped=True):
+        """First half of from_records on device records (karma_graph_records_begin):
+        the pipeline is enqueued up to its host synchronisation; .end() finishes."""
+        h = ctypes.c_void_p()
+        flags = _lib.KARMA_REC_SORTED if grouped else _lib.KARMA_REC_UNSORTED
+        call("karma_graph_records_begin", ctx.h, ctypes.c_void_p(device_ptr), n_records, n_contigs, flags, 1,
+             ctypes.byref(h))
+        return GraphJob(cls, ctx, h)
 
     @classmethod
     def from_eq(cls, ctx, cls_off, members, counts, pair_skip, n_contigs):
