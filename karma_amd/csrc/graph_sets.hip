@@ -196,6 +196,7 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 5  // 5: no spills at 96 VGPRs (0.504 vs 0.518 ms at 6 with 80)
 #endif
+template <bool HIST>  // HIST: per-block code-bucket histograms for code_append_kernel
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
 classify2_kernel(ClassArgs P) {
     const int lane = threadIdx.x & 63;
@@ -210,9 +211,9 @@ classify2_kernel(ClassArgs P) {
     __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][64 * 5];
     u32x4* tb = tbuf[wave];
     // the chunk's codes per code bucket, added to its partition block's row at the end
-    __shared__ uint32_t whist[kCW / 64][kMaxBc];
+    __shared__ uint32_t whist[kCW / 64][HIST ? kMaxBc : 1];
     uint32_t* wh = whist[wave];
-    const bool hist_on = P.blk_hist != nullptr;
+    constexpr bool hist_on = HIST;
     if (hist_on) {
         for (int b = lane; b < P.Bc; b += 64) wh[b] = 0;
         wave_sync();
@@ -1448,7 +1449,7 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
             ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags,
                         nullptr,   0,         0};
-            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<false>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags);
@@ -1609,7 +1610,10 @@ int SetsJob::launch() {
         ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
                     n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags,
                     append ? blk_hist.ptr : nullptr, g.bwc, g.Bc};
-        KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+        if (append)
+            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<true>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+        else
+            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<false>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
     } else {
         KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
