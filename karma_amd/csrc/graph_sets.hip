@@ -1137,7 +1137,9 @@ __global__ void __launch_bounds__(kFT) final_kernel(
     if (overflow[bucket]) return;  // generic path
     HTab<HF, kFT> t{hkeys, hvals, &nuniq};
     const int band_n = dbits >= 0 ? (1 << (bw + dbits)) : 0;
-    t.init();
+    // one group (HF == kHashR): its list is already unique, copied as is
+    constexpr bool one_list = HF == kHashR;
+    if (!one_list) t.init();
     for (int i = threadIdx.x; i < band_n; i += kFT) {
         uint32_t v = 0;
         for (int gi = 0; gi < n_pg; ++gi) {
@@ -1167,18 +1169,28 @@ __global__ void __launch_bounds__(kFT) final_kernel(
         }
         __syncthreads();
     }
-    for (int gi = 0; gi < n_pg; ++gi) {
-        const int64_t sl = (int64_t)bucket * n_pg + gi;
-        const int n = part_n[sl];
-        bool full = false;
-        for (int i = threadIdx.x; i < n; i += kFT)
-            full |= !t.insert(part_keys[sl * kHashR + i], part_cnt[sl * kHashR + i]);
-        if (__syncthreads_or(full)) {
-            if (threadIdx.x == 0) overflow[bucket] = 1;
-            return;
+    int nh;
+    if (one_list) {
+        nh = max(0, part_n[bucket]);
+        for (int i = threadIdx.x; i < nh; i += kFT) {
+            hkeys[i] = part_keys[(int64_t)bucket * kHashR + i];
+            hvals[i] = part_cnt[(int64_t)bucket * kHashR + i];
         }
+        __syncthreads();
+    } else {
+        for (int gi = 0; gi < n_pg; ++gi) {
+            const int64_t sl = (int64_t)bucket * n_pg + gi;
+            const int n = part_n[sl];
+            bool full = false;
+            for (int i = threadIdx.x; i < n; i += kFT)
+                full |= !t.insert(part_keys[sl * kHashR + i], part_cnt[sl * kHashR + i]);
+            if (__syncthreads_or(full)) {
+                if (threadIdx.x == 0) overflow[bucket] = 1;
+                return;
+            }
+        }
+        nh = t.compact(&cnt);
     }
-    const int nh = t.compact(&cnt);
     int p2 = 1;
     while (p2 < nh) p2 <<= 1;
     for (int i = nh + threadIdx.x; i < p2; i += kFT) {
