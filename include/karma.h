@@ -109,6 +109,11 @@ int karma_kmer_exceptions_get(karma_kmer_plan* p, uint64_t* dst_dev);
 int karma_kmer_exceptions_set(karma_kmer_plan* p, const uint64_t* src_dev, int64_t n);
 /* Column table = sorted() union of present k-mers (kmer.py:172-177). */
 int karma_kmer_plan_finalize(karma_kmer_plan* p, int64_t* M);
+/* The same in two halves: _async enqueues the column table and M's readback;
+ * _wait waits for those alone (not for later work on the stream).  One
+ * finalize in flight per context. */
+int karma_kmer_plan_finalize_async(karma_kmer_plan* p);
+int karma_kmer_plan_finalize_wait(karma_kmer_plan* p, int64_t* M);
 /* Column keys: byte-packed u64, big-endian bytes from bit 63; for k < 8 and 5p6
  * the low byte holds the k-mer length (so u64 order == Python str order). */
 int karma_kmer_columns(karma_kmer_plan* p, uint64_t* keys_host);
@@ -116,8 +121,9 @@ int karma_kmer_columns(karma_kmer_plan* p, uint64_t* keys_host);
  * out[r*ld + col] = count / key_len[r] (kmer.py:120, :231-233), zeros written. */
 int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_device);
 /* karma_kmer_profile into device memory, launched on `side` (a hipStream_t)
- * after everything already enqueued on the context's stream, so it overlaps
- * whatever the caller enqueues next on that stream.  Call karma_ctx_join
+ * after everything already enqueued on the context's stream -- or, while a
+ * karma_graph_records_begin job is open, after that job's classify kernel and
+ * this plan's column table -- so it overlaps the rest of the stream's work.  Call karma_ctx_join
  * before the plan or the output are used or destroyed.  side = NULL: the
  * context's stream. */
 int karma_kmer_profile_side(karma_kmer_plan* plan, double* out_dev, int64_t ld, void* side);

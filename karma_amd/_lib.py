@@ -66,6 +66,8 @@ _SIGS = {
     "karma_kmer_exceptions_get": [_c_p, _c_p],
     "karma_kmer_exceptions_set": [_c_p, _c_p, _i64],
     "karma_kmer_plan_finalize": [_c_p, _I64P],
+    "karma_kmer_plan_finalize_async": [_c_p],
+    "karma_kmer_plan_finalize_wait": [_c_p, _I64P],
     "karma_kmer_columns": [_c_p, _c_p],
     "karma_kmer_profile": [_c_p, _c_p, _i64, _i32],
     "karma_kmer_profile_side": [_c_p, _c_p, _i64, _c_p],

@@ -183,6 +183,8 @@ int karma_ctx_destroy(karma_ctx* ctx) {
     if (ctx->pinned) hipHostFree(ctx->pinned);
     if (ctx->job_pinned) hipHostFree(ctx->job_pinned);
     if (ctx->side_ev) hipEventDestroy(ctx->side_ev);
+    if (ctx->mark_ev) hipEventDestroy(ctx->mark_ev);
+    if (ctx->fin_pinned) hipHostFree(ctx->fin_pinned);
     delete ctx;
     return KARMA_OK;
 }

@@ -55,6 +55,9 @@ constexpr int kMaxBc = 512;           // code buckets
 // partition LDS is sized by the bucket count: the narrow variants (<= 512 pair
 // and <= 128 code buckets, n_contigs <= 2^19) keep 3 code-partition blocks per CU
 constexpr int kNarrowB = 512, kNarrowBc = 128;
+#ifndef KARMA_ONE_GROUP_B
+#define KARMA_ONE_GROUP_B 128
+#endif
 #ifndef KARMA_APPEND_MIN_BC
 #define KARMA_APPEND_MIN_BC 129  // code_append_kernel from this many code buckets on (n_contigs > 2^19)
 #endif
@@ -1593,7 +1596,10 @@ int SetsJob::setup() {
     // code reduce: one round (one 128 KB-LDS block per CU), at most ~4 flushes per group
     n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count / g.Bc, ceil_div(max_cflush, 4)))
                     : 0;
-    n_pg = (int)std::max<int64_t>(1, ceil_div(256, B));
+    // pair-reduce groups per bucket: enough blocks to fill the chip while
+    // buckets are few; one group from KARMA_ONE_GROUP_B buckets on, so the
+    // final kernel copies the bucket's single list instead of re-hashing
+    n_pg = B >= KARMA_ONE_GROUP_B ? 1 : (int)std::max<int64_t>(1, ceil_div(256, B));
     nsl = (int64_t)B * n_pg;
     if (n_cg) KARMA_TRY(part_ch.alloc(ctx, (int64_t)g.Bc * n_cg * (int64_t(8) << g.bwc)));
     KARMA_TRY(part_b.alloc(ctx, nsl * (int64_t)kBand));
@@ -1626,7 +1632,18 @@ int SetsJob::launch() {
             KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<true>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         else
             KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<false>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
-    } else {
+    }
+#ifndef KARMA_MARK_AFTER_CLASSIFY
+// 1: the side-stream profile may start right after classify.  Measured off:
+// sharing the chip slows the code partition 0.19 -> 0.5 ms (1.46 vs 1.37 ms/step)
+#define KARMA_MARK_AFTER_CLASSIFY 0
+#endif
+    if (KARMA_MARK_AFTER_CLASSIFY && attempt == 0) {  // side-stream work (the k-mer profile) may start once classify is done
+        if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
+        KARMA_HIP(hipEventRecord(ctx->mark_ev, ctx->stream));
+        ctx->mark_set = true;
+    }
+    if (A == 0) {
         KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
     }
@@ -1759,7 +1776,11 @@ int sets_begin(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob**
     j->A = A;
     j->N = N;
     KARMA_TRY(j->setup());
-    KARMA_TRY(j->launch());
+    const int rc = j->launch();
+    if (rc) {
+        ctx->mark_set = false;
+        return rc;
+    }
     ctx->job_open = true;
     *job = j.release();
     return KARMA_OK;
@@ -1768,12 +1789,14 @@ int sets_begin(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob**
 int sets_end(SetsJob* job, karma_pairs* out) {
     std::unique_ptr<SetsJob> j(job);
     j->ctx->job_open = false;
+    j->ctx->mark_set = false;
     return j->finish(out);
 }
 
 void sets_free(SetsJob* job) {
     if (!job) return;
     job->ctx->job_open = false;
+    job->ctx->mark_set = false;
     hipStreamSynchronize(job->ctx->stream);  // its kernels may still use the scratch
     delete job;
 }

@@ -58,7 +58,13 @@ struct karma_kmer_plan {
     DevArray<uint64_t> col_keys;
     DevArray<int64_t> row_tot;
     DevArray<int> err;  // zero-length-key guard flag of the profile kernels (the host checks first)
+    DevArray<int64_t> m_dev;
+    hipEvent_t fin_ev = nullptr;  // after the column table and M's readback
+    bool fin_pending = false;
     int64_t M = -1;
+    ~karma_kmer_plan() {
+        if (fin_ev) hipEventDestroy(fin_ev);
+    }
 };
 
 namespace {
@@ -1038,30 +1044,45 @@ int karma_kmer_exceptions_set(karma_kmer_plan* p, const uint64_t* src, int64_t n
     return KARMA_OK;
 }
 
-int karma_kmer_plan_finalize(karma_kmer_plan* p, int64_t* M) {
-    KARMA_CHECK(p && M, KARMA_ERR_ARG, "null argument");
+int karma_kmer_plan_finalize_async(karma_kmer_plan* p) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null argument");
     karma_ctx* ctx = p->ctx;
     KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(!p->fin_pending, KARMA_ERR_STATE, "finalize already in flight");
     int kmin, kmax;
     uint32_t S;
     bool with_len;
     KARMA_TRY(kmer_shape(p->kmode, &kmin, &kmax, &S, &with_len));
     int rc;
-    DevArray<int64_t> m_dev;
     if ((rc = p->col_of_ord.alloc(ctx, S)) || (rc = p->col_of_exc.alloc(ctx, p->n_exc ? p->n_exc : 1)) ||
-        (rc = p->col_keys.alloc(ctx, S + p->n_exc)) || (rc = m_dev.alloc(ctx, 1)))
+        (rc = p->col_keys.alloc(ctx, S + p->n_exc)) || (rc = p->m_dev.alloc(ctx, 1)))
         return rc;
     const size_t lds = (p->nwords + 1) * 4;
     KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->presence.ptr, (int)p->nwords, S,
                  p->kmode == KARMA_KMER_5P6, p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode, with_len, p->exc_keys.ptr,
-                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, m_dev.ptr);
-    void* hpin = nullptr;
-    KARMA_TRY(ctx_pinned(ctx, 8, &hpin));
-    KARMA_HIP(hipMemcpyAsync(hpin, m_dev.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    p->M = *static_cast<const int64_t*>(hpin);
+                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, p->m_dev.ptr);
+    if (!ctx->fin_pinned) KARMA_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->fin_pinned), 64, hipHostMallocDefault));
+    KARMA_HIP(hipMemcpyAsync(ctx->fin_pinned, p->m_dev.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (!p->fin_ev) KARMA_HIP(hipEventCreateWithFlags(&p->fin_ev, hipEventDisableTiming));
+    KARMA_HIP(hipEventRecord(p->fin_ev, ctx->stream));
+    p->fin_pending = true;
+    return KARMA_OK;
+}
+
+int karma_kmer_plan_finalize_wait(karma_kmer_plan* p, int64_t* M) {
+    KARMA_CHECK(p && M, KARMA_ERR_ARG, "null argument");
+    KARMA_CHECK(p->fin_pending, KARMA_ERR_STATE, "no finalize in flight");
+    KARMA_TRY(ctx_begin(p->ctx));
+    KARMA_HIP(hipEventSynchronize(p->fin_ev));  // the column table only, not later work on the stream
+    p->fin_pending = false;
+    p->M = *p->ctx->fin_pinned;
     *M = p->M;
     return KARMA_OK;
+}
+
+int karma_kmer_plan_finalize(karma_kmer_plan* p, int64_t* M) {
+    KARMA_TRY(karma_kmer_plan_finalize_async(p));
+    return karma_kmer_plan_finalize_wait(p, M);
 }
 
 int karma_kmer_columns(karma_kmer_plan* p, uint64_t* keys_host) {
@@ -1172,10 +1193,18 @@ int karma_kmer_profile_side(karma_kmer_plan* p, double* out_dev, int64_t ld, voi
     KARMA_TRY(ctx_begin(ctx));
     // the general kernel past 36,864 columns allocates scratch: main stream
     if (!side || (p->M > kWaveMaxM && p->M * 4 > 144 * 1024)) return karma_kmer_profile(p, out_dev, ld, 1);
-    if (!ctx->side_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming));
     hipStream_t s = static_cast<hipStream_t>(side);
-    KARMA_HIP(hipEventRecord(ctx->side_ev, ctx->stream));  // after everything enqueued on the main stream
-    KARMA_HIP(hipStreamWaitEvent(s, ctx->side_ev, 0));
+    KARMA_CHECK(p->fin_ev && p->M >= 0, KARMA_ERR_STATE, "karma_kmer_profile_side before finalize");
+    if (ctx->mark_set) {
+        // an open graph job: start once its classify kernel and this plan's
+        // column table are done (the job's later kernels overlap the profile)
+        KARMA_HIP(hipStreamWaitEvent(s, ctx->mark_ev, 0));
+        KARMA_HIP(hipStreamWaitEvent(s, p->fin_ev, 0));
+    } else {
+        if (!ctx->side_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->side_ev, hipEventDisableTiming));
+        KARMA_HIP(hipEventRecord(ctx->side_ev, ctx->stream));  // after everything enqueued on the main stream
+        KARMA_HIP(hipStreamWaitEvent(s, ctx->side_ev, 0));
+    }
     hipStream_t main_stream = ctx->stream;
     ctx->stream = s;  // launches and timing events go to the side stream
     // its one-round grid leaves a block slot per CU, so the main stream's

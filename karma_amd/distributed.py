@@ -228,6 +228,12 @@ class HipOps:
     def finalize(self, plan):
         return plan.finalize()
 
+    def finalize_async(self, plan):
+        plan.finalize_async()
+
+    def finalize_wait(self, plan):
+        return plan.finalize_wait()
+
     def columns(self, plan):
         return plan.columns()
 
@@ -359,11 +365,11 @@ class ShardedBuild:
 
     def run(self, store, records, n_records, keep=False):
         ops = self.ops
-        # Default order (one stream pair): k-mer columns, then the graph's big
-        # kernels alone on the chip, then the profile on the side stream while
-        # the graph's host-synchronised tail (assembly, exchange, weights) runs
-        # on the main stream.  The side stream is joined before anything uses
-        # the plan or the profile.
+        # Default order (one stream pair): k-mer columns, then the graph's
+        # kernels alone on the chip (classify .. final), then the profile on
+        # the side stream beside the graph's host-synchronised assembly,
+        # exchange and weights on the main stream.  The side stream is joined
+        # before anything uses the plan or the profile.
         side = self._pool is None and hasattr(ops, "graph_begin")
         try:
             return self._run(store, records, n_records, keep, side)
@@ -384,16 +390,23 @@ class ShardedBuild:
                 pres = comm.allreduce_max_(ops.presence_bytes(plan))
                 ops.set_presence_bytes(plan, pres)
                 ops.set_exceptions(plan, comm.all_gather_var(ops.exceptions(plan)))
-            M = ops.finalize(plan)
-            if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
-                self._prof = ops.profile_buffer(self.n_loc, M)
-            if side:  # ---- shared-read graph (read_graph.py:19-50), then the profile beside its tail ----
-                job = ops.graph_begin(records, n_records, self.n_glob)
+            if side:
+                # the column table, then the graph's kernels behind it on the
+                # main stream; M is read back without waiting for the graph,
+                # and the profile (side stream) starts after the graph's kernels
+                ops.finalize_async(plan)
+                job = ops.graph_begin(records, n_records, self.n_glob)  # ---- read_graph.py:19-50 ----
                 try:
+                    M = ops.finalize_wait(plan)
+                    if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
+                        self._prof = ops.profile_buffer(self.n_loc, M)
                     ops.profile_side(plan, self._prof)
                 finally:
                     local = ops.graph_end(job)
             else:
+                M = ops.finalize(plan)
+                if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
+                    self._prof = ops.profile_buffer(self.n_loc, M)
                 ops.profile(plan, self._prof)
         finally:
             if fut is not None:

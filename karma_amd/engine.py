@@ -130,6 +130,16 @@ class KmerPlan:
         self.M = m.value
         return self.M
 
+    def finalize_async(self):
+        """Enqueue the column table; finalize_wait() returns M."""
+        call("karma_kmer_plan_finalize_async", self.h)
+
+    def finalize_wait(self):
+        m = ctypes.c_int64()
+        call("karma_kmer_plan_finalize_wait", self.h, ctypes.byref(m))
+        self.M = m.value
+        return self.M
+
     def columns(self):
         keys = np.zeros(max(self.M, 1), dtype=np.uint64)
         call("karma_kmer_columns", self.h, ptr(keys))

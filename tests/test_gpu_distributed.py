@@ -23,7 +23,7 @@ def _inputs(rank, world):
     return blob, offs, key_len, rec
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, overlap):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from karma_amd import _lib, engine
     from karma_amd.distributed import Comm, ShardedBuild
@@ -31,8 +31,10 @@ def _worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     ctx = _lib.Context(0)
     blob, offs, key_len, rec = _inputs(rank, world)
-    # overlap: the local graph build runs concurrently on a second context
-    build = ShardedBuild(ctx, comm, -1, N_LOC * world, rank * N_LOC, N_LOC, overlap=True)
+    # overlap: the local graph build runs concurrently on a second context;
+    # otherwise the default order (profile on the side stream beside the
+    # graph's tail and the exchange)
+    build = ShardedBuild(ctx, comm, -1, N_LOC * world, rank * N_LOC, N_LOC, overlap=overlap)
     store = engine.ContigStore(ctx, blob, offs, key_len)
     rec_dev = torch.from_numpy(rec.view(np.int64).reshape(-1)).to(build.ops.dev)
     res = build.run(store, rec_dev.data_ptr(), len(rec), keep=True)
@@ -43,7 +45,8 @@ def _worker(rank, world, port, out_dir):
     comm.close()
 
 
-def test_two_gpu_ranks_match_oracle(tmp_path):
+@pytest.mark.parametrize("overlap", [True, False])
+def test_two_gpu_ranks_match_oracle(tmp_path, overlap):
     from karma_amd import engine
     from oracle import oracle
     s = socket.socket()
@@ -51,7 +54,7 @@ def test_two_gpu_ranks_match_oracle(tmp_path):
     port = s.getsockname()[1]
     s.close()
     world = 2
-    torch.multiprocessing.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    torch.multiprocessing.spawn(_worker, args=(world, port, str(tmp_path), overlap), nprocs=world, join=True)
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     seqs, recs = OrderedDict(), []
     for r in range(world):
