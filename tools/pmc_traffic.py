@@ -16,6 +16,10 @@ import sys
 NAMES = {
     "classify_kernel": "graph_classify",
     "classify2_kernel": "graph_classify",
+    "classify2_kernel<false>": "graph_classify",
+    "classify2_kernel<true>": "graph_classify",
+    "code_append_kernel<512>": "graph_code_partition",
+    "code_append_kernel<128>": "graph_code_partition",
     "partition_kernel<CodeStream>": "graph_code_partition",
     "partition_kernel<CodeStreamT<128> >": "graph_code_partition",
     "code_reduce_kernel": "graph_code_reduce",
