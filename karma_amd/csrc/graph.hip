@@ -527,7 +527,7 @@ int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
         for (std::vector<int64_t> o = off; o.size() > 2;) {  // plan: the largest temporary
             std::vector<int64_t> next{0};
             for (size_t j = 0; j + 1 < o.size(); j += 2) {
-                if (j + 2 < o.size()) {
+                if (j + 2 < o.size() && o[j + 1] > o[j] && o[j + 2] > o[j + 1]) {
                     size_t tb = 0;
                     KARMA_HIP(rocprim::merge(nullptr, tb, sk, sk, (uint64_t*)nullptr, sc, sc, (int64_t*)nullptr,
                                              (size_t)(o[j + 1] - o[j]), (size_t)(o[j + 2] - o[j + 1]),
@@ -551,16 +551,16 @@ int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
             std::vector<int64_t> next{0};
             for (size_t j = 0; j + 1 < o.size(); j += 2) {
                 const int64_t a0 = o[j], a1 = o[j + 1];
-                if (j + 2 < o.size()) {
-                    const int64_t a2 = o[j + 2];
+                const int64_t a2 = j + 2 < o.size() ? o[j + 2] : a1;
+                if (a1 > a0 && a2 > a1) {  // two non-empty runs (an empty merge would launch an empty grid)
                     size_t tb = need;
                     KARMA_HIP(rocprim::merge(tmp.ptr, tb, sk + a0, sk + a1, kb[dst].ptr + a0, sc + a0, sc + a1,
                                              cb[dst].ptr + a0, (size_t)(a1 - a0), (size_t)(a2 - a1),
                                              rocprim::less<uint64_t>(), ctx->stream));
-                } else if (a1 > a0) {  // odd run out: carried to the next level
-                    KARMA_HIP(hipMemcpyAsync(kb[dst].ptr + a0, sk + a0, (a1 - a0) * 8, hipMemcpyDeviceToDevice,
+                } else if (a2 > a0) {  // one run (odd one out, or its partner is empty): carried over
+                    KARMA_HIP(hipMemcpyAsync(kb[dst].ptr + a0, sk + a0, (a2 - a0) * 8, hipMemcpyDeviceToDevice,
                                              ctx->stream));
-                    KARMA_HIP(hipMemcpyAsync(cb[dst].ptr + a0, sc + a0, (a1 - a0) * 8, hipMemcpyDeviceToDevice,
+                    KARMA_HIP(hipMemcpyAsync(cb[dst].ptr + a0, sc + a0, (a2 - a0) * 8, hipMemcpyDeviceToDevice,
                                              ctx->stream));
                 }
                 next.push_back(o[std::min(j + 2, o.size() - 1)]);

@@ -358,3 +358,32 @@ def test_merge_runs_and_split(seed, n_runs, n):
         bad[off[r]], bad[off[r] + 1] = keys[off[r] + 1] + np.uint64(1), keys[off[r]]  # a descent inside a run
         with pytest.raises(_lib.KarmaError):
             engine.Pairs.merge(ctx, bad, counts, runs=lens.tolist())
+
+
+def test_graph_records_split_call():
+    # karma_graph_records_begin/_end: same list as the one-call form; one open
+    # job per context (a second begin raises), and _end consumes the job
+    import ctypes
+    rng = np.random.default_rng(71)
+    n, A = 3000, 200_000
+    rid = np.sort(rng.integers(0, A // 3, A)).astype(np.uint32)
+    cid = rng.integers(0, n, A).astype(np.uint32)
+    rec = np.stack([rid, cid], 1)
+    ctx = _lib.default_context()
+    ref = engine.Pairs.from_records(ctx, rec, n)
+    k0, c0, _ = ref.get()
+    dev = ctypes.c_void_p()  # device records through the library's own allocator
+    _lib.call("karma_dev_alloc", ctx.h, rec.nbytes, ctypes.byref(dev))
+    try:
+        _lib.call("karma_memcpy", ctx.h, dev, _lib.ptr(rec), rec.nbytes, 0)
+        job = engine.Pairs.from_records_begin(ctx, n, dev.value, A)
+        with pytest.raises(_lib.KarmaError):
+            engine.Pairs.from_records_begin(ctx, n, dev.value, A)
+        p = job.end()
+        k1, c1, _ = p.get()
+        assert np.array_equal(k0, k1) and np.array_equal(c0, c1)
+        job2 = engine.Pairs.from_records_begin(ctx, n, dev.value, A)  # the context is free again
+        k2, c2, _ = job2.end().get()
+        assert np.array_equal(k0, k2) and np.array_equal(c0, c2)
+    finally:
+        _lib.load().karma_dev_free(ctx.h, dev)
