@@ -144,6 +144,15 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise KarmaError(KARMA_ERR_HIP, f"{LIB_PATH} not built — run `make -C karma_amd/csrc` "
                                         "(or __graft_entry__.build()); there is no CPU fallback")
+    # PyTorch-ROCm bundles its own HIP runtime under the same SONAME
+    # (libamdhip64.so.7): whichever is loaded first serves the whole process.
+    # Load torch's first, so torch (device buffers, streams, RCCL) and this
+    # library share the runtime torch was built against, whatever the import
+    # order of the caller.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, argtypes in _SIGS.items():
         fn = getattr(lib, name)
