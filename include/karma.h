@@ -169,6 +169,12 @@ int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* count
  * n_runs + 1 offsets starting at 0. */
 int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, const int64_t* run_off,
                            int n_runs, int is_device, karma_pairs** out);
+/* The exchange's wire format: n x {i64 key, i64 count} interleaved in device
+ * memory.  _get_kc writes the list in it (stream-ordered, not waited for);
+ * _merge_runs_kc merges received runs of it. */
+int karma_pairs_get_kc(karma_pairs* p, int64_t* kc_dev);
+int karma_pairs_merge_runs_kc(karma_ctx* ctx, const int64_t* kc_dev, const int64_t* run_off, int n_runs,
+                              karma_pairs** out);
 int karma_pairs_destroy(karma_pairs* p);
 /* Later kernels on p run on ctx's stream (after p's current stream is drained);
  * p's memory stays with the allocator that made it.  Lets a list built on a

@@ -79,6 +79,8 @@ _SIGS = {
     "karma_graph_eq": [_c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i64, _i32, _PP],
     "karma_pairs_merge": [_c_p, _c_p, _c_p, _i64, _i32, _PP],
     "karma_pairs_merge_runs": [_c_p, _c_p, _c_p, _c_p, _i32, _i32, _PP],
+    "karma_pairs_merge_runs_kc": [_c_p, _c_p, _c_p, _i32, _PP],
+    "karma_pairs_get_kc": [_c_p, _c_p],
     "karma_pairs_destroy": [_c_p],
     "karma_pairs_rebind": [_c_p, _c_p],
     "karma_pairs_count": [_c_p, _I64P],

@@ -196,6 +196,22 @@ __global__ void split_kernel(const uint64_t* __restrict__ keys, int64_t n, const
     starts[r] = lo;
 }
 
+// (key, count) pairs <-> separate key and count arrays (the exchange's wire format)
+__global__ void interleave_kc_kernel(const uint64_t* __restrict__ k, const int64_t* __restrict__ c, int64_t n,
+                                     longlong2* __restrict__ kc) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        kc[i] = make_longlong2((long long)k[i], (long long)c[i]);
+}
+
+__global__ void deinterleave_kc_kernel(const longlong2* __restrict__ kc, int64_t n, uint64_t* __restrict__ k,
+                                       int64_t* __restrict__ c) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const longlong2 v = kc[i];
+        k[i] = (uint64_t)v.x;
+        c[i] = (int64_t)v.y;
+    }
+}
+
 // keys sorted within each run [off[r], off[r + 1]): a descent is allowed only
 // where a run starts
 __global__ void runs_check_kernel(const uint64_t* __restrict__ k, int64_t n, const int64_t* __restrict__ off, int nr,
@@ -483,8 +499,8 @@ int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* count
     return KARMA_OK;
 }
 
-int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, const int64_t* run_off,
-                           int n_runs, int is_device, karma_pairs** out) {
+static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, const int64_t* kc,
+                           const int64_t* run_off, int n_runs, int is_device, karma_pairs** out) {
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(out && run_off && n_runs >= 1, KARMA_ERR_ARG, "karma_pairs_merge_runs: bad arguments");
     std::vector<int64_t> off(run_off, run_off + n_runs + 1);
@@ -492,7 +508,7 @@ int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
     for (int r = 0; r < n_runs; ++r)
         KARMA_CHECK(off[r] <= off[r + 1], KARMA_ERR_ARG, "karma_pairs_merge_runs: run offsets decrease");
     const int64_t n = off[n_runs];
-    KARMA_CHECK(n == 0 || (keys && counts), KARMA_ERR_ARG, "karma_pairs_merge_runs: null keys or counts");
+    KARMA_CHECK(n == 0 || (keys && counts) || kc, KARMA_ERR_ARG, "karma_pairs_merge_runs: null keys or counts");
     KARMA_CHECK(n < (int64_t(1) << 31), KARMA_ERR_ARG, "karma_pairs_merge_runs: %lld items exceed 2^31", (long long)n);
     auto* p = new karma_pairs();
     p->ctx = ctx;
@@ -506,6 +522,14 @@ int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
         KARMA_TRY(cb[1].alloc(ctx, n));
         KARMA_HIP(hipMemcpyAsync(kb[1].ptr, keys, n * 8, hipMemcpyHostToDevice, ctx->stream));
         KARMA_HIP(hipMemcpyAsync(cb[1].ptr, counts, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        sk = kb[1].ptr;
+        sc = cb[1].ptr;
+    }
+    if (kc && n) {  // interleaved device input: split once into the merge's first buffers
+        KARMA_TRY(kb[1].alloc(ctx, n));
+        KARMA_TRY(cb[1].alloc(ctx, n));
+        KARMA_LAUNCH(ctx, "merge_split", deinterleave_kc_kernel, std::min<int64_t>(grid1(n), 4096), 256, 0,
+                     reinterpret_cast<const longlong2*>(kc), n, kb[1].ptr, cb[1].ptr);
         sk = kb[1].ptr;
         sc = cb[1].ptr;
     }
@@ -588,6 +612,25 @@ int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
     KARMA_CHECK(!h[1], KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
     p->n = h[0];
     *out = guard.release();
+    return KARMA_OK;
+}
+
+int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, const int64_t* run_off,
+                           int n_runs, int is_device, karma_pairs** out) {
+    return merge_runs_impl(ctx, keys, counts, nullptr, run_off, n_runs, is_device, out);
+}
+
+int karma_pairs_merge_runs_kc(karma_ctx* ctx, const int64_t* kc_dev, const int64_t* run_off, int n_runs,
+                              karma_pairs** out) {
+    return merge_runs_impl(ctx, nullptr, nullptr, kc_dev, run_off, n_runs, 1, out);
+}
+
+int karma_pairs_get_kc(karma_pairs* p, int64_t* kc_dev) {
+    KARMA_CHECK(p && (kc_dev || p->n == 0), KARMA_ERR_ARG, "karma_pairs_get_kc: bad arguments");
+    KARMA_TRY(ctx_begin(p->ctx));
+    if (p->n)
+        KARMA_LAUNCH(p->ctx, "pairs_interleave", interleave_kc_kernel, std::min<int64_t>(grid1(p->n), 4096), 256, 0,
+                     p->keys.ptr, p->counts.ptr, p->n, reinterpret_cast<longlong2*>(kc_dev));
     return KARMA_OK;
 }
 

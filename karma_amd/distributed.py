@@ -269,24 +269,20 @@ class HipOps:
         return self.engine.Pairs.from_records(self.ctx, None, n_contigs, grouped=True, device_ptr=records,
                                               n_records=n_records)
 
-    def pairs_split(self, pairs, bounds):
+    def pairs_kc_split(self, pairs, bounds):
+        """The list as interleaved (key, count) int64 pairs [n, 2] (the exchange's
+        wire format, written on the device) and the owners' start offsets."""
         t = self.torch
         starts = pairs.split(bounds)
         n = pairs.count()
-        keys = t.empty(max(n, 1), dtype=t.int64, device=self.dev)
-        counts = t.empty(max(n, 1), dtype=t.int64, device=self.dev)
-        if n:
-            from ._lib import call
-            import ctypes
-            call("karma_pairs_get", pairs.h, ctypes.c_void_p(keys.data_ptr()), ctypes.c_void_p(counts.data_ptr()),
-                 None, 1)
-        return keys[:n], counts[:n], starts
+        kc = t.empty((max(n, 1), 2), dtype=t.int64, device=self.dev)
+        pairs.get_kc(kc.data_ptr() if n else None)
+        return kc[:n], starts
 
-    def merge(self, keys, counts, runs):
-        """The owner's list from the senders' slices (runs: their lengths, each sorted)."""
-        return self.engine.Pairs.merge(self.ctx, keys.data_ptr() if keys.numel() else None,
-                                       counts.data_ptr() if counts.numel() else None, device=True, n=keys.numel(),
-                                       runs=runs)
+    def merge_kc(self, kc, runs):
+        """The owner's list from the senders' slices of interleaved pairs (runs: their lengths, each sorted)."""
+        kc = kc.contiguous()
+        return self.engine.Pairs.merge_runs_kc(self.ctx, kc.data_ptr() if kc.numel() else None, runs)
 
     def totals(self, pairs, n_contigs):
         tot = self.torch.zeros(n_contigs, dtype=self.torch.int64, device=self.dev)
@@ -421,17 +417,14 @@ class ShardedBuild:
             stats["pairs_local"] = ops.pair_count(local)
         if comm.world > 1 or self.emulate:
             if comm.world > 1:
-                keys, counts, starts = ops.pairs_split(local, self.bounds)
                 # one all-to-all-v of interleaved (key, count) int64 pairs; the
                 # owner receives one sorted slice per sender and merges them
-                import torch
-                kc, recv = comm.alltoallv(torch.stack([keys, counts], 1).reshape(-1), 2 * np.diff(starts))
-                kc = kc.reshape(-1, 2)
-                merged = ops.merge(kc[:, 0].contiguous(), kc[:, 1].contiguous(), [r // 2 for r in recv])
+                kc, starts = ops.pairs_kc_split(local, self.bounds)
+                recv_kc, recv = comm.alltoallv(kc.reshape(-1), 2 * np.diff(starts))
+                merged = ops.merge_kc(recv_kc, [r // 2 for r in recv])
             else:  # emulation: this rank's own W slices stand in for the W received ones
-                keys, counts, starts = ops.pairs_split(local, np.linspace(0, self.n_glob, self.emulate + 1)
-                                                       .astype(np.int64))
-                merged = ops.merge(keys, counts, np.diff(starts).tolist())
+                kc, starts = ops.pairs_kc_split(local, np.linspace(0, self.n_glob, self.emulate + 1).astype(np.int64))
+                merged = ops.merge_kc(kc.reshape(-1), np.diff(starts).tolist())
             # the owner's merged list holds the diagonal (a, a) of every a it owns:
             # complete readset sizes for its slice, gathered to every rank
             tot = comm.allgather_slices_(ops.totals(merged, self.n_glob), self.bounds)

@@ -263,6 +263,20 @@ class Pairs:
         return cls(ctx, h)
 
     @classmethod
+    def merge_runs_kc(cls, ctx, kc_dev_ptr, runs):
+        """Merge received runs of interleaved (key, count) int64 pairs in device memory."""
+        off = np.zeros(len(runs) + 1, np.int64)
+        np.cumsum(np.asarray(runs, np.int64), out=off[1:])
+        h = ctypes.c_void_p()
+        call("karma_pairs_merge_runs_kc", ctx.h, ctypes.c_void_p(kc_dev_ptr) if kc_dev_ptr else None, ptr(off),
+             len(runs), ctypes.byref(h))
+        return cls(ctx, h)
+
+    def get_kc(self, kc_dev_ptr):
+        """Interleaved (key, count) int64 pairs into device memory (stream-ordered)."""
+        call("karma_pairs_get_kc", self.h, ctypes.c_void_p(kc_dev_ptr) if kc_dev_ptr else None)
+
+    @classmethod
     def merge(cls, ctx, keys, counts, device=False, n=None, runs=None):
         """Sorted unique (key, count) list.  runs = lengths of consecutive runs that
         are each sorted by key (an exchange owner's received slices): merged by a

@@ -140,6 +140,14 @@ class OracleOps:
         return (torch.from_numpy(pairs["keys"].view(np.int64).copy()), torch.from_numpy(pairs["counts"].copy()),
                 starts)
 
+    def pairs_kc_split(self, pairs, bounds):
+        keys, counts, starts = self.pairs_split(pairs, bounds)
+        return torch.stack([keys, counts], 1), starts
+
+    def merge_kc(self, kc, runs):
+        kc = kc.reshape(-1, 2)
+        return self.merge(kc[:, 0].contiguous(), kc[:, 1].contiguous(), runs)
+
     def merge(self, keys, counts, runs):
         k = keys.numpy().view(np.uint64)
         # the contract of karma_pairs_merge_runs: one sorted slice per sender

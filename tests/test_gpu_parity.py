@@ -352,6 +352,25 @@ def test_merge_runs_and_split(seed, n_runs, n):
         bounds = [0, 200_000, 300_000, 400_000, n_contigs]
         assert np.array_equal(p.split(bounds), np.searchsorted(u, np.array(bounds, np.uint64) << np.uint64(32)))
         p.close()
+    # the exchange's wire format: interleaved (key, count) pairs in device memory
+    import ctypes
+    kc = np.stack([keys.view(np.int64), counts], 1).copy()
+    dev = ctypes.c_void_p()
+    _lib.call("karma_dev_alloc", ctx.h, max(16, kc.nbytes), ctypes.byref(dev))
+    try:
+        if n:
+            _lib.call("karma_memcpy", ctx.h, dev, _lib.ptr(kc), kc.nbytes, 0)
+        p = engine.Pairs.merge_runs_kc(ctx, dev.value if n else None, lens.tolist())
+        k3, c3, _ = p.get()
+        assert np.array_equal(k3, u) and np.array_equal(c3, c)
+        p.get_kc(dev.value if len(u) else None)  # and back out in the same format
+        back = np.zeros((len(u), 2), np.int64)
+        if len(u):
+            _lib.call("karma_memcpy", ctx.h, _lib.ptr(back), dev, back.nbytes, 1)
+        assert np.array_equal(back[:, 0].view(np.uint64), u) and np.array_equal(back[:, 1], c)
+        p.close()
+    finally:
+        _lib.load().karma_dev_free(ctx.h, dev)
     if n > 1 and lens.max() > 1:
         r = int(np.argmax(lens))
         bad = keys.copy()
