@@ -197,7 +197,7 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 }
 
 #ifndef KARMA_CLS2_WAVES
-#define KARMA_CLS2_WAVES 5  // 5: no spills at 96 VGPRs (0.504 vs 0.518 ms at 6 with 80)
+#define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
 template <bool HIST>  // HIST: per-block code-bucket histograms for code_append_kernel
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
