@@ -72,6 +72,7 @@ _SIGS = {
     "karma_kmer_profile": [_c_p, _c_p, _i64, _i32],
     "karma_kmer_profile_side": [_c_p, _c_p, _i64, _c_p],
     "karma_ctx_join": [_c_p, _c_p],
+    "karma_ctx_set_side_headroom": [_c_p, _i32],
     "karma_kmer_row_totals": [_c_p, _c_p],
     "karma_graph_records": [_c_p, _c_p, _i64, _i64, _i32, _i32, _PP],
     "karma_graph_records_begin": [_c_p, _c_p, _i64, _i64, _i32, _i32, _PP],
@@ -205,6 +206,9 @@ class Context:
 
     def sync(self):
         call("karma_ctx_sync", self.h)
+
+    def set_side_headroom(self, blocks_per_cu):
+        call("karma_ctx_set_side_headroom", self.h, int(blocks_per_cu))
 
     def join(self, side_stream_ptr):
         """This context's stream waits (on the device) for work on a side stream."""

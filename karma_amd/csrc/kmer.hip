@@ -1184,9 +1184,6 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
     return KARMA_OK;
 }
 
-#ifndef KARMA_SIDE_HEADROOM
-#define KARMA_SIDE_HEADROOM 1
-#endif
 int karma_kmer_profile_side(karma_kmer_plan* p, double* out_dev, int64_t ld, void* side) {
     KARMA_CHECK(p, KARMA_ERR_ARG, "null plan");
     karma_ctx* ctx = p->ctx;
@@ -1209,11 +1206,17 @@ int karma_kmer_profile_side(karma_kmer_plan* p, double* out_dev, int64_t ld, voi
     ctx->stream = s;  // launches and timing events go to the side stream
     // its one-round grid leaves a block slot per CU, so the main stream's
     // short kernels find room beside it instead of queueing behind it
-    ctx->grid_headroom = KARMA_SIDE_HEADROOM;
+    ctx->grid_headroom = ctx->side_headroom;
     const int rc = karma_kmer_profile(p, out_dev, ld, 1);
     ctx->grid_headroom = 0;
     ctx->stream = main_stream;
     return rc;
+}
+
+int karma_ctx_set_side_headroom(karma_ctx* ctx, int blocks_per_cu) {
+    KARMA_CHECK(ctx && blocks_per_cu >= 0, KARMA_ERR_ARG, "karma_ctx_set_side_headroom: bad arguments");
+    ctx->side_headroom = blocks_per_cu;
+    return KARMA_OK;
 }
 
 int karma_ctx_join(karma_ctx* ctx, void* side) {

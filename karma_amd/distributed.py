@@ -367,6 +367,11 @@ class ShardedBuild:
         # exchange and weights on the main stream.  The side stream is joined
         # before anything uses the plan or the profile.
         side = self._pool is None and hasattr(ops, "graph_begin")
+        if side:
+            # one GPU: nothing but short kernels share the chip with the profile,
+            # which then takes all of it (1.35 vs 1.36-1.39 ms/step); with an
+            # exchange, a block slot per CU stays free for its collectives
+            ops.ctx.set_side_headroom(1 if self.comm.world > 1 or self.emulate else 0)
         try:
             return self._run(store, records, n_records, keep, side)
         finally:
