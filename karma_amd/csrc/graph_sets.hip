@@ -1502,6 +1502,9 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
 // block readback; end() waits, checks, reruns on a full pair list, and
 // assembles.  Between the two the host may enqueue unrelated work (the k-mer
 // profile on a side stream).
+#ifndef KARMA_MARK_AT
+#define KARMA_MARK_AT 0
+#endif
 struct SetsJob {
     karma_ctx* ctx = nullptr;
     const uint2* rec = nullptr;
@@ -1633,16 +1636,18 @@ int SetsJob::launch() {
         else
             KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<false>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
     }
-#ifndef KARMA_MARK_AFTER_CLASSIFY
-// 1: the side-stream profile may start right after classify.  Measured off:
-// sharing the chip slows the code partition 0.19 -> 0.5 ms (1.46 vs 1.37 ms/step)
-#define KARMA_MARK_AFTER_CLASSIFY 0
-#endif
-    if (KARMA_MARK_AFTER_CLASSIFY && attempt == 0) {  // side-stream work (the k-mer profile) may start once classify is done
+    // where side-stream work (the k-mer profile) may start: 0 = after the whole
+    // pipeline (default), 1 = after classify, 2 = after the code partition.
+    // Measured: 1 slows the code partition 0.19 -> 0.5 ms (1.46 vs 1.37 ms/step);
+    // 2 stretches the profile to 0.60 ms beside the reduce (1.43 vs 1.35)
+    auto mark = [&](int at) -> int {
+        if (KARMA_MARK_AT != at || attempt != 0) return KARMA_OK;
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
         KARMA_HIP(hipEventRecord(ctx->mark_ev, ctx->stream));
         ctx->mark_set = true;
-    }
+        return KARMA_OK;
+    };
+    KARMA_TRY(mark(1));
     if (A == 0) {
         KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
@@ -1665,6 +1670,7 @@ int SetsJob::launch() {
         else
             KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr, kCChunk,
                          n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
+        KARMA_TRY(mark(2));
         KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
                      g.Bc, g.bwc, n_cg, part_ch.ptr);
     }
