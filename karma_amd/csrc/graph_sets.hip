@@ -1532,7 +1532,7 @@ struct SetsJob {
     DevArray<uint16_t> cent;
     DevArray<int64_t> cf_base;
     DevArray<uint32_t> cf_off;
-    DevArray<unsigned long long> blk_items;  // per partition block: codes, pairs
+    unsigned long long* blk_items = nullptr;  // per partition block: codes, pairs (after the control block)
     DevArray<uint32_t> blk_hist;             // per partition block: codes per code bucket (append)
     int64_t pcap = kCChunk / 8;
     DevArray<uint64_t> plist;
@@ -1575,7 +1575,10 @@ int SetsJob::setup() {
     KARMA_TRY(n_pl.alloc(ctx, n_chunks));
     KARMA_TRY(big_list.alloc(ctx, A / (kMaxFast + 1) + 1));
     ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8);
-    KARMA_TRY(ctrl.alloc(ctx, ctrl_words));
+    // one allocation (and one memset per attempt) for the control block and
+    // the per-partition-block item counts behind it
+    KARMA_TRY(ctrl.alloc(ctx, ctrl_words + 2 * n_pblk));
+    blk_items = reinterpret_cast<unsigned long long*>(ctrl.ptr + ctrl_words);
     flags = reinterpret_cast<int*>(ctrl.ptr);
     counters = reinterpret_cast<unsigned*>(ctrl.ptr + 2);
     n_per = ctrl.ptr + 6;
@@ -1588,7 +1591,6 @@ int SetsJob::setup() {
     // flushes only a full buffer, and once at its end
     max_cflush = n_pblk + ceil_div(A, CodeStream::kCap) + 1;
     ccap = A + max_cflush * (8 * (int64_t)g.Bc + 8);
-    KARMA_TRY(blk_items.alloc(ctx, 2 * n_pblk));
     if (append) KARMA_TRY(blk_hist.alloc(ctx, n_pblk * g.Bc));
     if (g.Bc > 0) {
         KARMA_TRY(cent.alloc(ctx, ccap + 16));
@@ -1624,12 +1626,11 @@ int SetsJob::launch() {
     KARMA_TRY(pent.alloc(ctx, pscap + 8));
     KARMA_TRY(pf_base.alloc(ctx, max_pflush));
     KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
-    KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, ctrl_words * 8, ctx->stream));
-    KARMA_HIP(hipMemsetAsync(blk_items.ptr, 0, 2 * n_pblk * 8, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk) * 8, ctx->stream));
     if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
     if (A > 0) {
         ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
-                    n_gen.ptr, blk_items.ptr, lpb, big_list.ptr, counters, flags,
+                    n_gen.ptr, blk_items, lpb, big_list.ptr, counters, flags,
                     append ? blk_hist.ptr : nullptr, g.bwc, g.Bc};
         if (append)
             KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<true>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
@@ -1653,9 +1654,9 @@ int SetsJob::launch() {
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
     }
     KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
-                 codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_pblk, lpb, flags);
-    const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items.ptr};
-    pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items.ptr + n_pblk};
+                 codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items + n_pblk, lpb, flags);
+    const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items};
+    pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items + n_pblk};
     if (g.Bc > 0) {
         uint16_t* const trash = cent.ptr + (ccap + 7) / 8 * 8;
         if (append && wide_c)
