@@ -6,17 +6,22 @@ One step = the whole hot path over one batch of device-resident synthetic input
   k-mer profile of 200k contigs (mean 800 bp, k = 5p6): presence pass, column
   table, dense float64 profile (N x M) written to HBM;
   shared-read graph of 100M paired fragments (~309M (read, contig) records):
-  one partition pass (a read -> one 2-byte (m0, M) code, or its pairs),
-  LDS histogram / hash reduces, per-bucket merge, weights.
+  one classification pass (a read -> one 2-byte (m0, M) code, or its pairs),
+  partition, LDS histogram / hash reduces, per-bucket merge, weights.
 Inputs (2-bit packed contigs + records) are resident in HBM before timing.
 
-Multi-GPU (torchrun, one rank per GPU): weak scaling — rank r owns contig rows
-[r*200k, (r+1)*200k) and fragments [r*100M, (r+1)*100M) of a global problem
-whose genes span all ranks; the step adds the presence OR-allreduce, the edge
-partial all-to-all (pre-reduced pairs routed to the owner of contig a) and the
-totals allgather over RCCL (karma_amd/distributed.py).
+Multi-GPU (torchrun, one rank per GPU, the library's own RCCL communicator;
+no PyTorch in the process):
+  default (weak)  rank r owns contig rows [r*200k, (r+1)*200k) and fragments
+                  [r*100M, (r+1)*100M) of a global problem whose genes span all
+                  ranks;
+  --strong        BASELINE configs[3]: config 3 itself (200k contigs, 100M
+                  fragments) divided over the N ranks.
+The step adds the presence all-gather, the exception-key all-gather, the edge
+partial all-to-all-v (pre-reduced pairs routed to the owner of contig a) and
+the totals all-gather (karma_amd/distributed.py, karma_amd/comm.py).
 
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0 (DESIGN.md §5 defines every field).
 """
 
 import argparse
@@ -33,6 +38,9 @@ sys.path.insert(0, REPO)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # kernels with an algorithmic-bytes figure: the roofline kernel is the slowest of these
 ROOFLINE_KERNELS = ("kmer_profile", "kmer_presence", "graph_classify", "graph_code_partition", "graph_code_reduce")
+# reference Python (karma/kmer.py:199-264 + read_graph.py:61-148, the path karma.py:197-240
+# runs) on config 3, measured in the survey container: ~300 s profile + 3.41 s graph
+REF_PY_CONFIG3_S = 300.0 + 3.41
 
 CONFIGS = {
     # name: (seed, contigs per GPU, fragments per GPU, paired, kmer)
@@ -50,21 +58,61 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-sample", type=float, default=0.1,
-                    help="fraction of the per-GPU workload the CPU baseline processes (0 disables)")
-    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling (BASELINE configs[3]): the config's contigs and fragments divided over "
+                         "the ranks (or over --emulate-ranks)")
     ap.add_argument("--emulate-ranks", type=int, default=1,
-                    help="diagnostic: one process runs rank 0's compute of a W-rank weak-scaled problem "
-                         "(global contig ids over W x the per-GPU contigs; the exchange's local work - device split, "
-                         "merge of W sorted slices, totals - without its collectives); not the metric")
+                    help="diagnostic: one process runs rank 0's compute of a W-rank problem (weak: global contig "
+                         "ids over W x the per-GPU contigs; --strong: 1/W of the config) with the exchange's local "
+                         "work (device split, merge of W sorted slices, totals) and no collectives; not the metric")
+    ap.add_argument("--shuffle-contigs", action="store_true",
+                    help="secondary number: contig ids randomly permuted (a FASTA without isoform adjacency; same "
+                         "graph up to relabelling)")
+    ap.add_argument("--cpu-baseline", choices=("full", "off"), default="full",
+                    help="full: the oracle's OpenMP twin on the whole per-GPU workload (rank 0, N = 1)")
+    ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end and eq-path legs")
     return ap.parse_args()
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def shard(total, world, rank):
+    return total * rank // world, total * (rank + 1) // world
+
+
+def make_inputs(args, rank, world):
+    """This rank's contigs and records.  Returns a dict (see keys below)."""
+    from karma_amd import engine
+
+    seed, n_cfg, f_cfg, paired, kmer = CONFIGS[args.config]
+    emu = max(1, args.emulate_ranks) if world == 1 else 1
+    parts = world * emu
+    if args.strong:
+        n_glob, f_glob = n_cfg, f_cfg
+        c_lo, c_hi = shard(n_glob, parts, rank)
+        f_lo, f_hi = shard(f_glob, parts, rank)
+    else:
+        n_glob, f_glob = n_cfg * parts, f_cfg * parts
+        c_lo, c_hi = rank * n_cfg, (rank + 1) * n_cfg
+        f_lo, f_hi = rank * f_cfg, (rank + 1) * f_cfg
+    blob, offs, key_len = engine.synth_contigs(seed, c_hi - c_lo, 400, 800, 0, first=c_lo)
+    genes = engine.synth_genes(seed, n_glob)
+    rec = engine.synth_records(seed, n_glob, f_lo, f_hi, paired, genes=genes)
+    perm = None
+    if args.shuffle_contigs:
+        # the same graph with contig ids relabelled by a fixed random permutation
+        perm = np.random.default_rng(12345).permutation(n_glob).astype(np.uint32)
+        rec = np.ascontiguousarray(rec)
+        rec[:, 1] = perm[rec[:, 1]]
+    return dict(seed=seed, paired=paired, kmer=kmer, emu=emu, n_glob=n_glob, f_glob=f_glob, c_lo=c_lo,
+                n_loc=c_hi - c_lo, f_lo=f_lo, f_loc=f_hi - f_lo, blob=blob, offs=offs, key_len=key_len,
+                genes=genes, rec=rec, perm=perm)
 
 
 def main():
@@ -75,40 +123,31 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
-    import torch
+    from karma_amd import _lib, comm as comm_mod, engine
+    from karma_amd.distributed import ShardedBuild
 
-    from karma_amd import _lib, engine
-    from karma_amd.distributed import Comm, ShardedBuild
-
-    seed, n_loc, f_loc, paired, kmer = CONFIGS[args.config]
     # KARMA_FORCE_DEVICE pins every rank to one device (multi-rank rehearsal on
-    # a 1-GPU box together with KARMA_DIST_BACKEND=gloo); unset in real runs
+    # a 1-GPU box together with KARMA_DIST_BACKEND=host); unset in real runs
     dev_index = int(os.environ.get("KARMA_FORCE_DEVICE", local_rank if world > 1 else 0))
-    comm = Comm.create(world, rank, dev_index)
     ctx = _lib.Context(dev_index)
-    torch.cuda.set_device(dev_index)
+    comm = comm_mod.create(ctx, world, rank)
 
-    # ---------------- synthetic input (host), then resident in HBM ----------------
     t_gen = time.time()
-    emu = max(1, args.emulate_ranks) if world == 1 else 1
-    n_glob, f_glob = n_loc * world * emu, f_loc * world * emu
-    c_lo = rank * n_loc
-    blob, offs, key_len = engine.synth_contigs(seed, n_loc, 400, 800, 0, first=c_lo)
-    genes = engine.synth_genes(seed, n_glob)
-    rec = engine.synth_records(seed, n_glob, rank * f_loc, (rank + 1) * f_loc, paired, genes=genes)
-    A = len(rec)
-    log(f"[rank {rank}] generated {n_loc} contigs ({int(offs[-1])} bases), {f_loc} fragments, {A} records "
+    inp = make_inputs(args, rank, world)
+    A = len(inp["rec"])
+    n_loc, f_loc = inp["n_loc"], inp["f_loc"]
+    log(f"[rank {rank}] generated {n_loc} contigs ({int(inp['offs'][-1])} bases), {f_loc} fragments, {A} records "
         f"in {time.time() - t_gen:.1f}s")
 
-    build = ShardedBuild(ctx, comm, engine.kmode_of(kmer), n_glob, c_lo, n_loc,
-                         emulate_ranks=emu)  # sets the shared stream
-    store = engine.ContigStore(ctx, blob, offs, key_len)
-    rec_dev = torch.from_numpy(rec.view(np.int64).reshape(-1)).to(build.ops.dev)
-    torch.cuda.synchronize()
-    packed_bytes = int(np.sum((np.diff(offs) + 3) // 4))  # sum ceil(L/4)
+    build = ShardedBuild(ctx, comm, engine.kmode_of(inp["kmer"]), inp["n_glob"], inp["c_lo"], n_loc,
+                         emulate_ranks=inp["emu"])  # sets the library-owned main + side streams
+    store = engine.ContigStore(ctx, inp["blob"], inp["offs"], inp["key_len"])
+    rec_dev = _lib.DevBuf.from_numpy(ctx, inp["rec"].view(np.int64).reshape(-1))
+    ctx.sync()
+    packed_bytes = int(np.sum((np.diff(inp["offs"]) + 3) // 4))  # sum ceil(L/4)
 
-    def step(keep=False):
-        return build.run(store, rec_dev.data_ptr(), A, keep=keep)
+    def step(keep=False, sequential=False):
+        return build.run(store, rec_dev.ptr, A, keep=keep, sequential=sequential)
 
     ctxs = build.contexts()  # main context (+ the concurrent graph build's)
 
@@ -116,42 +155,38 @@ def main():
         for c in ctxs:
             c.sync()
 
-    def timed_pass(only=None):
-        """args.steps steps with HIP-event timing (all kernels, or one) -> {kernel: (ms, launches)}."""
+    for _ in range(args.warmup):
+        step()
+    sync_all()
+    # Per-kernel breakdown, outside the timed region, with every launch timed
+    # and the profile on the main stream (sequential): kernels do not share the
+    # chip, so no launch is charged for time it spent queued behind another.
+    kern = {}
+    if not args.no_timing:
         for c in ctxs:
-            c.timing(True, only)
+            c.timing(True)
             c.timing_reset()
         for _ in range(args.steps):
-            step()
+            step(sequential=True)
         sync_all()
-        kern = {}
         for c in ctxs:
             for name, (ms, nl) in c.timing_read().items():
                 prev = kern.get(name, (0.0, 0))
                 kern[name] = (prev[0] + ms, prev[1] + nl)
             c.timing(False)
-        return kern
-
-    for _ in range(args.warmup):
-        step()
-    sync_all()
-    # per-kernel breakdown (events on every launch), outside the timed region
-    kern = timed_pass() if not args.no_timing else {}
     dom = max((k for k in kern if k in ROOFLINE_KERNELS), key=lambda k: kern[k][0], default=None)
-    # timed region: events only around the dominant kernel's launches (two
-    # per launch), so the wall time carries almost no instrumentation
+    # timed region: the production order (profile on the side stream), with
+    # events only around the dominant kernel's launches (two per launch)
     if dom:
         for c in ctxs:
             c.timing(True, dom)
             c.timing_reset()
     comm.barrier()
-    torch.cuda.synchronize()
     sync_all()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
     sync_all()
-    torch.cuda.synchronize()
     comm.barrier()
     t1 = time.perf_counter()
     dt = comm.max_float(t1 - t0)
@@ -162,36 +197,51 @@ def main():
             if got:
                 dom_live = got if dom_live is None else (dom_live[0] + got[0], dom_live[1] + got[1])
             c.timing(False)
+    rec = inp["rec"]
     n_reads = int(np.count_nonzero(rec[1:, 0] != rec[:-1, 0])) + 1 if A else 0
 
-    units = world * (n_loc + f_loc) * args.steps
+    units = comm.sum_int(n_loc + f_loc) * args.steps
     value = units / dt
     M = res["M"]
     E = comm.sum_int(res["E_local"])
-    # algorithmic bytes per launch, DESIGN.md §Measurement
+    # algorithmic bytes per launch; intermediates are diagnostic only
     per_kernel_bytes = {
         "kmer_profile": packed_bytes + 8 * n_loc * M,
         "kmer_presence": packed_bytes,
-        # records read once, one 4-byte code per (compact) read written
-        "graph_classify": 8 * A + 4 * n_reads,
-        # codes read, 2-byte bucket-local codes written
-        "graph_code_partition": 6 * n_reads,
+        "graph_classify": 8 * A,  # the records, read once
+    }
+    intermediate_bytes = {
+        "graph_classify": 4 * n_reads,  # one 4-byte code per compact read written
+        "graph_code_partition": 6 * n_reads,  # codes read, 2-byte bucket-local codes written
         "graph_code_reduce": 2 * n_reads,
     }
     roof = None
-    if dom_live and dom in per_kernel_bytes:
+    if dom_live:
         ms, nl = dom_live
         avg_s = ms / nl / 1e3
-        achieved = per_kernel_bytes[dom] / avg_s / 1e9
+        b = per_kernel_bytes.get(dom, 0)
+        achieved = b / avg_s / 1e9
+        traffic = pmc_traffic(args, world, dom)
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS,
-                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": pmc_traffic(dom),
-                "bytes_per_launch": per_kernel_bytes[dom], "avg_launch_ms": round(ms / nl, 4)}
+                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                "traffic": traffic, "bytes_per_launch": b,
+                "intermediate_bytes_per_launch": intermediate_bytes.get(dom, 0),
+                "avg_launch_ms": round(ms / nl, 4), "launches": nl}
     step_bytes = packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
+    step_s = dt / args.steps
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_e2e and inp["emu"] == 1 and not args.shuffle_contigs:
+        extra = end_to_end_legs(args, inp, ctx, build, store)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(seed, n_loc, f_loc, paired, kmer, args.cpu_sample, blob, offs, rec)
+    if rank == 0 and world == 1 and args.cpu_baseline != "off":
+        cpu = cpu_baseline(inp)
+    build.close()
+    store.close()
+    rec_dev.close()
 
     if rank == 0:
+        emu = inp["emu"]
+        ref_py_units_s = (200_000 + 100_000_000) / REF_PY_CONFIG3_S
         line = {
             "metric": "contigs+reads/sec for k-mer vec + shared-read graph build; HBM GB/s vs roofline",
             "value": round(value, 1),
@@ -199,64 +249,149 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "ms_per_step": round(step_s * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
+            "scaling": "strong" if args.strong else "weak",
+            # BASELINE.md publishes no number; this is the reference Python measured in
+            # the survey container on config 3, see vs_baseline_basis
+            "vs_baseline": round(value / ref_py_units_s, 1) if args.config == "config3" else None,
+            "vs_baseline_basis": (f"reference Python karma/kmer.py:199-264 + read_graph.py:61-148 on config 3 "
+                                  f"(BASELINE.md, survey container, 8 cores): {REF_PY_CONFIG3_S} s = "
+                                  f"{ref_py_units_s:.0f} units/s; not a published number"),
             "dtype": "u32 keys / i64 counts / f64 div",
-            "data": "synthetic (SplitMix64 generator, SURVEY.md §8(d))",
-            "config": {"workload": f"{args.config}: {n_loc} contigs (mean 800 bp) + {f_loc} "
-                                   f"{'paired' if paired else 'single-end'} fragments per GPU, k={kmer}",
-                       "contigs_per_gpu": n_loc, "fragments_per_gpu": f_loc, "records_per_gpu": A,
+            "data": "synthetic (SplitMix64 generator, SURVEY.md §8(d))"
+                    + (", contig ids shuffled" if args.shuffle_contigs else ""),
+            "config": {"workload": f"{args.config}{' strong' if args.strong else ''}: {n_loc} contigs (mean 800 bp) "
+                                   f"+ {f_loc} {'paired' if inp['paired'] else 'single-end'} fragments on rank 0 "
+                                   f"(global {inp['n_glob']} contigs / {inp['f_glob']} fragments), k={inp['kmer']}",
+                       "contigs_rank0": n_loc, "fragments_rank0": f_loc, "records_rank0": A,
                        "columns_M": M, "edges": E, "parallelism": f"contig+fragment shards x{world}",
-                       **({"emulated_ranks": emu, "global_contigs": n_glob} if emu > 1 else {})},
+                       **({"emulated_ranks": emu, "global_contigs": inp["n_glob"]} if emu > 1 else {})},
             "roofline": roof,
-            "step_hbm_bytes_per_gpu": step_bytes,
-            "step_achieved_GBs_per_gpu": round(step_bytes / (dt / args.steps) / 1e9, 1),
+            "step": {"hbm_bytes_per_gpu": step_bytes, "achieved_GBs": round(step_bytes / step_s / 1e9, 1),
+                     "frac": round(step_bytes / step_s / 1e9 / PEAK_HBM_GBS, 4),
+                     "formula": "sum ceil(L/4) + 8*N*M + 8*A + 16*E + 8*N (SURVEY.md 8(d))"},
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in kern.items()},
+            "kernels_ms_note": "sequential pass (profile on the main stream), every launch timed",
+            **extra,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    build.close()
-    store.close()
     comm.close()
+    ctx.close()
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+def pmc_traffic(args, world, kernel):
+    """HBM bytes per launch of `kernel` from a rocprofv3 PMC run of THIS
+    workload (profiles/pmc_traffic.json, written by tools/pmc_traffic.py and
+    keyed by workload), else None."""
+    key = f"{args.config}{'_strong' if args.strong else ''}{'_shuffled' if args.shuffle_contigs else ''}" \
+          f"_n{world * max(1, args.emulate_ranks)}"
     try:
-        with open(path) as f:
-            return json.load(f).get(kernel)
+        with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f).get(key, {}).get(kernel)
     except (OSError, ValueError):
         return None
 
 
-def cpu_baseline(seed, n_loc, f_loc, paired, kmer, frac, blob, offs, rec):
-    """Oracle (single-threaded C restatement, oracle/) on a bounded sample."""
-    try:
-        from collections import OrderedDict
+def end_to_end_legs(args, inp, ctx, build, store):
+    """Host-resident inputs -> host-resident outputs, as the drop-in classes see
+    them (kmer.py:264 returns a host ndarray; read_graph.py returns a graph):
+      records leg  FASTA text -> karma_fasta_parse -> pack/H2D -> profile -> D2H,
+                   and host records -> H2D -> graph -> edges D2H
+      eq leg       the path karma.py:240 calls (read_graph.py:61-148): this
+                   rank's fragments as salmon eq classes -> karma_graph_eq ->
+                   edges D2H."""
+    from karma_amd import _lib, engine, ingest
 
+    out = {}
+    n, blob, offs = inp["n_loc"], inp["blob"], inp["offs"]
+    # FASTA text of the contigs (one sequence line each)
+    names = [f">ctg{inp['c_lo'] + i}".encode() for i in range(n)]
+    seqb = bytes(blob[: int(offs[-1])])
+    parts = []
+    for i in range(n):
+        parts.append(names[i])
+        parts.append(seqb[int(offs[i]):int(offs[i + 1])])
+    fasta = b"\n".join(parts) + b"\n"
+    rec = inp["rec"]
+    kmode = engine.kmode_of(inp["kmer"])
+    prof_host = np.empty((n, 1), np.float64)
+
+    def e2e_once():
+        nonlocal prof_host
+        t0 = time.perf_counter()
+        fr = ingest.parse_fasta(fasta)
+        st = engine.ContigStore(ctx, fr.seq, fr.seq_off, fr.key_len)
+        plan = engine.KmerPlan(ctx, st, kmode)
+        M = plan.finalize()
+        if prof_host.shape != (n, M):
+            prof_host = np.empty((n, M), np.float64)
+        _lib.call("karma_kmer_profile", plan.h, _lib.ptr(prof_host), M, 0)
+        p = engine.Pairs.from_records(ctx, rec, inp["n_glob"])
+        e = p.edges(_lib.KARMA_MODE_READS, inp["n_glob"])
+        ea = e.get()
+        for x in (e, p, plan, st):
+            x.close()
+        return time.perf_counter() - t0, len(fasta), len(ea.a)
+
+    e2e_once()  # warm (allocator, pinned staging)
+    ts = [e2e_once() for _ in range(3)]
+    t = min(x[0] for x in ts)
+    out["end_to_end"] = {
+        "value": round((n + inp["f_loc"]) / t, 1), "unit": "(contigs+fragments)/s", "ms": round(t * 1e3, 2),
+        "includes": "FASTA parse (C++, host) + H2D + pack + profile + D2H of the f64 profile; host records H2D + "
+                    "graph + edge D2H",
+        "fasta_bytes": ts[0][1], "profile_bytes_d2h": int(prof_host.nbytes)}
+    # eq leg (read_graph.py:61-148)
+    cls_off, members, counts = engine.synth_eq_classes(inp["seed"], inp["n_glob"], inp["f_lo"],
+                                                       inp["f_lo"] + inp["f_loc"], inp["paired"], genes=inp["genes"])
+    skip = (np.diff(cls_off) == 1).astype(np.uint8)  # eq_size token "1"
+
+    def eq_once():
+        t0 = time.perf_counter()
+        e = engine.graph_from_eq(cls_off, members, counts, skip, inp["n_glob"], ctx=ctx)
+        return time.perf_counter() - t0, len(e.a)
+
+    eq_once()
+    te = [eq_once() for _ in range(5)]
+    out["eq_path"] = {"ms": round(min(x[0] for x in te) * 1e3, 3), "classes": int(len(counts)),
+                      "members": int(len(members)), "edges": te[0][1],
+                      "includes": "host eq arrays -> H2D -> sort/reduce -> weights -> edges D2H",
+                      "value": round((n + inp["f_loc"]) / min(x[0] for x in te), 1)}
+    return out
+
+
+def cpu_baseline(inp):
+    """The oracle's OpenMP twin (oracle/oracle.c, same arithmetic as the scalar
+    restatement) on the FULL per-GPU workload: profile of every contig + the
+    readset graph of every fragment, on all host cores."""
+    try:
         from oracle import oracle
     except Exception as e:  # oracle not built on this box
         return {"error": f"oracle unavailable: {e}"}
-    ns = max(1, int(n_loc * frac))
-    fs = max(1, int(f_loc * frac))
-    seqs = OrderedDict((f">ctg{i}", bytes(blob[offs[i]:offs[i + 1]]).decode()) for i in range(ns))
+    n, f = inp["n_loc"], inp["f_loc"]
+    from collections import OrderedDict
+
+    blob, offs = inp["blob"], inp["offs"]
+    key_len = inp["key_len"].astype(np.int64)
+    seqs = OrderedDict((f">ctg{i}", bytes(blob[offs[i]:offs[i + 1]]).decode()) for i in range(n))
     t0 = time.perf_counter()
-    oracle.calc_kmer_profile(seqs, kmer)
+    raw, M = oracle.kmer_columns(seqs, inp["kmer"])
+    oracle.omp_kmer_profile_packed(blob, offs, key_len, inp["kmer"], raw, M)
     t1 = time.perf_counter()
-    r = rec[rec[:, 0] < fs].astype(np.int64)
-    starts = np.flatnonzero(np.r_[True, r[1:, 0] != r[:-1, 0]])
-    off = np.r_[starts, len(r)]
+    rec = inp["rec"]
+    starts = np.flatnonzero(np.r_[True, rec[1:, 0] != rec[:-1, 0]])
+    off = np.r_[starts, len(rec)].astype(np.int64)
     t2 = time.perf_counter()
-    oracle.graph_groups(off, r[:, 1], None, None, n_loc, dedup=True)
+    oracle.omp_graph_reads(off, rec[:, 1], inp["n_glob"])
     t3 = time.perf_counter()
     secs = (t1 - t0) + (t3 - t2)
-    return {"value": round((ns + fs) / secs, 1), "unit": "(contigs+fragments)/s", "cores": 1, "kind": "port",
-            "sample": f"{ns} contigs k={kmer} profile ({t1 - t0:.2f}s) + graph of {fs} fragments / {len(r)} records "
-                      f"({t3 - t2:.2f}s) = {frac:.0%} of the per-GPU workload, oracle/ C restatement, 1 thread"}
+    return {"value": round((n + f) / secs, 1), "unit": "(contigs+fragments)/s", "cores": oracle.threads(),
+            "kind": "port",
+            "sample": f"full per-GPU workload: {n} contigs k={inp['kmer']} profile ({t1 - t0:.2f}s, column table "
+                      f"single-threaded) + readset graph of {f} fragments / {len(rec)} records ({t3 - t2:.2f}s); "
+                      f"oracle/ C restatement, OpenMP"}
 
 
 if __name__ == "__main__":

@@ -21,7 +21,7 @@
  *   karma_synth_*                   (new) deterministic synthetic inputs, SURVEY.md §8(d)
  *   karma_fasta_*                   read_fasta_file                      karma/karma.py:40-61
  *   karma_eq_*                      eq_classes.txt parse                 karma/read_graph.py:75-92
- *   karma_sam_*                     Contig readsets from SAM lines       karma/contig.py:24,34, hisat2.py:76-81
+ *   karma_sam_*                     Contig readsets from SAM lines       karma/contig.py:24,34, hisat2.py:49-53
  *   karma_adj_*                     graph consumers: unconnected nodes, node weights, edge_list
  *                                   karma/read_graph.py:150-190, :315-357
  *   karma_adj_cross_sums            --rearrange subcluster connections  karma/karma.py:103-118
@@ -50,6 +50,7 @@ extern "C" {
 #define KARMA_ERR_UNSORTED (-6)  /* records not grouped by read (read ids must not decrease)  */
 #define KARMA_ERR_STATE (-7)     /* call out of order (e.g. profile before finalize)          */
 #define KARMA_ERR_PARSE (-8)     /* input text outside what the C++ parser reproduces exactly */
+#define KARMA_ERR_COMM (-9)      /* RCCL communicator error                                   */
 
 #define KARMA_KMER_5P6 (-1) /* kmer.py:69 "5p6": all 5-mers + string-palindromic 6-mers */
 
@@ -79,6 +80,50 @@ int karma_timing_read(karma_ctx* ctx, char* names, double* total_ms, int64_t* la
 int karma_dev_alloc(karma_ctx* ctx, size_t bytes, void** out);
 int karma_dev_free(karma_ctx* ctx, void* p);
 int karma_memcpy(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int kind /*0 H2D,1 D2H,2 D2D*/);
+/* The same, ordered on the context's stream and not waited for (host memory
+ * must stay valid until the stream reaches the copy). */
+int karma_memcpy_async(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
+int karma_memset_async(karma_ctx* ctx, void* dst, int value, size_t bytes);
+/* Streams owned by the library (a side stream for the profile, a high-priority
+ * main stream); priority: 0 normal, < 0 higher (hipStreamCreateWithPriority). */
+int karma_stream_create(karma_ctx* ctx, int priority, void** stream);
+int karma_stream_destroy(karma_ctx* ctx, void* stream);
+int karma_stream_sync(karma_ctx* ctx, void* stream);
+
+/* ---- RCCL communicator (one per device and process) ----
+ * The multi-GPU build's two exchange steps (presence MAX-allreduce + exception
+ * all-gather for the column table; pair all-to-all-v + totals all-gather for the
+ * graph) run on it, enqueued on the bound context's stream.  The 128-byte unique
+ * id made by one rank reaches the others through the caller's bootstrap
+ * (karma_amd/hostgroup.py).  Replaces nothing in the reference (single process). */
+typedef struct karma_comm karma_comm;
+#define KARMA_DT_U8 0
+#define KARMA_DT_I32 1
+#define KARMA_DT_I64 2
+#define KARMA_DT_U64 3
+#define KARMA_DT_F64 4
+#define KARMA_OP_SUM 0
+#define KARMA_OP_MAX 1
+#define KARMA_OP_MIN 2
+int karma_comm_id_bytes(void);
+int karma_comm_unique_id(uint8_t* id);
+int karma_comm_create(karma_ctx* ctx, const uint8_t* id, int world, int rank, karma_comm** out);
+int karma_comm_destroy(karma_comm* c);
+int karma_comm_info(karma_comm* c, int* world, int* rank);
+/* In place on device memory, stream-ordered. */
+int karma_comm_allreduce(karma_comm* c, void* buf_dev, int64_t count, int dtype, int op);
+/* Host scalars (at most max(64, 8 * world) bytes); synchronises the stream. */
+int karma_comm_allreduce_host(karma_comm* c, void* buf_host, int64_t count, int dtype, int op);
+int karma_comm_barrier(karma_comm* c);
+/* recv_dev[r * bytes_per_rank ...] = rank r's send_dev; in place when
+ * send_dev == recv_dev + rank * bytes_per_rank. */
+int karma_comm_allgather(karma_comm* c, const void* send_dev, void* recv_dev, int64_t bytes_per_rank);
+/* recv_host[r] = send_host[rank] of rank r (world int64 each; synchronises). */
+int karma_comm_exchange_counts(karma_comm* c, const int64_t* send_host, int64_t* recv_host);
+/* Bytes send_dev[send_off[r], send_off[r+1]) go to rank r and land in its
+ * recv_dev[recv_off[me], ...); offsets are host arrays of world + 1 entries. */
+int karma_comm_alltoallv(karma_comm* c, const void* send_dev, const int64_t* send_off, void* recv_dev,
+                         const int64_t* recv_off);
 
 /* ---- contig store (device-resident, 2-bit packed + exception mask) -------- */
 typedef struct karma_contigs karma_contigs;
@@ -104,6 +149,9 @@ int karma_kmer_plan_destroy(karma_kmer_plan* p);
 int karma_kmer_presence_words(karma_kmer_plan* p, int64_t* nwords);
 int karma_kmer_presence_get(karma_kmer_plan* p, uint32_t* dst_dev);
 int karma_kmer_presence_set(karma_kmer_plan* p, const uint32_t* src_dev);
+/* presence = OR of n_sets bitmaps of presence_words each, back to back in
+ * device memory (the ranks' bitmaps after an all-gather). */
+int karma_kmer_presence_merge(karma_kmer_plan* p, const uint32_t* all_dev, int n_sets);
 int karma_kmer_exceptions_count(karma_kmer_plan* p, int64_t* n);
 int karma_kmer_exceptions_get(karma_kmer_plan* p, uint64_t* dst_dev);
 int karma_kmer_exceptions_set(karma_kmer_plan* p, const uint64_t* src_dev, int64_t n);
@@ -220,6 +268,12 @@ int karma_synth_read_counts(uint64_t seed, const int64_t* gene_first, const int3
                             int64_t frag_lo, int64_t frag_hi, int paired, int32_t* rec_count);
 int karma_synth_read_records(uint64_t seed, const int64_t* gene_first, const int32_t* gene_size, int64_t n_genes,
                              int64_t frag_lo, int64_t frag_hi, int paired, const int64_t* rec_off, uint32_t* records);
+/* Salmon-style eq classes of fragments [frag_lo, frag_hi): each fragment's
+ * deduplicated contig set, aggregated in order of first appearance (the
+ * karma_graph_eq input).  cls_off == NULL: only *n_classes and *n_members. */
+int karma_synth_eq_classes(uint64_t seed, const int64_t* gene_first, const int32_t* gene_size, int64_t n_genes,
+                           int64_t frag_lo, int64_t frag_hi, int paired, int64_t* n_classes, int64_t* n_members,
+                           int64_t* cls_off, uint32_t* members, int64_t* counts);
 
 /* ---- host ingestion (C++, std::threads; no device needed) ----------------
  * Parsers over an in-memory file image, with Python text-mode semantics

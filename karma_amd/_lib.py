@@ -25,6 +25,12 @@ KARMA_ERR_ZERO_DIV = -5
 KARMA_ERR_UNSORTED = -6
 KARMA_ERR_STATE = -7
 KARMA_ERR_PARSE = -8
+KARMA_ERR_COMM = -9
+
+KARMA_DT_U8, KARMA_DT_I32, KARMA_DT_I64, KARMA_DT_U64, KARMA_DT_F64 = 0, 1, 2, 3, 4
+KARMA_OP_SUM, KARMA_OP_MAX, KARMA_OP_MIN = 0, 1, 2
+_DTYPE_CODE = {np.dtype(np.uint8): KARMA_DT_U8, np.dtype(np.int32): KARMA_DT_I32, np.dtype(np.int64): KARMA_DT_I64,
+               np.dtype(np.uint64): KARMA_DT_U64, np.dtype(np.float64): KARMA_DT_F64}
 
 KARMA_KMER_5P6 = -1
 KARMA_REC_SORTED = 0
@@ -54,6 +60,21 @@ _SIGS = {
     "karma_dev_alloc": [_c_p, ctypes.c_size_t, _PP],
     "karma_dev_free": [_c_p, _c_p],
     "karma_memcpy": [_c_p, _c_p, _c_p, ctypes.c_size_t, _i32],
+    "karma_memcpy_async": [_c_p, _c_p, _c_p, ctypes.c_size_t, _i32],
+    "karma_memset_async": [_c_p, _c_p, _i32, ctypes.c_size_t],
+    "karma_stream_create": [_c_p, _i32, _PP],
+    "karma_stream_destroy": [_c_p, _c_p],
+    "karma_stream_sync": [_c_p, _c_p],
+    "karma_comm_unique_id": [_c_p],
+    "karma_comm_create": [_c_p, _c_p, _i32, _i32, _PP],
+    "karma_comm_destroy": [_c_p],
+    "karma_comm_info": [_c_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
+    "karma_comm_allreduce": [_c_p, _c_p, _i64, _i32, _i32],
+    "karma_comm_allreduce_host": [_c_p, _c_p, _i64, _i32, _i32],
+    "karma_comm_barrier": [_c_p],
+    "karma_comm_allgather": [_c_p, _c_p, _c_p, _i64],
+    "karma_comm_exchange_counts": [_c_p, _c_p, _c_p],
+    "karma_comm_alltoallv": [_c_p, _c_p, _c_p, _c_p, _c_p],
     "karma_contigs_create": [_c_p, _c_p, _c_p, _c_p, _i64, _i32, _PP],
     "karma_contigs_destroy": [_c_p],
     "karma_contigs_info": [_c_p, _I64P, _I64P, _I64P, _I64P],
@@ -62,6 +83,7 @@ _SIGS = {
     "karma_kmer_presence_words": [_c_p, _I64P],
     "karma_kmer_presence_get": [_c_p, _c_p],
     "karma_kmer_presence_set": [_c_p, _c_p],
+    "karma_kmer_presence_merge": [_c_p, _c_p, _i32],
     "karma_kmer_exceptions_count": [_c_p, _I64P],
     "karma_kmer_exceptions_get": [_c_p, _c_p],
     "karma_kmer_exceptions_set": [_c_p, _c_p, _i64],
@@ -99,6 +121,7 @@ _SIGS = {
     "karma_synth_genes": [_u64, _i64, _i32, _c_p, _c_p],
     "karma_synth_read_counts": [_u64, _c_p, _c_p, _i64, _i64, _i64, _i32, _c_p],
     "karma_synth_read_records": [_u64, _c_p, _c_p, _i64, _i64, _i64, _i32, _c_p, _c_p],
+    "karma_synth_eq_classes": [_u64, _c_p, _c_p, _i64, _i64, _i64, _i32, _I64P, _I64P, _c_p, _c_p, _c_p],
     "karma_fasta_parse": [_c_p, ctypes.c_size_t, _i32, _PP],
     "karma_fasta_info": [_c_p, _I64P, _I64P, _I64P, ctypes.POINTER(ctypes.c_int)],
     "karma_fasta_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
@@ -127,7 +150,7 @@ _SIGS = {
     "karma_repr_f64_host": [_c_p, _i64, _c_p, _i64, _I64P],
 }
 
-EXPORTED = tuple(_SIGS) + ("karma_last_error",)
+EXPORTED = tuple(_SIGS) + ("karma_last_error", "karma_comm_id_bytes")
 
 
 class KarmaError(RuntimeError):
@@ -147,15 +170,9 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise KarmaError(KARMA_ERR_HIP, f"{LIB_PATH} not built — run `make -C karma_amd/csrc` "
                                         "(or __graft_entry__.build()); there is no CPU fallback")
-    # PyTorch-ROCm bundles its own HIP runtime under the same SONAME
-    # (libamdhip64.so.7): whichever is loaded first serves the whole process.
-    # Load torch's first, so torch (device buffers, streams, RCCL) and this
-    # library share the runtime torch was built against, whatever the import
-    # order of the caller.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # No PyTorch on this path: device memory, streams and the RCCL
+    # communicator all come from the library itself, so the process holds one
+    # HIP runtime (ROCm's, /opt/rocm/lib) by construction.
     lib = ctypes.CDLL(LIB_PATH)
     for name, argtypes in _SIGS.items():
         fn = getattr(lib, name)
@@ -163,6 +180,8 @@ def load():
         fn.restype = ctypes.c_int
     lib.karma_last_error.argtypes = []
     lib.karma_last_error.restype = ctypes.c_char_p
+    lib.karma_comm_id_bytes.argtypes = []
+    lib.karma_comm_id_bytes.restype = ctypes.c_int
     _LIB = lib
     return lib
 
@@ -201,8 +220,10 @@ class Context:
         self.h = h
         self.device = device
 
-    def set_stream(self, stream_ptr):
-        call("karma_ctx_set_stream", self.h, ctypes.c_void_p(stream_ptr) if stream_ptr else None)
+    def set_stream(self, stream):
+        """Launch on `stream` (a Stream or a raw hipStream_t; None: the context's own)."""
+        raw = stream.ptr if isinstance(stream, Stream) else stream
+        call("karma_ctx_set_stream", self.h, ctypes.c_void_p(raw) if raw else None)
 
     def sync(self):
         call("karma_ctx_sync", self.h)
@@ -210,9 +231,10 @@ class Context:
     def set_side_headroom(self, blocks_per_cu):
         call("karma_ctx_set_side_headroom", self.h, int(blocks_per_cu))
 
-    def join(self, side_stream_ptr):
+    def join(self, side):
         """This context's stream waits (on the device) for work on a side stream."""
-        call("karma_ctx_join", self.h, ctypes.c_void_p(side_stream_ptr))
+        raw = side.ptr if isinstance(side, Stream) else side
+        call("karma_ctx_join", self.h, ctypes.c_void_p(raw))
 
     def timing(self, on=True, only=None):
         """Per-kernel HIP-event timing; `only` restricts it to one kernel name."""
@@ -245,6 +267,96 @@ class Context:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class Stream:
+    """A HIP stream owned by the library (karma_stream_create)."""
+
+    def __init__(self, ctx, priority=0):
+        h = ctypes.c_void_p()
+        call("karma_stream_create", ctx.h, int(priority), ctypes.byref(h))
+        self.ctx, self.ptr = ctx, h.value
+
+    def sync(self):
+        call("karma_stream_sync", self.ctx.h, ctypes.c_void_p(self.ptr))
+
+    def close(self):
+        if getattr(self, "ptr", None) and self.ctx.h:
+            load().karma_stream_destroy(self.ctx.h, ctypes.c_void_p(self.ptr))
+        self.ptr = None
+
+
+class DevBuf:
+    """Device memory from the context's caching allocator (karma_dev_alloc),
+    typed like a 1-D/2-D numpy array.  Copies in and out go through the
+    context's stream; `numpy()` and `copy_from()` wait for it."""
+
+    def __init__(self, ctx, shape, dtype, _ptr=None, _owner=None):
+        self.ctx = ctx
+        self.shape = (int(shape),) if np.isscalar(shape) else tuple(int(x) for x in shape)
+        self.dtype = np.dtype(dtype)
+        self.size = int(np.prod(self.shape)) if self.shape else 1
+        self.nbytes = self.size * self.dtype.itemsize
+        self._owner = _owner
+        if _ptr is not None:
+            self.ptr = _ptr
+            return
+        h = ctypes.c_void_p()
+        call("karma_dev_alloc", ctx.h, max(self.nbytes, 1), ctypes.byref(h))
+        self.ptr = h.value
+
+    @classmethod
+    def from_numpy(cls, ctx, arr):
+        arr = np.ascontiguousarray(arr)
+        b = cls(ctx, arr.shape, arr.dtype)
+        b.copy_from(arr)
+        return b
+
+    def view(self, start, n, shape=None):
+        """Elements [start, start + n) as a buffer that does not own its memory."""
+        assert 0 <= start and start + n <= self.size, "view out of range"
+        return DevBuf(self.ctx, shape or (n,), self.dtype, _ptr=self.ptr + start * self.dtype.itemsize,
+                      _owner=self)
+
+    def reshape(self, *shape):
+        shape = shape[0] if len(shape) == 1 and not np.isscalar(shape[0]) else shape
+        out = DevBuf(self.ctx, shape, self.dtype, _ptr=self.ptr, _owner=self)
+        assert out.size == self.size, "reshape changes the size"
+        return out
+
+    def numpy(self):
+        out = np.empty(self.shape, self.dtype)
+        if self.nbytes:
+            call("karma_memcpy", self.ctx.h, ptr(out), ctypes.c_void_p(self.ptr), self.nbytes, 1)
+        return out
+
+    def copy_from(self, arr):
+        arr = np.ascontiguousarray(arr, dtype=self.dtype)
+        assert arr.nbytes <= self.nbytes, "host array larger than the buffer"
+        if arr.nbytes:
+            call("karma_memcpy", self.ctx.h, ctypes.c_void_p(self.ptr), ptr(arr), arr.nbytes, 0)
+
+    def copy_from_device(self, src, nbytes=None, dst_offset=0, src_offset=0):
+        """Stream-ordered device-to-device copy (bytes)."""
+        n = src.nbytes if nbytes is None else nbytes
+        if n:
+            call("karma_memcpy_async", self.ctx.h, ctypes.c_void_p(self.ptr + dst_offset),
+                 ctypes.c_void_p(src.ptr + src_offset), n, 2)
+
+    def close(self):
+        if self._owner is None and getattr(self, "ptr", None) and self.ctx.h:
+            load().karma_dev_free(self.ctx.h, ctypes.c_void_p(self.ptr))
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def dtype_code(dtype):
+    return _DTYPE_CODE[np.dtype(dtype)]
 
 
 _DEFAULT_CTX = {}

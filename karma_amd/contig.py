@@ -61,7 +61,14 @@ def load_sam_records(sam, skip_headers=True, threads=0):
     """SAM lines -> ingest.SamRecords: one (read id, contig id) record per line,
     contig ids numbering RNAMEs (field 3) in order of first appearance
     (csrc/ingest.cpp, karma_sam_parse).  skip_headers drops "@" lines as the
-    hisat2 generator does (hisat2.py:76-81)."""
+    hisat2 generator does (hisat2.py:49-53).
+
+    Line splitting follows file mode (contig.py:31 iterates an open() file):
+    universal newlines.  The hisat2 generator instead splits samtools' stdout
+    on "\n" only and drops what follows the last "\n" (hisat2.py:51).  The two
+    agree on any text without "\r" and with a final newline, which is what
+    samtools writes; generator-style text holding "\r" keeps it inside the
+    line there, and must be normalised by the caller before it comes here."""
     data = _sam_bytes(sam)
     try:
         return ingest.parse_sam(data, skip_headers, threads), data

@@ -273,4 +273,47 @@ int karma_memcpy(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int k
     return KARMA_OK;
 }
 
+int karma_memcpy_async(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {
+    KARMA_TRY(ctx_begin(ctx));
+    if (!bytes) return KARMA_OK;
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    KARMA_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->stream));
+    return KARMA_OK;
+}
+
+int karma_memset_async(karma_ctx* ctx, void* dst, int value, size_t bytes) {
+    KARMA_TRY(ctx_begin(ctx));
+    if (!bytes) return KARMA_OK;
+    KARMA_HIP(hipMemsetAsync(dst, value, bytes, ctx->stream));
+    return KARMA_OK;
+}
+
+int karma_stream_create(karma_ctx* ctx, int priority, void** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out, KARMA_ERR_ARG, "null out");
+    int lo = 0, hi = 0;
+    KARMA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));  // hi is the numerically smallest (highest)
+    const int p = std::max(hi, std::min(lo, priority));
+    hipStream_t s = nullptr;
+    KARMA_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p));
+    *out = s;
+    return KARMA_OK;
+}
+
+int karma_stream_destroy(karma_ctx* ctx, void* s) {
+    KARMA_TRY(ctx_begin(ctx));
+    if (!s) return KARMA_OK;
+    KARMA_CHECK(s != ctx->own_stream, KARMA_ERR_ARG, "the context's own stream is destroyed with the context");
+    if (ctx->stream == s) ctx->stream = ctx->own_stream;
+    KARMA_HIP(hipStreamSynchronize(static_cast<hipStream_t>(s)));
+    KARMA_HIP(hipStreamDestroy(static_cast<hipStream_t>(s)));
+    return KARMA_OK;
+}
+
+int karma_stream_sync(karma_ctx* ctx, void* s) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_HIP(hipStreamSynchronize(s ? static_cast<hipStream_t>(s) : ctx->stream));
+    return KARMA_OK;
+}
+
 }  // extern "C"

@@ -320,16 +320,14 @@ int karma_graph_records_begin(karma_ctx* ctx, const uint32_t* records, int64_t A
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(out && (records || A == 0) && A >= 0, KARMA_ERR_ARG, "karma_graph_records: bad arguments");
     KARMA_CHECK(A < (int64_t(1) << 40), KARMA_ERR_ARG, "too many records");
-    auto* p = new karma_pairs();
-    p->ctx = ctx;
+    // held until the job owns it, so every early return (KARMA_HIP / KARMA_CHECK) frees it
+    std::unique_ptr<karma_pairs> ph(new karma_pairs());
+    ph->ctx = ctx;
     DevArray<uint2> own;
     const uint2* rec = reinterpret_cast<const uint2*>(records);
     int rc = KARMA_OK;
     if (!is_device || flags == KARMA_REC_UNSORTED) {
-        if ((rc = own.alloc(ctx, A))) {
-            delete p;
-            return rc;
-        }
+        if ((rc = own.alloc(ctx, A))) return rc;
         if (A) {
             KARMA_HIP(hipMemcpyAsync(own.ptr, records, A * 8, is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                                      ctx->stream));
@@ -340,35 +338,27 @@ int karma_graph_records_begin(karma_ctx* ctx, const uint32_t* records, int64_t A
         KARMA_CHECK(A < (int64_t(1) << 31), KARMA_ERR_ARG, "unsorted path limited to 2^31 records");
         DevArray<uint32_t> rid, cid, rid2, cid2;
         if ((rc = rid.alloc(ctx, A)) || (rc = cid.alloc(ctx, A)) || (rc = rid2.alloc(ctx, A)) ||
-            (rc = cid2.alloc(ctx, A))) {
-            delete p;
-            return rc;
-        }
+            (rc = cid2.alloc(ctx, A))) return rc;
         KARMA_LAUNCH(ctx, "deinterleave", deinterleave_kernel, grid1(A), 256, 0, own.ptr, A, rid.ptr, cid.ptr);
         size_t tb = 0;
         KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, rid.ptr, rid2.ptr, cid.ptr, cid2.ptr, (int)A, 0, 32,
                                                      ctx->stream));
         DevArray<uint8_t> tmp;
-        if ((rc = tmp.alloc(ctx, tb))) {
-            delete p;
-            return rc;
-        }
+        if ((rc = tmp.alloc(ctx, tb))) return rc;
         KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, rid.ptr, rid2.ptr, cid.ptr, cid2.ptr, (int)A, 0, 32,
                                                      ctx->stream));
         KARMA_LAUNCH(ctx, "interleave", interleave_kernel, grid1(A), 256, 0, rid2.ptr, cid2.ptr, A, own.ptr);
     }
     if (reinterpret_cast<uintptr_t>(rec) & 15) {  // the set pipeline streams 16-byte loads
         if (!own.ptr) {
-            if ((rc = own.alloc(ctx, A))) {
-                delete p;
-                return rc;
-            }
+            if ((rc = own.alloc(ctx, A))) return rc;
             KARMA_HIP(hipMemcpyAsync(own.ptr, rec, A * 8, hipMemcpyDeviceToDevice, ctx->stream));
             rec = own.ptr;
         }
     }
+    karma_pairs* p = ph.get();
     auto* job = new karma_graph_job();
-    job->p = p;
+    job->p = ph.release();
     job->own.swap(own);
     if (N > sets_max_contigs()) {  // wide path: runs to completion here
         rc = records_to_pairs_sets(ctx, rec, A, N, p);

@@ -3,7 +3,7 @@
 //
 //   karma_fasta_*  read_fasta_file              karma/karma.py:40-61
 //   karma_eq_*     the eq_classes.txt parse of  karma/read_graph.py:75-92
-//   karma_sam_*    Contig readsets from SAM     karma/contig.py:24,34 + hisat2.py:76-81
+//   karma_sam_*    Contig readsets from SAM     karma/contig.py:24,34 + hisat2.py:49-53
 //
 // Text semantics follow Python's text-mode open(): UTF-8 (strict) and
 // universal newlines ("\r\n", "\r" and "\n" each end a line and are not part
@@ -239,7 +239,7 @@ struct KeyTable {
 
 }  // namespace
 
-extern "C" int karma_fasta_parse(const char* data_c, size_t len, int threads, karma_fasta** out) {
+static int fasta_parse_impl(const char* data_c, size_t len, int threads, karma_fasta** out) {
     if (!out || (!data_c && len)) {
         set_error("karma_fasta_parse: null argument");
         return KARMA_ERR_ARG;
@@ -379,6 +379,20 @@ extern "C" int karma_fasta_parse(const char* data_c, size_t len, int threads, ka
     return KARMA_OK;
 }
 
+// Host allocation failures (e.g. a count in the input far beyond its size)
+// must not unwind through the C boundary.
+extern "C" int karma_fasta_parse(const char* data_c, size_t len, int threads, karma_fasta** out) {
+    try {
+        return fasta_parse_impl(data_c, len, threads, out);
+    } catch (const std::bad_alloc&) {
+        set_error("karma_fasta_parse: out of host memory");
+        return KARMA_ERR_OOM;
+    } catch (const std::exception& e) {
+        set_error("karma_fasta_parse: %s", e.what());
+        return KARMA_ERR_PARSE;
+    }
+}
+
 extern "C" int karma_fasta_info(karma_fasta* f, int64_t* n, int64_t* seq_bytes, int64_t* key_bytes, int* ascii) {
     if (!f) {
         set_error("karma_fasta_info: null handle");
@@ -503,7 +517,7 @@ void parse_eq_lines(const uint8_t* s, size_t lo, size_t hi, int64_t n, EqPart& P
 
 }  // namespace
 
-extern "C" int karma_eq_parse(const char* data_c, size_t len, int threads, karma_eq** out) {
+static int eq_parse_impl(const char* data_c, size_t len, int threads, karma_eq** out) {
     if (!out || (!data_c && len)) {
         set_error("karma_eq_parse: null argument");
         return KARMA_ERR_ARG;
@@ -530,7 +544,23 @@ extern "C" int karma_eq_parse(const char* data_c, size_t len, int threads, karma
     }
     p = next_line(s, len, e);
     p = next_line(s, len, line_end(s, len, p));  // line 2 ignored
-    auto* q = new karma_eq;
+    // Past EOF readline returns "" (read_graph.py:80): a second name read past
+    // the end duplicates the first one, which the :93 assert rejects.  Checked
+    // before anything is sized by the untrusted count n.
+    {
+        size_t pp = p;
+        int64_t avail = 0;
+        while (avail < n && pp < len) {
+            pp = next_line(s, len, line_end(s, len, pp));
+            ++avail;
+        }
+        if (n - avail >= 2) {
+            set_error("eq_classes: duplicate contig name (read_graph.py:93 assert: names past the end of the file)");
+            return KARMA_ERR_PARSE;
+        }
+    }
+    std::unique_ptr<karma_eq> qh(new karma_eq);
+    karma_eq* q = qh.get();
     q->name_off.assign(n + 1, 0);
     std::vector<std::pair<size_t, size_t>> nm((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
@@ -545,9 +575,8 @@ extern "C" int karma_eq_parse(const char* data_c, size_t len, int threads, karma
         uniq.reserve((size_t)n * 2);
         for (int64_t i = 0; i < n; ++i) {
             std::string_view v(reinterpret_cast<const char*>(s + nm[i].first), nm[i].second - nm[i].first);
-            memcpy(q->names.data() + q->name_off[i], v.data(), v.size());
+            if (!v.empty()) memcpy(q->names.data() + q->name_off[i], v.data(), v.size());
             if (!uniq.insert(v).second) {
-                delete q;
                 set_error("eq_classes: duplicate contig name (read_graph.py:93 assert)");
                 return KARMA_ERR_PARSE;
             }
@@ -563,7 +592,6 @@ extern "C" int karma_eq_parse(const char* data_c, size_t len, int threads, karma
     for (int t = 0; t < T; ++t) {
         if (parts[t].bad_line >= 0) {
             set_error("eq_classes: %s (eq line %lld)", parts[t].why, (long long)(line0 + parts[t].bad_line + 1));
-            delete q;
             return KARMA_ERR_PARSE;
         }
         line0 += parts[t].lines;
@@ -579,8 +607,22 @@ extern "C" int karma_eq_parse(const char* data_c, size_t len, int threads, karma
         q->counts.insert(q->counts.end(), P.counts.begin(), P.counts.end());
         q->pair_skip.insert(q->pair_skip.end(), P.skip.begin(), P.skip.end());
     }
-    *out = q;
+    *out = qh.release();
     return KARMA_OK;
+}
+
+// Host allocation failures (e.g. a count in the input far beyond its size)
+// must not unwind through the C boundary.
+extern "C" int karma_eq_parse(const char* data_c, size_t len, int threads, karma_eq** out) {
+    try {
+        return eq_parse_impl(data_c, len, threads, out);
+    } catch (const std::bad_alloc&) {
+        set_error("karma_eq_parse: out of host memory");
+        return KARMA_ERR_OOM;
+    } catch (const std::exception& e) {
+        set_error("karma_eq_parse: %s", e.what());
+        return KARMA_ERR_PARSE;
+    }
 }
 
 extern "C" int karma_eq_info(karma_eq* q, int64_t* n_contigs, int64_t* n_classes, int64_t* n_members,
@@ -620,7 +662,7 @@ extern "C" int karma_eq_destroy(karma_eq* q) {
 // SAM — Contig readsets (karma/contig.py:24,34): per line
 //   read, _, name, position, *_ = line.split("\t")   (>= 4 fields)
 // and the readset is set(read).  Lines starting with "@" are dropped when
-// skip_headers is set (the hisat2 generator filter, hisat2.py:76-81).  One
+// skip_headers is set (the hisat2 generator filter, hisat2.py:49-53).  One
 // record (read id, contig id) per line; contig ids number the RNAMEs (field 3)
 // in order of first appearance, read ids are an injective numbering of the
 // QNAMEs (the graph depends only on which records share a read).
@@ -689,7 +731,7 @@ void parse_sam_lines(const uint8_t* s, size_t lo, size_t hi, bool skip_headers, 
 
 }  // namespace
 
-extern "C" int karma_sam_parse(const char* data_c, size_t len, int skip_headers, int threads, karma_sam** out) {
+static int sam_parse_impl(const char* data_c, size_t len, int skip_headers, int threads, karma_sam** out) {
     if (!out || (!data_c && len)) {
         set_error("karma_sam_parse: null argument");
         return KARMA_ERR_ARG;
@@ -826,6 +868,20 @@ extern "C" int karma_sam_parse(const char* data_c, size_t len, int skip_headers,
     S->id_bound = nreads ? (int64_t)maxid + 1 : 0;
     *out = S;
     return KARMA_OK;
+}
+
+// Host allocation failures (e.g. a count in the input far beyond its size)
+// must not unwind through the C boundary.
+extern "C" int karma_sam_parse(const char* data_c, size_t len, int skip_headers, int threads, karma_sam** out) {
+    try {
+        return sam_parse_impl(data_c, len, skip_headers, threads, out);
+    } catch (const std::bad_alloc&) {
+        set_error("karma_sam_parse: out of host memory");
+        return KARMA_ERR_OOM;
+    } catch (const std::exception& e) {
+        set_error("karma_sam_parse: %s", e.what());
+        return KARMA_ERR_PARSE;
+    }
 }
 
 extern "C" int karma_sam_info(karma_sam* S, int64_t* n_records, int64_t* n_reads, int64_t* n_contigs,

@@ -784,6 +784,16 @@ int kmer_shape(int kmode, int* kmin, int* kmax, uint32_t* S, bool* with_len) {
 
 }  // namespace
 
+// OR of n_sets presence bitmaps laid out one after another (the ranks' bitmaps
+// after an all-gather): the global column set is the union (kmer.py:146-179).
+static __global__ void presence_or_kernel(const uint32_t* __restrict__ all, int n_sets, int64_t nw, uint32_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nw) return;
+    uint32_t v = 0;
+    for (int r = 0; r < n_sets; ++r) v |= all[(int64_t)r * nw + i];
+    out[i] = v;
+}
+
 extern "C" {
 
 int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offsets, const int32_t* key_len, int64_t n,
@@ -997,6 +1007,17 @@ int karma_kmer_presence_set(karma_kmer_plan* p, const uint32_t* src) {
     KARMA_CHECK(p && src, KARMA_ERR_ARG, "null argument");
     KARMA_TRY(ctx_begin(p->ctx));
     KARMA_HIP(hipMemcpyAsync(p->presence.ptr, src, p->nwords * 4, hipMemcpyDeviceToDevice, p->ctx->stream));
+    p->M = -1;
+    return KARMA_OK;
+}
+
+int karma_kmer_presence_merge(karma_kmer_plan* p, const uint32_t* all, int n_sets) {
+    KARMA_CHECK(p && all && n_sets >= 1, KARMA_ERR_ARG, "bad argument");
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    const int64_t nw = p->nwords;
+    KARMA_LAUNCH(ctx, "kmer_presence_merge", presence_or_kernel, (int)ceil_div(nw, 256), 256, 0, all, n_sets, nw,
+                 p->presence.ptr);
     p->M = -1;
     return KARMA_OK;
 }

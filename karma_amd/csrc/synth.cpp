@@ -2,8 +2,10 @@
 // Counter-based SplitMix64: every value depends only on (seed, stream, index), so
 // ranges can be generated independently (per rank, per thread) and still match
 // the pure-Python generator byte for byte (tests/test_synth.py).
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <vector>
 
 #include "../../include/karma.h"
 
@@ -132,6 +134,55 @@ int karma_synth_read_records(uint64_t seed, const int64_t* gf, const int32_t* gs
                     out += 2;
                 }
         }
+    }
+    return KARMA_OK;
+}
+
+int karma_synth_eq_classes(uint64_t seed, const int64_t* gf, const int32_t* gs, int64_t n_genes, int64_t lo, int64_t hi,
+                           int paired, int64_t* n_classes, int64_t* n_members, int64_t* cls_off, uint32_t* members,
+                           int64_t* counts) {
+    // synth.py eq_classes: a fragment's class is its deduplicated contig set
+    // (gene j, mask1 | mask2); classes in order of first appearance, ids ascending.
+    if (!gf || !gs || !n_classes || !n_members || n_genes < 1 || hi < lo) return KARMA_ERR_ARG;
+    int gmax = 1;
+    for (int64_t j = 0; j < n_genes; ++j) gmax = std::max(gmax, (int)gs[j]);
+    if (gmax > 16 || (n_genes << gmax) > ((int64_t)1 << 34)) return KARMA_ERR_ARG;
+    const int64_t K = n_genes << gmax;
+    std::vector<int64_t> first((size_t)K, INT64_MAX), cnt((size_t)K, 0);
+    const uint64_t kf = skey(seed, S_FGENE);
+#pragma omp parallel for schedule(static)
+    for (int64_t r = lo; r < hi; ++r) {
+        Frag f = frag_masks(seed, r, gf, gs, n_genes, paired);
+        const int64_t j = (int64_t)(at(kf, (uint64_t)r) % (uint64_t)n_genes);
+        const int64_t k = (j << gmax) | (int64_t)(f.m1 | f.m2);
+        __atomic_fetch_add(&cnt[(size_t)k], 1, __ATOMIC_RELAXED);
+        int64_t cur = __atomic_load_n(&first[(size_t)k], __ATOMIC_RELAXED);
+        while (r < cur && !__atomic_compare_exchange_n(&first[(size_t)k], &cur, r, true, __ATOMIC_RELAXED,
+                                                       __ATOMIC_RELAXED)) {
+        }
+    }
+    std::vector<int64_t> keys;
+    int64_t nm = 0;
+    for (int64_t k = 0; k < K; ++k)
+        if (cnt[(size_t)k]) {
+            keys.push_back(k);
+            nm += __builtin_popcount((uint32_t)(k & ((1 << gmax) - 1)));
+        }
+    *n_classes = (int64_t)keys.size();
+    *n_members = nm;
+    if (!cls_off) return KARMA_OK;
+    if (!members || !counts) return KARMA_ERR_ARG;
+    std::sort(keys.begin(), keys.end(), [&](int64_t a, int64_t b) { return first[(size_t)a] < first[(size_t)b]; });
+    cls_off[0] = 0;
+    int64_t m = 0;
+    for (size_t c = 0; c < keys.size(); ++c) {
+        const int64_t k = keys[c];
+        const int64_t g0 = gf[k >> gmax];
+        const uint32_t mask = (uint32_t)(k & ((1 << gmax) - 1));
+        for (int b = 0; mask >> b; ++b)
+            if (mask >> b & 1) members[m++] = (uint32_t)(g0 + b);
+        cls_off[c + 1] = m;
+        counts[c] = cnt[(size_t)k];
     }
     return KARMA_OK;
 }

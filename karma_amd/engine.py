@@ -113,6 +113,10 @@ class KmerPlan:
     def presence_set(self, src_dev_ptr):
         call("karma_kmer_presence_set", self.h, ctypes.c_void_p(src_dev_ptr))
 
+    def presence_merge(self, all_dev_ptr, n_sets):
+        """Presence = OR of n_sets bitmaps back to back in device memory."""
+        call("karma_kmer_presence_merge", self.h, ctypes.c_void_p(all_dev_ptr), int(n_sets))
+
     def exceptions_count(self):
         n = ctypes.c_int64()
         call("karma_kmer_exceptions_count", self.h, ctypes.byref(n))
@@ -468,3 +472,18 @@ def synth_records(seed, n_contigs, frag_lo, frag_hi, paired, gene_max=4, genes=N
     call("karma_synth_read_records", seed, ptr(gf), ptr(gs), len(gf), frag_lo, frag_hi, int(paired), ptr(off),
          ptr(rec))
     return rec[: int(off[-1])]
+
+
+def synth_eq_classes(seed, n_contigs, frag_lo, frag_hi, paired, gene_max=4, genes=None):
+    """(cls_off int64[C+1], members uint32[], counts int64[C]) of the fragments'
+    eq classes, first-seen order (native twin of synth.eq_classes)."""
+    gf, gs = genes if genes is not None else synth_genes(seed, n_contigs, gene_max)
+    nc, nm = ctypes.c_int64(), ctypes.c_int64()
+    call("karma_synth_eq_classes", seed, ptr(gf), ptr(gs), len(gf), frag_lo, frag_hi, int(paired), ctypes.byref(nc),
+         ctypes.byref(nm), None, None, None)
+    off = np.zeros(nc.value + 1, np.int64)
+    mem = np.zeros(max(nm.value, 1), np.uint32)
+    cnt = np.zeros(max(nc.value, 1), np.int64)
+    call("karma_synth_eq_classes", seed, ptr(gf), ptr(gs), len(gf), frag_lo, frag_hi, int(paired), ctypes.byref(nc),
+         ctypes.byref(nm), ptr(off), ptr(mem), ptr(cnt))
+    return off, mem[: nm.value], cnt[: nc.value]

@@ -1,0 +1,215 @@
+"""Host-side process groups: bootstrap and host-staged transport (stdlib only).
+
+Two uses, neither of them on the data path of a real multi-GPU run:
+  * bootstrap of the library's RCCL communicator (karma_amd/comm.py RcclComm):
+    rank 0's 128-byte unique id reaches the other ranks, and host scalars
+    (timings, counts) are gathered;
+  * the transport of HostComm, which stages the exchange through host memory
+    for rehearsals where RCCL cannot run: several ranks on ONE GPU (RCCL
+    refuses duplicate devices), or CPU-only tests of the sharding logic.
+
+SocketGroup is a TCP star on the launcher's rendezvous address (one process
+per rank, e.g. under torchrun); ThreadGroup holds the ranks as threads of one
+process.  Both expose the same two calls: allgather(ndarray) -> list of every
+rank's array, and barrier().
+"""
+
+from __future__ import annotations
+
+import os
+import socket
+import struct
+import threading
+import time
+
+import numpy as np
+
+
+def _send_msg(sock, payload: bytes):
+    sock.sendall(struct.pack("<Q", len(payload)) + payload)
+
+
+def _recv_exact(sock, n):
+    buf = bytearray(n)
+    view = memoryview(buf)
+    got = 0
+    while got < n:
+        k = sock.recv_into(view[got:], n - got)
+        if k == 0:
+            raise ConnectionError("host group peer closed the connection")
+        got += k
+    return bytes(buf)
+
+
+def _recv_msg(sock) -> bytes:
+    (n,) = struct.unpack("<Q", _recv_exact(sock, 8))
+    return _recv_exact(sock, n)
+
+
+def _pack(arr: np.ndarray) -> bytes:
+    arr = np.ascontiguousarray(arr).reshape(-1)
+    dt = arr.dtype.str.encode()
+    return struct.pack("<B", len(dt)) + dt + arr.tobytes()
+
+
+def _unpack(b: bytes) -> np.ndarray:
+    n = b[0]
+    dt = np.dtype(b[1:1 + n].decode())
+    return np.frombuffer(b[1 + n:], dtype=dt).copy()
+
+
+class SocketGroup:
+    """TCP star: rank 0 listens on (addr, port), the others connect.
+
+    allgather: every rank sends its array to rank 0, which returns the list of
+    all of them to every rank.  Message sizes are whatever the arrays hold."""
+
+    def __init__(self, world, rank, addr="127.0.0.1", port=29600, timeout=300.0):
+        self.world, self.rank = world, rank
+        self.peers = {}
+        self.sock = None
+        if world == 1:
+            return
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, port))
+            srv.listen(world)
+            srv.settimeout(timeout)
+            try:
+                while len(self.peers) < world - 1:
+                    c, _ = srv.accept()
+                    c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    c.settimeout(None)
+                    (r,) = struct.unpack("<i", _recv_exact(c, 4))
+                    if not 0 < r < world or r in self.peers:
+                        c.close()
+                        raise ConnectionError(f"host group: unexpected rank {r}")
+                    self.peers[r] = c
+            finally:
+                srv.close()
+        else:
+            deadline = time.time() + timeout
+            while True:
+                try:
+                    s = socket.create_connection((addr, port), timeout=10)
+                    break
+                except OSError:
+                    if time.time() > deadline:
+                        raise
+                    time.sleep(0.05)
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            s.settimeout(None)
+            s.sendall(struct.pack("<i", rank))
+            self.sock = s
+
+    @classmethod
+    def from_env(cls, world=None, rank=None):
+        """Ranks started by a launcher (torchrun): RANK / WORLD_SIZE / MASTER_ADDR,
+        port KARMA_GROUP_PORT or MASTER_PORT + 1 (torchrun's own store holds
+        MASTER_PORT)."""
+        world = int(os.environ.get("WORLD_SIZE", "1")) if world is None else world
+        rank = int(os.environ.get("RANK", "0")) if rank is None else rank
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("KARMA_GROUP_PORT") or int(os.environ.get("MASTER_PORT", "29500")) + 1)
+        return cls(world, rank, addr, port)
+
+    def allgather(self, arr) -> list:
+        arr = np.asarray(arr)
+        if self.world == 1:
+            return [np.ascontiguousarray(arr).reshape(-1).copy()]
+        if self.rank == 0:
+            parts = [None] * self.world
+            parts[0] = _pack(arr)
+            for r, c in self.peers.items():
+                parts[r] = _recv_msg(c)
+            blob = struct.pack("<i", self.world) + b"".join(struct.pack("<Q", len(p)) + p for p in parts)
+            for c in self.peers.values():
+                _send_msg(c, blob)
+        else:
+            _send_msg(self.sock, _pack(arr))
+            blob = _recv_msg(self.sock)
+        (w,) = struct.unpack_from("<i", blob, 0)
+        out, off = [], 4
+        for _ in range(w):
+            (n,) = struct.unpack_from("<Q", blob, off)
+            off += 8
+            out.append(_unpack(blob[off:off + n]))
+            off += n
+        return out
+
+    def barrier(self):
+        self.allgather(np.zeros(0, np.uint8))
+
+    def close(self):
+        for c in self.peers.values():
+            c.close()
+        self.peers = {}
+        if self.sock is not None:
+            self.sock.close()
+            self.sock = None
+
+
+class _ThreadState:
+    def __init__(self, world):
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.slots = [None] * world
+
+
+class ThreadGroup:
+    """Ranks as threads of one process (host-staged multi-rank rehearsal).
+
+    ThreadGroup.create(W) returns the W per-rank handles; each rank's thread
+    uses its own handle."""
+
+    def __init__(self, state, rank):
+        self.state, self.rank, self.world = state, rank, state.world
+
+    @classmethod
+    def create(cls, world):
+        st = _ThreadState(world)
+        return [cls(st, r) for r in range(world)]
+
+    def allgather(self, arr) -> list:
+        st = self.state
+        st.slots[self.rank] = np.ascontiguousarray(arr).reshape(-1).copy()
+        st.barrier.wait()
+        out = list(st.slots)
+        st.barrier.wait()  # nobody overwrites a slot before everyone has read it
+        return out
+
+    def barrier(self):
+        self.state.barrier.wait()
+
+    def close(self):
+        pass
+
+
+def run_ranks(world, fn, *args):
+    """Run fn(group, rank, *args) on `world` threads sharing one ThreadGroup;
+    returns the per-rank results (re-raises the first failure, after breaking
+    the group's barrier so no rank waits forever)."""
+    groups = ThreadGroup.create(world)
+    results = [None] * world
+    errors = [None] * world
+
+    def body(r):
+        try:
+            results[r] = fn(groups[r], r, *args)
+        except BaseException as e:  # noqa: BLE001 (re-raised below)
+            errors[r] = e
+            groups[r].state.barrier.abort()
+
+    threads = [threading.Thread(target=body, args=(r,), name=f"karma-rank{r}") for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for e in errors:
+        if e is not None and not isinstance(e, threading.BrokenBarrierError):
+            raise e
+    for e in errors:
+        if e is not None:
+            raise e
+    return results

@@ -27,6 +27,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define OK_MAXK 15
 
@@ -347,5 +350,182 @@ int64_t oracle_update_pairs(const int64_t* o_off, const uint32_t* o_ids, int64_t
                 E++;
             }
         }
+    return E <= cap ? E : -E;
+}
+
+/* ------------------------------------------------------------------------- */
+/* OpenMP twins (the on-node CPU baseline; bench.py        */
+/* cpu_baseline).  Same arithmetic as the scalar functions above, checked      */
+/* against them by tests/test_oracle_golden.py; only the work is split over    */
+/* threads.                                                                    */
+/* ------------------------------------------------------------------------- */
+
+int oracle_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+/* oracle_kmer_profile over rows in parallel (no counts_out). */
+int oracle_omp_kmer_profile(const uint8_t* seq, const int64_t* offsets, const int64_t* key_len, int64_t n,
+                            int kmode, const uint8_t* keys, int64_t M, double* out) {
+    int rc = 0;
+#pragma omp parallel
+    {
+        int64_t* counts = (int64_t*)calloc((size_t)(M ? M : 1), sizeof(int64_t));
+        count_ctx_t ctx = {(const okey_t*)keys, M, counts, 0};
+        int my = 0;
+#pragma omp for schedule(dynamic, 256)
+        for (int64_t r = 0; r < n; ++r) {
+            memset(counts, 0, (size_t)M * sizeof(int64_t));
+            enum_kmers(seq + offsets[r], offsets[r + 1] - offsets[r], kmode, count_emit, &ctx);
+            for (int64_t j = 0; j < M; ++j) {
+                double v = 0.0;
+                if (counts[j]) {
+                    if (key_len[r] == 0) my = 2;
+                    else v = (double)counts[j] / (double)key_len[r]; /* kmer.py:120 */
+                }
+                out[r * M + j] = v;
+            }
+        }
+        if (ctx.miss) my = 1;
+#pragma omp critical
+        if (my > rc) rc = my;
+        free(counts);
+    }
+    return rc;
+}
+
+static int u64_cmp(const void* pa, const void* pb) {
+    uint64_t a = *(const uint64_t*)pa, b = *(const uint64_t*)pb;
+    return a < b ? -1 : (a > b);
+}
+
+/* oracle_graph_groups for reads (dedup = 1, mult = 1, no pair_skip, no first
+ * position): pairs emitted per thread, scattered into NB buckets by a, each
+ * bucket sorted and run-length counted on its own.  Buckets are ranges of a, so
+ * concatenating them gives the (a, b) order.  Returns E, or -E if cap < E. */
+int64_t oracle_omp_graph_reads(const int64_t* grp_off, const uint32_t* members, int64_t G, int64_t N,
+                               int64_t* totals, uint32_t* ea, uint32_t* eb, int64_t* es, double* ew, int64_t cap,
+                               int* zero_div) {
+    const int T = oracle_threads();
+    const int NB = 1024;
+    uint64_t** tv = (uint64_t**)calloc((size_t)T, sizeof(uint64_t*));
+    int64_t* tn = (int64_t*)calloc((size_t)T, sizeof(int64_t));
+    int64_t* tb = (int64_t*)calloc((size_t)T * NB, sizeof(int64_t)); /* per thread per bucket counts */
+    int64_t* ttot = (int64_t*)calloc((size_t)T * (size_t)(N ? N : 1), sizeof(int64_t));
+    const uint64_t nn = (uint64_t)(N ? N : 1);
+#pragma omp parallel num_threads(T)
+    {
+        int t = 0;
+#ifdef _OPENMP
+        t = omp_get_thread_num();
+#endif
+        int64_t g0 = G * t / T, g1 = G * (t + 1) / T;
+        int64_t cap_t = 1024, n_t = 0;
+        uint64_t* v = (uint64_t*)malloc((size_t)cap_t * 8);
+        int64_t* tot = ttot + (size_t)t * nn;
+        uint32_t buf[4096];
+        for (int64_t g = g0; g < g1; ++g) {
+            int64_t lo = grp_off[g], m = grp_off[g + 1] - lo;
+            uint32_t* b = m <= 4096 ? buf : (uint32_t*)malloc((size_t)m * 4);
+            memcpy(b, members + lo, (size_t)m * 4);
+            qsort(b, (size_t)m, 4, u32_cmp);
+            int64_t u = m ? 1 : 0;
+            for (int64_t i = 1; i < m; ++i)
+                if (b[i] != b[u - 1]) b[u++] = b[i];
+            for (int64_t i = 0; i < u; ++i) tot[b[i]] += 1;
+            for (int64_t i = 0; i < u; ++i)
+                for (int64_t j = i + 1; j < u; ++j) {
+                    if (n_t == cap_t) {
+                        cap_t *= 2;
+                        v = (uint64_t*)realloc(v, (size_t)cap_t * 8);
+                    }
+                    v[n_t++] = ((uint64_t)b[i] << 32) | b[j];
+                    tb[(size_t)t * NB + (int64_t)((uint64_t)b[i] * NB / nn)]++;
+                }
+            if (b != buf) free(b);
+        }
+        tv[t] = v;
+        tn[t] = n_t;
+    }
+    /* bucket offsets: bucket-major, thread-minor */
+    int64_t* boff = (int64_t*)calloc((size_t)NB + 1, sizeof(int64_t));
+    int64_t* woff = (int64_t*)calloc((size_t)T * NB, sizeof(int64_t));
+    int64_t P = 0;
+    for (int k = 0; k < NB; ++k) {
+        boff[k] = P;
+        for (int t = 0; t < T; ++t) {
+            woff[(size_t)t * NB + k] = P;
+            P += tb[(size_t)t * NB + k];
+        }
+    }
+    boff[NB] = P;
+    uint64_t* all = (uint64_t*)malloc((size_t)(P ? P : 1) * 8);
+#pragma omp parallel for num_threads(T) schedule(static, 1)
+    for (int t = 0; t < T; ++t) {
+        int64_t* w = woff + (size_t)t * NB;
+        for (int64_t i = 0; i < tn[t]; ++i) {
+            uint64_t k = tv[t][i];
+            all[w[(int64_t)((k >> 32) * NB / nn)]++] = k;
+        }
+        free(tv[t]);
+    }
+#pragma omp parallel for num_threads(T) schedule(static)
+    for (int64_t c = 0; c < N; ++c) {
+        int64_t s = 0;
+        for (int t = 0; t < T; ++t) s += ttot[(size_t)t * nn + c];
+        totals[c] = s;
+    }
+    /* per bucket: sort, count unique keys */
+    int64_t* bu = (int64_t*)calloc((size_t)NB + 1, sizeof(int64_t));
+#pragma omp parallel for num_threads(T) schedule(dynamic, 1)
+    for (int k = 0; k < NB; ++k) {
+        uint64_t* a = all + boff[k];
+        int64_t n = boff[k + 1] - boff[k];
+        if (n > 1) qsort(a, (size_t)n, 8, u64_cmp);
+        int64_t u = 0;
+        for (int64_t i = 0; i < n; ++i)
+            if (i == 0 || a[i] != a[i - 1]) ++u;
+        bu[k + 1] = u;
+    }
+    for (int k = 0; k < NB; ++k) bu[k + 1] += bu[k];
+    const int64_t E = bu[NB];
+    int zd = 0;
+    if (E <= cap) {
+#pragma omp parallel for num_threads(T) schedule(dynamic, 1) reduction(| : zd)
+        for (int k = 0; k < NB; ++k) {
+            uint64_t* a = all + boff[k];
+            int64_t n = boff[k + 1] - boff[k], e = bu[k];
+            for (int64_t i = 0; i < n;) {
+                int64_t j = i;
+                while (j < n && a[j] == a[i]) ++j;
+                uint32_t x = (uint32_t)(a[i] >> 32), y = (uint32_t)a[i];
+                int64_t s = j - i;
+                ea[e] = x;
+                eb[e] = y;
+                es[e] = s;
+                if (totals[x] == 0 || totals[y] == 0) {
+                    zd = 1;
+                    ew[e] = 0.0;
+                } else {
+                    ew[e] = ((double)s / (double)totals[x] + (double)s / (double)totals[y]) / 2.0;
+                }
+                ++e;
+                i = j;
+            }
+        }
+    }
+    *zero_div = zd;
+    free(all);
+    free(bu);
+    free(boff);
+    free(woff);
+    free(tb);
+    free(tn);
+    free(tv);
+    free(ttot);
     return E <= cap ? E : -E;
 }

@@ -56,6 +56,14 @@ def lib():
         L.oracle_update_pairs.argtypes = [_i64p, _u32p, ctypes.c_int64, _i64p, _u32p, ctypes.c_int64, _u32p, _u32p,
                                           _i64p, _f64p, ctypes.c_int64]
         L.oracle_update_pairs.restype = ctypes.c_int64
+        L.oracle_threads.argtypes = []
+        L.oracle_threads.restype = ctypes.c_int
+        L.oracle_omp_kmer_profile.argtypes = [ctypes.c_void_p, _i64p, _i64p, ctypes.c_int64, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_int64, _f64p]
+        L.oracle_omp_kmer_profile.restype = ctypes.c_int
+        L.oracle_omp_graph_reads.argtypes = [_i64p, _u32p, ctypes.c_int64, ctypes.c_int64, _i64p, _u32p, _u32p,
+                                             _i64p, _f64p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_omp_graph_reads.restype = ctypes.c_int64
         _LIB = L
     return _LIB
 
@@ -319,7 +327,7 @@ def read_fasta_file(path):
 
 def sam_groups(text, skip_headers=True):
     """SAM text -> [(RNAME, set(QNAME))] in order of first RNAME appearance:
-    contig.py:29-35's readset per RNAME group (universal newlines, hisat2.py:76-81
+    contig.py:29-35's readset per RNAME group (universal newlines, hisat2.py:49-53
     header filter)."""
     import io
 
@@ -330,3 +338,51 @@ def sam_groups(text, skip_headers=True):
         read, _, name, position, *_ = line.split("\t")
         groups.setdefault(name, set()).add(read)
     return list(groups.items())
+
+
+# ---------------------------------------------------------------------------
+# OpenMP twins: the on-node CPU baseline (bench.py cpu_baseline, SURVEY.md
+# §8(d)(2)).  Same results as the scalar functions (tests/test_oracle_golden.py).
+# ---------------------------------------------------------------------------
+
+def threads() -> int:
+    """OpenMP threads the twins use (OMP_NUM_THREADS, else all host cores)."""
+    return int(lib().oracle_threads())
+
+
+def omp_kmer_profile_packed(blob, offs, key_len, kmer_size, raw_keys, M):
+    """Dense profile of packed sequences against a column table from kmer_columns."""
+    N = len(offs) - 1
+    key_len = np.ascontiguousarray(key_len, np.int64)
+    prof = np.empty((N, M), dtype=np.float64)
+    rc = lib().oracle_omp_kmer_profile(_p(blob, ctypes.c_void_p), _p(np.ascontiguousarray(offs, np.int64), _i64p),
+                                       _p(key_len, _i64p), N, kmode_of(kmer_size), _p(raw_keys, ctypes.c_void_p), M,
+                                       _p(prof, _f64p))
+    if rc == 1:
+        raise AssertionError("oracle: k-mer missing from column set")
+    if rc == 2:
+        raise ZeroDivisionError("division by zero")
+    return prof
+
+
+def omp_graph_reads(grp_off, members, n_nodes):
+    """graph_groups(..., mult=None, pair_skip=None, dedup=True) on all host cores
+    (no first-emission positions)."""
+    grp_off = np.ascontiguousarray(grp_off, dtype=np.int64)
+    members = np.ascontiguousarray(members, dtype=np.uint32)
+    totals = np.zeros(max(n_nodes, 1), dtype=np.int64)
+    cap = max(1024, len(grp_off))
+    L = lib()
+    while True:
+        ea = np.zeros(cap, np.uint32)
+        eb = np.zeros(cap, np.uint32)
+        es = np.zeros(cap, np.int64)
+        ew = np.zeros(cap, np.float64)
+        zd = ctypes.c_int(0)
+        E = L.oracle_omp_graph_reads(_p(grp_off, _i64p), _p(members if len(members) else np.zeros(1, np.uint32), _u32p),
+                                     len(grp_off) - 1, n_nodes, _p(totals, _i64p), _p(ea, _u32p), _p(eb, _u32p),
+                                     _p(es, _i64p), _p(ew, _f64p), cap, ctypes.byref(zd))
+        if E >= 0:
+            break
+        cap = -E
+    return dict(a=ea[:E], b=eb[:E], shared=es[:E], weight=ew[:E], totals=totals[:n_nodes], zero_div=bool(zd.value))

@@ -109,7 +109,7 @@ def main():
     sm = {}
     for name, data in SAM.items():
         lines = data.decode("utf-8").splitlines()
-        lines = [ln for ln in lines if not ln.startswith("@")]  # hisat2.py:76-81
+        lines = [ln for ln in lines if not ln.startswith("@")]  # hisat2.py:49-53
         groups = OrderedDict()
         try:
             for ln in lines:

@@ -1,13 +1,17 @@
-"""World-size-2 gloo test of the sharded build's exchange logic (CPU only).
+"""Multi-rank CPU tests of the sharded build's exchange logic (no GPU, no torch).
 
 karma_amd.distributed.ShardedBuild is the production driver; here its compute
 backend is an oracle-backed CPU implementation of the same ops interface
 (presence bytes in the HIP ordinal layout, exception keys in the karma.h key
 encoding, sorted (a << 32 | b, count) pair lists), so what is under test is the
-sharding, the presence MAX-allreduce, the exception all-gather, the pair
-all-to-all-v to contig owners, the owned-totals all-gather and the owner-side
-weights.  The result must equal a single-process oracle run bit for bit.
+sharding, the presence all-gather + OR merge, the exception all-gather, the
+pair all-to-all-v to contig owners, the owned-totals all-gather and the
+owner-side weights, over the host-staged transport (karma_amd/comm.py HostComm)
+with ranks as processes (TCP star, karma_amd/hostgroup.py SocketGroup) or as
+threads (ThreadGroup).  The result must equal a single-process oracle run bit
+for bit.
 """
+import multiprocessing as mp
 import os
 import socket
 from collections import OrderedDict
@@ -15,11 +19,11 @@ from collections import OrderedDict
 import numpy as np
 import pytest
 
-torch = pytest.importorskip("torch")
-
-from karma_amd import engine  # noqa: E402  (host-only synth functions)
-from karma_amd.distributed import Comm, ShardedBuild  # noqa: E402
-from oracle import oracle  # noqa: E402
+from karma_amd import engine  # host-only synth functions
+from karma_amd.comm import HostComm
+from karma_amd.distributed import ShardedBuild
+from karma_amd.hostgroup import SocketGroup, ThreadGroup, run_ranks
+from oracle import oracle
 
 KMODE_5P6 = -1
 
@@ -63,7 +67,7 @@ class OracleOps:
     def kmer_plan(self, store, kmode):
         return {"seqs": store, "kmode": kmode}
 
-    def presence_bytes(self, plan):
+    def presence_words(self, plan):
         S = ordinal_space(plan["kmode"])
         pres = np.zeros(S, np.uint8)
         exc = set()
@@ -74,16 +78,18 @@ class OracleOps:
                 else:
                     exc.add(key_of(km, plan["kmode"]))
         plan["exc"] = sorted(exc)
-        return torch.from_numpy(pres)
+        plan["pres"] = pres
+        return np.packbits(pres, bitorder="little").view(np.uint32).copy()
 
-    def set_presence_bytes(self, plan, pres):
-        plan["pres"] = pres.numpy().copy()
+    def presence_merge(self, plan, all_words, n_sets):
+        w = np.bitwise_or.reduce(np.asarray(all_words, np.uint32).reshape(n_sets, -1), axis=0)
+        plan["pres"] = np.unpackbits(w.view(np.uint8), bitorder="little")[: ordinal_space(plan["kmode"])]
 
     def exceptions(self, plan):
-        return torch.tensor([np.int64(np.uint64(k).view(np.int64)) for k in plan["exc"]], dtype=torch.int64)
+        return np.array(plan["exc"], np.uint64)
 
     def set_exceptions(self, plan, keys):
-        plan["exc_all"] = sorted(set(int(np.int64(k).view(np.uint64)) for k in keys.tolist()))
+        plan["exc_all"] = sorted(set(int(k) for k in np.asarray(keys, np.uint64).tolist()))
 
     def finalize(self, plan):
         kmode = plan["kmode"]
@@ -100,7 +106,7 @@ class OracleOps:
         return len(plan["cols"])
 
     def profile_buffer(self, n, M):
-        return torch.zeros((n, M), dtype=torch.float64)
+        return np.zeros((n, M), dtype=np.float64)
 
     def profile(self, plan, out):
         seqs = plan["seqs"]
@@ -118,7 +124,7 @@ class OracleOps:
             key_len.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(seqs), plan["kmode"],
             raw.ctypes.data_as(ctypes.c_void_p), M, prof.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), None)
         assert rc == 0
-        out.copy_(torch.from_numpy(prof))
+        out[...] = prof
 
     def columns(self, plan):
         return plan["cols"]
@@ -135,28 +141,24 @@ class OracleOps:
         order = np.argsort(np.array(keys, np.uint64), kind="stable")
         return {"keys": np.array(keys, np.uint64)[order], "counts": np.array(counts, np.int64)[order]}
 
-    def pairs_split(self, pairs, bounds):
-        starts = np.searchsorted(pairs["keys"], np.asarray(bounds, np.uint64) << np.uint64(32))
-        return (torch.from_numpy(pairs["keys"].view(np.int64).copy()), torch.from_numpy(pairs["counts"].copy()),
-                starts)
-
     def pairs_kc_split(self, pairs, bounds):
-        keys, counts, starts = self.pairs_split(pairs, bounds)
-        return torch.stack([keys, counts], 1), starts
+        starts = np.searchsorted(pairs["keys"], np.asarray(bounds, np.uint64) << np.uint64(32))
+        kc = np.stack([pairs["keys"].view(np.int64), pairs["counts"]], 1).reshape(-1)
+        return kc, starts
 
     def merge_kc(self, kc, runs):
-        kc = kc.reshape(-1, 2)
-        return self.merge(kc[:, 0].contiguous(), kc[:, 1].contiguous(), runs)
+        kc = np.asarray(kc, np.int64).reshape(-1, 2)
+        return self.merge(kc[:, 0].copy(), kc[:, 1].copy(), runs)
 
     def merge(self, keys, counts, runs):
-        k = keys.numpy().view(np.uint64)
+        k = keys.view(np.uint64)
         # the contract of karma_pairs_merge_runs: one sorted slice per sender
         off = np.r_[0, np.cumsum(runs)]
         assert off[-1] == len(k) and all(np.all(k[off[r] + 1:off[r + 1]] >= k[off[r]:off[r + 1] - 1])
                                          for r in range(len(runs)))
         u, inv = np.unique(k, return_inverse=True)
         c = np.zeros(len(u), np.int64)
-        np.add.at(c, inv, counts.numpy())
+        np.add.at(c, inv, counts)
         return {"keys": u, "counts": c}
 
     def totals(self, pairs, n):
@@ -165,10 +167,10 @@ class OracleOps:
         b = (pairs["keys"] & np.uint64(0xFFFFFFFF)).astype(np.int64)
         d = a == b
         t[a[d]] = pairs["counts"][d]
-        return torch.from_numpy(t)
+        return t
 
     def edges(self, pairs, n, totals=None):
-        tot = self.totals(pairs, n).numpy() if totals is None else totals.numpy()
+        tot = self.totals(pairs, n) if totals is None else np.asarray(totals)
         a = (pairs["keys"] >> np.uint64(32)).astype(np.int64)
         b = (pairs["keys"] & np.uint64(0xFFFFFFFF)).astype(np.int64)
         keep = (a != b) & (pairs["counts"] != 0)
@@ -205,17 +207,22 @@ def shard_inputs(rank, world):
     return seqs, rec
 
 
-def _worker(rank, world, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    comm = Comm.create(world, rank, backend="gloo")
+def run_rank(group, rank):
+    comm = HostComm(group)
+    world = group.world
     seqs, rec = shard_inputs(rank, world)
     build = ShardedBuild(None, comm, KMODE_5P6, N_LOC * world, rank * N_LOC, N_LOC, ops=OracleOps())
     res = build.run(seqs, rec, len(rec), keep=True)
     e = res["edges"]
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), profile=res["profile"].numpy(),
-             cols=np.array(res["columns"], np.uint64), a=e["a"], b=e["b"], w=e["weight"], s=e["shared"],
-             tot=e["totals"])
-    comm.close()
+    return dict(profile=res["profile"], cols=np.array(res["columns"], np.uint64), a=e["a"], b=e["b"],
+                w=e["weight"], s=e["shared"], tot=e["totals"])
+
+
+def _proc_worker(rank, world, port, out_dir):
+    g = SocketGroup(world, rank, "127.0.0.1", port)
+    out = run_rank(g, rank)
+    g.close()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out)
 
 
 def free_port():
@@ -226,10 +233,7 @@ def free_port():
     return p
 
 
-def test_sharded_build_world2_matches_single_process(tmp_path):
-    world = 2
-    torch.multiprocessing.spawn(_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
-    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+def check_union(parts, world):
     # single-process reference on the union of the shards
     all_seqs, all_rec = OrderedDict(), []
     for r in range(world):
@@ -255,5 +259,69 @@ def test_sharded_build_world2_matches_single_process(tmp_path):
     for r, p in enumerate(parts):
         assert np.all((p["a"] >= r * N_LOC) & (p["a"] < (r + 1) * N_LOC))
         assert np.array_equal(p["tot"], o["totals"])
-    # the exchange is real: some fragments of each rank touch the other rank's contigs
+    # the exchange is real: some fragments of each rank touch the other ranks' contigs
     assert len(np.unique(a // N_LOC)) == world
+
+
+def test_sharded_build_world2_processes_match_single_process(tmp_path):
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = free_port()
+    procs = [ctx.Process(target=_proc_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    check_union([dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)], world)
+
+
+@pytest.mark.parametrize("world", [3, 4, 8])
+def test_sharded_build_thread_ranks_match_single_process(world):
+    check_union(run_ranks(world, run_rank), world)
+
+
+@pytest.mark.parametrize("kind", ["threads", "sockets"])
+def test_host_comm_collectives(kind, tmp_path):
+    world = 3
+
+    def body(group, rank):
+        c = HostComm(group)
+        out = {}
+        out["max"] = c.max_float(rank * 1.5)
+        out["sum"] = c.sum_int(rank + 1)
+        out["fixed"] = c.allgather_fixed(np.full(4, rank, np.uint32))
+        out["var"] = c.allgather_var(np.arange(rank, dtype=np.int64))
+        bounds = np.array([0, 2, 2, 7])
+        buf = np.full(7, -1, np.int64)
+        buf[bounds[rank]:bounds[rank + 1]] = 10 * rank + np.arange(bounds[rank + 1] - bounds[rank])
+        out["slices"] = c.allgather_slices_(buf, bounds).copy()
+        send = np.concatenate([np.full(r + 1, 100 * rank + r, np.int64) for r in range(world)])
+        out["a2a"], out["recv"] = c.alltoallv(send, [r + 1 for r in range(world)])
+        c.barrier()
+        return out
+
+    if kind == "threads":
+        outs = run_ranks(world, body)
+    else:
+        port = free_port()
+        import threading
+        outs = [None] * world
+
+        def t(r):
+            g = SocketGroup(world, r, "127.0.0.1", port)
+            outs[r] = body(g, r)
+            g.close()
+
+        ts = [threading.Thread(target=t, args=(r,)) for r in range(world)]
+        for x in ts:
+            x.start()
+        for x in ts:
+            x.join(60)
+    for r, o in enumerate(outs):
+        assert o["max"] == 3.0 and o["sum"] == 6
+        assert np.array_equal(o["fixed"], np.repeat(np.arange(world, dtype=np.uint32), 4))
+        assert np.array_equal(o["var"], np.array([0, 0, 1], np.int64))
+        assert np.array_equal(o["slices"], np.array([0, 1, 20, 21, 22, 23, 24], np.int64))
+        assert o["recv"] == [r + 1] * world
+        assert np.array_equal(o["a2a"], np.concatenate([np.full(r + 1, 100 * s + r) for s in range(world)]))

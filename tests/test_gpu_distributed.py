@@ -1,21 +1,31 @@
-"""Two GPU ranks (one process each, sharing cuda:0, gloo with host staging)
-through the production ShardedBuild + HipOps path; the union of the ranks'
-outputs must equal the single-process oracle bit for bit."""
-import os
-import socket
+"""GPU ranks sharing cuda:0 through the production ShardedBuild + HipOps path.
+
+RCCL refuses two ranks on one device, so on the one-GPU box the ranks are
+threads of one process, each with its own karma context and streams, and the
+exchange goes through the host-staged transport (karma_amd/comm.py HostComm
+over a ThreadGroup).  Everything else -- presence bitmaps, exception keys, the
+device split, the wire format, the owner's merge, totals, weights -- is the
+production code.  The union of the ranks' outputs must equal the
+single-process oracle bit for bit."""
+import subprocess
+import sys
 from collections import OrderedDict
 
 import numpy as np
 import pytest
 
-torch = pytest.importorskip("torch")
+from karma_amd import _lib, engine
+from karma_amd.comm import HostComm, SoloComm
+from karma_amd.distributed import ShardedBuild
+from karma_amd.hostgroup import run_ranks
+from oracle import oracle
+
 pytestmark = pytest.mark.gpu
 
 N_LOC, F_LOC, SEED, NRATE = 700, 60_000, 23, 300
 
 
 def _inputs(rank, world):
-    from karma_amd import engine
     n_glob = N_LOC * world
     blob, offs, key_len = engine.synth_contigs(SEED, N_LOC, 30, 900, NRATE, first=rank * N_LOC)
     genes = engine.synth_genes(SEED, n_glob)
@@ -23,39 +33,32 @@ def _inputs(rank, world):
     return blob, offs, key_len, rec
 
 
-def _worker(rank, world, port, out_dir, overlap):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    from karma_amd import _lib, engine
-    from karma_amd.distributed import Comm, ShardedBuild
-    comm = Comm.create(world, rank, backend="gloo")
-    torch.cuda.set_device(0)
+def _rank(group, rank, overlap):
+    world = group.world
     ctx = _lib.Context(0)
-    blob, offs, key_len, rec = _inputs(rank, world)
-    # overlap: the local graph build runs concurrently on a second context;
-    # otherwise the default order (profile on the side stream beside the
-    # graph's tail and the exchange)
-    build = ShardedBuild(ctx, comm, -1, N_LOC * world, rank * N_LOC, N_LOC, overlap=overlap)
-    store = engine.ContigStore(ctx, blob, offs, key_len)
-    rec_dev = torch.from_numpy(rec.view(np.int64).reshape(-1)).to(build.ops.dev)
-    res = build.run(store, rec_dev.data_ptr(), len(rec), keep=True)
-    e = res["edges"]
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), profile=res["profile"].cpu().numpy(),
-             cols=res["columns"], a=e.a, b=e.b, w=e.weight, tot=e.totals)
-    store.close()
-    comm.close()
+    try:
+        comm = HostComm(group)
+        blob, offs, key_len, rec = _inputs(rank, world)
+        # overlap: the local graph build runs concurrently on a second context;
+        # otherwise the default order (profile on the side stream beside the
+        # graph's tail and the exchange)
+        build = ShardedBuild(ctx, comm, -1, N_LOC * world, rank * N_LOC, N_LOC, overlap=overlap)
+        store = engine.ContigStore(ctx, blob, offs, key_len)
+        rec_dev = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))
+        res = build.run(store, rec_dev.ptr, len(rec), keep=True)
+        e = res["edges"]
+        out = dict(profile=res["profile"].numpy(), cols=res["columns"], a=e.a, b=e.b, w=e.weight, tot=e.totals)
+        build.close()
+        store.close()
+        rec_dev.close()
+        return out
+    finally:
+        ctx.close()
 
 
-@pytest.mark.parametrize("overlap", [True, False])
-def test_two_gpu_ranks_match_oracle(tmp_path, overlap):
-    from karma_amd import engine
-    from oracle import oracle
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    world = 2
-    torch.multiprocessing.spawn(_worker, args=(world, port, str(tmp_path), overlap), nprocs=world, join=True)
-    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+@pytest.mark.parametrize("world,overlap", [(2, True), (2, False), (3, False)])
+def test_gpu_ranks_match_oracle(world, overlap):
+    parts = run_ranks(world, _rank, overlap)
     seqs, recs = OrderedDict(), []
     for r in range(world):
         blob, offs, _, rec = _inputs(r, world)
@@ -81,24 +84,50 @@ def test_two_gpu_ranks_match_oracle(tmp_path, overlap):
 
 def test_overlap_equals_sequential_single_gpu():
     # the graph build on a second context/stream, concurrent with the profile,
-    # gives the same bytes as the sequential build
-    from karma_amd import _lib, engine
-    from karma_amd.distributed import Comm, ShardedBuild
-    comm = Comm.create(1, 0)
+    # gives the same bytes as the sequential and the side-stream builds
     ctx = _lib.Context(0)
     blob, offs, key_len, rec = _inputs(0, 1)
     store = engine.ContigStore(ctx, blob, offs, key_len)
+    rec_dev = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))
     outs = []
-    for overlap in (False, True):
-        build = ShardedBuild(ctx, comm, -1, N_LOC, 0, N_LOC, overlap=overlap)
-        rec_dev = torch.from_numpy(rec.view(np.int64).reshape(-1)).to(build.ops.dev)
-        res = build.run(store, rec_dev.data_ptr(), len(rec), keep=True)
+    for overlap, sequential in ((False, False), (True, False), (False, True)):
+        build = ShardedBuild(ctx, SoloComm(), -1, N_LOC, 0, N_LOC, overlap=overlap)
+        res = build.run(store, rec_dev.ptr, len(rec), keep=True, sequential=sequential)
         e = res["edges"]
-        outs.append([res["profile"].cpu().numpy().copy(), np.array(e.a), np.array(e.b), np.array(e.weight),
-                     np.array(e.totals)])
+        outs.append([res["profile"].numpy(), np.array(e.a), np.array(e.b), np.array(e.weight), np.array(e.totals)])
         build.close()
-    for x, y in zip(*outs):
-        assert x.shape == y.shape and np.array_equal(x.view(np.uint8), y.view(np.uint8))
+    for other in outs[1:]:
+        for x, y in zip(outs[0], other):
+            assert x.shape == y.shape and np.array_equal(x.view(np.uint8), y.view(np.uint8))
     assert len(outs[0][1]) > 0
     store.close()
+    rec_dev.close()
     ctx.close()
+
+
+def test_product_path_never_imports_torch():
+    # north_star: no PyTorch on this path -- the drop-in classes, the sharded
+    # driver and the bench run with torch absent from sys.modules
+    code = (
+        "import sys; sys.path.insert(0, '.')\n"
+        "from collections import OrderedDict\n"
+        "from karma_amd import engine, _lib\n"
+        "from karma_amd.kmer import KmerClustering\n"
+        "from karma_amd.read_graph import ReadGraph\n"
+        "from karma_amd.distributed import ShardedBuild\n"
+        "from karma_amd.comm import SoloComm\n"
+        "import numpy as np\n"
+        "blob, offs, kl = engine.synth_contigs(3, 200, 50, 500, 0)\n"
+        "seqs = OrderedDict((f'>ctg{i}', bytes(blob[offs[i]:offs[i+1]]).decode()) for i in range(200))\n"
+        "KmerClustering(seqs, '/tmp', '5p6', 2)._KmerClustering__calc_kmer_profile()\n"
+        "ctx = _lib.Context(0)\n"
+        "rec = engine.synth_records(3, 200, 0, 5000, True)\n"
+        "b = ShardedBuild(ctx, SoloComm(), -1, 200, 0, 200)\n"
+        "st = engine.ContigStore(ctx, blob, offs, kl)\n"
+        "d = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))\n"
+        "b.run(st, d.ptr, len(rec)); b.close()\n"
+        "assert 'torch' not in sys.modules, 'torch was imported'\n"
+        "print('no-torch ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "no-torch ok" in r.stdout

@@ -7,7 +7,7 @@ mkdir -p $OUT
 export KARMA_OVERLAP=0
 run() {
   local tag=$1 lib=$2
-  KARMA_LIB=$lib timeout -k 10 150 python $REPO/bench.py --cpu-sample 0 --steps ${AB_STEPS:-10} > $OUT/$tag.json 2> $OUT/$tag.err
+  KARMA_LIB=$lib timeout -k 10 150 python $REPO/bench.py --cpu-baseline off --no-e2e --steps ${AB_STEPS:-10} > $OUT/$tag.json 2> $OUT/$tag.err
   local rc=$?
   python -c "
 import json; d=json.load(open('$OUT/$tag.json')); k=d['kernels_ms_per_step']

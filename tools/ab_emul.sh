@@ -8,7 +8,7 @@ export KARMA_OVERLAP=0
 W=$1; shift
 for v in base "$@"; do
   lib=""; [ $v != base ] && lib=$REPO/karma_amd/variants/libkarma_$v.so
-  KARMA_LIB=$lib timeout -k 10 150 python $REPO/bench.py --cpu-sample 0 --steps ${AB_STEPS:-10} --emulate-ranks $W > $OUT/emu${W}_$v.json 2> $OUT/emu${W}_$v.err
+  KARMA_LIB=$lib timeout -k 10 150 python $REPO/bench.py --cpu-baseline off --no-e2e --steps ${AB_STEPS:-10} --emulate-ranks $W > $OUT/emu${W}_$v.json 2> $OUT/emu${W}_$v.err
   rc=$?
   python -c "
 import json; d=json.load(open('$OUT/emu${W}_$v.json')); k=d['kernels_ms_per_step']

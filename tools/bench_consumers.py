@@ -31,6 +31,12 @@ from karma_amd import rearrange  # noqa: E402
 from karma_amd.read_graph import ReadGraph  # noqa: E402
 
 
+
+def _lookup(nesting):
+    """index -> {previous_cluster, mcl_subcluster}, the shape karma.py:78-100 builds."""
+    flat = [(no, sub) for no, cl in enumerate(nesting, 1) for sub in cl]
+    return {i: {"previous_cluster": no, "mcl_subcluster": sub} for i, (no, sub) in enumerate(flat)}
+
 def ref_edge_list(g):
     return "\n".join(f"{A} {B} {data['weight']}" for A, B, data in g.edges(data=True)).encode("utf-8")
 
@@ -204,7 +210,7 @@ def main():
             parts.append(cl[s0:c])
             s0 = c
         nest.append(parts)
-    subs = rearrange.create_lookup_dict(nest, nodes)
+    subs = _lookup(nest)
     rearrange.calc_connections_between_mcl_subclusters(subs, 0.05, full_graph=g)  # warm
     t = time.perf_counter()
     groups = rearrange.calc_connections_between_mcl_subclusters(subs, 0.05, full_graph=g)
@@ -212,7 +218,7 @@ def main():
     # the reference's walk is O(S^2): time it on the first clusters and scale by (S / s)^2
     small = nest[: max(1, len(nest) // 25)]
     small_nodes = [x for c in small for sc in c for x in sc]
-    ssubs = rearrange.create_lookup_dict(small, small_nodes)
+    ssubs = _lookup(small)
     t = time.perf_counter()
     ref_small = ref_calc(ssubs, g, 0.05)
     t_ref_small = time.perf_counter() - t
