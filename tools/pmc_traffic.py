@@ -7,7 +7,11 @@ MI355X_MICROARCH.md §HBM prescribes: on gfx950 FETCH_SIZE reports 1/2 of a
 wide (16 B/lane) streaming read, so reads are doubled; WRITE_SIZE is exact for
 16-B stores.  graph_classify, the partition and kmer_profile move 16 B per lane.
 
-Usage: python tools/pmc_traffic.py pmc_summary.json [out.json]
+The output is keyed by workload (bench.py pmc_traffic(): "<config>[_strong]
+[_shuffled]_n<ranks>"), so a number is only ever reported for the workload
+whose PMC runs produced it; other keys in an existing out.json are kept.
+
+Usage: python tools/pmc_traffic.py pmc_summary.json out.json WORKLOAD_KEY [SOURCE]
 """
 import json
 import sys
@@ -35,9 +39,16 @@ def main():
     for k, v in src.items():
         if k in NAMES and v.get("fetch_MB") == v.get("fetch_MB"):  # skip NaN
             out[NAMES[k]] = int(round((2 * v["fetch_MB"] + v["write_MB"]) * 1024 * 1024))
-    dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
-    json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
-    print(json.dumps(out))
+    dst, key = sys.argv[2], sys.argv[3]
+    try:
+        allw = json.load(open(dst))
+    except (OSError, ValueError):
+        allw = {}
+    if len(sys.argv) > 4:
+        out["_source"] = sys.argv[4]
+    allw[key] = out
+    json.dump(allw, open(dst, "w"), indent=1, sort_keys=True)
+    print(json.dumps(allw[key]))
 
 
 if __name__ == "__main__":
