@@ -32,7 +32,15 @@ namespace {
 
 using karma::set_error;
 
+// Minimum work per thread is divided by this; the sanitizer fuzz build
+// (Makefile `asan`) raises it so that small random texts still split into
+// many thread chunks and the chunk-merge code runs under the sanitizers.
+#ifndef KARMA_INGEST_SPLIT_DIV
+#define KARMA_INGEST_SPLIT_DIV 1
+#endif
+
 int clamp_threads(int threads, size_t work, size_t per_thread) {
+    per_thread = std::max<size_t>(1, per_thread / KARMA_INGEST_SPLIT_DIV);
     int t = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
     t = std::max(1, std::min(t, 64));
     const size_t by_work = std::max<size_t>(1, work / per_thread);
@@ -406,6 +414,12 @@ extern "C" int karma_fasta_info(karma_fasta* f, int64_t* n, int64_t* seq_bytes, 
     return KARMA_OK;
 }
 
+// Output copies of the get calls: nothing to do for a null destination or an
+// empty array (whose data() may be null, which memcpy must not see).
+static inline void copy_out(void* dst, const void* src, size_t bytes) {
+    if (dst && bytes) memcpy(dst, src, bytes);
+}
+
 extern "C" int karma_fasta_get(karma_fasta* f, uint8_t* seq, int64_t* seq_off, char* keys, int64_t* key_off,
                                int32_t* key_len) {
     if (!f) {
@@ -413,11 +427,11 @@ extern "C" int karma_fasta_get(karma_fasta* f, uint8_t* seq, int64_t* seq_off, c
         return KARMA_ERR_ARG;
     }
     const int64_t N = (int64_t)f->key_len.size();
-    if (seq) memcpy(seq, f->seq.get(), (size_t)f->seq_off[N] + 16);
-    if (seq_off) memcpy(seq_off, f->seq_off.data(), sizeof(int64_t) * (N + 1));
-    if (keys) memcpy(keys, f->keys.get(), (size_t)f->key_off[N]);
-    if (key_off) memcpy(key_off, f->key_off.data(), sizeof(int64_t) * (N + 1));
-    if (key_len) memcpy(key_len, f->key_len.data(), sizeof(int32_t) * N);
+    copy_out(seq, f->seq.get(), (size_t)f->seq_off[N] + 16);
+    copy_out(seq_off, f->seq_off.data(), sizeof(int64_t) * (N + 1));
+    copy_out(keys, f->keys.get(), (size_t)f->key_off[N]);
+    copy_out(key_off, f->key_off.data(), sizeof(int64_t) * (N + 1));
+    copy_out(key_len, f->key_len.data(), sizeof(int32_t) * N);
     return KARMA_OK;
 }
 
@@ -644,12 +658,12 @@ extern "C" int karma_eq_get(karma_eq* q, char* names, int64_t* name_off, int64_t
         set_error("karma_eq_get: null handle");
         return KARMA_ERR_ARG;
     }
-    if (names) memcpy(names, q->names.data(), q->names.size());
-    if (name_off) memcpy(name_off, q->name_off.data(), q->name_off.size() * sizeof(int64_t));
-    if (cls_off) memcpy(cls_off, q->cls_off.data(), q->cls_off.size() * sizeof(int64_t));
-    if (members) memcpy(members, q->members.data(), q->members.size() * sizeof(uint32_t));
-    if (counts) memcpy(counts, q->counts.data(), q->counts.size() * sizeof(int64_t));
-    if (pair_skip) memcpy(pair_skip, q->pair_skip.data(), q->pair_skip.size());
+    copy_out(names, q->names.data(), q->names.size());
+    copy_out(name_off, q->name_off.data(), q->name_off.size() * sizeof(int64_t));
+    copy_out(cls_off, q->cls_off.data(), q->cls_off.size() * sizeof(int64_t));
+    copy_out(members, q->members.data(), q->members.size() * sizeof(uint32_t));
+    copy_out(counts, q->counts.data(), q->counts.size() * sizeof(int64_t));
+    copy_out(pair_skip, q->pair_skip.data(), q->pair_skip.size());
     return KARMA_OK;
 }
 
@@ -905,11 +919,11 @@ extern "C" int karma_sam_get(karma_sam* S, uint32_t* records, char* rnames, int6
         return KARMA_ERR_ARG;
     }
     const size_t L = S->q_len.size();
-    if (records) memcpy(records, S->records.data(), L * 2 * sizeof(uint32_t));
-    if (rnames) memcpy(rnames, S->rnames.data(), S->rnames.size());
-    if (rname_off) memcpy(rname_off, S->rname_off.data(), S->rname_off.size() * sizeof(int64_t));
-    if (q_start) memcpy(q_start, S->q_start.data(), L * sizeof(int64_t));
-    if (q_len) memcpy(q_len, S->q_len.data(), L * sizeof(int32_t));
+    copy_out(records, S->records.data(), L * 2 * sizeof(uint32_t));
+    copy_out(rnames, S->rnames.data(), S->rnames.size());
+    copy_out(rname_off, S->rname_off.data(), S->rname_off.size() * sizeof(int64_t));
+    copy_out(q_start, S->q_start.data(), L * sizeof(int64_t));
+    copy_out(q_len, S->q_len.data(), L * sizeof(int32_t));
     return KARMA_OK;
 }
 
