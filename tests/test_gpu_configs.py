@@ -45,12 +45,11 @@ def device_profile_digests(prof, plain=True, threads=8, in_flight=12):
     from concurrent.futures import ThreadPoolExecutor
 
     n, M = prof.shape
-    flat = prof.reshape(-1)
     h = hashlib.sha256()
     digs, pend = [], []
     with ThreadPoolExecutor(threads) as pool, ThreadPoolExecutor(1) as seq:
         for lo in range(0, n, D.BLOCK_ROWS):
-            blk = flat.view(lo * M, (min(n, lo + D.BLOCK_ROWS) - lo) * M).numpy()
+            blk = prof.view(lo * M, (min(n, lo + D.BLOCK_ROWS) - lo) * M).numpy()
             mv = memoryview(blk).cast("B")
             pend.append((pool.submit(lambda m: hashlib.sha256(m).digest(), mv),
                          seq.submit(h.update, mv) if plain else None))
