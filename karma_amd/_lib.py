@@ -193,8 +193,22 @@ def check(rc):
     return rc
 
 
+# diagnostic: per-entry-point host time (KARMA_CALL_TIMES=1; tools/host_profile.py)
+CALL_TIMES = {} if os.environ.get("KARMA_CALL_TIMES") == "1" else None
+
+
 def call(name, *args):
-    return check(getattr(load(), name)(*args))
+    if CALL_TIMES is None:
+        return check(getattr(load(), name)(*args))
+    import time
+
+    t0 = time.perf_counter()
+    try:
+        return check(getattr(load(), name)(*args))
+    finally:
+        dt = time.perf_counter() - t0
+        n, tot = CALL_TIMES.get(name, (0, 0.0))
+        CALL_TIMES[name] = (n + 1, tot + dt)
 
 
 def ptr(a):

@@ -228,6 +228,122 @@ __global__ void runs_check_kernel(const uint64_t* __restrict__ k, int64_t n, con
     }
 }
 
+
+// ---- owner merge of W sorted runs: one ranking pass ------------------------------
+// Element j of run r (key k) lands at j + sum over the other runs s of the
+// number of their elements that precede it: < k for s > r, <= k for s < r
+// (stable, so equal keys from different runs end up adjacent in run order).
+// A block takes a tile of kMergeTile consecutive elements of one run.  For each
+// other run, the counts of the tile's first and last keys bound the counts of
+// every key in between: that window of run s is searched once per block (two
+// global binary searches), staged in LDS when it fits, and each element's
+// count is a short search inside it.  The same pass flags a descent inside a
+// run.  Replaces a merge tree of W - 1 pairwise merges (2 launches each).
+constexpr int kMergeMaxRuns = 64;
+constexpr int kMergeTile = 1024;     // elements per block (4 per thread)
+constexpr int kMergeLds = 6144;      // staged window keys per block (48 KB)
+struct RunOffs {
+    int64_t o[kMergeMaxRuns + 1];    // run offsets
+    int64_t t[kMergeMaxRuns + 1];    // first tile of each run (prefix of ceil(len / kMergeTile))
+};
+
+// number of elements of sorted run [lo, hi) preceding key k (<= k when le, else < k)
+template <typename KeyAt>
+__device__ __forceinline__ int64_t count_before(KeyAt key_at, int64_t lo, int64_t hi, uint64_t k, bool le) {
+    int64_t n = hi - lo, base = lo;
+    while (n > 0) {
+        const int64_t half = n >> 1;
+        const uint64_t m = key_at(base + half);
+        const bool before = le ? m <= k : m < k;
+        base = before ? base + half + 1 : base;
+        n = before ? n - half - 1 : half;
+    }
+    return base;
+}
+
+__global__ void __launch_bounds__(256) merge_rank_kernel(const uint64_t* __restrict__ keys,
+                                                         const int64_t* __restrict__ counts,
+                                                         const longlong2* __restrict__ kc, RunOffs R, int nr,
+                                                         uint64_t* __restrict__ ko, int64_t* __restrict__ co,
+                                                         int64_t* __restrict__ bad) {
+    __shared__ int64_t wlo[kMergeMaxRuns], whi[kMergeMaxRuns];  // window of run s: [wlo, whi] (counts)
+    __shared__ int wbase[kMergeMaxRuns];                        // its LDS slot (-1: searched in place)
+    __shared__ uint64_t wkeys[kMergeLds];
+    __shared__ int r_s;
+    auto key_at = [&](int64_t i) -> uint64_t { return kc ? (uint64_t)kc[i].x : keys[i]; };
+    const int64_t tile = blockIdx.x;
+    if (threadIdx.x == 0) {
+        int r = 0;
+        while (r + 1 < nr && R.t[r + 1] <= tile) ++r;
+        r_s = r;
+    }
+    __syncthreads();
+    const int r = r_s;
+    const int64_t t0 = R.o[r] + (tile - R.t[r]) * kMergeTile;
+    const int64_t t1 = min(R.o[r + 1], t0 + kMergeTile);
+    // window bounds: thread 2s searches for the tile's first key, 2s + 1 for its last
+    if (threadIdx.x < 2 * nr) {
+        const int sr = threadIdx.x >> 1;
+        if (sr != r) {
+            const uint64_t k = key_at((threadIdx.x & 1) ? t1 - 1 : t0);
+            const int64_t c = count_before(key_at, R.o[sr], R.o[sr + 1], k, sr < r);
+            if (threadIdx.x & 1) whi[sr] = c;
+            else wlo[sr] = c;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int used = 0;
+        for (int sr = 0; sr < nr; ++sr) {
+            if (sr == r) continue;
+            if (whi[sr] < wlo[sr]) whi[sr] = wlo[sr];  // an unsorted run (flagged below): stay in bounds
+            const int64_t len = whi[sr] - wlo[sr];
+            if (used + len <= kMergeLds) {
+                wbase[sr] = used;
+                used += (int)len;
+            } else {
+                wbase[sr] = -1;
+            }
+        }
+    }
+    __syncthreads();
+    for (int sr = 0; sr < nr; ++sr) {
+        if (sr == r || wbase[sr] < 0) continue;
+        const int64_t lo = wlo[sr];
+        const int len = (int)(whi[sr] - lo);
+        for (int i = threadIdx.x; i < len; i += blockDim.x) wkeys[wbase[sr] + i] = key_at(lo + i);
+    }
+    __syncthreads();
+    for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+        uint64_t k;
+        int64_t c;
+        if (kc) {
+            const longlong2 v = kc[i];
+            k = (uint64_t)v.x;
+            c = (int64_t)v.y;
+        } else {
+            k = keys[i];
+            c = counts[i];
+        }
+        if (i > R.o[r] && key_at(i - 1) > k) *bad = 1;
+        int64_t pos = i - R.o[r];
+        for (int sr = 0; sr < nr; ++sr) {
+            if (sr == r) continue;
+            const int64_t lo = wlo[sr], hi = whi[sr];
+            int64_t cnt;
+            if (wbase[sr] >= 0) {
+                const uint64_t* w = wkeys + wbase[sr] - lo;  // w[x] = key of element x of the window
+                cnt = count_before([&](int64_t x) { return w[x]; }, lo, hi, k, sr < r);
+            } else {
+                cnt = count_before(key_at, lo, hi, k, sr < r);
+            }
+            pos += cnt - R.o[sr];
+        }
+        ko[pos] = k;
+        co[pos] = c;
+    }
+}
+
 }  // namespace
 
 namespace karma {
@@ -515,73 +631,93 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
         sk = kb[1].ptr;
         sc = cb[1].ptr;
     }
-    if (kc && n) {  // interleaved device input: split once into the merge's first buffers
-        KARMA_TRY(kb[1].alloc(ctx, n));
-        KARMA_TRY(cb[1].alloc(ctx, n));
-        KARMA_LAUNCH(ctx, "merge_split", deinterleave_kc_kernel, std::min<int64_t>(grid1(n), 4096), 256, 0,
-                     reinterpret_cast<const longlong2*>(kc), n, kb[1].ptr, cb[1].ptr);
-        sk = kb[1].ptr;
-        sc = cb[1].ptr;
-    }
     // st: [0] unique keys (ReduceByKey's run count), [1] order violation
-    DevArray<int64_t> st, doff;
+    DevArray<int64_t> st;
     KARMA_TRY(st.alloc(ctx, 2));
-    KARMA_TRY(doff.alloc(ctx, n_runs + 1));
     KARMA_HIP(hipMemsetAsync(st.ptr, 0, 16, ctx->stream));
     void* hpin = nullptr;
     KARMA_TRY(ctx_pinned(ctx, std::max<size_t>(16, (n_runs + 1) * 8), &hpin));
-    std::memcpy(hpin, off.data(), (n_runs + 1) * 8);
-    KARMA_HIP(hipMemcpyAsync(doff.ptr, hpin, (n_runs + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-    if (n > 1)
-        KARMA_LAUNCH(ctx, "runs_check", runs_check_kernel, std::min<int64_t>(grid1(n), 4096), 256, 0, sk, n, doff.ptr,
-                     n_runs, st.ptr + 1);
-    // pairwise merge tree over the runs (rocprim merge path), ping-pong buffers
-    if (n_runs > 1 && n) {
-        size_t need = 0;
-        for (std::vector<int64_t> o = off; o.size() > 2;) {  // plan: the largest temporary
-            std::vector<int64_t> next{0};
-            for (size_t j = 0; j + 1 < o.size(); j += 2) {
-                if (j + 2 < o.size() && o[j + 1] > o[j] && o[j + 2] > o[j + 1]) {
-                    size_t tb = 0;
-                    KARMA_HIP(rocprim::merge(nullptr, tb, sk, sk, (uint64_t*)nullptr, sc, sc, (int64_t*)nullptr,
-                                             (size_t)(o[j + 1] - o[j]), (size_t)(o[j + 2] - o[j + 1]),
-                                             rocprim::less<uint64_t>(), ctx->stream));
-                    need = std::max(need, tb);
-                }
-                next.push_back(o[std::min(j + 2, o.size() - 1)]);
-            }
-            o.swap(next);
-        }
-        DevArray<uint8_t> tmp;
-        KARMA_TRY(tmp.alloc(ctx, std::max<size_t>(need, 1)));
+    if (n_runs <= kMergeMaxRuns) {
+        // one ranking pass into merged order (reads the interleaved wire format directly)
+        RunOffs R{};
+        for (int r = 0; r <= n_runs; ++r) R.o[r] = off[r];
         KARMA_TRY(kb[0].alloc(ctx, n));
         KARMA_TRY(cb[0].alloc(ctx, n));
-        if (!kb[1].ptr) {
+        int64_t tiles = 0;
+        for (int r = 0; r < n_runs; ++r) {
+            R.t[r] = tiles;
+            tiles += ceil_div(off[r + 1] - off[r], kMergeTile);
+        }
+        R.t[n_runs] = tiles;
+        if (tiles)
+            KARMA_LAUNCH(ctx, "merge_rank", merge_rank_kernel, tiles, 256, 0, sk, sc,
+                         reinterpret_cast<const longlong2*>(kc), R, n_runs, kb[0].ptr, cb[0].ptr, st.ptr + 1);
+        sk = kb[0].ptr;
+        sc = cb[0].ptr;
+    } else {
+        if (kc && n) {  // interleaved device input: split once into the merge's first buffers
             KARMA_TRY(kb[1].alloc(ctx, n));
             KARMA_TRY(cb[1].alloc(ctx, n));
+            KARMA_LAUNCH(ctx, "merge_split", deinterleave_kc_kernel, std::min<int64_t>(grid1(n), 4096), 256, 0,
+                         reinterpret_cast<const longlong2*>(kc), n, kb[1].ptr, cb[1].ptr);
+            sk = kb[1].ptr;
+            sc = cb[1].ptr;
         }
-        int dst = 0;
-        for (std::vector<int64_t> o = off; o.size() > 2; dst ^= 1) {
-            std::vector<int64_t> next{0};
-            for (size_t j = 0; j + 1 < o.size(); j += 2) {
-                const int64_t a0 = o[j], a1 = o[j + 1];
-                const int64_t a2 = j + 2 < o.size() ? o[j + 2] : a1;
-                if (a1 > a0 && a2 > a1) {  // two non-empty runs (an empty merge would launch an empty grid)
-                    size_t tb = need;
-                    KARMA_HIP(rocprim::merge(tmp.ptr, tb, sk + a0, sk + a1, kb[dst].ptr + a0, sc + a0, sc + a1,
-                                             cb[dst].ptr + a0, (size_t)(a1 - a0), (size_t)(a2 - a1),
-                                             rocprim::less<uint64_t>(), ctx->stream));
-                } else if (a2 > a0) {  // one run (odd one out, or its partner is empty): carried over
-                    KARMA_HIP(hipMemcpyAsync(kb[dst].ptr + a0, sk + a0, (a2 - a0) * 8, hipMemcpyDeviceToDevice,
-                                             ctx->stream));
-                    KARMA_HIP(hipMemcpyAsync(cb[dst].ptr + a0, sc + a0, (a2 - a0) * 8, hipMemcpyDeviceToDevice,
-                                             ctx->stream));
+        DevArray<int64_t> doff;
+        KARMA_TRY(doff.alloc(ctx, n_runs + 1));
+        std::memcpy(hpin, off.data(), (n_runs + 1) * 8);
+        KARMA_HIP(hipMemcpyAsync(doff.ptr, hpin, (n_runs + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (n > 1)
+            KARMA_LAUNCH(ctx, "runs_check", runs_check_kernel, std::min<int64_t>(grid1(n), 4096), 256, 0, sk, n, doff.ptr,
+                         n_runs, st.ptr + 1);
+        // pairwise merge tree over the runs (rocprim merge path), ping-pong buffers
+        if (n_runs > 1 && n) {
+            size_t need = 0;
+            for (std::vector<int64_t> o = off; o.size() > 2;) {  // plan: the largest temporary
+                std::vector<int64_t> next{0};
+                for (size_t j = 0; j + 1 < o.size(); j += 2) {
+                    if (j + 2 < o.size() && o[j + 1] > o[j] && o[j + 2] > o[j + 1]) {
+                        size_t tb = 0;
+                        KARMA_HIP(rocprim::merge(nullptr, tb, sk, sk, (uint64_t*)nullptr, sc, sc, (int64_t*)nullptr,
+                                                 (size_t)(o[j + 1] - o[j]), (size_t)(o[j + 2] - o[j + 1]),
+                                                 rocprim::less<uint64_t>(), ctx->stream));
+                        need = std::max(need, tb);
+                    }
+                    next.push_back(o[std::min(j + 2, o.size() - 1)]);
                 }
-                next.push_back(o[std::min(j + 2, o.size() - 1)]);
+                o.swap(next);
             }
-            o.swap(next);
-            sk = kb[dst].ptr;
-            sc = cb[dst].ptr;
+            DevArray<uint8_t> tmp;
+            KARMA_TRY(tmp.alloc(ctx, std::max<size_t>(need, 1)));
+            KARMA_TRY(kb[0].alloc(ctx, n));
+            KARMA_TRY(cb[0].alloc(ctx, n));
+            if (!kb[1].ptr) {
+                KARMA_TRY(kb[1].alloc(ctx, n));
+                KARMA_TRY(cb[1].alloc(ctx, n));
+            }
+            int dst = 0;
+            for (std::vector<int64_t> o = off; o.size() > 2; dst ^= 1) {
+                std::vector<int64_t> next{0};
+                for (size_t j = 0; j + 1 < o.size(); j += 2) {
+                    const int64_t a0 = o[j], a1 = o[j + 1];
+                    const int64_t a2 = j + 2 < o.size() ? o[j + 2] : a1;
+                    if (a1 > a0 && a2 > a1) {  // two non-empty runs (an empty merge would launch an empty grid)
+                        size_t tb = need;
+                        KARMA_HIP(rocprim::merge(tmp.ptr, tb, sk + a0, sk + a1, kb[dst].ptr + a0, sc + a0, sc + a1,
+                                                 cb[dst].ptr + a0, (size_t)(a1 - a0), (size_t)(a2 - a1),
+                                                 rocprim::less<uint64_t>(), ctx->stream));
+                    } else if (a2 > a0) {  // one run (odd one out, or its partner is empty): carried over
+                        KARMA_HIP(hipMemcpyAsync(kb[dst].ptr + a0, sk + a0, (a2 - a0) * 8, hipMemcpyDeviceToDevice,
+                                                 ctx->stream));
+                        KARMA_HIP(hipMemcpyAsync(cb[dst].ptr + a0, sc + a0, (a2 - a0) * 8, hipMemcpyDeviceToDevice,
+                                                 ctx->stream));
+                    }
+                    next.push_back(o[std::min(j + 2, o.size() - 1)]);
+                }
+                o.swap(next);
+                sk = kb[dst].ptr;
+                sc = cb[dst].ptr;
+            }
         }
     }
     // equal keys (from different runs, or repeated in one) are now adjacent
