@@ -201,6 +201,31 @@ def kmer_profile(sequences, kmer_size, ctx=None):
     return prof, cols, tot
 
 
+def kmer_profile_device(sequences, kmer_size, ctx=None):
+    """kmer_profile with the profile left in HBM:
+    returns (DeviceProfile, columns list[str], row_totals int64[N]); nothing of
+    size N x M crosses PCIe."""
+    from .device_profile import profile_to_device
+
+    ctx = ctx or _lib.default_context()
+    kmode = kmode_of(kmer_size)
+    packed = getattr(sequences, "karma_packed", None)
+    blob, offs, key_len = packed if packed is not None else encode_sequences(sequences)
+    store = ContigStore(ctx, blob, offs, key_len)
+    try:
+        plan = KmerPlan(ctx, store, kmode)
+        try:
+            plan.finalize()
+            cols = decode_keys(plan.columns(), kmode)
+            dev = profile_to_device(ctx, plan, cols)
+            tot = plan.row_totals()
+        finally:
+            plan.close()
+    finally:
+        store.close()
+    return dev, cols, tot
+
+
 # ---------------------------------------------------------------------------
 # Graph
 # ---------------------------------------------------------------------------

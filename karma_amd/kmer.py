@@ -49,9 +49,19 @@ class KmerClustering:
         """kmer.py:199-264 on the GPU.  Same return value, side effects
         (self.kmers, self.sorted_kmer_set) and failure modes (ZeroDivisionError
         for a zero-length key, logger.error + exit(1) for an all-zero row)."""
+        return self.__profile(engine.kmer_profile)
+
+    def calc_kmer_profile_device(self):
+        """The same profile left in HBM for a GPU consumer (SURVEY.md §8(f) row 4,
+        the UMAP input of kmer.py:283-290): a device_profile.DeviceProfile
+        (DLPack / __cuda_array_interface__, float64 N x M row-major), with the
+        same side effects and failure modes as __calc_kmer_profile."""
+        return self.__profile(engine.kmer_profile_device)
+
+    def __profile(self, compute):
         logger.info("Extracting kmers from contigs.")
         try:
-            profile, columns, row_totals = engine.kmer_profile(self.sequences, self.kmer_size)
+            profile, columns, row_totals = compute(self.sequences, self.kmer_size)
         except engine._lib.KarmaError as e:
             if e.code == engine._lib.KARMA_ERR_ZERO_DIV:
                 raise ZeroDivisionError("division by zero") from e
