@@ -26,12 +26,12 @@ int ctx_begin(karma_ctx* ctx) {
 
 int ctx_alloc(karma_ctx* ctx, size_t bytes, void** out) {
     bytes = (bytes + 255) & ~size_t(255);
-    auto it = ctx->free_list.find(bytes);
+    auto it = ctx->free_list.find({ctx->stream, bytes});
     if (it != ctx->free_list.end()) {
         *out = it->second;
         ctx->free_list.erase(it);
         ctx->cached_bytes -= bytes;
-        ctx->live[*out] = bytes;
+        ctx->live[*out] = {bytes, ctx->stream};
         return KARMA_OK;
     }
     void* p = nullptr;
@@ -39,7 +39,7 @@ int ctx_alloc(karma_ctx* ctx, size_t bytes, void** out) {
     if (e != hipSuccess) {
         // drop the cache and retry once
         (void)hipGetLastError();
-        hipStreamSynchronize(ctx->stream);
+        hipDeviceSynchronize();  // cached blocks of every stream are idle
         for (auto& kv : ctx->free_list) hipFree(kv.second);
         ctx->free_list.clear();
         ctx->cached_bytes = 0;
@@ -49,7 +49,7 @@ int ctx_alloc(karma_ctx* ctx, size_t bytes, void** out) {
         set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
         return KARMA_ERR_OOM;
     }
-    ctx->live[p] = bytes;
+    ctx->live[p] = {bytes, ctx->stream};
     *out = p;
     return KARMA_OK;
 }
@@ -59,8 +59,8 @@ void ctx_free(karma_ctx* ctx, void* p) {
     auto it = ctx->live.find(p);
     if (it == ctx->live.end()) return;
     // stream-ordered reuse: later work on the same stream runs after earlier frees' readers
-    ctx->free_list.emplace(it->second, p);
-    ctx->cached_bytes += it->second;
+    ctx->free_list.emplace(std::make_pair(it->second.second, it->second.first), p);
+    ctx->cached_bytes += it->second.first;
     ctx->live.erase(it);
 }
 
@@ -306,6 +306,16 @@ int karma_stream_destroy(karma_ctx* ctx, void* s) {
     KARMA_CHECK(s != ctx->own_stream, KARMA_ERR_ARG, "the context's own stream is destroyed with the context");
     if (ctx->stream == s) ctx->stream = ctx->own_stream;
     KARMA_HIP(hipStreamSynchronize(static_cast<hipStream_t>(s)));
+    // its cached blocks are idle now: hand them to the context's own stream
+    // (a later stream may reuse this handle value)
+    for (auto it = ctx->free_list.begin(); it != ctx->free_list.end();) {
+        if (it->first.first == s) {
+            ctx->free_list.emplace(std::make_pair(ctx->own_stream, it->first.second), it->second);
+            it = ctx->free_list.erase(it);
+        } else {
+            ++it;
+        }
+    }
     KARMA_HIP(hipStreamDestroy(static_cast<hipStream_t>(s)));
     return KARMA_OK;
 }

@@ -209,9 +209,17 @@ classify2_kernel(ClassArgs P) {
     if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
     const int64_t c_hi = min(P.A, c_lo + kCChunk);
     uint32_t* out = P.codes + c_lo;
-    // transpose buffer: lane l's 8 records at byte 80l (16 bytes of padding per
-    // lane make both the 16-byte stores and the lane-sequential reads conflict-free)
-    __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][64 * 5];
+    // the chunk's region as a buffer resource built from wave-uniform values
+    const uint64_t out_u = (uint64_t)out;
+    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(out_u >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)out_u)),
+        0, kCChunk * 4, 0x00020000);
+    // transpose buffer: lane l's 8 records in row l (4 units of 16 bytes), the
+    // unit index XOR-ed with (l >> 2) & 3: conflict-free for the 16-byte stores
+    // (8-lane groups, banks mod 32) and for the row reads (16-lane groups,
+    // banks mod 64) alike
+    __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][64 * 4];
     u32x4* tb = tbuf[wave];
     // the chunk's codes per code bucket, added to its partition block's row at the end
     __shared__ uint32_t whist[kCW / 64][HIST ? kMaxBc : 1];
@@ -254,11 +262,14 @@ classify2_kernel(ClassArgs P) {
         uint32_t rid[8], ctg[8];
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
 #pragma unroll
-        for (int u = 0; u < kCPer; ++u) tb[5 * (16 * u + (lane >> 2)) + (lane & 3)] = buf[u];
+        for (int u = 0; u < kCPer; ++u) {
+            const int row = 16 * u + (lane >> 2);
+            tb[4 * row + ((lane & 3) ^ ((row >> 2) & 3))] = buf[u];
+        }
         wave_sync();
 #pragma unroll
         for (int u = 0; u < kCPer; ++u) {
-            const u32x4 q = tb[5 * lane + u];
+            const u32x4 q = tb[4 * lane + (u ^ ((lane >> 2) & 3))];
             rid[2 * u] = q.x;
             ctg[2 * u] = q.y;
             rid[2 * u + 1] = q.z;
@@ -282,75 +293,92 @@ classify2_kernel(ClassArgs P) {
         bad_order |= bo;
         bad_contig |= bc;
         // emission: codes from the front of the chunk's region, general read
-        // starts (chunk-relative) from the back, big reads to the big list
-        auto emit = [&](bool e, uint32_t code, uint32_t pos, bool big) {
-            const bool ec = e && !big && code != kEmpty;
-            const unsigned long long b = __ballot(ec);
-            if (ec) {
-                out[nc + rank_below(b)] = code;
-                if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
-            }
-            nc += __popcll(b);
-            const bool eg = e && !big && code == kEmpty;
-            const unsigned long long g = __ballot(eg);
-            if (g) {  // rare
-                if (eg) out[kCChunk - 1 - (ng + rank_below(g))] = pos;
-                ng += __popcll(g);
-            }
-            if (__ballot(e && big)) {
-                if (e && big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + pos;
-            }
-        };
-        // walk the lane (branch-free state updates): an own read ending at
-        // record i < 7 is emitted there
+        // starts (chunk-relative) from the back, big reads to the big list.
+        // The walk runs once for the codes; only when some lane met a general
+        // or a big read does it run again to emit those (rare on assembled
+        // transcriptomes), so the common pass carries no branches for them.
+        // Codes go out through a buffer store whose range check drops the lanes
+        // without one (offset past the chunk's region): no exec-mask branch.
         RState st, hd;
-        rs_reset(st, ctg[0]);
-        hd = st;
-        // head = records before the first read start (8: no start in the lane)
-        const uint32_t hlen = (sm & 1u) ? 0u : (sm ? (uint32_t)__builtin_ctz(sm) : 8u);
-        uint32_t spos = 0;
+        uint32_t spos = 0, hlen = 0;
         const uint32_t ubase = (uint32_t)(t0 - c_lo) + 8u * lane;
+        uint32_t rare = 0;
+        auto walk = [&](auto rare_pass) {
+            constexpr bool RARE = decltype(rare_pass)::value;
+            auto emit = [&](bool e, uint32_t code, uint32_t pos, bool big) {
+                if (!RARE) {
+                    const bool ec = e && !big && code != kEmpty;
+                    const unsigned long long b = __ballot(ec);
+                    const uint32_t boff = ec ? (nc + (uint32_t)rank_below(b)) * 4u : 0x80000000u;
+                    __builtin_amdgcn_raw_buffer_store_b32(code, out_rsrc, (int)boff, 0, 0);
+                    if (hist_on && ec) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
+                    nc += __popcll(b);
+                    rare |= (e && (big || code == kEmpty)) ? 1u : 0u;
+                } else {
+                    const bool eg = e && !big && code == kEmpty;
+                    const unsigned long long g = __ballot(eg);
+                    if (g) {
+                        if (eg) out[kCChunk - 1 - (ng + rank_below(g))] = pos;
+                        ng += __popcll(g);
+                    }
+                    if (__ballot(e && big)) {
+                        if (e && big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + pos;
+                    }
+                }
+            };
+            // walk the lane (branch-free state updates): an own read ending at
+            // record i < 7 is emitted there
+            rs_reset(st, ctg[0]);
+            hd = st;
+            // head = records before the first read start (8: no start in the lane)
+            hlen = (sm & 1u) ? 0u : (sm ? (uint32_t)__builtin_ctz(sm) : 8u);
+            spos = 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (i > 0) {
-                const bool si = (sm >> i) & 1u;
-                const bool cap = (uint32_t)i == hlen;  // first start: the head ends here
-                hd.fm3 = cap ? st.fm3 : hd.fm3;
-                hd.win = cap ? st.win : hd.win;
-                hd.mn = cap ? st.mn : hd.mn;
-                hd.mx = cap ? st.mx : hd.mx;
-                spos = si ? (uint32_t)i : spos;
-                const uint32_t c = ctg[i];
-                const uint32_t fm3 = si ? c - 3u : st.fm3;
-                const uint32_t bit = 1u << ((c - fm3) & 31u);
-                st.win = si ? bit : (st.win | bit);
-                st.fm3 = fm3;
-                st.mn = si ? c : min(st.mn, c);
-                st.mx = si ? c : max(st.mx, c);
+            for (int i = 0; i < 8; ++i) {
+                if (i > 0) {
+                    const bool si = (sm >> i) & 1u;
+                    const bool cap = (uint32_t)i == hlen;  // first start: the head ends here
+                    hd.fm3 = cap ? st.fm3 : hd.fm3;
+                    hd.win = cap ? st.win : hd.win;
+                    hd.mn = cap ? st.mn : hd.mn;
+                    hd.mx = cap ? st.mx : hd.mx;
+                    spos = si ? (uint32_t)i : spos;
+                    const uint32_t c = ctg[i];
+                    const uint32_t fm3 = si ? c - 3u : st.fm3;
+                    const uint32_t bit = 1u << ((c - fm3) & 31u);
+                    st.win = si ? bit : (st.win | bit);
+                    st.fm3 = fm3;
+                    st.mn = si ? c : min(st.mn, c);
+                    st.mx = si ? c : max(st.mx, c);
+                }
+                if (i < 7) {
+                    const bool e = ((sm >> (i + 1)) & 1u) && hlen <= (uint32_t)i && (int)spos < nval;
+                    emit(e, rs_code(st, P.N, P.compact), ubase + spos, false);
+                }
             }
-            if (i < 7) {
-                const bool e = ((sm >> (i + 1)) & 1u) && hlen <= (uint32_t)i && (int)spos < nval;
-                emit(e, rs_code(st, P.N, P.compact), ubase + spos, false);
-            }
-        }
-        if (hlen == 8u) hd = st;  // no read starts here: the whole lane is a head
-        // this lane's tail (an own read reaching record 7) -> the next lane
-        const bool t_ok = hlen < 8u && (int)spos < nval;
-        const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
-        RState in;
-        in.fm3 = dpp_shr1(ct.fm3, st.fm3);
-        in.win = dpp_shr1(ct.win, st.win);
-        in.mn = dpp_shr1(ct.mn, st.mn);
-        in.mx = dpp_shr1(ct.mx, st.mx);
-        const uint32_t in_pk = dpp_shr1(ct_ok ? (ct_len | ct_pos << 8) : kEmpty, t_ok ? (t_len | t_pos << 8) : kEmpty);
-        // the incoming tail, merged with this lane's head when the read continues
-        {
+            if (hlen == 8u) hd = st;  // no read starts here: the whole lane is a head
+            // the incoming tail (the previous lane's last read), merged with this
+            // lane's head when the read continues
+            const bool t_ok = hlen < 8u && (int)spos < nval;
+            const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
+            RState in;
+            in.fm3 = dpp_shr1(ct.fm3, st.fm3);
+            in.win = dpp_shr1(ct.win, st.win);
+            in.mn = dpp_shr1(ct.mn, st.mn);
+            in.mx = dpp_shr1(ct.mx, st.mx);
+            const uint32_t in_pk =
+                dpp_shr1(ct_ok ? (ct_len | ct_pos << 8) : kEmpty, t_ok ? (t_len | t_pos << 8) : kEmpty);
             const bool have = in_pk != kEmpty;
             const uint32_t in_len = in_pk & 255u, in_pos = in_pk >> 8;
             const bool cont = !(sm & 1u);
             const bool big = cont && in_len + hlen > (uint32_t)kMaxFast;
             emit(have, cont ? rs_code2(in, hd, P.N, P.compact) : rs_code(in, P.N, P.compact), in_pos, big);
-        }
+        };
+        walk(std::false_type{});
+        if (__ballot(rare != 0)) walk(std::true_type{});
+        // this lane's tail (an own read reaching record 7) -> the next lane
+        const bool t_ok = hlen < 8u && (int)spos < nval;
+        const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
         // carry lane 63 into the next step
         ct_ok = __builtin_amdgcn_readlane((int)t_ok, 63) != 0;
         ct.fm3 = (uint32_t)__builtin_amdgcn_readlane((int)st.fm3, 63);
@@ -948,8 +976,13 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
     const int64_t R = f_hi - f_lo;
     const int S = R > 0 ? (int)min<int64_t>(64, (2 * kCRT + R - 1) / R) : 1;
     bool stop = false;
+    // LDS slot of counter c = (m0_local << 3 | M): the low five bits XOR-ed with
+    // m0_local >> 2, so that codes of one wave instruction spread over all 32
+    // banks (unswizzled, the bank is (m0 & 3) << 3 | M, and M is mostly 0)
+    auto slot = [](uint32_t c) { return c ^ ((c >> 5) & 31u); };
     auto add = [&](uint32_t c) {
-        if (c != CodeStream::kPadV) __hip_atomic_fetch_add(&h[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (c != CodeStream::kPadV)
+            __hip_atomic_fetch_add(&h[slot(c)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     stream_runs(
         reinterpret_cast<const u32x4*>(cent), f_lo * S, f_hi * S, kCRT,
@@ -969,7 +1002,7 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
         &stop);
     __syncthreads();
     uint32_t* out = part_ch + (int64_t)blockIdx.x * hn;
-    for (int i = threadIdx.x; i < hn; i += kCRT) out[i] = h[i];
+    for (int i = threadIdx.x; i < hn; i += kCRT) out[i] = h[slot(i)];
 }
 
 // ---- pair reduce --------------------------------------------------------------------

@@ -52,8 +52,14 @@ struct karma_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     // exact-size caching allocator: repeated steps of identical shape never hipMalloc
-    std::multimap<size_t, void*> free_list;
-    std::map<void*, size_t> live;
+    // cached device blocks by (stream they were allocated on, bytes): a block
+    // is reused only by allocations on that same stream, whose later work
+    // stream order puts after every earlier reader there (a side stream's
+    // temporaries never reach the main stream's allocations while its kernels
+    // may still read them).  Work on another stream that reads a block is
+    // joined back before its owner frees it (the side-stream profile: ctx_join).
+    std::multimap<std::pair<hipStream_t, size_t>, void*> free_list;
+    std::map<void*, std::pair<size_t, hipStream_t>> live;  // bytes, allocating stream
     size_t cached_bytes = 0;
     // per-kernel event timing
     bool timing = false;

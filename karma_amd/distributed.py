@@ -57,6 +57,19 @@ class HipOps:
     def kmer_plan(self, store, kmode):
         return self.engine.KmerPlan(self.ctx, store, kmode)
 
+    def kmer_plan_side(self, store, kmode):
+        """The presence pass and the column table enqueued on the side stream
+        (no exchange between them on one rank), so that the graph's kernels on
+        the main stream start at once, beside them; finalize_wait() waits for
+        the column table alone."""
+        self.ctx.set_stream(self.side)
+        try:
+            plan = self.engine.KmerPlan(self.ctx, store, kmode)
+            plan.finalize_async()
+        finally:
+            self.ctx.set_stream(self.stream)
+        return plan
+
     def presence_words(self, plan):
         words = DevBuf(self.ctx, (plan.presence_words(),), np.uint32)
         plan.presence_get(words.ptr)
@@ -239,7 +252,20 @@ class ShardedBuild:
         local = None
         try:
             # ---- k-mer profile (kmer.py:199-233) ----
-            plan = ops.kmer_plan(store, self.kmode)
+            # one rank with a side stream: the graph's kernels are enqueued
+            # first, then the presence pass and the column table on the side
+            # stream, beside them (no exchange between presence and columns)
+            early = side and comm.world == 1 and hasattr(ops, "kmer_plan_side")
+            job = None
+            if early:
+                job = ops.graph_begin(records, n_records, self.n_glob)  # ---- read_graph.py:19-50 ----
+                try:
+                    plan = ops.kmer_plan_side(store, self.kmode)
+                except BaseException:
+                    ops.graph_end(job)
+                    raise
+            else:
+                plan = ops.kmer_plan(store, self.kmode)
             if comm.world > 1:
                 # column set = global union: OR of every rank's presence bitmap,
                 # union of every rank's exception keys (kmer.py:146-179)
@@ -249,8 +275,9 @@ class ShardedBuild:
                 # the column table, then the graph's kernels behind it on the
                 # main stream; M is read back without waiting for the graph,
                 # and the profile (side stream) starts after the graph's kernels
-                ops.finalize_async(plan)
-                job = ops.graph_begin(records, n_records, self.n_glob)  # ---- read_graph.py:19-50 ----
+                if not early:
+                    ops.finalize_async(plan)
+                    job = ops.graph_begin(records, n_records, self.n_glob)  # ---- read_graph.py:19-50 ----
                 try:
                     M = ops.finalize_wait(plan)
                     if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
