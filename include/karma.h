@@ -335,6 +335,16 @@ int karma_adj_from_lists(karma_ctx* ctx, int64_t n, const uint32_t* ids, const i
  * the view's node order (host).  Adjacency rebuilt as from_dict_of_dicts does.
  * Stream-ordered: no host synchronisation. */
 int karma_adj_view(karma_adj* src, const int64_t* order, int64_t k, karma_adj** out);
+/* The consumers of a small view in one launch and one host synchronisation:
+ * for nx.Graph(G.subgraph(nodes)) of G = src (order as karma_adj_view), deg[k]
+ * (karma_adj_degrees), w[k] (karma_adj_node_weights) and, when with_text, the
+ * edge_list text (karma_adj_edge_list; names / name_off on the device) into
+ * text[text_cap].  *done = 0 (nothing computed) when the view exceeds one
+ * block: k > 1024 nodes, > 4096 adjacency entries or text over text_cap (or
+ * about 1 MB); the caller then takes karma_adj_view and the calls above. */
+int karma_adj_view_summary(karma_adj* src, const int64_t* order, int64_t k, const uint8_t* names,
+                           const int64_t* name_off, int with_text, int64_t* deg, double* w, uint8_t* text,
+                           int64_t text_cap, int64_t* text_len, int* done);
 /* G.remove_nodes_from: keep[n] (host, 1 = stays), n_keep = ones in keep;
  * remaining orders unchanged.  No host synchronisation. */
 int karma_adj_keep(karma_adj* src, const uint8_t* keep, int64_t n_keep, karma_adj** out);

@@ -139,6 +139,8 @@ _SIGS = {
     "karma_adj_from_lists": [_c_p, _i64, _c_p, _c_p, _c_p, _c_p, _i32, _PP],
     "karma_adj_view": [_c_p, _c_p, _i64, _PP],
     "karma_adj_keep": [_c_p, _c_p, _i64, _PP],
+    "karma_adj_view_summary": [_c_p, _c_p, _i64, _c_p, _c_p, _i32, _c_p, _c_p, _c_p, _i64, _I64P,
+                               ctypes.POINTER(ctypes.c_int)],
     "karma_adj_node_stats": [_c_p, _c_p, _c_p],
     "karma_adj_info": [_c_p, _I64P, _I64P],
     "karma_adj_get": [_c_p, _c_p, _c_p, _c_p, _c_p],

@@ -64,6 +64,10 @@ class NameTable:
             self._dev = None
 
 
+SMALL_VIEW = 1024  # nodes of a view copy served by one launch (karma_adj_view_summary)
+_TEXT_BUF = np.empty(1 << 20, np.uint8)  # edge_list bytes of one-launch view summaries
+
+
 class DeviceAdj:
     """A karma_adj: graph layout in networkx iteration order on the device."""
 
@@ -108,6 +112,23 @@ class DeviceAdj:
             raise ValueError("view order: positions must be distinct and in range")
         call("karma_adj_view", self.h, ptr(order), len(order), ctypes.byref(h))
         return DeviceAdj(self.ctx, h, len(order))
+
+    def view_summary(self, order, names: "NameTable", with_text: bool):
+        """Degrees, node weights and (with_text) the edge_list bytes of
+        nx.Graph(G.subgraph(nodes at `order`)) in one launch; None when the view
+        is over the one-block limits (karma_adj_view_summary)."""
+        order = np.ascontiguousarray(order, np.int64)
+        k = len(order)
+        deg = np.empty(k, np.int64)
+        w = np.empty(k, np.float64)
+        done = ctypes.c_int(0)
+        tl = _lib._i64(0)
+        dn, do = names.device() if with_text else (None, None)
+        call("karma_adj_view_summary", self.h, ptr(order), k, dn, do, 1 if with_text else 0, ptr(deg), ptr(w),
+             ptr(_TEXT_BUF) if with_text else None, len(_TEXT_BUF), ctypes.byref(tl), ctypes.byref(done))
+        if not done.value:
+            return None
+        return deg, w, (_TEXT_BUF[:tl.value].tobytes() if with_text else None)
 
     def keep(self, mask):
         """G.remove_nodes_from(nodes at positions where mask == 0)."""

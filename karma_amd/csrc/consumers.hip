@@ -340,6 +340,243 @@ __global__ void cross_sum_kernel(const uint64_t* __restrict__ key, const uint32_
     out_over[o] = over;
 }
 
+// ---- small views in one launch ------------------------------------------------
+// karma.py's cluster loop (:255-282) copies a few dozen nodes per k-mer cluster;
+// there the separate view / stats / text launches and their host round trips
+// cost more than the reference's whole Python walk.  One block does the view,
+// degrees, node weights and edge_list text of nx.Graph(G.subgraph(order)) and
+// writes them straight into mapped pinned host memory: one launch, one sync.
+constexpr int kSumT = 1024;     // threads: one per view node
+constexpr int kSumHash = 2048;  // LDS hash slots (src position -> view index)
+constexpr int kSumEnt = 4096;   // view adjacency entries held in LDS
+constexpr int kSumNames = 16384;  // name bytes of the view's nodes in LDS
+constexpr int kSumText = 24576;   // edge_list bytes composed in LDS
+
+struct SumHeader {
+    int32_t status;  // 0 done, 1 exceeds the one-block limits, 2 bad order
+    int32_t pad;
+    int64_t text_len;
+};
+
+// exclusive block scan (kSumT threads); *total for everyone
+__device__ int64_t block_exscan(int64_t v, int64_t* wtot, int64_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    int64_t base = 0, all = 0;
+    for (int w = 0; w < kSumT / 64; ++w) {
+        const int64_t t = wtot[w];
+        base += w < wave ? t : 0;
+        all += t;
+    }
+    *total = all;
+    __syncthreads();
+    return base + x - v;
+}
+
+// The block's last act: every thread's results are out, then the status (the
+// host polls it in mapped memory instead of waiting for the stream).
+__device__ __forceinline__ void publish(SumHeader* hdr, int status) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(&hdr->status, status, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ void __launch_bounds__(kSumT) view_summary_kernel(
+    const int64_t* __restrict__ order, int k, int64_t n_src, const int64_t* __restrict__ off,
+    const uint32_t* __restrict__ nbr, const double* __restrict__ w, const uint32_t* __restrict__ ids,
+    const uint8_t* __restrict__ names, const int64_t* __restrict__ name_off, int with_text, int64_t text_cap,
+    SumHeader* hdr, int32_t* __restrict__ deg_out, double* __restrict__ w_out, uint32_t* __restrict__ text_out) {
+    __shared__ uint32_t hk[kSumHash];  // source position -> view index
+    __shared__ uint16_t hv[kSumHash];
+    __shared__ uint32_t ek[kSumEnt];   // copy-order key: x < i ? x : k + (rank in G.adj[u])
+    __shared__ double ew[kSumEnt];     // weight
+    __shared__ uint16_t ex[kSumEnt];   // neighbour's view index
+    __shared__ int32_t se0[kSumT];     // node: first entry, degree, first text line, name in sname
+    __shared__ int32_t sd[kSumT];
+    __shared__ int32_t sl[kSumT + 1];
+    __shared__ int32_t sn0[kSumT + 1];
+    __shared__ int64_t snb[kSumT];     // node's name in the device name table
+    __shared__ __attribute__((aligned(16))) uint8_t sname[kSumNames];
+    __shared__ __attribute__((aligned(16))) uint8_t stext[kSumText];
+    __shared__ int64_t wtot[kSumT / 64];
+    __shared__ int bad;
+    const int i = threadIdx.x;
+    for (int t = i; t < kSumHash; t += kSumT) hk[t] = 0xFFFFFFFFu;
+    if (i == 0) bad = 0;
+    __syncthreads();
+    auto lookup = [&](uint32_t key) -> int {
+        uint32_t h = (key * 2654435761u) >> 21;  // 11 bits
+        while (true) {
+            const uint32_t c = hk[h];
+            if (c == key) return hv[h];
+            if (c == 0xFFFFFFFFu) return -1;
+            h = (h + 1) & (kSumHash - 1);
+        }
+    };
+    uint32_t u = 0;
+    if (i < k) {
+        const int64_t o = order[i];
+        if (o < 0 || o >= n_src) {
+            bad = 2;
+        } else {
+            u = (uint32_t)o;
+            uint32_t h = (u * 2654435761u) >> 21;
+            while (true) {
+                const uint32_t c = atomicCAS(&hk[h], 0xFFFFFFFFu, u);
+                if (c == 0xFFFFFFFFu) {
+                    hv[h] = (uint16_t)i;
+                    break;
+                }
+                if (c == u) {
+                    bad = 2;  // a node twice
+                    break;
+                }
+                h = (h + 1) & (kSumHash - 1);
+            }
+        }
+    }
+    __syncthreads();
+    if (bad) {
+        publish(hdr, bad);
+        return;
+    }
+    const int64_t j0 = i < k ? off[u] : 0, j1 = i < k ? off[u + 1] : 0;
+    int64_t nb0 = 0, nl = 0;
+    if (with_text && i < k) {
+        const uint32_t a = ids[u];
+        nb0 = name_off[a];
+        nl = name_off[a + 1] - nb0;
+    }
+    int64_t d = 0;
+    for (int64_t j = j0; j < j1; ++j) d += lookup(nbr[j]) >= 0;
+    int64_t m, NB;
+    const int64_t e0 = block_exscan(d, wtot, &m);
+    const int64_t n0 = block_exscan(nl, wtot, &NB);
+    if (m > kSumEnt || NB > kSumNames) {
+        publish(hdr, 1);
+        return;
+    }
+    // this node's entries in copy order: neighbours before it by position, then
+    // the rest in G.adj[u] order (from_dict_of_dicts over the view; karma_adj_view)
+    {
+        uint32_t r = 0;
+        int64_t e = e0;
+        for (int64_t j = j0; j < j1; ++j) {
+            const int x = lookup(nbr[j]);
+            if (x < 0) continue;
+            const uint32_t key = x < i ? (uint32_t)x : (uint32_t)k + r;
+            const double wj = w[j];
+            int64_t p = e;  // insertion sort of the segment as it fills
+            while (p > e0 && ek[p - 1] > key) {
+                ek[p] = ek[p - 1];
+                ew[p] = ew[p - 1];
+                ex[p] = ex[p - 1];
+                --p;
+            }
+            ek[p] = key;
+            ew[p] = wj;
+            ex[p] = (uint16_t)x;
+            ++e;
+            ++r;
+        }
+    }
+    if (i < k) {
+        double s = 0.0;  // read_graph.py:183-187: 0 + w_1 + w_2 + ..., left to right
+        for (int64_t e = e0; e < e0 + d; ++e) s = __dadd_rn(s, ew[e]);
+        deg_out[i] = (int32_t)d;
+        w_out[i] = s;
+        se0[i] = (int32_t)e0;
+        sd[i] = (int32_t)d;
+        sn0[i] = (int32_t)n0;
+        snb[i] = nb0;
+    }
+    if (!with_text) {
+        if (i == 0) hdr->text_len = -1;
+        publish(hdr, 0);
+        return;
+    }
+    if (i == 0) sn0[k] = (int32_t)NB;
+    // G.edges(): each edge from its earlier end, i.e. the entries x >= i (keys
+    // >= k: the tail of the node's segment), in order; one text line each
+    int64_t nt = 0;
+    for (int64_t e = e0; e < e0 + d; ++e) nt += ek[e] >= (uint32_t)k;
+    int64_t NL;
+    const int64_t l0 = block_exscan(nt, wtot, &NL);  // (its barriers order the stores above)
+    if (i < k) sl[i] = (int32_t)l0;
+    if (i == 0) sl[k] = (int32_t)NL;
+    // the view's names into LDS: byte b of the concatenation, node by search
+    for (int64_t b = i; b < NB; b += kSumT) {
+        int lo = 0, hi = k;  // last node whose name starts at or before b
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (sn0[mid] <= b) lo = mid;
+            else hi = mid;
+        }
+        sname[b] = names[snb[lo] + (b - sn0[lo])];
+    }
+    __syncthreads();
+    // lines [q0, q1) of this thread, contiguous so one scan places them
+    const int64_t per = (NL + kSumT - 1) / kSumT;
+    const int64_t q0 = min(NL, per * i), q1 = min(NL, q0 + per);
+    auto line_at = [&](int64_t q, int* node, int* ent) {
+        int lo = 0, hi = k;  // last node whose lines start at or before q
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (sl[mid] <= q) lo = mid;
+            else hi = mid;
+        }
+        // skip nodes without lines that share the start
+        while (lo + 1 < k && sl[lo + 1] <= q) ++lo;
+        const int nl_node = sl[lo + 1] - sl[lo];
+        *node = lo;
+        *ent = se0[lo] + sd[lo] - nl_node + (int)(q - sl[lo]);
+    };
+    int64_t len = 0;
+    for (int64_t q = q0; q < q1; ++q) {
+        int nd, e;
+        line_at(q, &nd, &e);
+        const int x = ex[e];
+        len += (sn0[nd + 1] - sn0[nd]) + 1 + (sn0[x + 1] - sn0[x]) + 1 +
+               karma_repr::parts_len(karma_repr::parts(ew[e])) + 1;
+    }
+    int64_t T;
+    const int64_t t0 = block_exscan(len, wtot, &T);
+    if (T > min<int64_t>(text_cap, kSumText)) {
+        publish(hdr, 1);
+        return;
+    }
+    {
+        int64_t p = t0;
+        for (int64_t q = q0; q < q1; ++q) {
+            int nd, e;
+            line_at(q, &nd, &e);
+            const int x = ex[e];
+            for (int t = sn0[nd]; t < sn0[nd + 1]; ++t) stext[p++] = sname[t];
+            stext[p++] = ' ';
+            for (int t = sn0[x]; t < sn0[x + 1]; ++t) stext[p++] = sname[t];
+            stext[p++] = ' ';
+            const karma_repr::Parts pr = karma_repr::parts(ew[e]);
+            karma_repr::parts_write(pr, stext + p);
+            p += karma_repr::parts_len(pr);
+            stext[p++] = '\n';
+        }
+    }
+    __syncthreads();
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(stext);
+    for (int64_t t = i; t < (T + 3) / 4; t += kSumT) text_out[t] = src[t];
+    if (i == 0) hdr->text_len = T ? T - 1 : 0;  // "\n".join: no newline after the last line
+    publish(hdr, 0);
+}
+
 int scan_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
     size_t tb = 0;
     KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, ctx->stream));
@@ -503,6 +740,63 @@ int karma_adj_view(karma_adj* src, const int64_t* order, int64_t k, karma_adj** 
     KARMA_TRY(g->ids.alloc(ctx, k ? k : 1));
     if (k) KARMA_LAUNCH(ctx, "adj_ids", gather_ids_kernel, grid_of(k), 256, 0, dorder.ptr, k, src->ids.ptr, g->ids.ptr);
     *out = g.release();
+    return KARMA_OK;
+}
+
+int karma_adj_view_summary(karma_adj* src, const int64_t* order, int64_t k, const uint8_t* names,
+                           const int64_t* name_off, int with_text, int64_t* deg, double* w, uint8_t* text,
+                           int64_t text_cap, int64_t* text_len, int* done) {
+    KARMA_CHECK(src && done && (k == 0 || (order && deg && w)) && k >= 0 && (!with_text || (names && name_off && text_len)),
+                KARMA_ERR_ARG, "karma_adj_view_summary: bad arguments");
+    *done = 0;
+    if (k > kSumT) return KARMA_OK;  // more than one block: the caller takes the general path
+    karma_ctx* ctx = src->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    if (k == 0) {
+        if (with_text) *text_len = 0;
+        *done = 1;
+        return KARMA_OK;
+    }
+    auto al = [](int64_t x) { return (x + 15) & ~int64_t(15); };
+    const int64_t o_hdr = al(8 * k), o_deg = o_hdr + 16, o_w = al(o_deg + 4 * k), o_text = al(o_w + 8 * k);
+    constexpr int64_t kMapped = 1 << 20;
+    const int64_t cap = with_text ? std::max<int64_t>(0, std::min<int64_t>(text_cap, kMapped - o_text - 16)) : 0;
+    void *hbuf = nullptr, *dbuf = nullptr;
+    KARMA_TRY(ctx_mapped(ctx, kMapped, &hbuf, &dbuf));
+    uint8_t* hb = static_cast<uint8_t*>(hbuf);
+    uint8_t* db = static_cast<uint8_t*>(dbuf);
+    std::memcpy(hb, order, 8 * k);
+    auto* hdr = reinterpret_cast<SumHeader*>(hb + o_hdr);
+    hdr->status = -1;
+    KARMA_LAUNCH(ctx, "adj_view_summary", view_summary_kernel, 1, kSumT, 0, reinterpret_cast<const int64_t*>(db),
+                 (int)k, src->n, src->off.ptr, src->nbr.ptr, src->w.ptr, src->ids.ptr, names, name_off, with_text,
+                 cap, reinterpret_cast<SumHeader*>(db + o_hdr), reinterpret_cast<int32_t*>(db + o_deg),
+                 reinterpret_cast<double*>(db + o_w), reinterpret_cast<uint32_t*>(db + o_text));
+    // poll the status the kernel publishes (a stream synchronisation costs more
+    // than the kernel); the stream's own state ends the wait on any failure
+    int st = -1;
+    for (uint64_t spin = 1;; ++spin) {
+        st = __atomic_load_n(&hdr->status, __ATOMIC_ACQUIRE);
+        if (st != -1) break;
+        if ((spin & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(ctx->stream);
+            if (q == hipErrorNotReady) continue;
+            KARMA_HIP(q);
+            st = __atomic_load_n(&hdr->status, __ATOMIC_ACQUIRE);
+            break;
+        }
+    }
+    KARMA_CHECK(st != 2, KARMA_ERR_ARG, "view order: positions must be distinct and in range");
+    KARMA_CHECK(st == 0 || st == 1, KARMA_ERR_HIP, "view summary kernel did not finish (status %d)", st);
+    if (st == 1) return KARMA_OK;  // over the one-block limits
+    const int32_t* d32 = reinterpret_cast<const int32_t*>(hb + o_deg);
+    for (int64_t i = 0; i < k; ++i) deg[i] = d32[i];
+    std::memcpy(w, hb + o_w, 8 * k);
+    if (with_text) {
+        *text_len = hdr->text_len;
+        if (hdr->text_len && text) std::memcpy(text, hb + o_text, hdr->text_len);
+    }
+    *done = 1;
     return KARMA_OK;
 }
 

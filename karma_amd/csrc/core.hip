@@ -121,6 +121,21 @@ int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out) {
     return KARMA_OK;
 }
 
+int ctx_mapped(karma_ctx* ctx, size_t bytes, void** host, void** dev) {
+    if (ctx->mapped_bytes < bytes) {
+        if (ctx->mapped) KARMA_HIP(hipHostFree(ctx->mapped));
+        ctx->mapped = ctx->mapped_dev = nullptr;
+        ctx->mapped_bytes = 0;
+        const size_t want = std::max<size_t>(bytes, 256 * 1024);
+        KARMA_HIP(hipHostMalloc(&ctx->mapped, want, hipHostMallocMapped | hipHostMallocCoherent));
+        ctx->mapped_bytes = want;
+        KARMA_HIP(hipHostGetDevicePointer(&ctx->mapped_dev, ctx->mapped, 0));
+    }
+    *host = ctx->mapped;
+    *dev = ctx->mapped_dev;
+    return KARMA_OK;
+}
+
 }  // namespace karma
 
 using namespace karma;
@@ -185,6 +200,7 @@ int karma_ctx_destroy(karma_ctx* ctx) {
     if (ctx->side_ev) hipEventDestroy(ctx->side_ev);
     if (ctx->mark_ev) hipEventDestroy(ctx->mark_ev);
     if (ctx->fin_pinned) hipHostFree(ctx->fin_pinned);
+    if (ctx->mapped) hipHostFree(ctx->mapped);
     delete ctx;
     return KARMA_OK;
 }

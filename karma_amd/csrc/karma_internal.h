@@ -80,6 +80,11 @@ struct karma_ctx {
     hipEvent_t mark_ev = nullptr;  // recorded by an open graph job after its classify kernel
     bool mark_set = false;
     int64_t* fin_pinned = nullptr;  // M of an in-flight karma_kmer_plan_finalize_async
+    // mapped, coherent pinned host memory that kernels read and write directly
+    // (one-launch consumers of small views: no copy launches)
+    void* mapped = nullptr;
+    void* mapped_dev = nullptr;
+    size_t mapped_bytes = 0;
 };
 
 namespace karma {
@@ -92,6 +97,8 @@ int ctx_begin(karma_ctx* ctx);  // hipSetDevice
 int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int64_t work);
 // Pinned host scratch of >= bytes (valid until the next call on this ctx).
 int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out);
+// Mapped coherent pinned scratch of >= bytes: host and device addresses.
+int ctx_mapped(karma_ctx* ctx, size_t bytes, void** host, void** dev);
 // Pinned scratch owned by the open split graph call (valid until its _end).
 int ctx_job_pinned(karma_ctx* ctx, size_t bytes, void** out);
 // Wrap a launch with HIP events when timing is on.

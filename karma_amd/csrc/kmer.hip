@@ -73,52 +73,62 @@ constexpr int kBlock = 256;
 constexpr int kPBlock = 512;  // profile: 8 waves share one LDS column table
 constexpr int kPadWords = 80;    // zero words after the store (stages may read past the last contig)
 
-__device__ __forceinline__ int base_code(uint8_t b) {
-    // A C G T -> 0 1 2 3 ; anything else -> -1 (exception)
-    return b == 'A' ? 0 : b == 'C' ? 1 : b == 'G' ? 2 : b == 'T' ? 3 : -1;
+// ---------------------------------------------------------------- pack -------
+// One wave per contig (grid-stride over contigs), lane l packs word w = l + 64t:
+// bases 16w .. 16w + 15 come from five aligned dword loads (a dword that starts
+// inside the contig cannot cross a page, so nothing past the buffer is touched)
+// and alignbyte.  Four bases at a time (SWAR): code = ((b >> 1) ^ (b >> 2)) & 3
+// maps A C G T to 0 1 2 3; a byte is an exception when "ACGT"[code] (v_perm)
+// differs from it, and then packs as 0 with its mask bit set.
+__device__ __forceinline__ uint32_t pack4(uint32_t x, uint32_t nvalid, uint32_t* m4, uint32_t* nexc) {
+    // nvalid (0..4): bytes of x inside the contig; the others pack as 0, no mask
+    const uint32_t keep = nvalid >= 4 ? 0xFFFFFFFFu : (1u << (8 * nvalid)) - 1u;
+    uint32_t t = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+    const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, t);  // 'A' 'C' 'G' 'T' by code
+    const uint32_t d = expect ^ x;
+    const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u & keep;  // exception bytes
+    t &= ~((nz >> 7) * 3u) & keep;
+    *nexc += (uint32_t)__builtin_popcount(nz);
+    *m4 = (nz >> 4 & 8u) | (nz >> 13 & 4u) | (nz >> 22 & 2u) | (nz >> 31);
+    return (t << 6 & 0xC0u) | (t >> 4 & 0x30u) | (t >> 14 & 0x0Cu) | (t >> 24 & 0x03u);
 }
 
-// ---------------------------------------------------------------- pack -------
 __global__ void __launch_bounds__(kBlock) pack_kernel(const uint8_t* __restrict__ raw, const int64_t* __restrict__ off,
                                                       const int64_t* __restrict__ woff, int64_t n,
                                                       uint32_t* __restrict__ packed, uint16_t* __restrict__ mask,
                                                       uint8_t* __restrict__ has_exc,
                                                       unsigned long long* __restrict__ exc_count) {
-    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
+    for (int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); c < n; c += waves) {
         const int64_t s = off[c], L = off[c + 1] - s, w0 = woff[c], nw = woff[c + 1] - w0;
-        unsigned local_exc = 0;
-        for (int64_t w = threadIdx.x; w < nw; w += blockDim.x) {
-            uint32_t word = 0;
-            uint32_t m = 0;
-            const int64_t j0 = w * 16;
+        uint32_t nexc = 0;
+        for (int64_t w = lane; w < nw; w += 64) {
+            const uint64_t p = (uint64_t)(raw + s + 16 * w);  // absolute byte address
+            const uint64_t end = (uint64_t)(raw + s + L);     // first byte past the contig
+            const uint64_t abyte = p & ~uint64_t(3);
+            const uint32_t* a = reinterpret_cast<const uint32_t*>(abyte);
+            const uint32_t sh = (uint32_t)(p & 3);
+            uint32_t d[5];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                int code = 0;
-                if (j0 + j < L) {
-                    int cc = base_code(raw[s + j0 + j]);
-                    if (cc < 0) {
-                        m |= 1u << (15 - j);
-                        ++local_exc;
-                    } else {
-                        code = cc;
-                    }
-                }
-                word |= (uint32_t)code << (30 - 2 * j);
+            for (int i = 0; i < 5; ++i) d[i] = abyte + 4 * i < end ? a[i] : 0u;
+            const int64_t rem = (int64_t)(end - p);  // bases of this word inside the contig (>= 1)
+            uint32_t word = 0, m = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t x = __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh);
+                const int64_t nv = rem - 4 * q;
+                uint32_t m4;
+                const uint32_t v = pack4(x, nv <= 0 ? 0u : nv >= 4 ? 4u : (uint32_t)nv, &m4, &nexc);
+                word |= v << (24 - 8 * q);
+                m |= m4 << (12 - 4 * q);
             }
             packed[w0 + w] = word;
             mask[w0 + w] = (uint16_t)m;
         }
-        // block-wide OR of "has exception"
-        __shared__ unsigned blk_exc;
-        if (threadIdx.x == 0) blk_exc = 0;
-        __syncthreads();
-        if (local_exc) atomicAdd(&blk_exc, local_exc);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            has_exc[c] = blk_exc ? 1 : 0;
-            if (blk_exc) atomicAdd(exc_count, (unsigned long long)blk_exc);
-        }
-        __syncthreads();
+        if (nexc) atomicAdd(exc_count, (unsigned long long)nexc);
+        const bool any = __ballot(nexc != 0) != 0;
+        if (lane == 0) has_exc[c] = any ? 1 : 0;
     }
 }
 
@@ -856,7 +866,8 @@ int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offs
     }
     KARMA_HIP(hipMemsetAsync(stat.ptr, 0, 3 * sizeof(unsigned long long), ctx->stream));
     if (n) {
-        KARMA_LAUNCH(ctx, "pack_2bit", pack_kernel, grid_for(n, 8192), kBlock, 0, c->raw, c->off, c->woff.ptr, n,
+        KARMA_LAUNCH(ctx, "pack_2bit", pack_kernel, grid_for(ceil_div(n, kBlock / 64), 8192), kBlock, 0, c->raw,
+                     c->off, c->woff.ptr, n,
                      c->packed.ptr, c->mask.ptr, c->has_exc.ptr, stat.ptr);
         KARMA_LAUNCH(ctx, "zero_key", zero_key_kernel, ceil_div(n, 256), 256, 0, c->off, c->keylen, n, stat.ptr + 1,
                      stat.ptr + 2);

@@ -166,76 +166,116 @@ __host__ __device__ inline Decimal shortest(uint64_t ieee_m, uint32_t ieee_e) {
     return Decimal{out, e10 + removed};
 }
 
+// repr(x) as (sign, digit string, decimal point) and the layout rules, with no
+// local arrays: device code keeps everything in registers (a char buffer would
+// live in scratch memory, one slow round trip per byte).
+struct Parts {
+    int kind;         // 0 nan, 1 inf, 2 finite
+    bool neg;
+    uint64_t digits;  // shortest digits as an integer ("0" for zero)
+    int nd;           // their number
+    int32_t decpt;    // decimal point position relative to the digits
+};
+
+__host__ __device__ inline Parts parts(double x) {
+    Parts p;
+    const uint64_t bits = __builtin_bit_cast(uint64_t, x);
+    p.neg = (bits >> 63) != 0;
+    const uint64_t ieee_m = bits & ((1ull << 52) - 1);
+    const uint32_t ieee_e = (uint32_t)((bits >> 52) & 0x7FF);
+    p.digits = 0;
+    p.nd = 1;
+    p.decpt = 1;
+    if (ieee_e == 0x7FF) {
+        p.kind = ieee_m ? 0 : 1;
+        return p;
+    }
+    p.kind = 2;
+    if (ieee_e == 0 && ieee_m == 0) return p;  // "0.0"
+    const Decimal d = shortest(ieee_m, ieee_e);
+    p.digits = d.digits;
+    uint64_t t = 10;
+    while (p.nd < 19 && d.digits >= t) {  // at most 17 digits
+        ++p.nd;
+        t *= 10;
+    }
+    p.decpt = d.exp10 + p.nd;
+    return p;
+}
+
+__host__ __device__ inline int parts_len(const Parts& p) {
+    if (p.kind == 0) return 3;                   // nan (repr drops the sign)
+    if (p.kind == 1) return 3 + (p.neg ? 1 : 0);  // inf, -inf
+    int n = p.neg ? 1 : 0;
+    if (p.decpt <= -4 || p.decpt > 16) {  // d.ddde-05
+        int ex = p.decpt - 1;
+        ex = ex < 0 ? -ex : ex;
+        return n + 1 + (p.nd > 1 ? p.nd : 0) + 2 + (ex >= 100 ? 3 : 2);
+    }
+    if (p.decpt <= 0) return n + 2 - p.decpt + p.nd;  // 0.000ddd
+    if (p.decpt < p.nd) return n + p.nd + 1;          // dd.ddd
+    return n + p.decpt + 2;                           // ddd00.0
+}
+
+// writes parts_len(p) bytes at dst (any address space)
+template <typename Out>
+__host__ __device__ inline void parts_write(const Parts& p, Out* dst) {
+    if (p.kind == 0) {
+        dst[0] = 'n', dst[1] = 'a', dst[2] = 'n';
+        return;
+    }
+    int o = 0;
+    if (p.neg) dst[o++] = '-';
+    if (p.kind == 1) {
+        dst[o] = 'i', dst[o + 1] = 'n', dst[o + 2] = 'f';
+        return;
+    }
+    const int nd = p.nd, dp = p.decpt;
+    const bool expo = dp <= -4 || dp > 16;
+    // digit t (0 = most significant) goes to o + pos(t); written last to first
+    uint64_t v = p.digits;
+    for (int t = nd - 1; t >= 0; --t) {
+        const uint64_t q = v / 10;
+        const char ch = (char)('0' + (uint32_t)(v - 10 * q));
+        v = q;
+        int pos;
+        if (expo) pos = t == 0 ? 0 : t + 1;
+        else if (dp <= 0) pos = 2 - dp + t;
+        else pos = t < dp ? t : t + 1;
+        dst[o + pos] = ch;
+    }
+    if (expo) {
+        int n = o + 1;
+        if (nd > 1) {
+            dst[o + 1] = '.';
+            n = o + nd + 1;
+        }
+        int ex = dp - 1;
+        dst[n++] = 'e';
+        dst[n++] = ex < 0 ? '-' : '+';
+        if (ex < 0) ex = -ex;
+        if (ex >= 100) dst[n++] = (char)('0' + ex / 100);
+        dst[n++] = (char)('0' + (ex / 10) % 10);
+        dst[n] = (char)('0' + ex % 10);
+    } else if (dp <= 0) {
+        dst[o] = '0';
+        dst[o + 1] = '.';
+        for (int t = 0; t < -dp; ++t) dst[o + 2 + t] = '0';
+    } else if (dp < nd) {
+        dst[o + dp] = '.';
+    } else {
+        for (int t = nd; t < dp; ++t) dst[o + t] = '0';
+        dst[o + dp] = '.';
+        dst[o + dp + 1] = '0';
+    }
+}
+
 // Writes repr(x) (no terminator) to dst, returns its length (<= kMaxRepr).
 // dst == nullptr: length only.
 __host__ __device__ inline int repr_f64(double x, char* dst) {
-    char buf[kMaxRepr];
-    int n = 0;
-    const uint64_t bits = __builtin_bit_cast(uint64_t, x);
-    const bool neg = (bits >> 63) != 0;
-    const uint64_t ieee_m = bits & ((1ull << 52) - 1);
-    const uint32_t ieee_e = (uint32_t)((bits >> 52) & 0x7FF);
-    if (ieee_e == 0x7FF) {  // inf / nan
-        if (ieee_m) {
-            buf[n++] = 'n', buf[n++] = 'a', buf[n++] = 'n';
-        } else {
-            if (neg) buf[n++] = '-';
-            buf[n++] = 'i', buf[n++] = 'n', buf[n++] = 'f';
-        }
-    } else {
-        if (neg) buf[n++] = '-';
-        char dig[20];
-        int nd;
-        int32_t decpt;
-        if (ieee_e == 0 && ieee_m == 0) {
-            dig[0] = '0';
-            nd = 1;
-            decpt = 1;
-        } else {
-            const Decimal d = shortest(ieee_m, ieee_e);
-            char rev[20];
-            int r = 0;
-            uint64_t v = d.digits;
-            do {
-                rev[r++] = (char)('0' + v % 10);
-                v /= 10;
-            } while (v);
-            for (int t = 0; t < r; ++t) dig[t] = rev[r - 1 - t];
-            nd = r;
-            decpt = d.exp10 + nd;
-        }
-        if (decpt <= -4 || decpt > 16) {  // exponent form
-            buf[n++] = dig[0];
-            if (nd > 1) {
-                buf[n++] = '.';
-                for (int t = 1; t < nd; ++t) buf[n++] = dig[t];
-            }
-            int ex = decpt - 1;
-            buf[n++] = 'e';
-            buf[n++] = ex < 0 ? '-' : '+';
-            if (ex < 0) ex = -ex;
-            if (ex >= 100) buf[n++] = (char)('0' + ex / 100);
-            buf[n++] = (char)('0' + (ex / 10) % 10);
-            buf[n++] = (char)('0' + ex % 10);
-        } else if (decpt <= 0) {  // 0.000ddd
-            buf[n++] = '0';
-            buf[n++] = '.';
-            for (int t = 0; t < -decpt; ++t) buf[n++] = '0';
-            for (int t = 0; t < nd; ++t) buf[n++] = dig[t];
-        } else if (decpt < nd) {  // dd.ddd
-            for (int t = 0; t < decpt; ++t) buf[n++] = dig[t];
-            buf[n++] = '.';
-            for (int t = decpt; t < nd; ++t) buf[n++] = dig[t];
-        } else {  // ddd00.0
-            for (int t = 0; t < nd; ++t) buf[n++] = dig[t];
-            for (int t = nd; t < decpt; ++t) buf[n++] = '0';
-            buf[n++] = '.';
-            buf[n++] = '0';
-        }
-    }
-    if (dst)
-        for (int t = 0; t < n; ++t) dst[t] = buf[t];
-    return n;
+    const Parts p = parts(x);
+    if (dst) parts_write(p, dst);
+    return parts_len(p);
 }
 
 }  // namespace karma_repr

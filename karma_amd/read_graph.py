@@ -92,6 +92,8 @@ def _invalidating(name):
     def method(self, *args, **kw):
         self._mirror = None
         self._mirror_spec = None
+        self._view_root = None
+        self._summary = None
         return base(self, *args, **kw)
 
     method.__name__ = name
@@ -121,6 +123,8 @@ class ReadGraph(nx.Graph):
         self._mirror = None        # consumers.Mirror of this graph's layout
         self._mirror_spec = None   # or how to build it on first use
         self._mirror_dirty = False  # nodes removed since the mirror was taken
+        self._view_root = None      # mirror this graph is a (node-removed) view copy of
+        self._summary = None        # one-launch consumer results of a small view copy
         src = incoming_graph_data
         # nx.Graph(G.subgraph(nodes)) / nx.Graph(G) of a mirrored ReadGraph: the
         # copy's layout is derived from G's on the device
@@ -131,7 +135,9 @@ class ReadGraph(nx.Graph):
                 if getattr(src, "_EDGE_OK", None) is not nx.filters.no_filter:
                     base = None
             if isinstance(base, ReadGraph) and (base._mirror is not None or base._mirror_spec is not None):
-                self._mirror_spec = ("view", base._device_mirror(), list(self))
+                root = base._device_mirror()
+                self._mirror_spec = ("view", root, list(self))
+                self._view_root = root
 
     for _name in ("add_node", "add_nodes_from", "add_edge", "add_edges_from", "add_weighted_edges_from",
                   "remove_edge", "remove_edges_from", "update", "clear", "clear_edges"):
@@ -269,14 +275,52 @@ class ReadGraph(nx.Graph):
             self.add_edge(orig[o].name, contigs[j].name, weight=wt)
 
     # ---------------------------------------------------------- queries ----
+    def _small_view(self):
+        """(nodes, degrees, node weights, edge_list bytes or None) of a small view
+        copy (<= 1024 nodes) from one device launch (karma_adj_view_summary), or
+        None: not a view copy, too large, or mutated other than by removals.
+        A view copy with nodes removed is the view of the remaining nodes in the
+        same order (removal keeps both adjacency orders), so the summary is
+        recomputed from the root mirror; removing only nodes without edges leaves
+        every other result as it was, and the cached one is filtered instead."""
+        root = self._view_root
+        n = len(self)
+        if root is None or n > consumers.SMALL_VIEW:
+            return None
+        c = self._summary
+        if c is not None:
+            if c[0] == n:  # removals only: an unchanged count is an unchanged node set
+                return c[1:]
+            alive = self._node
+            mask = np.fromiter((x in alive for x in c[1]), bool, len(c[1]))
+            if not c[2][~mask].any():
+                c = (n, [x for x, k in zip(c[1], mask) if k], c[2][mask], c[3][mask], c[4])
+                self._summary = c
+                return c[1:]
+        nodes = list(self)
+        pos = root.pos()
+        order = np.fromiter((pos[x] for x in nodes), np.int64, n)
+        # the text comes in the same launch: karma.py asks for it next (:318)
+        r = root.adj.view_summary(order, root.names, True)
+        if r is None:
+            return None
+        self._summary = (n, nodes) + r
+        return self._summary[1:]
+
     def get_unconnected_nodes(self) -> list:
         """Nodes without any neighbour, in node order (read_graph.py:150-160); degrees on the device."""
+        s = self._small_view()
+        if s is not None:
+            return [s[0][i] for i in np.flatnonzero(s[1] == 0).tolist()]
         m = self._device_mirror()
         deg = m.adj.degrees()
         return [m.nodes[i] for i in np.flatnonzero(deg == 0).tolist()]
 
     def get_connected_nodes(self) -> list:
         """Nodes with at least one neighbour (read_graph.py:162-172); degrees on the device."""
+        s = self._small_view()
+        if s is not None:
+            return [s[0][i] for i in np.flatnonzero(s[1] != 0).tolist()]
         m = self._device_mirror()
         deg = m.adj.degrees()
         return [m.nodes[i] for i in np.flatnonzero(deg != 0).tolist()]
@@ -284,12 +328,17 @@ class ReadGraph(nx.Graph):
     def __calculate_node_weights(self) -> dict:
         """Sum of incident edge weights in adjacency order (read_graph.py:174-190):
         0 + w_1 + w_2 + ... in f64 on the device; a node without edges keeps the int 0."""
-        m = self._device_mirror()
-        deg, w = m.adj.node_stats()
+        s = self._small_view()
+        if s is not None:
+            nodes, deg, w = s[0], s[1], s[2]
+        else:
+            m = self._device_mirror()
+            nodes = m.nodes
+            deg, w = m.adj.node_stats()
         w = w.tolist()
         for i in np.flatnonzero(deg == 0).tolist():
             w[i] = 0
-        weights = dict(zip(m.nodes, w))
+        weights = dict(zip(nodes, w))
         if logger.isEnabledFor(logging.DEBUG):
             logger.debug(f"Node weights: {weights}")
         return weights
@@ -350,6 +399,9 @@ class ReadGraph(nx.Graph):
     def edge_list(self) -> str:
         """MCL stdin text "A B w" per edge, UTF-8 (read_graph.py:350-357): names and
         repr(weight) written on the device, edges in G.edges() order."""
+        s = self._small_view()
+        if s is not None:
+            return s[3]
         m = self._device_mirror()
         return m.adj.edge_list(m.names)
 

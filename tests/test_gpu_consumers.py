@@ -238,3 +238,36 @@ def test_consumers_non_float_weight_raises():
     h2.add_edge("a", "b")
     with pytest.raises(KeyError):
         h2.edge_list()
+
+
+def test_small_view_one_launch_path(tmp_path):
+    """karma.py:255-282's cluster loop on gene-sized clusters goes through the
+    one-launch view summary (karma_adj_view_summary); views over its limits
+    (> 1024 nodes, > 4096 adjacency entries) take the general path.  Both are
+    compared with the reference's expressions."""
+    g = eq_graph(tmp_path, 35, 3000, 200_000, True)
+    nodes = list(g.nodes())
+    for i in range(0, 1200, 40):
+        cl = nodes[i:i + 40]
+        sg = ReadGraph(g.subgraph(cl))
+        un = sg.get_unconnected_nodes()
+        assert sg._summary is not None, "small view did not take the one-launch path"
+        assert un == ref_unconnected(sg)
+        sg.remove_nodes_from(un)
+        check_against_reference(sg, chunks(sg.nodes(), 5))
+        # removing nodes that have edges: recomputed as the view of what is left
+        if len(sg) > 3:
+            sg.remove_nodes_from(list(sg.nodes())[1:3])
+            check_against_reference(sg, chunks(sg.nodes(), 4))
+    big = ReadGraph(g.subgraph(nodes[:1500]))
+    check_against_reference(big)
+    assert big._summary is None
+    # a clique of 100 contigs: 9,900 adjacency entries, over the LDS budget
+    names = [f"q{i}" for i in range(100)]
+    clique = ReadGraph.from_contigs(make_contigs(names, [["shared", f"own{i}"] for i in range(100)]))
+    sq = ReadGraph(clique.subgraph(names[::-1]))
+    check_against_reference(sq, chunks(sq.nodes(), 10))
+    assert sq._summary is None
+    sq.remove_nodes_from(names[:60])  # 40 nodes left: 1,560 entries, one launch again
+    check_against_reference(sq, chunks(sq.nodes(), 10))
+    assert sq._summary is not None

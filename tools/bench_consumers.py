@@ -136,9 +136,18 @@ def main():
         t_ref += time.perf_counter() - t
         assert un == un2 and txt == txt2 and reps == reps2
         nbytes += len(txt)
+    # one karma_adj_view_summary call (one launch + the status poll), repeated
+    root = g._device_mirror()
+    pos = root.pos()
+    order = np.array([pos[x] for x in clusters[0]], np.int64)
+    root.adj.view_summary(order, root.names, True)
+    t = time.perf_counter()
+    for _ in range(200):
+        root.adj.view_summary(order, root.names, True)
+    t_call = (time.perf_counter() - t) / 200
     res["clusters"] = {"count": len(clusters), "size": args.cluster, "subgraph_copy_s": round(t_copy, 3),
                        "gpu_s": round(t_gpu, 3), "ref_s": round(t_ref, 3), "speedup": round(t_ref / t_gpu, 2),
-                       "edge_list_bytes": nbytes}
+                       "edge_list_bytes": nbytes, "summary_call_us": round(t_call * 1e6, 1)}
 
     # ---- karma.py:301-345: cluster + every unlabeled contig, MCL text, trims, reps ----
     rng = np.random.default_rng(5)
