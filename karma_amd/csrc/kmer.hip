@@ -74,6 +74,8 @@ constexpr int kPBlock = 512;  // profile: 8 waves share one LDS column table
 constexpr int kPadWords = 80;    // zero words after the store (stages may read past the last contig)
 
 // ---------------------------------------------------------------- pack -------
+typedef unsigned int u32x4a __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-byte load
+
 // One wave per contig (grid-stride over contigs), lane l packs word w = l + 64t:
 // bases 16w .. 16w + 15 come from five aligned dword loads (a dword that starts
 // inside the contig cannot cross a page, so nothing past the buffer is touched)
@@ -100,18 +102,31 @@ __global__ void __launch_bounds__(kBlock) pack_kernel(const uint8_t* __restrict_
                                                       unsigned long long* __restrict__ exc_count) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
-    for (int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); c < n; c += waves) {
-        const int64_t s = off[c], L = off[c + 1] - s, w0 = woff[c], nw = woff[c + 1] - w0;
+    int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    // the next contig's offsets are loaded while this one's bytes are in flight
+    int64_t s = 0, e = 0, w0 = 0, w1 = 0;
+    if (c < n) s = off[c], e = off[c + 1], w0 = woff[c], w1 = woff[c + 1];
+    while (c < n) {
+        const int64_t cn = c + waves;
+        int64_t sn = 0, en = 0, w0n = 0, w1n = 0;
+        if (cn < n) sn = off[cn], en = off[cn + 1], w0n = woff[cn], w1n = woff[cn + 1];
+        const int64_t nw = w1 - w0;
+        const uint64_t end = (uint64_t)(raw + e);  // first byte past the contig
         uint32_t nexc = 0;
         for (int64_t w = lane; w < nw; w += 64) {
             const uint64_t p = (uint64_t)(raw + s + 16 * w);  // absolute byte address
-            const uint64_t end = (uint64_t)(raw + s + L);     // first byte past the contig
             const uint64_t abyte = p & ~uint64_t(3);
             const uint32_t* a = reinterpret_cast<const uint32_t*>(abyte);
             const uint32_t sh = (uint32_t)(p & 3);
             uint32_t d[5];
+            if (abyte + 20 <= end) {  // whole window inside the contig
+                const u32x4a v = *reinterpret_cast<const u32x4a*>(a);
+                d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
+                d[4] = a[4];
+            } else {  // the contig's last word: dwords that start inside it only
 #pragma unroll
-            for (int i = 0; i < 5; ++i) d[i] = abyte + 4 * i < end ? a[i] : 0u;
+                for (int t = 0; t < 5; ++t) d[t] = abyte + 4 * t < end ? a[t] : 0u;
+            }
             const int64_t rem = (int64_t)(end - p);  // bases of this word inside the contig (>= 1)
             uint32_t word = 0, m = 0;
 #pragma unroll
@@ -129,6 +144,7 @@ __global__ void __launch_bounds__(kBlock) pack_kernel(const uint8_t* __restrict_
         if (nexc) atomicAdd(exc_count, (unsigned long long)nexc);
         const bool any = __ballot(nexc != 0) != 0;
         if (lane == 0) has_exc[c] = any ? 1 : 0;
+        c = cn, s = sn, e = en, w0 = w0n, w1 = w1n;
     }
 }
 
