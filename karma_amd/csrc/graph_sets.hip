@@ -163,33 +163,60 @@ __device__ __forceinline__ int rank_below(unsigned long long m) {
 //   * a read longer than 8 records (a tail plus a head of > 8 records, or a
 //     lane without any read start) goes to the big-read list from the lane
 //     that merges its tail.
-// A read's contigs are tracked as min, max and a bit window relative to its
-// first contig - 3; a compact read (max - min < 4) becomes (m0 | M << 24).
+// A read's contigs are tracked as a bit window relative to its first contig
+// minus 3: bit (c - fm3), clamped to bit 31 for a contig outside [fm3, fm3 + 30]
+// (the read then spans more than 4 contigs).  At the read's end m0 = fm3 +
+// ctz(win) and rel = win >> ctz(win): the read is compact when rel < 16 (its
+// contigs lie in [m0, m0 + 3]) and m0 + 3 < N (reads on the last three
+// contigs, and contigs out of range, take the general path, which checks the
+// range); it becomes (m0 | M << 24), M = rel >> 1.
 struct RState {
-    uint32_t fm3, win, mn, mx;  // first contig - 3, bits (c - fm3), min, max
+    uint32_t fm3, win;  // first contig - 3, bits (c - fm3)
 };
 
 __device__ __forceinline__ void rs_reset(RState& s, uint32_t c) {
     s.fm3 = c - 3u;
     s.win = 8u;
-    s.mn = c;
-    s.mx = c;
 }
-__device__ __forceinline__ void rs_add(RState& s, uint32_t c) {
-    s.win |= 1u << ((c - s.fm3) & 31u);
-    s.mn = min(s.mn, c);
-    s.mx = max(s.mx, c);
+__device__ __forceinline__ void rs_add(RState& s, uint32_t c) { s.win |= 1u << min(c - s.fm3, 31u); }
+// compact code of a read: *code valid when the result is true
+template <bool COMPACT>
+__device__ __forceinline__ bool rs_code(const RState& s, uint32_t Nm3, uint32_t* code) {
+    const uint32_t z = (uint32_t)__builtin_ctz(s.win);  // bit 3 (the first contig) is always set
+    const uint32_t rel = s.win >> z, m0 = s.fm3 + z;
+    *code = m0 | (rel >> 1) << 24;
+    return COMPACT && rel < 16u && m0 < Nm3;
 }
-// compact code, or kEmpty when the read is general
-__device__ __forceinline__ uint32_t rs_code(const RState& s, uint32_t N, int compact) {
-    const uint32_t rel = s.win >> ((s.mn - s.fm3) & 31u);
-    return compact && s.mx - s.mn < 4u && s.mx < N ? (s.mn | (rel >> 1) << 24) : kEmpty;
+// the same for a read seen in two parts (a tail and the next lane's head).  A
+// marker bit shifted out of 32 bits leaves the first contig's bit at >= 4, so
+// the read is still general.
+template <bool COMPACT>
+__device__ __forceinline__ bool rs_code2(const RState& a, const RState& b, uint32_t Nm3, uint32_t* code) {
+    const uint32_t za = (uint32_t)__builtin_ctz(a.win), zb = (uint32_t)__builtin_ctz(b.win);
+    const uint32_t ma = a.fm3 + za, mb = b.fm3 + zb, m0 = min(ma, mb);
+    const uint32_t rel = ((a.win >> za) << min(ma - m0, 31u)) | ((b.win >> zb) << min(mb - m0, 31u));
+    *code = m0 | (rel >> 1) << 24;
+    return COMPACT && rel < 16u && m0 < Nm3;
 }
-__device__ __forceinline__ uint32_t rs_code2(const RState& a, const RState& b, uint32_t N, int compact) {
-    const uint32_t m0 = min(a.mn, b.mn), mx = max(a.mx, b.mx);
-    const uint32_t ra = (a.win >> ((a.mn - a.fm3) & 31u)) << ((a.mn - m0) & 31u);
-    const uint32_t rb = (b.win >> ((b.mn - b.fm3) & 31u)) << ((b.mn - m0) & 31u);
-    return compact && mx - m0 < 4u && mx < N ? (m0 | ((ra | rb) >> 1) << 24) : kEmpty;
+
+// lane-mask forms for the wave's walk: the compares go straight into SGPR lane
+// masks, which feed selects through inverse ballots (no 0/1 VGPR round trips)
+__device__ __forceinline__ uint64_t lanes(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+__device__ __forceinline__ bool in_mask(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+template <bool COMPACT>
+__device__ __forceinline__ uint64_t rs_code_m(const RState& s, uint32_t Nm3, uint32_t* code) {
+    const uint32_t z = (uint32_t)__builtin_ctz(s.win);
+    const uint32_t rel = s.win >> z, m0 = s.fm3 + z;
+    *code = m0 | (rel >> 1) << 24;
+    return COMPACT ? lanes(rel < 16u) & lanes(m0 < Nm3) : 0ull;
+}
+template <bool COMPACT>
+__device__ __forceinline__ uint64_t rs_code2_m(const RState& a, const RState& b, uint32_t Nm3, uint32_t* code) {
+    const uint32_t za = (uint32_t)__builtin_ctz(a.win), zb = (uint32_t)__builtin_ctz(b.win);
+    const uint32_t ma = a.fm3 + za, mb = b.fm3 + zb, m0 = min(ma, mb);
+    const uint32_t rel = ((a.win >> za) << min(ma - m0, 31u)) | ((b.win >> zb) << min(mb - m0, 31u));
+    *code = m0 | (rel >> 1) << 24;
+    return COMPACT ? lanes(rel < 16u) & lanes(m0 < Nm3) : 0ull;
 }
 
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lane l <- lane l - 1; lane 0 <- old
@@ -199,7 +226,9 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
-template <bool HIST>  // HIST: per-block code-bucket histograms for code_append_kernel
+// HIST: per-block code-bucket histograms for code_append_kernel; COMPACT: the
+// compact-code path exists (n_contigs <= 2^21)
+template <bool HIST, bool COMPACT>
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
 classify2_kernel(ClassArgs P) {
     const int lane = threadIdx.x & 63;
@@ -208,6 +237,7 @@ classify2_kernel(ClassArgs P) {
     const int64_t c_lo = chunk * kCChunk;
     if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
     const int64_t c_hi = min(P.A, c_lo + kCChunk);
+    const uint32_t Nm3 = P.N > 3u ? P.N - 3u : 0u;
     uint32_t* out = P.codes + c_lo;
     // the chunk's region as a buffer resource built from wave-uniform values
     const uint64_t out_u = (uint64_t)out;
@@ -230,7 +260,8 @@ classify2_kernel(ClassArgs P) {
         wave_sync();
     }
 
-    // records [t0, hi) of a step, coalesced: unit u of lane l = records t0 + 128u + 2l, + 1
+    // records [t0, hi) of a step, coalesced: unit u of lane l = records t0 + 128u + 2l, + 1.
+    // Past the chunk: read id kEmpty (a read of its own that is never emitted), contig 0.
     auto prefetch = [&](u32x4 (&dst)[kCPer], int64_t t0, int64_t hi) {
         const int64_t gb = t0 + 2 * lane;
         if (t0 + kCIter <= hi) {
@@ -241,8 +272,8 @@ classify2_kernel(ClassArgs P) {
 #pragma unroll
             for (int u = 0; u < kCPer; ++u) {
                 const int64_t gi = gb + 128 * u;
-                const uint2 r0 = gi < hi ? P.rec[gi] : make_uint2(kEmpty, kEmpty);
-                const uint2 r1 = gi + 1 < hi ? P.rec[gi + 1] : make_uint2(kEmpty, kEmpty);
+                const uint2 r0 = gi < hi ? P.rec[gi] : make_uint2(kEmpty, 0u);
+                const uint2 r1 = gi + 1 < hi ? P.rec[gi + 1] : make_uint2(kEmpty, 0u);
                 dst[u] = u32x4{r0.x, r0.y, r1.x, r1.y};
             }
         }
@@ -254,11 +285,14 @@ classify2_kernel(ClassArgs P) {
     RState ct{};
     uint32_t ct_len = 0, ct_pos = 0;
     uint32_t nc = 0, ng = 0;
-    int bad_order = 0, bad_contig = 0;
+    uint64_t bad_order = 0, bad_contig = 0;  // lane masks
     // one 512-record step from `buf`, which then takes the next step's loads
     // (two steps in flight -- a second register set at 4 waves/SIMD -- measured
     // the same: the walk already runs at ~5.7 TB/s of records + codes)
-    auto step = [&](u32x4 (&buf)[kCPer], int64_t t0) {
+    // FULL: all 512 records of the step are inside the chunk (every step but a
+    // chunk's last): no per-record validity tests
+    auto step = [&](auto full_tag, u32x4 (&buf)[kCPer], int64_t t0) {
+        constexpr bool FULL = decltype(full_tag)::value;
         uint32_t rid[8], ctg[8];
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
 #pragma unroll
@@ -278,121 +312,143 @@ classify2_kernel(ClassArgs P) {
         wave_sync();
         if (t0 + kCIter < c_hi) prefetch(buf, t0 + kCIter, c_hi);
         // valid records of this lane (own reads start at a valid record)
-        const int nval = (int)max<int64_t>(0, min<int64_t>(8, c_hi - (t0 + 8 * lane)));
-        const bool first_any = have_prev || lane > 0;
+        const int nval = FULL ? 8 : (int)max<int64_t>(0, min<int64_t>(8, c_hi - (t0 + 8 * lane)));
         const uint32_t prev_last = dpp_shr1(prev_rid, rid[7]);
-        uint32_t sm = (!first_any || rid[0] != prev_last) ? 1u : 0u;  // bit i: a read starts at record i
-        int bo = (nval > 0 && first_any && prev_last > rid[0]) ? 1 : 0;
-        int bc = (nval > 0 && ctg[0] >= P.N) ? 1 : 0;
-#pragma unroll
-        for (int i = 1; i < 8; ++i) {
-            sm |= (rid[i] != rid[i - 1] ? 1u : 0u) << i;
-            bo |= (i < nval && rid[i - 1] > rid[i]) ? 1 : 0;
-            bc |= (i < nval && ctg[i] >= P.N) ? 1 : 0;
-        }
-        bad_order |= bo;
-        bad_contig |= bc;
-        // emission: codes from the front of the chunk's region, general read
-        // starts (chunk-relative) from the back, big reads to the big list.
-        // The walk runs once for the codes; only when some lane met a general
-        // or a big read does it run again to emit those (rare on assembled
-        // transcriptomes), so the common pass carries no branches for them.
-        // Codes go out through a buffer store whose range check drops the lanes
-        // without one (offset past the chunk's region): no exec-mask branch.
-        RState st, hd;
-        uint32_t spos = 0, hlen = 0;
+        // order and range checks as lane masks (padding: read id kEmpty, contig
+        // 0); the order of records inside the lane is checked during the walk
+        bad_order |= lanes(prev_last > rid[0]) & (have_prev ? ~0ull : ~1ull);
+        bad_contig |= lanes(max(max(max(ctg[0], ctg[1]), max(ctg[2], ctg[3])),
+                                max(max(ctg[4], ctg[5]), max(ctg[6], ctg[7]))) >= P.N);
         const uint32_t ubase = (uint32_t)(t0 - c_lo) + 8u * lane;
-        uint32_t rare = 0;
-        auto walk = [&](auto rare_pass) {
+        // The lane's walk (branch-free: no lane predicate lives across a branch,
+        // so the compiler keeps them as SGPR lane masks).  Emission: codes from
+        // the front of the chunk's region, general read starts (chunk-relative)
+        // from the back, big reads to the big list.  The walk runs once for the
+        // codes; only when some lane met a general or a big read does it run
+        // again to emit those (rare on assembled transcriptomes).  Codes go out
+        // through a buffer store whose range check drops the lanes without one.
+        // Outputs: the lane's last read (st, spos), whether one started in the
+        // lane, and the mask of lanes with a general or big read.
+        auto walk = [&](auto rare_pass, RState& st, uint32_t& spos, uint64_t& started) -> uint64_t {
             constexpr bool RARE = decltype(rare_pass)::value;
-            auto emit = [&](bool e, uint32_t code, uint32_t pos, bool big) {
+            uint64_t rare = 0;
+            // e: lanes where a read ends here; ok: ... it is compact (code); big: ... it has > 8 records
+            auto emit = [&](uint64_t e, uint64_t ok, uint32_t code, uint32_t pos, uint64_t big) {
                 if (!RARE) {
-                    const bool ec = e && !big && code != kEmpty;
-                    const unsigned long long b = __ballot(ec);
-                    const uint32_t boff = ec ? (nc + (uint32_t)rank_below(b)) * 4u : 0x80000000u;
+                    const uint64_t b = e & ok & ~big;
+                    // lanes without a code store past the region (bit 31): dropped
+                    const uint32_t boff = ((nc + (uint32_t)rank_below(b)) * 4u) | (in_mask(b) ? 0u : 0x80000000u);
                     __builtin_amdgcn_raw_buffer_store_b32(code, out_rsrc, (int)boff, 0, 0);
-                    if (hist_on && ec) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
+                    if (hist_on && in_mask(b)) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
                     nc += __popcll(b);
-                    rare |= (e && (big || code == kEmpty)) ? 1u : 0u;
+                    rare |= e & (big | ~ok);
                 } else {
-                    const bool eg = e && !big && code == kEmpty;
-                    const unsigned long long g = __ballot(eg);
+                    const uint64_t g = e & ~big & ~ok;
                     if (g) {
-                        if (eg) out[kCChunk - 1 - (ng + rank_below(g))] = pos;
+                        if (in_mask(g)) out[kCChunk - 1 - (ng + rank_below(g))] = pos;
                         ng += __popcll(g);
                     }
-                    if (__ballot(e && big)) {
-                        if (e && big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + pos;
+                    const uint64_t bg = e & big;
+                    if (bg) {
+                        if (in_mask(bg)) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + pos;
                     }
                 }
             };
-            // walk the lane (branch-free state updates): an own read ending at
-            // record i < 7 is emitted there
+            // S(i): lanes where a read starts at record i (lane 0 of a chunk's
+            // first step: always); computed where used, so few masks are live
+            auto S = [&](int i) -> uint64_t {
+                return i == 0 ? lanes(rid[0] != prev_last) | (have_prev ? 0ull : 1ull) : lanes(rid[i] != rid[i - 1]);
+            };
+            const uint64_t S0 = S(0);
+            RState hd;
             rs_reset(st, ctg[0]);
             hd = st;
-            // head = records before the first read start (8: no start in the lane)
-            hlen = (sm & 1u) ? 0u : (sm ? (uint32_t)__builtin_ctz(sm) : 8u);
             spos = 0;
+            uint32_t hlen = in_mask(S0) ? 0u : 8u;  // head: records before the first start (8: none)
+            started = S0;
+            uint64_t Si = S0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 if (i > 0) {
-                    const bool si = (sm >> i) & 1u;
-                    const bool cap = (uint32_t)i == hlen;  // first start: the head ends here
-                    hd.fm3 = cap ? st.fm3 : hd.fm3;
-                    hd.win = cap ? st.win : hd.win;
-                    hd.mn = cap ? st.mn : hd.mn;
-                    hd.mx = cap ? st.mx : hd.mx;
-                    spos = si ? (uint32_t)i : spos;
+                    const uint64_t cap = Si & ~started;  // the first start: the head ends here
+                    hd.fm3 = in_mask(cap) ? st.fm3 : hd.fm3;
+                    hd.win = in_mask(cap) ? st.win : hd.win;
+                    hlen = in_mask(cap) ? (uint32_t)i : hlen;
+                    started |= Si;
+                    spos = in_mask(Si) ? (uint32_t)i : spos;
                     const uint32_t c = ctg[i];
-                    const uint32_t fm3 = si ? c - 3u : st.fm3;
-                    const uint32_t bit = 1u << ((c - fm3) & 31u);
-                    st.win = si ? bit : (st.win | bit);
+                    const uint32_t fm3 = in_mask(Si) ? c - 3u : st.fm3;
+                    // a new read: bit 3 alone (c - fm3 = 3)
+                    st.win = (in_mask(Si) ? 0u : st.win) | (1u << min(c - fm3, 31u));
                     st.fm3 = fm3;
-                    st.mn = si ? c : min(st.mn, c);
-                    st.mx = si ? c : max(st.mx, c);
+                    if (!RARE) bad_order |= lanes(rid[i - 1] > rid[i]);
                 }
                 if (i < 7) {
-                    const bool e = ((sm >> (i + 1)) & 1u) && hlen <= (uint32_t)i && (int)spos < nval;
-                    emit(e, rs_code(st, P.N, P.compact), ubase + spos, false);
+                    // an own read ends at i (the next record starts one); it
+                    // started at a valid record iff i < nval
+                    const uint64_t Sn = S(i + 1);
+                    const uint64_t e = Sn & started & (FULL ? ~0ull : lanes(i < nval));
+                    Si = Sn;
+                    uint32_t code;
+                    const uint64_t ok = rs_code_m<COMPACT>(st, Nm3, &code);
+                    emit(e, ok, code, ubase + spos, 0ull);
                 }
             }
-            if (hlen == 8u) hd = st;  // no read starts here: the whole lane is a head
+            hd.fm3 = in_mask(started) ? hd.fm3 : st.fm3;  // no read starts here: the whole lane is a head
+            hd.win = in_mask(started) ? hd.win : st.win;
             // the incoming tail (the previous lane's last read), merged with this
-            // lane's head when the read continues
-            const bool t_ok = hlen < 8u && (int)spos < nval;
+            // lane's head when the read continues (else with itself: the same code)
+            const uint64_t t_ok = started & (FULL ? ~0ull : lanes((int)spos < nval));
             const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
             RState in;
             in.fm3 = dpp_shr1(ct.fm3, st.fm3);
             in.win = dpp_shr1(ct.win, st.win);
-            in.mn = dpp_shr1(ct.mn, st.mn);
-            in.mx = dpp_shr1(ct.mx, st.mx);
             const uint32_t in_pk =
-                dpp_shr1(ct_ok ? (ct_len | ct_pos << 8) : kEmpty, t_ok ? (t_len | t_pos << 8) : kEmpty);
-            const bool have = in_pk != kEmpty;
+                dpp_shr1(ct_ok ? (ct_len | ct_pos << 8) : kEmpty, in_mask(t_ok) ? (t_len | t_pos << 8) : kEmpty);
+            const uint64_t have = lanes(in_pk != kEmpty);
             const uint32_t in_len = in_pk & 255u, in_pos = in_pk >> 8;
-            const bool cont = !(sm & 1u);
-            const bool big = cont && in_len + hlen > (uint32_t)kMaxFast;
-            emit(have, cont ? rs_code2(in, hd, P.N, P.compact) : rs_code(in, P.N, P.compact), in_pos, big);
+            const uint64_t cont = ~S0;
+            const uint64_t big = cont & lanes(in_len + hlen > (uint32_t)kMaxFast);
+            RState hm;
+            hm.fm3 = in_mask(cont) ? hd.fm3 : in.fm3;
+            hm.win = in_mask(cont) ? hd.win : in.win;
+            uint32_t code;
+            const uint64_t ok = rs_code2_m<COMPACT>(in, hm, Nm3, &code);
+            emit(have, ok, code, in_pos, big);
+            return rare;
         };
-        walk(std::false_type{});
-        if (__ballot(rare != 0)) walk(std::true_type{});
-        // this lane's tail (an own read reaching record 7) -> the next lane
-        const bool t_ok = hlen < 8u && (int)spos < nval;
-        const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
+        RState st;
+        uint32_t spos;
+        uint64_t started;
+        const uint64_t rare = walk(std::false_type{}, st, spos, started);
+        // this lane's tail (an own read reaching record 7) -> the next lane;
         // carry lane 63 into the next step
-        ct_ok = __builtin_amdgcn_readlane((int)t_ok, 63) != 0;
-        ct.fm3 = (uint32_t)__builtin_amdgcn_readlane((int)st.fm3, 63);
-        ct.win = (uint32_t)__builtin_amdgcn_readlane((int)st.win, 63);
-        ct.mn = (uint32_t)__builtin_amdgcn_readlane((int)st.mn, 63);
-        ct.mx = (uint32_t)__builtin_amdgcn_readlane((int)st.mx, 63);
-        ct_len = (uint32_t)__builtin_amdgcn_readlane((int)t_len, 63);
-        ct_pos = (uint32_t)__builtin_amdgcn_readlane((int)t_pos, 63);
+        const uint64_t t_ok = started & (FULL ? ~0ull : lanes((int)spos < nval));
+        const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
+        const bool ct_ok_next = (t_ok >> 63) != 0;
+        RState ct_next;
+        ct_next.fm3 = (uint32_t)__builtin_amdgcn_readlane((int)st.fm3, 63);
+        ct_next.win = (uint32_t)__builtin_amdgcn_readlane((int)st.win, 63);
+        const uint32_t ct_len_next = (uint32_t)__builtin_amdgcn_readlane((int)t_len, 63);
+        const uint32_t ct_pos_next = (uint32_t)__builtin_amdgcn_readlane((int)t_pos, 63);
+        if (rare) {
+            RState st2;
+            uint32_t spos2;
+            uint64_t started2;
+            walk(std::true_type{}, st2, spos2, started2);
+        }
+        ct_ok = ct_ok_next;
+        ct = ct_next;
+        ct_len = ct_len_next;
+        ct_pos = ct_pos_next;
         prev_rid = (uint32_t)__builtin_amdgcn_readlane((int)rid[7], 63);
         have_prev = true;
     };
     u32x4 buf[kCPer];
     prefetch(buf, c_lo, c_hi);
-    for (int64_t t0 = c_lo; t0 < c_hi; t0 += kCIter) step(buf, t0);
+    int64_t t0 = c_lo;
+    for (; t0 + kCIter <= c_hi; t0 += kCIter) step(std::true_type{}, buf, t0);
+    if (t0 < c_hi) step(std::false_type{}, buf, t0);
     // the chunk's last tail read continues into the next chunk's first records
     // (at most 8 of them matter): uniform scalar walk
     if (ct_ok) {
@@ -405,16 +461,17 @@ classify2_kernel(ClassArgs P) {
             else rs_add(h, r.y);
         }
         const bool big = ct_len + hl > (uint32_t)kMaxFast;
-        const uint32_t code = big ? kEmpty : hl ? rs_code2(ct, h, P.N, P.compact) : rs_code(ct, P.N, P.compact);
+        uint32_t code;
+        const bool ok = !big && (hl ? rs_code2<COMPACT>(ct, h, Nm3, &code) : rs_code<COMPACT>(ct, Nm3, &code));
         if (lane == 0) {
             if (big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + ct_pos;
-            else if (code != kEmpty) {
+            else if (ok) {
                 out[nc] = code;
                 if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
             } else out[kCChunk - 1 - ng] = ct_pos;
         }
-        nc += !big && code != kEmpty ? 1u : 0u;
-        ng += !big && code == kEmpty ? 1u : 0u;
+        nc += ok ? 1u : 0u;
+        ng += !big && !ok ? 1u : 0u;
     }
     if (lane == 0) {
         P.n_codes[chunk] = nc;
@@ -429,8 +486,10 @@ classify2_kernel(ClassArgs P) {
             if (k) atomicAdd(gh + b, k);
         }
     }
-    if (bad_order) P.flags[0] = 1;
-    if (bad_contig) P.flags[1] = 1;
+    if (lane == 0) {
+        if (bad_order) P.flags[0] = 1;
+        if (bad_contig) P.flags[1] = 1;
+    }
 }
 
 // ---- general reads -----------------------------------------------------------------
@@ -1497,7 +1556,7 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
             ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags,
                         nullptr,   0,         0};
-            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<false>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false>), ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags);
@@ -1666,9 +1725,10 @@ int SetsJob::launch() {
                     n_gen.ptr, blk_items, lpb, big_list.ptr, counters, flags,
                     append ? blk_hist.ptr : nullptr, g.bwc, g.Bc};
         if (append)
-            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<true>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true>), ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         else
-            KARMA_LAUNCH(ctx, "graph_classify", classify2_kernel<false>, ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true>), ceil_div(n_chunks, kCW / 64), kCW, 0,
+                         C);
     }
     // where side-stream work (the k-mer profile) may start: 0 = after the whole
     // pipeline (default), 1 = after classify, 2 = after the code partition.
