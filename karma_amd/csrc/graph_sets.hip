@@ -167,9 +167,11 @@ __device__ __forceinline__ int rank_below(unsigned long long m) {
 // minus 3: bit (c - fm3), clamped to bit 31 for a contig outside [fm3, fm3 + 30]
 // (the read then spans more than 4 contigs).  At the read's end m0 = fm3 +
 // ctz(win) and rel = win >> ctz(win): the read is compact when rel < 16 (its
-// contigs lie in [m0, m0 + 3]) and m0 + 3 < N (reads on the last three
-// contigs, and contigs out of range, take the general path, which checks the
-// range); it becomes (m0 | M << 24), M = rel >> 1.
+// contigs lie in [m0, m0 + 3]) and m0 < N; it becomes (m0 | M << 24), M =
+// rel >> 1.  (m0 < N keeps every bucket and histogram index in range; a
+// contig >= N elsewhere in the read is caught by the range check, which fails
+// the call.  Testing m0 + 3 < N instead sent the reads of the last gene to the
+// general path and woke its whole pipeline: +0.03 ms.)
 struct RState {
     uint32_t fm3, win;  // first contig - 3, bits (c - fm3)
 };
@@ -181,22 +183,22 @@ __device__ __forceinline__ void rs_reset(RState& s, uint32_t c) {
 __device__ __forceinline__ void rs_add(RState& s, uint32_t c) { s.win |= 1u << min(c - s.fm3, 31u); }
 // compact code of a read: *code valid when the result is true
 template <bool COMPACT>
-__device__ __forceinline__ bool rs_code(const RState& s, uint32_t Nm3, uint32_t* code) {
+__device__ __forceinline__ bool rs_code(const RState& s, uint32_t N, uint32_t* code) {
     const uint32_t z = (uint32_t)__builtin_ctz(s.win);  // bit 3 (the first contig) is always set
     const uint32_t rel = s.win >> z, m0 = s.fm3 + z;
     *code = m0 | (rel >> 1) << 24;
-    return COMPACT && rel < 16u && m0 < Nm3;
+    return COMPACT && rel < 16u && m0 < N;
 }
 // the same for a read seen in two parts (a tail and the next lane's head).  A
 // marker bit shifted out of 32 bits leaves the first contig's bit at >= 4, so
 // the read is still general.
 template <bool COMPACT>
-__device__ __forceinline__ bool rs_code2(const RState& a, const RState& b, uint32_t Nm3, uint32_t* code) {
+__device__ __forceinline__ bool rs_code2(const RState& a, const RState& b, uint32_t N, uint32_t* code) {
     const uint32_t za = (uint32_t)__builtin_ctz(a.win), zb = (uint32_t)__builtin_ctz(b.win);
     const uint32_t ma = a.fm3 + za, mb = b.fm3 + zb, m0 = min(ma, mb);
     const uint32_t rel = ((a.win >> za) << min(ma - m0, 31u)) | ((b.win >> zb) << min(mb - m0, 31u));
     *code = m0 | (rel >> 1) << 24;
-    return COMPACT && rel < 16u && m0 < Nm3;
+    return COMPACT && rel < 16u && m0 < N;
 }
 
 // lane-mask forms for the wave's walk: the compares go straight into SGPR lane
@@ -204,19 +206,19 @@ __device__ __forceinline__ bool rs_code2(const RState& a, const RState& b, uint3
 __device__ __forceinline__ uint64_t lanes(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 __device__ __forceinline__ bool in_mask(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 template <bool COMPACT>
-__device__ __forceinline__ uint64_t rs_code_m(const RState& s, uint32_t Nm3, uint32_t* code) {
+__device__ __forceinline__ uint64_t rs_code_m(const RState& s, uint32_t N, uint32_t* code) {
     const uint32_t z = (uint32_t)__builtin_ctz(s.win);
     const uint32_t rel = s.win >> z, m0 = s.fm3 + z;
     *code = m0 | (rel >> 1) << 24;
-    return COMPACT ? lanes(rel < 16u) & lanes(m0 < Nm3) : 0ull;
+    return COMPACT ? lanes(rel < 16u) & lanes(m0 < N) : 0ull;
 }
 template <bool COMPACT>
-__device__ __forceinline__ uint64_t rs_code2_m(const RState& a, const RState& b, uint32_t Nm3, uint32_t* code) {
+__device__ __forceinline__ uint64_t rs_code2_m(const RState& a, const RState& b, uint32_t N, uint32_t* code) {
     const uint32_t za = (uint32_t)__builtin_ctz(a.win), zb = (uint32_t)__builtin_ctz(b.win);
     const uint32_t ma = a.fm3 + za, mb = b.fm3 + zb, m0 = min(ma, mb);
     const uint32_t rel = ((a.win >> za) << min(ma - m0, 31u)) | ((b.win >> zb) << min(mb - m0, 31u));
     *code = m0 | (rel >> 1) << 24;
-    return COMPACT ? lanes(rel < 16u) & lanes(m0 < Nm3) : 0ull;
+    return COMPACT ? lanes(rel < 16u) & lanes(m0 < N) : 0ull;
 }
 
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lane l <- lane l - 1; lane 0 <- old
@@ -237,7 +239,6 @@ classify2_kernel(ClassArgs P) {
     const int64_t c_lo = chunk * kCChunk;
     if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
     const int64_t c_hi = min(P.A, c_lo + kCChunk);
-    const uint32_t Nm3 = P.N > 3u ? P.N - 3u : 0u;
     uint32_t* out = P.codes + c_lo;
     // the chunk's region as a buffer resource built from wave-uniform values
     const uint64_t out_u = (uint64_t)out;
@@ -390,7 +391,7 @@ classify2_kernel(ClassArgs P) {
                     const uint64_t e = Sn & started & (FULL ? ~0ull : lanes(i < nval));
                     Si = Sn;
                     uint32_t code;
-                    const uint64_t ok = rs_code_m<COMPACT>(st, Nm3, &code);
+                    const uint64_t ok = rs_code_m<COMPACT>(st, P.N, &code);
                     emit(e, ok, code, ubase + spos, 0ull);
                 }
             }
@@ -413,7 +414,7 @@ classify2_kernel(ClassArgs P) {
             hm.fm3 = in_mask(cont) ? hd.fm3 : in.fm3;
             hm.win = in_mask(cont) ? hd.win : in.win;
             uint32_t code;
-            const uint64_t ok = rs_code2_m<COMPACT>(in, hm, Nm3, &code);
+            const uint64_t ok = rs_code2_m<COMPACT>(in, hm, P.N, &code);
             emit(have, ok, code, in_pos, big);
             return rare;
         };
@@ -462,7 +463,7 @@ classify2_kernel(ClassArgs P) {
         }
         const bool big = ct_len + hl > (uint32_t)kMaxFast;
         uint32_t code;
-        const bool ok = !big && (hl ? rs_code2<COMPACT>(ct, h, Nm3, &code) : rs_code<COMPACT>(ct, Nm3, &code));
+        const bool ok = !big && (hl ? rs_code2<COMPACT>(ct, h, P.N, &code) : rs_code<COMPACT>(ct, P.N, &code));
         if (lane == 0) {
             if (big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + ct_pos;
             else if (ok) {
@@ -1811,6 +1812,14 @@ int SetsJob::finish(karma_pairs* out) {
         KARMA_TRY(launch());
     }
     const unsigned n_big = hc[0];
+    if (std::getenv("KARMA_DEBUG_GEN")) {  // diagnostic: reads on the general path, big reads
+        std::vector<uint32_t> hg(n_chunks);
+        KARMA_HIP(hipMemcpy(hg.data(), n_gen.ptr, n_chunks * 4, hipMemcpyDeviceToHost));
+        uint64_t tot = 0;
+        for (uint32_t x : hg) tot += x;
+        std::fprintf(stderr, "[karma] general reads %llu, big reads %u, pair flushes %u\n", (unsigned long long)tot,
+                     n_big, hc[2]);
+    }
     DevArray<const uint64_t*> pk;
     DevArray<const int64_t*> pc;
     KARMA_TRY(pk.alloc(ctx, B));

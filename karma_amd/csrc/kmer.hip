@@ -41,6 +41,8 @@ struct karma_contigs {
     DevArray<uint32_t> packed;
     DevArray<uint16_t> mask;
     DevArray<uint8_t> has_exc;
+    DevArray<uint32_t> exc_list;  // contigs with exception bases (any order), count in exc_n
+    DevArray<unsigned> exc_n;
 };
 
 struct karma_kmer_plan {
@@ -99,7 +101,8 @@ __global__ void __launch_bounds__(kBlock) pack_kernel(const uint8_t* __restrict_
                                                       const int64_t* __restrict__ woff, int64_t n,
                                                       uint32_t* __restrict__ packed, uint16_t* __restrict__ mask,
                                                       uint8_t* __restrict__ has_exc,
-                                                      unsigned long long* __restrict__ exc_count) {
+                                                      unsigned long long* __restrict__ exc_count,
+                                                      uint32_t* __restrict__ exc_list, unsigned* __restrict__ exc_n) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
     int64_t c = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
@@ -143,7 +146,10 @@ __global__ void __launch_bounds__(kBlock) pack_kernel(const uint8_t* __restrict_
         }
         if (nexc) atomicAdd(exc_count, (unsigned long long)nexc);
         const bool any = __ballot(nexc != 0) != 0;
-        if (lane == 0) has_exc[c] = any ? 1 : 0;
+        if (lane == 0) {
+            has_exc[c] = any ? 1 : 0;
+            if (any) exc_list[atomicAdd(exc_n, 1u)] = (uint32_t)c;
+        }
         c = cn, s = sn, e = en, w0 = w0n, w1 = w1n;
     }
 }
@@ -309,7 +315,9 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
                                                           int nwords, bool with_len, uint32_t* __restrict__ presence,
                                                           uint64_t* __restrict__ exc_buf, int64_t exc_cap,
                                                           unsigned long long* __restrict__ exc_cnt,
-                                                          int64_t c_begin, const int* __restrict__ full) {
+                                                          int64_t c_begin, const int* __restrict__ full,
+                                                          const uint32_t* __restrict__ exc_list,
+                                                          const unsigned* __restrict__ exc_n) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     // once every ACGT ordinal is present, only contigs with exception bases can
@@ -324,8 +332,7 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
         const unsigned long long slot = atomicAdd(exc_cnt, 1ull);
         if ((int64_t)slot < exc_cap) exc_buf[slot] = key;
     };
-    for (int64_t c = c_begin + (int64_t)blockIdx.x * wpb + wave; c < n; c += (int64_t)gridDim.x * wpb) {
-        if (saturated && !has_exc[c]) continue;
+    auto scan = [&](int64_t c) {
         const int64_t L = off[c + 1] - off[c];
         const uint8_t* craw = raw + off[c];
         for_each_window(packed, mask, has_exc[c] != 0, woff[c], L - kmin + 1, wbuf, mbuf, lane,
@@ -346,6 +353,16 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
                 else push_exc(key_from_bytes(craw + i, k, with_len));
             }
         });
+    };
+    const int64_t w0 = (int64_t)blockIdx.x * wpb + wave, ws = (int64_t)gridDim.x * wpb;
+    if (saturated) {  // only the listed contigs past the prefix (scanned before)
+        const int64_t ne = *exc_n;
+        for (int64_t i = w0; i < ne; i += ws) {
+            const int64_t c = exc_list[i];
+            if (c >= c_begin && c < n) scan(c);
+        }
+    } else {
+        for (int64_t c = c_begin + w0; c < n; c += ws) scan(c);
     }
     __syncthreads();
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
@@ -854,7 +871,8 @@ int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offs
     c->total = total;
     // word offsets: exclusive scan of ceil(L/16)
     DevArray<int64_t> wc;
-    if ((rc = wc.alloc(ctx, n + 1)) || (rc = c->woff.alloc(ctx, n + 1)) || (rc = c->has_exc.alloc(ctx, n ? n : 1))) {
+    if ((rc = wc.alloc(ctx, n + 1)) || (rc = c->woff.alloc(ctx, n + 1)) || (rc = c->has_exc.alloc(ctx, n ? n : 1)) ||
+        (rc = c->exc_list.alloc(ctx, n ? n : 1)) || (rc = c->exc_n.alloc(ctx, 1))) {
         delete c;
         return rc;
     }
@@ -881,10 +899,11 @@ int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offs
         return rc;
     }
     KARMA_HIP(hipMemsetAsync(stat.ptr, 0, 3 * sizeof(unsigned long long), ctx->stream));
+    KARMA_HIP(hipMemsetAsync(c->exc_n.ptr, 0, sizeof(unsigned), ctx->stream));
     if (n) {
         KARMA_LAUNCH(ctx, "pack_2bit", pack_kernel, grid_for(ceil_div(n, kBlock / 64), 8192), kBlock, 0, c->raw,
                      c->off, c->woff.ptr, n,
-                     c->packed.ptr, c->mask.ptr, c->has_exc.ptr, stat.ptr);
+                     c->packed.ptr, c->mask.ptr, c->has_exc.ptr, stat.ptr, c->exc_list.ptr, c->exc_n.ptr);
         KARMA_LAUNCH(ctx, "zero_key", zero_key_kernel, ceil_div(n, 256), 256, 0, c->off, c->keylen, n, stat.ptr + 1,
                      stat.ptr + 2);
     }
@@ -958,11 +977,13 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
             if (p56)
                 KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<true>, grid, kBlock, lds, c->packed.ptr,
                              c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, hi, kmode, (int)p->nwords,
-                             with_len, p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, f);
+                             with_len, p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, f, c->exc_list.ptr,
+                             c->exc_n.ptr);
             else
                 KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<false>, grid, kBlock, lds, c->packed.ptr,
                              c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, hi, kmode, (int)p->nwords,
-                             with_len, p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, f);
+                             with_len, p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, f, c->exc_list.ptr,
+                             c->exc_n.ptr);
             return KARMA_OK;
         };
         KARMA_TRY(launch(0, nA, nullptr));
