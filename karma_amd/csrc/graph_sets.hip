@@ -1692,7 +1692,12 @@ int SetsJob::setup() {
     }
     // reduce geometry: grids fixed here, flush ranges from device counters
     // code reduce: one round (one 128 KB-LDS block per CU), at most ~4 flushes per group
-    n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count / g.Bc, ceil_div(max_cflush, 4)))
+    // Groups also cost a 128 KB histogram clear and write-back each (and the
+    // final kernel sums them), so a bucket gets one group per ~256K records it
+    // may hold (8-way strong scaling of config 3: 3 groups; one group took
+    // 0.076 ms against 0.047 for five).
+    n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>({ctx->cu_count / g.Bc, ceil_div(max_cflush, 4),
+                                                                     ceil_div(A, (int64_t)g.Bc << 18)}))
                     : 0;
     // pair-reduce groups per bucket: enough blocks to fill the chip while
     // buckets are few; one group from KARMA_ONE_GROUP_B buckets on, so the

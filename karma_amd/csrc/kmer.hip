@@ -365,9 +365,12 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
         for (int64_t c = c_begin + w0; c < n; c += ws) scan(c);
     }
     __syncthreads();
+    // OR-flush only the bits the global bitmap lacks: every block of the
+    // prefix sets nearly every bit, and one atomic per block and word queued
+    // ~1,000 deep on the same 160 words
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) {
         const uint32_t b = lds_bits[w];
-        if (b) atomicOr(&presence[w], b);
+        if (b & ~__hip_atomic_load(&presence[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicOr(&presence[w], b);
     }
 }
 
@@ -404,16 +407,26 @@ __global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* __re
     const int lo = threadIdx.x * per, hi = min(nwords, lo + per);
     uint32_t s = 0;
     for (int w = lo; w < hi; ++w) s += __popc(presence[w]);
-    chunk_sum[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int t = 0; t < kColBlock; ++t) {
-            uint32_t v = chunk_sum[t];
-            chunk_sum[t] = run;
-            run += v;
+    // exclusive scan of the chunk sums over the block: wave scans, then the
+    // wave totals (a serial loop in one thread took ~15 us)
+    {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        uint32_t x = s;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
         }
-        prefix[nwords] = run;
+        __shared__ uint32_t wtot[kColBlock / 64];
+        if (lane == 63) wtot[wave] = x;
+        __syncthreads();
+        uint32_t base = 0, all = 0;
+        for (int w = 0; w < kColBlock / 64; ++w) {
+            base += w < wave ? wtot[w] : 0u;
+            all += wtot[w];
+        }
+        chunk_sum[threadIdx.x] = base + x - s;
+        if (threadIdx.x == 0) prefix[nwords] = all;
     }
     __syncthreads();
     uint32_t run = chunk_sum[threadIdx.x];
