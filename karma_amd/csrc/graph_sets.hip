@@ -143,6 +143,9 @@ struct ClassArgs {
     int* flags;  // 0 order, 1 contig range (2: general pair list full)
     uint32_t* blk_hist;  // per partition block: codes per code bucket (null: no compact path)
     int bwc, Bc;
+    const uint32_t* remap;  // contig relabelling (classify2_kernel<.., REMAP>), new id by old id
+    int64_t c0;             // first chunk of this launch
+    const unsigned* skip;   // set: leave the chunks empty (a relabelled rerun follows)
 };
 
 // lanes below this one with their bit set in a wave mask
@@ -229,15 +232,23 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
 // HIST: per-block code-bucket histograms for code_append_kernel; COMPACT: the
-// compact-code path exists (n_contigs <= 2^21)
-template <bool HIST, bool COMPACT>
+// compact-code path exists (n_contigs <= 2^21); REMAP: contig ids relabelled
+// through P.remap as they are read (contig order without locality, see relabel)
+template <bool HIST, bool COMPACT, bool REMAP = false>
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
 classify2_kernel(ClassArgs P) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t chunk = (int64_t)blockIdx.x * (kCW / 64) + wave;
+    const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
     const int64_t c_lo = chunk * kCChunk;
     if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
+    if (P.skip && *P.skip) {  // the sample chunks asked for a relabelled rerun
+        if (lane == 0) {
+            P.n_codes[chunk] = 0;
+            P.n_gen[chunk] = 0;
+        }
+        return;
+    }
     const int64_t c_hi = min(P.A, c_lo + kCChunk);
     uint32_t* out = P.codes + c_lo;
     // the chunk's region as a buffer resource built from wave-uniform values
@@ -312,6 +323,10 @@ classify2_kernel(ClassArgs P) {
         }
         wave_sync();
         if (t0 + kCIter < c_hi) prefetch(buf, t0 + kCIter, c_hi);
+        if (REMAP) {  // ids out of range stay out of range (the range check fails the call)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ctg[i] = ctg[i] < P.N ? P.remap[ctg[i]] : ctg[i];
+        }
         // valid records of this lane (own reads start at a valid record)
         const int nval = FULL ? 8 : (int)max<int64_t>(0, min<int64_t>(8, c_hi - (t0 + 8 * lane)));
         const uint32_t prev_last = dpp_shr1(prev_rid, rid[7]);
@@ -458,8 +473,9 @@ classify2_kernel(ClassArgs P) {
         for (; hl < (uint32_t)kMaxFast && c_hi + hl < P.A; ++hl) {
             const uint2 r = P.rec[c_hi + hl];
             if (r.x != prev_rid) break;
-            if (hl == 0) rs_reset(h, r.y);
-            else rs_add(h, r.y);
+            const uint32_t cy = REMAP && r.y < P.N ? P.remap[r.y] : r.y;
+            if (hl == 0) rs_reset(h, cy);
+            else rs_add(h, cy);
         }
         const bool big = ct_len + hl > (uint32_t)kMaxFast;
         uint32_t code;
@@ -504,11 +520,14 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
                                                        uint64_t* __restrict__ pairs, int64_t pcap,
                                                        uint32_t* __restrict__ n_pairs,
                                                        unsigned long long* __restrict__ blk_items,
-                                                       int lists_per_block, int* __restrict__ flags) {
+                                                       int lists_per_block, int* __restrict__ flags,
+                                                       const uint32_t* __restrict__ remap,
+                                                       const unsigned* __restrict__ relabel) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t chunk = (int64_t)blockIdx.x * (kGW / 64) + wave;
     if (chunk >= n_chunks) return;
-    const uint32_t ng = n_gen[chunk];
+    // a relabelled rerun follows (relabel_probe_kernel): no pairs now
+    const uint32_t ng = relabel && *relabel ? 0u : n_gen[chunk];
     uint32_t np = 0;
     uint64_t* out = pairs + chunk * pcap;
     const int64_t c_lo = chunk * kCChunk;
@@ -528,7 +547,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
                 uint2 r = make_uint2(kEmpty, kEmpty);
                 if (v && s + t < A) r = rec[s + t];
                 v = v && r.x == rid;
-                rs.m[t] = v && r.y < N ? r.y : kEmpty;
+                rs.m[t] = v && r.y < N ? (remap ? remap[r.y] : r.y) : kEmpty;
             }
             sort_dedup(rs);
         }
@@ -1404,11 +1423,13 @@ __global__ void bucket_widen_kernel(const uint32_t* __restrict__ pent, RunDir di
 // big reads (> 8 records): pair keys, one thread per read, O(m^3) dedup
 __global__ void big_pairs_kernel(const uint2* __restrict__ rec, int64_t A, const int64_t* __restrict__ big_list,
                                  int64_t n_big, uint32_t N, uint64_t* __restrict__ out,
-                                 unsigned long long* __restrict__ n_out, int count_only) {
+                                 unsigned long long* __restrict__ n_out, int count_only,
+                                 const uint32_t* __restrict__ remap) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_big) return;
     unsigned long long c = 0;
-    read_pairs_slow(rec, A, big_list[k], [&](uint32_t a, uint32_t b) {
+    auto map = [&](uint32_t x) { return remap && x < N ? remap[x] : x; };
+    read_pairs_slow(rec, A, big_list[k], map, [&](uint32_t a, uint32_t b) {
         if (b >= N) return;
         if (count_only) ++c;
         else out[atomicAdd(n_out, 1ull)] = ((uint64_t)a << 32) | b;
@@ -1462,7 +1483,8 @@ namespace karma {
 // The sorted unique list (mk, mc, U) plus the pairs of reads with > 8 records
 // (big_list) -> out.
 int finish_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, const int64_t* big_list, unsigned n_big,
-                 DevArray<uint64_t>& mk, DevArray<int64_t>& mc, int64_t U, karma_pairs* out) {
+                 DevArray<uint64_t>& mk, DevArray<int64_t>& mc, int64_t U, karma_pairs* out,
+                 const uint32_t* remap = nullptr) {
     out->n_contigs = N;
     if (n_big == 0) {
         // no synchronisation: later work on this stream is ordered after the
@@ -1477,7 +1499,7 @@ int finish_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, const i
     KARMA_TRY(np.alloc(ctx, 1));
     KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
     KARMA_LAUNCH(ctx, "graph_big_count", big_pairs_kernel, grid_n(n_big, 64), 64, 0, rec, A, big_list,
-                 (int64_t)n_big, (uint32_t)N, (uint64_t*)nullptr, np.ptr, 1);
+                 (int64_t)n_big, (uint32_t)N, (uint64_t*)nullptr, np.ptr, 1, remap);
     unsigned long long hp = 0;
     KARMA_HIP(hipMemcpyAsync(&hp, np.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
@@ -1491,7 +1513,7 @@ int finish_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, const i
     }
     KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
     KARMA_LAUNCH(ctx, "graph_big_pairs", big_pairs_kernel, grid_n(n_big, 64), 64, 0, rec, A, big_list,
-                 (int64_t)n_big, (uint32_t)N, allk.ptr + U, np.ptr, 0);
+                 (int64_t)n_big, (uint32_t)N, allk.ptr + U, np.ptr, 0, remap);
     KARMA_LAUNCH(ctx, "fill_ones", fill_ones_i64_kernel, grid_n(hp), 256, 0, allc.ptr + U, (int64_t)hp);
     KARMA_TRY(sort_reduce_pairs(ctx, allk.ptr, allc.ptr, nullptr, U + (int64_t)hp, 64, out->keys, out->counts,
                                 nullptr, &out->n));
@@ -1556,11 +1578,12 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         if (A > 0) {
             ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags,
-                        nullptr,   0,         0};
+                        nullptr,   0,         0,       nullptr, 0, nullptr};
             KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false>), ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
-                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags);
+                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags,
+                     (const uint32_t*)nullptr, (const unsigned*)nullptr);
         KARMA_LAUNCH(ctx, "widen_counts", widen_counts_kernel, grid_n(n_chunks + 1), 256, 0, n_pl.ptr, n_chunks,
                      widths.ptr);
         KARMA_TRY(scan_excl_i64(ctx, widths.ptr, off.ptr, n_chunks + 1));
@@ -1587,6 +1610,118 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
     int64_t U = 0;
     KARMA_TRY(sort_reduce_pairs(ctx, keys.ptr, ones.ptr, nullptr, P, 32 + bbits, mk, mc, nullptr, &U));
     return finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out);
+}
+
+// ---- relabelling for contig orders without locality ---------------------------
+// The compact path needs the contigs of a read within 4 ids.  When the FASTA
+// order does not list isoforms together, most reads take the general path
+// (8.7 ms instead of 1.3 at config 3).  relabel_probe_kernel then asks for one
+// relabelled rerun (> 1/8 of the probed reads span more than 4 ids; classify
+// and the general kernel skip this pass): each contig is hooked to the smallest
+// contig it shares a
+// read with, the hooks are followed to a root, and contigs are renumbered
+// root by root, so contigs that share reads get adjacent ids.  The pipeline
+// reruns on the new ids (read through the remap table as records are read) and
+// the resulting pair keys are mapped back and re-sorted: the output is the
+// same; only the reads' path changes.
+// The decision, before classify: kRelabelProbes reads at evenly spaced
+// record positions (the next read start at or after each), non-compact when
+// their distinct contigs span more than 4 ids.  One block, one round of loads.
+constexpr int kRelabelProbes = 256;
+
+__global__ void __launch_bounds__(kRelabelProbes) relabel_probe_kernel(const uint2* __restrict__ rec, int64_t A,
+                                                                       uint32_t N, unsigned* __restrict__ relabel) {
+    __shared__ unsigned wide;
+    if (threadIdx.x == 0) wide = 0;
+    __syncthreads();
+    // a window of 32 records from an even position, loaded at once (16 B each)
+    constexpr int kW = 32;
+    const int64_t p = (A * (int64_t)threadIdx.x / kRelabelProbes) & ~int64_t(1);
+    uint32_t rid[kW], ctg[kW];
+    if (p + kW <= A) {
+        const u32x4* v = reinterpret_cast<const u32x4*>(rec + p);
+#pragma unroll
+        for (int u = 0; u < kW / 2; ++u) {
+            const u32x4 q = v[u];
+            rid[2 * u] = q.x, ctg[2 * u] = q.y, rid[2 * u + 1] = q.z, ctg[2 * u + 1] = q.w;
+        }
+        // the first read that starts inside the window and ends inside it
+        int s0 = -1, e0 = -1;
+#pragma unroll
+        for (int j = 1; j < kW; ++j) {
+            const bool start = rid[j] != rid[j - 1];
+            if (start && s0 >= 0 && e0 < 0) e0 = j;
+            if (start && s0 < 0) s0 = j;
+        }
+        if (s0 > 0 && e0 > 0) {
+            uint32_t mn = kEmpty, mx = 0;
+#pragma unroll
+            for (int j = 0; j < kW; ++j)
+                if (j >= s0 && j < e0) mn = min(mn, ctg[j]), mx = max(mx, ctg[j]);
+            if (mx - mn > 3u && mx < N) atomicAdd(&wide, 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && wide * 8 > kRelabelProbes) *relabel = 1;
+}
+
+__global__ void iota_u32_kernel(uint32_t* __restrict__ v, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (uint32_t)i;
+}
+
+// one thread per record; the thread at a read's first record hooks each of the
+// read's contigs to the read's smallest contig (test before the atomic)
+__global__ void relabel_hook_kernel(const uint2* __restrict__ rec, int64_t A, uint32_t N, uint32_t* __restrict__ rep) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A) return;
+    const uint32_t rid = rec[i].x;
+    if (i > 0 && rec[i - 1].x == rid) return;
+    uint32_t m = kEmpty;
+    int64_t e = i;
+    for (; e < A && rec[e].x == rid; ++e)
+        if (rec[e].y < N) m = min(m, rec[e].y);
+    if (m == kEmpty) return;
+    for (int64_t j = i; j < e; ++j) {
+        const uint32_t c = rec[j].y;
+        if (c < N && rep[c] > m) atomicMin(&rep[c], m);
+    }
+}
+
+// root of each contig (hooks only point to smaller ids), and the roots' sizes
+__global__ void relabel_root_kernel(const uint32_t* __restrict__ rep, uint32_t N, uint32_t* __restrict__ root,
+                                    int64_t* __restrict__ size) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > N) return;
+    if (c == N) {
+        size[N] = 0;
+        return;
+    }
+    uint32_t r = (uint32_t)c;
+    while (rep[r] != r) r = rep[r];
+    root[c] = r;
+    atomicAdd(reinterpret_cast<unsigned long long*>(size + r), 1ull);
+}
+
+// new id = the root's base + a slot in its group (order inside a group is free)
+__global__ void relabel_assign_kernel(const uint32_t* __restrict__ root, const int64_t* __restrict__ base, uint32_t N,
+                                      unsigned* __restrict__ fill, uint32_t* __restrict__ remap,
+                                      uint32_t* __restrict__ inv) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= N) return;
+    const uint32_t r = root[c];
+    const uint32_t id = (uint32_t)base[r] + atomicAdd(&fill[r], 1u);
+    remap[c] = id;
+    inv[id] = (uint32_t)c;
+}
+
+// pair keys (a << 32 | b) in new ids -> original ids, a <= b again
+__global__ void relabel_back_kernel(uint64_t* __restrict__ keys, int64_t n, const uint32_t* __restrict__ inv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    const uint32_t a = inv[(uint32_t)(k >> 32)], b = inv[(uint32_t)k];
+    keys[i] = (uint64_t)min(a, b) << 32 | max(a, b);
 }
 
 // Records (grouped by read, 16-byte aligned) -> sorted unique (a<<32|b, count).
@@ -1639,9 +1774,12 @@ struct SetsJob {
     DevArray<int64_t> slot_c;
     RunDir pdir{};
     int attempt = 0;
+    bool relabeled = false;                 // a relabelled rerun (see relabel_probe_kernel)
+    DevArray<uint32_t> remap_map, remap_inv;  // new id by old id, old id by new id
 
     int setup();
     int launch();
+    int relabel();
     int finish(karma_pairs* out);
 };
 
@@ -1729,12 +1867,29 @@ int SetsJob::launch() {
     if (A > 0) {
         ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
                     n_gen.ptr, blk_items, lpb, big_list.ptr, counters, flags,
-                    append ? blk_hist.ptr : nullptr, g.bwc, g.Bc};
-        if (append)
-            KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true>), ceil_div(n_chunks, kCW / 64), kCW, 0, C);
-        else
-            KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true>), ceil_div(n_chunks, kCW / 64), kCW, 0,
-                         C);
+                    append ? blk_hist.ptr : nullptr, g.bwc, g.Bc, relabeled ? remap_map.ptr : nullptr, 0, nullptr};
+        auto classify = [&](int64_t c_from, int64_t c_to) -> int {
+            C.c0 = c_from;
+            const int64_t cg = ceil_div(c_to - c_from, kCW / 64);
+            if (cg <= 0) return KARMA_OK;
+            if (append && relabeled)
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true, true>), cg, kCW, 0, C);
+            else if (append)
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true>), cg, kCW, 0, C);
+            else if (relabeled)
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, true>), cg, kCW, 0, C);
+            else
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true>), cg, kCW, 0, C);
+            return KARMA_OK;
+        };
+        if (!relabeled) {
+            // a probe of the reads decides: when many span more than 4 contig
+            // ids, this pass is skipped and a relabelled rerun follows
+            KARMA_LAUNCH(ctx, "relabel_probe", relabel_probe_kernel, 1, kRelabelProbes, 0, rec, A, (uint32_t)N,
+                         counters + 3);
+            C.skip = counters + 3;
+        }
+        KARMA_TRY(classify(0, n_chunks));
     }
     // where side-stream work (the k-mer profile) may start: 0 = after the whole
     // pipeline (default), 1 = after classify, 2 = after the code partition.
@@ -1753,7 +1908,8 @@ int SetsJob::launch() {
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
     }
     KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
-                 codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items + n_pblk, lpb, flags);
+                 codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items + n_pblk, lpb, flags,
+                 relabeled ? (const uint32_t*)remap_map.ptr : nullptr, (const unsigned*)(counters + 3));
     const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items};
     pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items + n_pblk};
     if (g.Bc > 0) {
@@ -1796,8 +1952,35 @@ int SetsJob::launch() {
     return KARMA_OK;
 }
 
+int SetsJob::relabel() {
+    const uint32_t n = (uint32_t)N;
+    DevArray<uint32_t> rep, root;
+    DevArray<unsigned> fill;
+    DevArray<int64_t> size, base;
+    KARMA_TRY(remap_map.alloc(ctx, N));
+    KARMA_TRY(remap_inv.alloc(ctx, N));
+    KARMA_TRY(rep.alloc(ctx, N));
+    KARMA_TRY(root.alloc(ctx, N));
+    KARMA_TRY(fill.alloc(ctx, N));
+    KARMA_TRY(size.alloc(ctx, N + 1));
+    KARMA_TRY(base.alloc(ctx, N + 1));
+    KARMA_LAUNCH(ctx, "relabel_iota", iota_u32_kernel, grid_n(N), 256, 0, rep.ptr, N);
+    // hooks from a sample of the reads (the records' first eighth, >= 4M
+    // records): a gene's contigs join through a few of its reads, and a contig
+    // left out only keeps its reads on the general path
+    const int64_t As = std::min<int64_t>(A, std::max<int64_t>(A / 8, int64_t(1) << 22));
+    if (As) KARMA_LAUNCH(ctx, "relabel_hook", relabel_hook_kernel, grid_n(As), 256, 0, rec, As, n, rep.ptr);
+    KARMA_HIP(hipMemsetAsync(size.ptr, 0, (N + 1) * 8, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(fill.ptr, 0, N * 4, ctx->stream));
+    KARMA_LAUNCH(ctx, "relabel_root", relabel_root_kernel, grid_n(N + 1), 256, 0, rep.ptr, n, root.ptr, size.ptr);
+    KARMA_TRY(scan_excl_i64(ctx, size.ptr, base.ptr, N + 1));
+    KARMA_LAUNCH(ctx, "relabel_assign", relabel_assign_kernel, grid_n(N), 256, 0, root.ptr, base.ptr, n, fill.ptr,
+                 remap_map.ptr, remap_inv.ptr);
+    return KARMA_OK;
+}
+
 int SetsJob::finish(karma_pairs* out) {
-    unsigned hc[3] = {0, 0, 0};
+    unsigned hc[4] = {0, 0, 0, 0};
     std::vector<uint8_t> hovf(B);
     int64_t U = 0;
     for (;;) {
@@ -1810,6 +1993,12 @@ int SetsJob::finish(karma_pairs* out) {
         KARMA_CHECK(!hf[0], KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
         KARMA_CHECK(!hf[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
         KARMA_CHECK(!hf[3], KARMA_ERR_STATE, "code partition: block counts disagree with the classify histogram");
+        if (!relabeled && hc[3]) {  // most reads were general: rerun on relabelled contigs
+            KARMA_TRY(relabel());
+            relabeled = true;
+            KARMA_TRY(launch());
+            continue;
+        }
         if (!hf[2]) break;
         KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "pair list capacity exceeded twice");
         attempt = 1;
@@ -1876,7 +2065,19 @@ int SetsJob::finish(karma_pairs* out) {
     KARMA_TRY(mk.alloc(ctx, U));
     KARMA_TRY(mc.alloc(ctx, U));
     KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, pk.ptr, pc.ptr, n_per, dst, mk.ptr, mc.ptr);
-    return finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out);
+    if (!relabeled) return finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out);
+    KARMA_TRY(finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out, remap_map.ptr));
+    // back to the original ids, sorted again (keys stay unique: the map is a bijection)
+    if (out->n) KARMA_LAUNCH(ctx, "relabel_back", relabel_back_kernel, grid_n(out->n), 256, 0, out->keys.ptr, out->n,
+                             remap_inv.ptr);
+    DevArray<uint64_t> k2;
+    DevArray<int64_t> c2;
+    int64_t n2 = 0;
+    KARMA_TRY(sort_reduce_pairs(ctx, out->keys.ptr, out->counts.ptr, nullptr, out->n, 64, k2, c2, nullptr, &n2));
+    out->keys.swap(k2);
+    out->counts.swap(c2);
+    out->n = n2;
+    return KARMA_OK;
 }
 
 int64_t sets_max_contigs() { return kMaxCompactN; }

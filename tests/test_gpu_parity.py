@@ -271,6 +271,21 @@ def test_records_big_reads_and_duplicates(n):
     check_records(np.array(rows, np.uint32), n)
 
 
+@pytest.mark.parametrize("n,nf", [(20_000, 400_000), (600_000, 1_000_000)])
+def test_records_shuffled_contig_ids_relabel(n, nf):
+    """Contig ids without isoform adjacency: most reads leave the compact path,
+    so the job relabels the contigs (graph_sets.hip relabel_gate_kernel) and
+    reruns on the new ids; reads of > 8 records and a contig-id shuffle of the
+    same records must give the oracle's result on the original ids."""
+    rec = np.ascontiguousarray(engine.synth_records(21, n, 0, nf, True))
+    perm = np.random.default_rng(3).permutation(n).astype(np.uint32)
+    rec[:, 1] = perm[rec[:, 1]]
+    rng = np.random.default_rng(4)
+    r0 = int(rec[-1, 0]) + 1
+    big = [(r0 + r, int(c)) for r in range(300) for c in rng.integers(0, n, int(rng.choice([9, 12, 30])))]
+    check_records(np.concatenate([rec, np.array(big, np.uint32)]), n)
+
+
 def test_records_empty_and_bad_contig():
     e = engine.graph_from_records(np.zeros((0, 2), np.uint32), 10)
     assert len(e.a) == 0 and e.totals.tolist() == [0] * 10
