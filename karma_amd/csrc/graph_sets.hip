@@ -303,7 +303,17 @@ classify2_kernel(ClassArgs P) {
     // the same: the walk already runs at ~5.7 TB/s of records + codes)
     // FULL: all 512 records of the step are inside the chunk (every step but a
     // chunk's last): no per-record validity tests
-    auto step = [&](auto full_tag, u32x4 (&buf)[kCPer], int64_t t0) {
+    // REMAP: the contigs of the step after next are relabelled here (gathers
+    // from the remap table into `nxt`, loaded a step earlier), a full step
+    // before they are used; `buf` then takes the records two steps ahead
+    auto remap_units = [&](u32x4 (&b)[kCPer]) {
+#pragma unroll
+        for (int u = 0; u < kCPer; ++u) {  // ids out of range stay out of range (the range check fails the call)
+            b[u].y = b[u].y < P.N ? P.remap[b[u].y] : b[u].y;
+            b[u].w = b[u].w < P.N ? P.remap[b[u].w] : b[u].w;
+        }
+    };
+    auto step = [&](auto full_tag, u32x4 (&buf)[kCPer], u32x4 (&nxt)[kCPer], int64_t t0) {
         constexpr bool FULL = decltype(full_tag)::value;
         uint32_t rid[8], ctg[8];
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
@@ -322,10 +332,11 @@ classify2_kernel(ClassArgs P) {
             ctg[2 * u + 1] = q.w;
         }
         wave_sync();
-        if (t0 + kCIter < c_hi) prefetch(buf, t0 + kCIter, c_hi);
-        if (REMAP) {  // ids out of range stay out of range (the range check fails the call)
-#pragma unroll
-            for (int i = 0; i < 8; ++i) ctg[i] = ctg[i] < P.N ? P.remap[ctg[i]] : ctg[i];
+        if (REMAP) {
+            if (t0 + kCIter < c_hi) remap_units(nxt);
+            if (t0 + 2 * kCIter < c_hi) prefetch(buf, t0 + 2 * kCIter, c_hi);
+        } else if (t0 + kCIter < c_hi) {
+            prefetch(buf, t0 + kCIter, c_hi);
         }
         // valid records of this lane (own reads start at a valid record)
         const int nval = FULL ? 8 : (int)max<int64_t>(0, min<int64_t>(8, c_hi - (t0 + 8 * lane)));
@@ -462,9 +473,24 @@ classify2_kernel(ClassArgs P) {
     };
     u32x4 buf[kCPer];
     prefetch(buf, c_lo, c_hi);
-    int64_t t0 = c_lo;
-    for (; t0 + kCIter <= c_hi; t0 += kCIter) step(std::true_type{}, buf, t0);
-    if (t0 < c_hi) step(std::false_type{}, buf, t0);
+    if (!REMAP) {
+        int64_t t0 = c_lo;
+        for (; t0 + kCIter <= c_hi; t0 += kCIter) step(std::true_type{}, buf, buf, t0);
+        if (t0 < c_hi) step(std::false_type{}, buf, buf, t0);
+    } else {  // two register sets, alternating
+        u32x4 buf2[kCPer];
+        if (c_lo + kCIter < c_hi) prefetch(buf2, c_lo + kCIter, c_hi);
+        remap_units(buf);
+        for (int64_t t0 = c_lo; t0 < c_hi;) {
+            if (t0 + kCIter <= c_hi) step(std::true_type{}, buf, buf2, t0);
+            else step(std::false_type{}, buf, buf2, t0);
+            t0 += kCIter;
+            if (t0 >= c_hi) break;
+            if (t0 + kCIter <= c_hi) step(std::true_type{}, buf2, buf, t0);
+            else step(std::false_type{}, buf2, buf, t0);
+            t0 += kCIter;
+        }
+    }
     // the chunk's last tail read continues into the next chunk's first records
     // (at most 8 of them matter): uniform scalar walk
     if (ct_ok) {
@@ -1965,10 +1991,10 @@ int SetsJob::relabel() {
     KARMA_TRY(size.alloc(ctx, N + 1));
     KARMA_TRY(base.alloc(ctx, N + 1));
     KARMA_LAUNCH(ctx, "relabel_iota", iota_u32_kernel, grid_n(N), 256, 0, rep.ptr, N);
-    // hooks from a sample of the reads (the records' first eighth, >= 4M
+    // hooks from a sample of the reads (the records' first 1/32, >= 4M
     // records): a gene's contigs join through a few of its reads, and a contig
-    // left out only keeps its reads on the general path
-    const int64_t As = std::min<int64_t>(A, std::max<int64_t>(A / 8, int64_t(1) << 22));
+    // left out only keeps its (few) reads on the general path
+    const int64_t As = std::min<int64_t>(A, std::max<int64_t>(A / 32, int64_t(1) << 22));
     if (As) KARMA_LAUNCH(ctx, "relabel_hook", relabel_hook_kernel, grid_n(As), 256, 0, rec, As, n, rep.ptr);
     KARMA_HIP(hipMemsetAsync(size.ptr, 0, (N + 1) * 8, ctx->stream));
     KARMA_HIP(hipMemsetAsync(fill.ptr, 0, N * 4, ctx->stream));

@@ -16,29 +16,33 @@ Usage: python tools/pmc_traffic.py pmc_summary.json out.json WORKLOAD_KEY [SOURC
 import json
 import sys
 
-# rocprof kernel name -> bench.py kernel (KARMA_LAUNCH) name
+# rocprof kernel name (template arguments dropped) -> bench.py kernel (KARMA_LAUNCH) name
 NAMES = {
     "classify_kernel": "graph_classify",
     "classify2_kernel": "graph_classify",
-    "classify2_kernel<false>": "graph_classify",
-    "classify2_kernel<true>": "graph_classify",
-    "code_append_kernel<512>": "graph_code_partition",
-    "code_append_kernel<128>": "graph_code_partition",
-    "partition_kernel<CodeStream>": "graph_code_partition",
-    "partition_kernel<CodeStreamT<128> >": "graph_code_partition",
+    "code_append_kernel": "graph_code_partition",
+    "partition_kernel<CodeStream": "graph_code_partition",
     "code_reduce_kernel": "graph_code_reduce",
-    "profile_kernel<true, true, true>": "kmer_profile",
-    "profile_wave_kernel<true, true>": "kmer_profile",
-    "presence_kernel<true>": "kmer_presence",
+    "profile_kernel": "kmer_profile",
+    "profile_wave_kernel": "kmer_profile",
+    "presence_kernel": "kmer_presence",
 }
+
+
+def bench_name(k):
+    base = k.split("<")[0]
+    if base == "partition_kernel":  # the pair partition is another kernel name in bench.py
+        return NAMES["partition_kernel<CodeStream"] if "CodeStream" in k else None
+    return NAMES.get(base)
 
 
 def main():
     src = json.load(open(sys.argv[1]))
     out = {}
     for k, v in src.items():
-        if k in NAMES and v.get("fetch_MB") == v.get("fetch_MB"):  # skip NaN
-            out[NAMES[k]] = int(round((2 * v["fetch_MB"] + v["write_MB"]) * 1024 * 1024))
+        name = bench_name(k)
+        if name and v.get("fetch_MB") == v.get("fetch_MB"):  # skip NaN
+            out[name] = int(round((2 * v["fetch_MB"] + v["write_MB"]) * 1024 * 1024))
     dst, key = sys.argv[2], sys.argv[3]
     try:
         allw = json.load(open(dst))
