@@ -119,40 +119,139 @@ __global__ void diag_totals_kernel(const uint64_t* __restrict__ keys, const int6
     }
 }
 
-__global__ void edge_flags_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, int64_t n,
-                                  int mode, int64_t* __restrict__ flags) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const uint64_t k = keys[i];
-        const bool diag = (uint32_t)(k >> 32) == (uint32_t)k;
-        flags[i] = (counts[i] != 0 && !(diag && mode == KARMA_MODE_READS)) ? 1 : 0;
+// ---- compaction in two launches ----------------------------------------------------
+// A count kernel writes each 1024-element block's number of kept elements; the
+// write kernel places block j at the sum of the counts before it (read by the
+// whole block: <= a few thousand words) and an element at that base plus its
+// rank among the block's kept elements (ballots, then the waves before).  No
+// scan launches, no host round trip.
+constexpr int kET = 1024;
+
+struct BlockPlace {
+    int64_t base;    // kept elements of the blocks before this one
+    int64_t rank;    // this thread's rank among the block's kept elements
+    int64_t total;   // kept elements of this block
+};
+
+__device__ __forceinline__ BlockPlace block_place(const int64_t* __restrict__ blk_cnt, bool keep) {
+    __shared__ int64_t wsum[kET / 64];
+    __shared__ int64_t base_s;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t b = 0;
+    for (int64_t j = threadIdx.x; j < (int64_t)blockIdx.x; j += kET) b += blk_cnt[j];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) b += __shfl_xor(b, d, 64);
+    if (lane == 0) wsum[wave] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+        for (int w = 0; w < kET / 64; ++w) t += wsum[w];
+        base_s = t;
     }
+    const uint64_t m = __ballot(keep);
+    const int64_t r = __popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();  // base_s is set; wsum is free again
+    if (lane == 0) wsum[wave] = __popcll(m);
+    __syncthreads();
+    BlockPlace p;
+    p.base = base_s;
+    p.rank = r;
+    p.total = 0;
+    for (int w = 0; w < kET / 64; ++w) {
+        if (w == wave) p.rank += p.total;
+        p.total += wsum[w];
+    }
+    return p;
 }
 
-__global__ void edge_write_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts,
-                                  const uint64_t* __restrict__ first, const int64_t* __restrict__ flags,
-                                  const int64_t* __restrict__ pos, int64_t n, const int64_t* __restrict__ totals,
-                                  uint32_t* __restrict__ ea, uint32_t* __restrict__ eb, int64_t* __restrict__ es,
-                                  double* __restrict__ ew, uint64_t* __restrict__ ef, int* __restrict__ zero_div) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !flags[i]) return;
-    const int64_t o = pos[i];
-    const uint64_t k = keys[i];
-    const uint32_t a = (uint32_t)(k >> 32), b = (uint32_t)k;
-    const int64_t s = counts[i], ta = totals[a], tb = totals[b];
+// The edge stage: edges_count_kernel flags the keys that are edges (count !=
+// 0; the diagonal is not an edge of the readset graph), writing the diagonal
+// totals on the way when the pair list owns them; edges_write_kernel writes
+// (a, b, s, w) of each edge at its place.
+__device__ __forceinline__ bool edge_flag(uint64_t k, int64_t c, int mode) {
+    const bool diag = (uint32_t)(k >> 32) == (uint32_t)k;
+    return c != 0 && !(diag && mode == KARMA_MODE_READS);
+}
+
+__global__ void __launch_bounds__(kET) edges_count_kernel(const uint64_t* __restrict__ keys,
+                                                          const int64_t* __restrict__ counts, int64_t n, int mode,
+                                                          int64_t* __restrict__ totals, int64_t* __restrict__ blk_cnt) {
+    const int64_t i = (int64_t)blockIdx.x * kET + threadIdx.x;
+    bool f = false;
+    if (i < n) {
+        const uint64_t k = keys[i];
+        const int64_t c = counts[i];
+        if (totals && (uint32_t)(k >> 32) == (uint32_t)k) totals[(uint32_t)k] = c;
+        f = edge_flag(k, c, mode);
+    }
+    const int cnt = __syncthreads_count(f);
+    if (threadIdx.x == 0) blk_cnt[blockIdx.x] = cnt;
+}
+
+__global__ void __launch_bounds__(kET) edges_write_kernel(
+    const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, const uint64_t* __restrict__ first,
+    int64_t n, int mode, const int64_t* __restrict__ totals, const int64_t* __restrict__ blk_cnt,
+    uint32_t* __restrict__ ea, uint32_t* __restrict__ eb, int64_t* __restrict__ es, double* __restrict__ ew,
+    uint64_t* __restrict__ ef, int64_t* __restrict__ st) {
+    const int64_t i = (int64_t)blockIdx.x * kET + threadIdx.x;
+    uint64_t k = 0;
+    int64_t c = 0;
+    bool f = false;
+    if (i < n) {
+        k = keys[i];
+        c = counts[i];
+        f = edge_flag(k, c, mode);
+    }
+    const BlockPlace pl = block_place(blk_cnt, f);
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) st[1] = pl.base + pl.total;  // the edge count
+    if (!f) return;
+    const int64_t o = pl.base + pl.rank;
+    const uint32_t a = (uint32_t)(k >> 32), bb = (uint32_t)k;
+    const int64_t ta = totals[a], tb = totals[bb];
     ea[o] = a;
-    eb[o] = b;
-    es[o] = s;
+    eb[o] = bb;
+    es[o] = c;
     if (ef) ef[o] = first[i];
     if (ta == 0 || tb == 0) {
-        *zero_div = 1;
+        reinterpret_cast<int*>(st)[0] = 1;
         ew[o] = 0.0;
         return;
     }
     // read_graph.py:39-42 / :128-130: ((s / tA) + (s / tB)) / 2, IEEE binary64, no FMA
-    const double x = __ddiv_rn((double)s, (double)ta);
-    const double y = __ddiv_rn((double)s, (double)tb);
+    const double x = __ddiv_rn((double)c, (double)ta);
+    const double y = __ddiv_rn((double)c, (double)tb);
     ew[o] = __dadd_rn(x, y) * 0.5;
+}
+
+// Sum of the counts of equal adjacent keys (a merged list: a key occurs at
+// most once per run): the first of each group is kept and sums its group.
+__global__ void __launch_bounds__(kET) group_count_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                          int64_t* __restrict__ blk_cnt) {
+    const int64_t i = (int64_t)blockIdx.x * kET + threadIdx.x;
+    const bool head = i < n && (i == 0 || keys[i] != keys[i - 1]);
+    const int cnt = __syncthreads_count(head);
+    if (threadIdx.x == 0) blk_cnt[blockIdx.x] = cnt;
+}
+
+__global__ void __launch_bounds__(kET) group_sum_kernel(const uint64_t* __restrict__ keys,
+                                                        const int64_t* __restrict__ counts, int64_t n,
+                                                        const int64_t* __restrict__ blk_cnt,
+                                                        uint64_t* __restrict__ ko, int64_t* __restrict__ co,
+                                                        int64_t* __restrict__ n_out) {
+    const int64_t i = (int64_t)blockIdx.x * kET + threadIdx.x;
+    uint64_t k = 0;
+    bool head = false;
+    if (i < n) {
+        k = keys[i];
+        head = i == 0 || keys[i - 1] != k;
+    }
+    const BlockPlace pl = block_place(blk_cnt, head);
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_out = pl.base + pl.total;
+    if (!head) return;
+    int64_t c = counts[i];
+    for (int64_t j = i + 1; j < n && keys[j] == k; ++j) c += counts[j];
+    ko[pl.base + pl.rank] = k;
+    co[pl.base + pl.rank] = c;
 }
 
 int scan_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
@@ -240,11 +339,14 @@ __global__ void runs_check_kernel(const uint64_t* __restrict__ k, int64_t n, con
 // count is a short search inside it.  The same pass flags a descent inside a
 // run.  Replaces a merge tree of W - 1 pairwise merges (2 launches each).
 constexpr int kMergeMaxRuns = 64;
-constexpr int kMergeTile = 1024;     // elements per block (4 per thread)
 constexpr int kMergeLds = 6144;      // staged window keys per block (48 KB)
+// elements per block (4 per thread).  A window that does not fit the stage is
+// searched in global memory; halving the tile so that 8 runs' windows fit
+// measured slower (0.103 vs 0.076 ms for 1.6M pairs: twice the window searches)
+constexpr int kMergeTile = 1024;
 struct RunOffs {
     int64_t o[kMergeMaxRuns + 1];    // run offsets
-    int64_t t[kMergeMaxRuns + 1];    // first tile of each run (prefix of ceil(len / kMergeTile))
+    int64_t t[kMergeMaxRuns + 1];    // first tile of each run (prefix of ceil(len / tile))
 };
 
 // number of elements of sorted run [lo, hi) preceding key k (<= k when le, else < k)
@@ -261,35 +363,53 @@ __device__ __forceinline__ int64_t count_before(KeyAt key_at, int64_t lo, int64_
     return base;
 }
 
+// The window bounds of every (tile, other run): one thread per bound, all in
+// one round (searched inside merge_rank_kernel, 14 dependent binary searches
+// per block made each block a chain of global-load latencies; beside the
+// profile kernel, with few free CU slots, 1.6M pairs took 0.28 ms).
+__device__ __forceinline__ int tile_run(const RunOffs& R, int nr, int64_t tile) {
+    int lo = 0, hi = nr - 1;  // the last run r with R.t[r] <= tile
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (R.t[mid] <= tile) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) merge_bounds_kernel(const uint64_t* __restrict__ keys,
+                                                           const longlong2* __restrict__ kc, RunOffs R, int nr,
+                                                           int64_t tiles, int64_t* __restrict__ wb) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= tiles * nr * 2) return;
+    auto key_at = [&](int64_t i) -> uint64_t { return kc ? (uint64_t)kc[i].x : keys[i]; };
+    const int64_t tile = q / (2 * nr);
+    const int sr = (int)((q >> 1) % nr);
+    const int r = tile_run(R, nr, tile);
+    if (sr == r) return;
+    const int64_t t0 = R.o[r] + (tile - R.t[r]) * kMergeTile;
+    const int64_t t1 = min(R.o[r + 1], t0 + kMergeTile);
+    const uint64_t k = key_at((q & 1) ? t1 - 1 : t0);
+    wb[q] = count_before(key_at, R.o[sr], R.o[sr + 1], k, sr < r);
+}
+
 __global__ void __launch_bounds__(256) merge_rank_kernel(const uint64_t* __restrict__ keys,
                                                          const int64_t* __restrict__ counts,
                                                          const longlong2* __restrict__ kc, RunOffs R, int nr,
-                                                         uint64_t* __restrict__ ko, int64_t* __restrict__ co,
-                                                         int64_t* __restrict__ bad) {
+                                                         const int64_t* __restrict__ wb, uint64_t* __restrict__ ko,
+                                                         int64_t* __restrict__ co, int64_t* __restrict__ bad) {
     __shared__ int64_t wlo[kMergeMaxRuns], whi[kMergeMaxRuns];  // window of run s: [wlo, whi] (counts)
     __shared__ int wbase[kMergeMaxRuns];                        // its LDS slot (-1: searched in place)
     __shared__ uint64_t wkeys[kMergeLds];
-    __shared__ int r_s;
     auto key_at = [&](int64_t i) -> uint64_t { return kc ? (uint64_t)kc[i].x : keys[i]; };
     const int64_t tile = blockIdx.x;
-    if (threadIdx.x == 0) {
-        int r = 0;
-        while (r + 1 < nr && R.t[r + 1] <= tile) ++r;
-        r_s = r;
-    }
-    __syncthreads();
-    const int r = r_s;
+    const int r = tile_run(R, nr, tile);
     const int64_t t0 = R.o[r] + (tile - R.t[r]) * kMergeTile;
     const int64_t t1 = min(R.o[r + 1], t0 + kMergeTile);
-    // window bounds: thread 2s searches for the tile's first key, 2s + 1 for its last
-    if (threadIdx.x < 2 * nr) {
-        const int sr = threadIdx.x >> 1;
-        if (sr != r) {
-            const uint64_t k = key_at((threadIdx.x & 1) ? t1 - 1 : t0);
-            const int64_t c = count_before(key_at, R.o[sr], R.o[sr + 1], k, sr < r);
-            if (threadIdx.x & 1) whi[sr] = c;
-            else wlo[sr] = c;
-        }
+    if (threadIdx.x < 2 * nr && (threadIdx.x >> 1) != r) {
+        const int64_t c = wb[tile * nr * 2 + threadIdx.x];
+        if (threadIdx.x & 1) whi[threadIdx.x >> 1] = c;
+        else wlo[threadIdx.x >> 1] = c;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -631,10 +751,12 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
         sk = kb[1].ptr;
         sc = cb[1].ptr;
     }
-    // st: [0] unique keys (ReduceByKey's run count), [1] order violation
-    DevArray<int64_t> st;
-    KARMA_TRY(st.alloc(ctx, 2));
-    KARMA_HIP(hipMemsetAsync(st.ptr, 0, 16, ctx->stream));
+    // st (mapped host memory, written by the kernels): [0] unique keys
+    // (ReduceByKey's run count), [1] order violation
+    void *hst = nullptr, *dst_ = nullptr;
+    KARMA_TRY(ctx_mapped(ctx, 16, &hst, &dst_));
+    std::memset(hst, 0, 16);
+    int64_t* const st = static_cast<int64_t*>(dst_);
     void* hpin = nullptr;
     KARMA_TRY(ctx_pinned(ctx, std::max<size_t>(16, (n_runs + 1) * 8), &hpin));
     if (n_runs <= kMergeMaxRuns) {
@@ -649,9 +771,14 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
             tiles += ceil_div(off[r + 1] - off[r], kMergeTile);
         }
         R.t[n_runs] = tiles;
-        if (tiles)
+        if (tiles) {
+            DevArray<int64_t> wb;
+            KARMA_TRY(wb.alloc(ctx, tiles * n_runs * 2));
+            KARMA_LAUNCH(ctx, "merge_bounds", merge_bounds_kernel, grid1(tiles * n_runs * 2), 256, 0, sk,
+                         reinterpret_cast<const longlong2*>(kc), R, n_runs, tiles, wb.ptr);
             KARMA_LAUNCH(ctx, "merge_rank", merge_rank_kernel, tiles, 256, 0, sk, sc,
-                         reinterpret_cast<const longlong2*>(kc), R, n_runs, kb[0].ptr, cb[0].ptr, st.ptr + 1);
+                         reinterpret_cast<const longlong2*>(kc), R, n_runs, wb.ptr, kb[0].ptr, cb[0].ptr, st + 1);
+        }
         sk = kb[0].ptr;
         sc = cb[0].ptr;
     } else {
@@ -669,7 +796,7 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
         KARMA_HIP(hipMemcpyAsync(doff.ptr, hpin, (n_runs + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
         if (n > 1)
             KARMA_LAUNCH(ctx, "runs_check", runs_check_kernel, std::min<int64_t>(grid1(n), 4096), 256, 0, sk, n, doff.ptr,
-                         n_runs, st.ptr + 1);
+                         n_runs, st + 1);
         // pairwise merge tree over the runs (rocprim merge path), ping-pong buffers
         if (n_runs > 1 && n) {
             size_t need = 0;
@@ -724,17 +851,15 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
     KARMA_TRY(p->keys.alloc(ctx, n));
     KARMA_TRY(p->counts.alloc(ctx, n));
     if (n) {
-        size_t tb = 0;
-        KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, sk, p->keys.ptr, sc, p->counts.ptr, st.ptr,
-                                                    hipcub::Sum(), (int)n, ctx->stream));
-        DevArray<uint8_t> tmp;
-        KARMA_TRY(tmp.alloc(ctx, tb));
-        KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(tmp.ptr, tb, sk, p->keys.ptr, sc, p->counts.ptr, st.ptr,
-                                                    hipcub::Sum(), (int)n, ctx->stream));
+        const int64_t nb = ceil_div(n, kET);
+        DevArray<int64_t> blk;
+        KARMA_TRY(blk.alloc(ctx, nb));
+        KARMA_LAUNCH(ctx, "merge_groups", group_count_kernel, nb, kET, 0, sk, n, blk.ptr);
+        KARMA_LAUNCH(ctx, "merge_sum", group_sum_kernel, nb, kET, 0, sk, sc, n, blk.ptr, p->keys.ptr, p->counts.ptr,
+                     st);
     }
-    KARMA_HIP(hipMemcpyAsync(hpin, st.ptr, 16, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    const int64_t* h = static_cast<const int64_t*>(hpin);
+    const volatile int64_t* h = static_cast<const volatile int64_t*>(hst);
     KARMA_CHECK(!h[1], KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
     p->n = h[0];
     *out = guard.release();
@@ -806,17 +931,16 @@ int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t
     KARMA_CHECK(p && bounds && starts && nranks >= 1, KARMA_ERR_ARG, "bad arguments");
     karma_ctx* ctx = p->ctx;
     KARMA_TRY(ctx_begin(ctx));
-    // binary searches on the device: only the nranks + 1 starts cross PCIe
+    // binary searches on the device; bounds and starts live in mapped host
+    // memory (no copy launches: beside a running profile kernel those waited
+    // for free CUs, 0.24 ms in the 8-rank emulation)
     const int nb = nranks + 1;
-    DevArray<int64_t> d;
-    KARMA_TRY(d.alloc(ctx, 2 * nb));
-    void* hpin = nullptr;
-    KARMA_TRY(ctx_pinned(ctx, 2 * nb * 8, &hpin));
-    int64_t* h = static_cast<int64_t*>(hpin);
+    void *hb = nullptr, *db = nullptr;
+    KARMA_TRY(ctx_mapped(ctx, 2 * nb * 8, &hb, &db));
+    int64_t* h = static_cast<int64_t*>(hb);
+    int64_t* d = static_cast<int64_t*>(db);
     std::memcpy(h, bounds, nb * 8);
-    KARMA_HIP(hipMemcpyAsync(d.ptr, h, nb * 8, hipMemcpyHostToDevice, ctx->stream));
-    KARMA_LAUNCH(ctx, "pairs_split", split_kernel, grid1(nb, 64), 64, 0, p->keys.ptr, p->n, d.ptr, nb, d.ptr + nb);
-    KARMA_HIP(hipMemcpyAsync(h + nb, d.ptr + nb, nb * 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_LAUNCH(ctx, "pairs_split", split_kernel, grid1(nb, 64), 64, 0, p->keys.ptr, p->n, d, nb, d + nb);
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
     std::memcpy(starts, h + nb, nb * 8);
     return KARMA_OK;
@@ -844,43 +968,44 @@ int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64
     std::unique_ptr<karma_edges> guard(e);
     KARMA_TRY(e->totals.alloc(ctx, N));
     const int64_t* tot = totals_dev;
+    bool diag_here = false;
     if (!tot) {
         if (mode == KARMA_MODE_EQ) {
             KARMA_CHECK(p->has_totals && p->n_contigs == N, KARMA_ERR_STATE, "eq pair list without totals");
             if (N) KARMA_HIP(hipMemcpyAsync(e->totals.ptr, p->totals.ptr, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        } else {
-            KARMA_TRY(karma_pairs_totals(p, e->totals.ptr, N));
+        } else {  // the diagonal counts, written by the edge count kernel
+            if (N) KARMA_HIP(hipMemsetAsync(e->totals.ptr, 0, N * 8, ctx->stream));
+            diag_here = true;
         }
     } else if (N) {
         KARMA_HIP(hipMemcpyAsync(e->totals.ptr, tot, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
     }
     const int64_t n = p->n;
-    DevArray<int64_t> flags, pos, st;  // st: 0 zero-division flag, 1 edge count
-    KARMA_TRY(flags.alloc(ctx, n + 1));
-    KARMA_TRY(pos.alloc(ctx, n + 1));
-    KARMA_TRY(st.alloc(ctx, 2));
-    KARMA_HIP(hipMemsetAsync(st.ptr, 0, 16, ctx->stream));
-    KARMA_HIP(hipMemsetAsync(flags.ptr + n, 0, 8, ctx->stream));
-    if (n) KARMA_LAUNCH(ctx, "edge_flags", edge_flags_kernel, grid1(n), 256, 0, p->keys.ptr, p->counts.ptr, n, mode, flags.ptr);
-    KARMA_TRY(scan_i64(ctx, flags.ptr, pos.ptr, n + 1));
-    // edges <= pairs: write them before the count is known on the host
+    DevArray<int64_t> blk;
+    const int64_t nb = std::max<int64_t>(1, ceil_div(n, kET));
+    KARMA_TRY(blk.alloc(ctx, nb));
+    // st (mapped host memory, written by the last kernel): 0 zero-division flag, 1 edge count
+    void *hst = nullptr, *dst_ = nullptr;
+    KARMA_TRY(ctx_mapped(ctx, 16, &hst, &dst_));
+    std::memset(hst, 0, 16);
+    int64_t* const st = static_cast<int64_t*>(dst_);
+    // edges <= pairs: written before the count is known on the host
     KARMA_TRY(e->a.alloc(ctx, n));
     KARMA_TRY(e->b.alloc(ctx, n));
     KARMA_TRY(e->s.alloc(ctx, n));
     KARMA_TRY(e->w.alloc(ctx, n));
     e->has_first = p->has_first;
     if (e->has_first) KARMA_TRY(e->first.alloc(ctx, n));
-    if (n)
-        KARMA_LAUNCH(ctx, "edge_weights", edge_write_kernel, grid1(n), 256, 0, p->keys.ptr, p->counts.ptr,
-                     p->has_first ? p->first.ptr : (const uint64_t*)nullptr, flags.ptr, pos.ptr, n, e->totals.ptr,
+    if (n) {
+        KARMA_LAUNCH(ctx, "edge_count", edges_count_kernel, nb, kET, 0, p->keys.ptr, p->counts.ptr, n, mode,
+                     diag_here ? e->totals.ptr : (int64_t*)nullptr, blk.ptr);
+        KARMA_LAUNCH(ctx, "edge_weights", edges_write_kernel, nb, kET, 0, p->keys.ptr, p->counts.ptr,
+                     p->has_first ? p->first.ptr : (const uint64_t*)nullptr, n, mode, e->totals.ptr, blk.ptr,
                      e->a.ptr, e->b.ptr, e->s.ptr, e->w.ptr, e->has_first ? e->first.ptr : (uint64_t*)nullptr,
-                     reinterpret_cast<int*>(st.ptr));
-    KARMA_HIP(hipMemcpyAsync(st.ptr + 1, pos.ptr + n, 8, hipMemcpyDeviceToDevice, ctx->stream));
-    void* hpin = nullptr;
-    KARMA_TRY(ctx_pinned(ctx, 16, &hpin));
-    KARMA_HIP(hipMemcpyAsync(hpin, st.ptr, 16, hipMemcpyDeviceToHost, ctx->stream));
+                     st);
+    }
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    const int64_t* hs = static_cast<const int64_t*>(hpin);
+    const volatile int64_t* hs = static_cast<const volatile int64_t*>(hst);
     KARMA_CHECK(!(int)hs[0], KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
     const int64_t E = hs[1];
     e->E = E;

@@ -474,6 +474,14 @@ constexpr int kWaveMaxM = 4096;
 #define KARMA_PROF_C16 1
 #endif
 typedef double d2 __attribute__((ext_vector_type(2)));
+#ifndef KARMA_PROF_NT
+#define KARMA_PROF_NT 1  // profile rows written with non-temporal stores
+#endif
+template <typename T>
+__device__ __forceinline__ void row_store(T v, T* p) {
+    if (KARMA_PROF_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 template <bool P56, typename Add>
 __device__ __forceinline__ void count_contig(const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask,
@@ -638,13 +646,13 @@ __device__ __forceinline__ void write_row_wave(double* __restrict__ row, uint32_
             d2 v;
             v.x = val(a);
             v.y = val(b);
-            __builtin_nontemporal_store(v, reinterpret_cast<d2*>(row) + j);
+            row_store(v, reinterpret_cast<d2*>(row) + j);
         }
         if ((M & 1) && lane == 0) {
             const uint32_t a = C16 ? counts[M >> 1] & 0xFFFFu : counts[M - 1];
             counts[C16 ? M >> 1 : M - 1] = 0;
             if (a && klen == 0) *err = 1;
-            __builtin_nontemporal_store(val(a), row + M - 1);
+            row_store(val(a), row + M - 1);
         }
     } else {
         uint16_t* c16 = reinterpret_cast<uint16_t*>(counts);
@@ -653,7 +661,7 @@ __device__ __forceinline__ void write_row_wave(double* __restrict__ row, uint32_
             if (C16) c16[j] = 0;
             else counts[j] = 0;
             if (a && klen == 0) *err = 1;
-            __builtin_nontemporal_store(val(a), row + j);
+            row_store(val(a), row + j);
         }
     }
 }

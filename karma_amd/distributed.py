@@ -148,8 +148,7 @@ class HipOps:
 
     def totals(self, pairs, n_contigs):
         tot = DevBuf(self.ctx, (n_contigs,), np.int64)
-        _lib.call("karma_memset_async", self.ctx.h, _lib.ctypes.c_void_p(tot.ptr), 0, tot.nbytes)
-        pairs.totals_device(tot.ptr, n_contigs)
+        pairs.totals_device(tot.ptr, n_contigs)  # zeroes, then the diagonal
         return tot
 
     def edges(self, pairs, n_contigs, totals=None):
