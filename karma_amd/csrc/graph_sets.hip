@@ -649,6 +649,25 @@ struct RunDir {
     const unsigned long long* blk_items;  // per partition block: items (from the producers)
 };
 
+// A buffer resource over [base, base + bytes) from block-uniform values (read
+// from the first lane), for stores whose out-of-range lanes are dropped.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t u = (uint64_t)base;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u)),
+        0, (int)(uint32_t)__builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
+}
+
+// N vector stores that the range check drops (an empty buffer resource;
+// volatile, so none is merged away)
+template <int N>
+__device__ __forceinline__ void dropped_stores() {
+    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0x00020000);
+#pragma unroll
+    for (int t = 0; t < N; ++t) __builtin_amdgcn_raw_buffer_store_b32(0u, none, 4 * t, 0, 1 << 31);
+}
+
 // A partition block's items (blk_items, summed by the producers), flushes
 // (every flush but the last holds cap items) and an output bound (items + <
 // pad per run): the bases of block b are these sums over blocks < b, so each
@@ -667,6 +686,8 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
     using S = typename T::S;
     using D = typename T::D;
     constexpr int kPer = T::kCap / kPT;  // items per thread per fill
+    constexpr int kVMax = (T::kCap + T::kMaxNb * (T::kPad - 1)) * (int)sizeof(D) / 16;  // vectors per flush, at most
+    constexpr int kCopyIt = (kVMax + kPT - 1) / kPT;
     __shared__ S buf[T::kCap];
     __shared__ D sorted[T::kCap + T::kMaxNb * (T::kPad - 1)];
     __shared__ uint32_t hist[2][T::kMaxNb + 1];  // by fill parity: reset while the other fills
@@ -747,6 +768,9 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
         }
     };
     load(0);
+    // every path into the flush loop has kCopyIt stores after the fill's loads
+    // (here dropped ones), so the loop's wait for a fill stays vmcnt(kCopyIt)
+    dropped_stores<kCopyIt>();
     int parity = 0;
     // a thread scatters the items it counted (its own slots of the fill),
     // staged in LDS across the flush's barriers while v takes the next
@@ -802,10 +826,19 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
         // h and cur are free: the next fill may start once this block's
         // 16-byte stores are issued (their completion is never waited for)
         for (int b = threadIdx.x; b < nb; b += kPT) h[b] = 0;
-        u32x4* dst = reinterpret_cast<u32x4*>(out + at);
-        const u32x4* src = reinterpret_cast<const u32x4*>(sorted);
+        // copy-out: a fixed number of 16-byte buffer stores per thread, the
+        // range check dropping those past the flush.  vmcnt counts loads and
+        // stores together, in issue order: with a runtime-length copy loop the
+        // next fill's wait for its (earlier) loads was vmcnt(0) and drained
+        // this flush's stores; with a fixed count it is vmcnt(kCopyIt).
         const uint32_t nv = total * (uint32_t)sizeof(D) / 16u;
-        for (uint32_t i = threadIdx.x; i < nv; i += kPT) dst[i] = src[i];
+        const __amdgpu_buffer_rsrc_t drs = uniform_rsrc(out + at, nv * 16u);
+        const u32x4* src = reinterpret_cast<const u32x4*>(sorted);
+#pragma unroll
+        for (int r = 0; r < kCopyIt; ++r) {
+            const uint32_t i = threadIdx.x + r * kPT;
+            __builtin_amdgcn_raw_buffer_store_b128(src[min(i, (uint32_t)kVMax - 1u)], drs, (int)(i * 16u), 0, 0);
+        }
     }
 }
 
