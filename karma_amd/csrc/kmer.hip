@@ -76,7 +76,6 @@ constexpr int kPBlock = 512;  // profile: 8 waves share one LDS column table
 constexpr int kPadWords = 80;    // zero words after the store (stages may read past the last contig)
 
 // ---------------------------------------------------------------- pack -------
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4a __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-byte load
 
 // One wave per contig (grid-stride over contigs), lane l packs word w = l + 64t:
@@ -475,9 +474,6 @@ constexpr int kWaveMaxM = 4096;
 #define KARMA_PROF_C16 1
 #endif
 typedef double d2 __attribute__((ext_vector_type(2)));
-#ifndef KARMA_PROF_FIX
-#define KARMA_PROF_FIX 1  // write_row_fixed for the 5p6 rows (0: the runtime-length loop everywhere)
-#endif
 #ifndef KARMA_PROF_ABLATE
 #define KARMA_PROF_ABLATE 0  // diagnostic builds only (tools/build_variant.sh): 1 rows only, 2 counting only
 #endif
@@ -686,93 +682,6 @@ __device__ __forceinline__ unsigned wave_total(unsigned x) {
     return (unsigned)__builtin_amdgcn_readlane((int)x, 63);
 }
 
-// write_row_wave for the common 5p6 shape (M <= 2 * 64 * kFixT columns, M even,
-// 16-byte aligned rows): every row issues exactly kFixT + 2 vector stores --
-// its kFixT 16-byte row stores, the row total and the error flag -- as buffer
-// stores whose lanes without data get an out-of-range offset (dropped by the
-// range check).  vmcnt counts loads and stores together, in issue order; with a
-// fixed store count per row the compiler waits for the next contig's
-// prefetched words with vmcnt(kFixT + 2) instead of vmcnt(0), so a wave no
-// longer drains its row's stores before it counts the next contig (the
-// runtime-length loop forced vmcnt(0): 0.342 ms for the rows alone, against
-// 0.26 ms for bare 8.7 KB row writes on this chip).
-constexpr int kFixT = 9;
-constexpr int kFixMaxM = 2 * 64 * kFixT;  // 1152 >= the 1088 columns of 5p6 plus a few exception k-mers
-constexpr int kBufWord3 = 0x00020000;    // buffer resource flags (raw, dword-granular range check)
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* base, uint32_t bytes) {
-    const uint64_t u = (uint64_t)base;
-    return __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
-                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u)),
-        0, bytes, kBufWord3);
-}
-
-// N vector stores that the range check drops (an empty buffer resource)
-template <int N>
-__device__ __forceinline__ void dropped_stores() {
-    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, kBufWord3);
-#pragma unroll
-    for (int t = 0; t < N; ++t) __builtin_amdgcn_raw_buffer_store_b32(0u, none, 4 * t, 0, 1 << 31);  // volatile: kept
-}
-
-template <bool C16>
-__device__ __forceinline__ void write_row_fixed(double* __restrict__ row, uint32_t* __restrict__ counts, int M,
-                                                int32_t klen, int* __restrict__ err, double* __restrict__ lut,
-                                                int lane, int64_t* __restrict__ row_tot, int64_t c, int64_t n,
-                                                unsigned my) {
-    constexpr uint32_t kOut = 0x80000000u;  // past every range: the store is dropped
-    constexpr int kNT = 2;                  // slc: non-temporal on gfx950
-    const double len = (double)klen;
-    lut[lane] = lane ? (double)lane / len : 0.0;  // IEEE correctly rounded (kmer.py:120)
-    wave_lds_sync();
-    auto val = [&](uint32_t a) {
-        double v = lut[min(a, 63u)];
-        if (a >= 64u) v = (double)a / len;
-        return v;
-    };
-    const int M2 = M >> 1;
-    // the row's range is its M * 8 bytes: the lanes past the row are out of it
-    const __amdgpu_buffer_rsrc_t rr = wave_rsrc(row, (uint32_t)M * 8u);
-    // lane's first offset, opaque to loop-invariant code motion (nine hoisted
-    // offsets stayed live across the contig loop and spilled)
-    uint32_t off0 = (uint32_t)lane * 16u;
-    asm volatile("" : "+v"(off0));
-    bool bad = false;
-#pragma unroll
-    for (int t = 0; t < kFixT; ++t) {
-        const int j = lane + 64 * t;
-        const bool in = j < M2;
-        uint32_t a = 0, b = 0;
-        if (in) {
-            if (C16) {
-                const uint32_t ab = counts[j];
-                counts[j] = 0;
-                a = ab & 0xFFFFu;
-                b = ab >> 16;
-            } else {
-                const uint2 ab = reinterpret_cast<uint2*>(counts)[j];
-                reinterpret_cast<uint2*>(counts)[j] = make_uint2(0u, 0u);
-                a = ab.x;
-                b = ab.y;
-            }
-        }
-        bad |= (a | b) && klen == 0;
-        const double x = val(a), y = val(b);
-        const u32x4 v = {(uint32_t)__double2loint(x), (uint32_t)__double2hiint(x), (uint32_t)__double2loint(y),
-                         (uint32_t)__double2hiint(y)};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rr, (int)(off0 + 1024u * t), 0, kNT);
-    }
-    // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
-    const __amdgpu_buffer_rsrc_t rt = wave_rsrc(row_tot, (uint32_t)(n * 8));
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    const u32x2 mv = {my, 0u};
-    __builtin_amdgcn_raw_buffer_store_b64(mv, rt, (int)(lane == 0 ? (uint32_t)c * 8u : kOut), 0, 0);
-    const bool any_bad = __ballot(bad) != 0;
-    const __amdgpu_buffer_rsrc_t re = wave_rsrc(err, 4u);
-    __builtin_amdgcn_raw_buffer_store_b32(1u, re, (int)(lane == 0 && any_bad ? 0u : kOut), 0, 0);
-}
-
 // u32 slots of a wave's histogram
 __host__ __device__ constexpr int64_t hist_words(int64_t M, bool c16) {
     return c16 ? (((M + 1) >> 1) + 3) & ~int64_t(3) : (M + 3) & ~int64_t(3);
@@ -780,7 +689,7 @@ __host__ __device__ constexpr int64_t hist_words(int64_t M, bool c16) {
 // column-table entries (u16) in LDS
 __host__ __device__ constexpr int64_t tab_entries(bool p56, uint32_t S) { return p56 ? 1088 : (int64_t)S; }
 
-template <bool P56, bool C16, bool FIX>
+template <bool P56, bool C16>
 // 8 waves per SIMD (4 blocks per CU with u16 counters)
 #ifndef KARMA_PROF_WAVES
 #define KARMA_PROF_WAVES 8
@@ -791,8 +700,7 @@ profile_wave_kernel(
     const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
     const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
     const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
-    double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
-    const uint32_t* __restrict__ list, const unsigned* __restrict__ list_n) {
+    double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     // wave index in an SGPR: contig offsets and lengths load with scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
@@ -823,45 +731,34 @@ profile_wave_kernel(
     // software pipeline over this wave's contigs: the next contig's offsets
     // load at the top of the current one, and its first stage of packed
     // words before the current row is written
-    // items: every contig, or (list) the contigs list[0 .. *list_n)
     struct Meta {
-        int64_t c = 0, s = 0, L = 0, w0 = 0;
+        int64_t s = 0, L = 0, w0 = 0;
         int32_t klen = 0;
         bool exc = false;
     };
-    const int64_t n_items = list ? (int64_t)*list_n : n;
-    auto meta = [&](int64_t i, Meta& m) {
-        if (i < n_items) {
-            const int64_t cc = list ? (int64_t)list[i] : i;
-            m.c = cc;
+    auto meta = [&](int64_t cc, Meta& m) {
+        if (cc < n) {
             m.s = off[cc];
             m.L = off[cc + 1] - m.s;
             m.w0 = woff[cc];
             m.klen = keylen[cc];
             // the flag byte from its dword by a scalar load (a byte load is a
-            // vector load, and its wait would drain the previous row's stores)
+            // vector load, whose wait also drains the previous row's stores)
             const uint32_t hw = reinterpret_cast<const uint32_t*>(has_exc)[cc >> 2];
             m.exc = ((hw >> (8 * (cc & 3))) & 0xFFu) != 0;
         }
     };
     const int64_t stride = (int64_t)gridDim.x * wpb;
-    int64_t i = (int64_t)blockIdx.x * wpb + wave;
+    int64_t c = (int64_t)blockIdx.x * wpb + wave;
     Meta cur, nxt;
     Stage st0;
-    meta(i, cur);
-    // FIX: contigs with exception bases are left to a second launch over the
-    // exception list, so this loop's only loads are the prefetched words
-    if (i < n_items) st0.load(packed, mask, FIX ? false : cur.exc, cur.w0, lane);
-    // FIX: every path into the loop head has issued kFixT + 2 stores since the
-    // last prefetch (here: dropped ones), so its wait stays vmcnt(kFixT + 2)
-    if (FIX) dropped_stores<kFixT + 2>();
-    for (; i < n_items; i += stride) {
-        meta(i + stride, nxt);
-        const int64_t c = cur.c;
+    meta(c, cur);
+    if (c < n) st0.load(packed, mask, cur.exc, cur.w0, lane);
+    for (; c < n; c += stride) {
+        meta(c + stride, nxt);
         const int64_t L = cur.L;
         unsigned my = 0;
-        if (KARMA_PROF_ABLATE == 1 || (FIX && cur.exc)) {
-            // ablation: rows only; FIX: a zero row now, the exception launch writes it
+        if (KARMA_PROF_ABLATE == 1) {  // diagnostic build: rows only, no counting
         } else if (!cur.exc) {
             count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
         } else {
@@ -891,20 +788,15 @@ profile_wave_kernel(
                 }
             }, &st0);
         }
-        if (i + stride < n_items) st0.load(packed, mask, FIX ? false : nxt.exc, nxt.w0, lane);
-        asm volatile("" ::: "memory");  // the prefetch stays ahead of the row's stores
+        if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
         // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
         my = wave_total(my);
 #if KARMA_PROF_ABLATE == 2  // diagnostic build: counting only, no rows
         if (lane == 0) row_tot[c] = (int64_t)my;
         for (int j = lane; j < h_words; j += 64) counts[j] = 0;
 #else
-        if (FIX) {
-            write_row_fixed<C16>(out + c * ld, counts, (int)M, cur.klen, err, lut, lane, row_tot, c, n, my);
-        } else {
-            if (lane == 0) row_tot[c] = (int64_t)my;
-            write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
-        }
+        if (lane == 0) row_tot[c] = (int64_t)my;
+        write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
 #endif
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1362,35 +1254,21 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
         const bool c16 = KARMA_PROF_C16 && c->max_len < 65536;
         const size_t lds = (size_t)((tab_entries(p56, p->S) + 7) & ~7) * 2 +
                            (kPBlock / 64) * (size_t)(hist_words(M, c16) + kProfWin) * 4;
-#define KARMA_WAVE_LAUNCH(P56, C16, FIX)                                                                         \
+#define KARMA_WAVE_LAUNCH(P56, C16)                                                                              \
     do {                                                                                                         \
-        const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_wave_kernel<P56, C16, FIX>),     \
-                                     kPBlock, lds, ceil_div(n, kPBlock / 64));                                   \
-        KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16, FIX>), g_, kPBlock, lds, c->packed.ptr, \
+        const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_wave_kernel<P56, C16>), kPBlock, \
+                                     lds, ceil_div(n, kPBlock / 64));                                            \
+        KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16>), g_, kPBlock, lds, c->packed.ptr,      \
                      c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len,        \
                      p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err,       \
-                     (int)p->S, p->row_tot.ptr, (const uint32_t*)nullptr, (const unsigned*)nullptr);             \
-        if (FIX) /* the contigs with exception bases */                                                          \
-            KARMA_LAUNCH(ctx, "kmer_profile_exc", (profile_wave_kernel<P56, C16, false>), g_, kPBlock, lds,       \
-                         c->packed.ptr, c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n,   \
-                         k, with_len, p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, \
-                         err, (int)p->S, p->row_tot.ptr, (const uint32_t*)c->exc_list.ptr,                        \
-                         (const unsigned*)c->exc_n.ptr);                                                          \
+                     (int)p->S, p->row_tot.ptr);                                                                 \
     } while (0)
-        // fixed store count per row (write_row_fixed): 5p6, M even and <= kFixMaxM, 16-byte aligned rows
-        const bool fix = p56 && KARMA_PROF_FIX && (M & 1) == 0 && M <= kFixMaxM && (ld & 1) == 0 &&
-                         (reinterpret_cast<uintptr_t>(dst) & 15) == 0 && n * 8 < (int64_t(1) << 31);
         if (p56) {
-            if (fix) {
-                if (c16) KARMA_WAVE_LAUNCH(true, true, true);
-                else KARMA_WAVE_LAUNCH(true, false, true);
-            } else {
-                if (c16) KARMA_WAVE_LAUNCH(true, true, false);
-                else KARMA_WAVE_LAUNCH(true, false, false);
-            }
+            if (c16) KARMA_WAVE_LAUNCH(true, true);
+            else KARMA_WAVE_LAUNCH(true, false);
         } else {
-            if (c16) KARMA_WAVE_LAUNCH(false, true, false);
-            else KARMA_WAVE_LAUNCH(false, false, false);
+            if (c16) KARMA_WAVE_LAUNCH(false, true);
+            else KARMA_WAVE_LAUNCH(false, false);
         }
 #undef KARMA_WAVE_LAUNCH
     } else {
