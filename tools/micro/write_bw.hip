@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
         ms /= reps;
         printf("%-28s %.4f ms  %.2f TB/s\n", name, ms, bytes / (ms * 1e-3) / 1e12);
     };
-    for (int bpc : {4, 8, 16}) {
+    for (int bpc : {1, 2, 4, 8}) {
         const int g = cus * bpc;
         char nm[64];
         snprintf(nm, sizeof nm, "stream NT  %d blk/CU", bpc);
