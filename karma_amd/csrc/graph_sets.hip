@@ -55,6 +55,9 @@ constexpr int kMaxBc = 512;           // code buckets
 // partition LDS is sized by the bucket count: the narrow variants (<= 512 pair
 // and <= 128 code buckets, n_contigs <= 2^19) keep 3 code-partition blocks per CU
 constexpr int kNarrowB = 512, kNarrowBc = 128;
+#ifndef KARMA_CG_SHIFT
+#define KARMA_CG_SHIFT 18  // a code bucket gets one reduce group per 2^18 records it may hold
+#endif
 #ifndef KARMA_ONE_GROUP_B
 #define KARMA_ONE_GROUP_B 128
 #endif
@@ -1896,7 +1899,7 @@ int SetsJob::setup() {
     // may hold (8-way strong scaling of config 3: 3 groups; one group took
     // 0.076 ms against 0.047 for five).
     n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>({ctx->cu_count / g.Bc, ceil_div(max_cflush, 4),
-                                                                     ceil_div(A, (int64_t)g.Bc << 18)}))
+                                                                     ceil_div(A, (int64_t)g.Bc << KARMA_CG_SHIFT)}))
                     : 0;
     // pair-reduce groups per bucket: enough blocks to fill the chip while
     // buckets are few; one group from KARMA_ONE_GROUP_B buckets on, so the
