@@ -55,6 +55,9 @@ constexpr int kMaxBc = 512;           // code buckets
 // partition LDS is sized by the bucket count: the narrow variants (<= 512 pair
 // and <= 128 code buckets, n_contigs <= 2^19) keep 3 code-partition blocks per CU
 constexpr int kNarrowB = 512, kNarrowBc = 128;
+#ifndef KARMA_PART_SUB
+#define KARMA_PART_SUB 1  // counter copies of the narrow code partition (1, 2 or 4; see partition_kernel)
+#endif
 #ifndef KARMA_CG_SHIFT
 #define KARMA_CG_SHIFT 18  // a code bucket gets one reduce group per 2^18 records it may hold
 #endif
@@ -616,6 +619,7 @@ struct CodeStreamT {
     static constexpr int kCap = 8192;   // codes per flush (32 KB of LDS)
     static constexpr int kPad = 8;      // 16 B of u16
     static constexpr int kMaxNb = NB;
+    static constexpr int kSub = NB <= 128 ? KARMA_PART_SUB : 1;  // partition counter copies (LDS)
     static constexpr D kPadV = 0xFFFF;  // codes are < 2^15
     __device__ static int nb(const Geo& g) { return g.Bc; }
     __device__ static uint32_t bucket(S s, const Geo& g) { return (s & 0xFFFFFFu) >> g.bwc; }
@@ -632,6 +636,7 @@ struct PairStreamT {
     static constexpr int kCap = 4096;
     static constexpr int kPad = 4;
     static constexpr int kMaxNb = NB;
+    static constexpr int kSub = 1;
     static constexpr D kPadV = kEmpty;  // pair keys are < 2^31
     __device__ static int nb(const Geo& g) { return g.B; }
     __device__ static uint32_t bucket(S s, const Geo& g) { return (uint32_t)(s >> 32) >> g.bw; }
@@ -693,9 +698,19 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
     constexpr int kCopyIt = (kVMax + kPT - 1) / kPT;
     __shared__ S buf[T::kCap];
     __shared__ D sorted[T::kCap + T::kMaxNb * (T::kPad - 1)];
-    __shared__ uint32_t hist[2][T::kMaxNb + 1];  // by fill parity: reset while the other fills
+    // Per-bucket counters, optionally in kSub copies (lane l using copy
+    // l % kSub, so lanes of one wave instruction that hit the same bucket hit
+    // kSub different words).  The flush's scan turns the counts into scatter
+    // cursors (cur), writes the runs' padding and clears the counts, so one
+    // set of each serves every fill (double-buffered counts, a separate base
+    // table and a pad pass took 0.176-0.184 ms; this layout 0.172-0.174).
+    // Copies cost LDS: 2 or 4 copies leave 2 blocks per CU instead of 3
+    // (0.204 and 0.173 ms), so one copy is the default.
+    constexpr int kSub = T::kSub;
+    constexpr int kHS = T::kMaxNb + (kSub > 1 ? 4 : 0);  // words per copy (LDS: 3 blocks per CU need <= 53 KB)
+    __shared__ uint32_t hist[kSub * kHS];
     __shared__ uint32_t toff[T::kMaxNb + 1];
-    __shared__ uint32_t cur[T::kMaxNb];
+    __shared__ uint32_t cur[kSub * kHS];  // copy q of bucket b scatters to cur[q * kHS + b]++
     __shared__ uint32_t lpre[kMaxListsPerBlock + 1];
     __shared__ int64_t red_s[2][kPT / 64];
     const int nb = T::nb(g);
@@ -732,7 +747,8 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
         }
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int b = threadIdx.x; b <= nb; b += kPT) hist[0][b] = hist[1][b] = 0;
+    const int sub = (lane & (kSub - 1)) * kHS;  // this thread's copy
+    for (int b = threadIdx.x; b < kSub * kHS; b += kPT) hist[b] = 0;
 
     // the block's lists as one concatenated range: prefix of their lengths
     const int64_t l_lo = (int64_t)blockIdx.x * per_block;
@@ -774,32 +790,46 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
     // every path into the flush loop has kCopyIt stores after the fill's loads
     // (here dropped ones), so the loop's wait for a fill stays vmcnt(kCopyIt)
     dropped_stores<kCopyIt>();
-    int parity = 0;
     // a thread scatters the items it counted (its own slots of the fill),
     // staged in LDS across the flush's barriers while v takes the next
     // fill's loads (held in registers instead: 104 VGPRs, 2 blocks per CU,
     // measured slower)
 #define PART_ITEM(k) buf[threadIdx.x + (k) * kPT]
-    for (uint32_t base = 0; base < items; base += T::kCap, parity ^= 1) {
+    for (uint32_t base = 0; base < items; base += T::kCap) {
         const uint32_t n = min(items - base, (uint32_t)T::kCap);
-        uint32_t* h = hist[parity];
+        uint32_t* const h = hist;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const uint32_t i = threadIdx.x + k * kPT;
             PART_ITEM(k) = v[k];
-            if (i < n) atomicAdd(&h[T::bucket(v[k], g)], 1u);
+            if (i < n) atomicAdd(&h[sub + T::bucket(v[k], g)], 1u);
         }
         load(base + T::kCap);  // the next fill's loads overlap this flush
         // ---- flush: counting sort of buf by bucket into padded runs ----
         __syncthreads();
-        for (int b = threadIdx.x; b < nb; b += kPT) cur[b] = 0;
         if (wave == 0) {
             uint32_t c2 = 0;
             for (int b0 = 0; b0 < nb; b0 += 64) {
-                const uint32_t val =
-                    b0 + lane < nb ? (h[b0 + lane] + (T::kPad - 1)) & ~(uint32_t)(T::kPad - 1) : 0u;
+                const int bb = b0 + lane;
+                uint32_t cnt[kSub], tot = 0;
+#pragma unroll
+                for (int q = 0; q < kSub; ++q) {
+                    cnt[q] = bb < nb ? h[q * kHS + bb] : 0u;
+                    if (bb < nb) h[q * kHS + bb] = 0;  // counted: clear for the next fill
+                    tot += cnt[q];
+                }
+                const uint32_t val = (tot + (T::kPad - 1)) & ~(uint32_t)(T::kPad - 1);
                 const uint32_t x = wave_scan_incl(val);
-                if (b0 + lane < nb) toff[b0 + lane] = c2 + x - val;
+                if (bb < nb) {
+                    uint32_t o = c2 + x - val;
+                    toff[bb] = o;
+#pragma unroll
+                    for (int q = 0; q < kSub; ++q) {
+                        cur[q * kHS + bb] = o;
+                        o += cnt[q];
+                    }
+                    for (uint32_t i = o; i < c2 + x; ++i) sorted[i] = T::kPadV;  // the run's padding
+                }
                 c2 += lane63(x);
             }
             if (lane == 0) toff[nb] = c2;
@@ -813,23 +843,20 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
         used += total;
         {
             for (int b = threadIdx.x; b <= nb; b += kPT) dir.off[(int64_t)f * (nb + 1) + b] = toff[b];
-            for (int b = threadIdx.x; b < nb; b += kPT)
-                for (uint32_t i = toff[b] + h[b]; i < toff[b + 1]; ++i) sorted[i] = T::kPadV;
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 if (threadIdx.x + k * kPT < n) {
                     const S it = PART_ITEM(k);
                     const uint32_t b = T::bucket(it, g);
-                    sorted[toff[b] + atomicAdd(&cur[b], 1u)] = T::value(it, g);
+                    sorted[atomicAdd(&cur[sub + b], 1u)] = T::value(it, g);
                 }
             }
 #undef PART_ITEM
         }
         __syncthreads();
-        // h and cur are free: the next fill may start once this block's
-        // 16-byte stores are issued (their completion is never waited for)
-        for (int b = threadIdx.x; b < nb; b += kPT) h[b] = 0;
-        // copy-out: a fixed number of 16-byte buffer stores per thread, the
+        // the counters are clear (scan) and the cursors spent: the next fill
+        // may start once this block's 16-byte stores are issued (their
+        // completion is never waited for).  Copy-out: a fixed number of 16-byte buffer stores per thread, the
         // range check dropping those past the flush.  vmcnt counts loads and
         // stores together, in issue order: with a runtime-length copy loop the
         // next fill's wait for its (earlier) loads was vmcnt(0) and drained
