@@ -1955,6 +1955,11 @@ int SetsJob::launch() {
     KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
     KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk) * 8, ctx->stream));
     if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
+    if (KARMA_MARK_AT == 3 && attempt == 0 && !relabeled) {  // side-stream work may start beside classify
+        if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
+        KARMA_HIP(hipEventRecord(ctx->mark_ev, ctx->stream));
+        ctx->mark_set = true;
+    }
     if (A > 0) {
         ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
                     n_gen.ptr, blk_items, lpb, big_list.ptr, counters, flags,
@@ -1983,9 +1988,11 @@ int SetsJob::launch() {
         KARMA_TRY(classify(0, n_chunks));
     }
     // where side-stream work (the k-mer profile) may start: 0 = after the whole
-    // pipeline (default), 1 = after classify, 2 = after the code partition.
+    // pipeline (default), 1 = after classify, 2 = after the code partition,
+    // 3 = at once (beside classify).
     // Measured: 1 slows the code partition 0.19 -> 0.5 ms (1.46 vs 1.37 ms/step);
-    // 2 stretches the profile to 0.60 ms beside the reduce (1.43 vs 1.35)
+    // 2 stretches the profile to 0.60 ms beside the reduce (1.43 vs 1.35);
+    // 3 stretches classify 0.54 -> 0.74 ms (1.35 vs 1.25): HBM is already full
     auto mark = [&](int at) -> int {
         if (KARMA_MARK_AT != at || attempt != 0) return KARMA_OK;
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
