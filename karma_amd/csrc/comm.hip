@@ -21,8 +21,8 @@ struct karma_comm {
     ncclComm_t nc = nullptr;
     int world = 1, rank = 0;
     size_t scalar_bytes = 64;       // max(64, 8 * world): host scalars one call may reduce
-    int32_t* scratch = nullptr;     // device: barrier word / host-scalar staging (scalar_bytes)
-    void* pinned = nullptr;         // host: scalar staging (scalar_bytes), then 2 * world int64 of counts
+    int32_t* scratch = nullptr;     // device: barrier word / host-scalar staging (scalar_bytes; host side:
+                                    // the context's mapped buffer, ctx_mapped)
     int64_t* counts_dev = nullptr;  // device: all-to-all count exchange (2 * world int64)
 };
 
@@ -66,6 +66,16 @@ int comm_begin(karma_comm* c) {
 
 using namespace karma;
 
+namespace {
+// Host scalars in and out through mapped host memory, moved by a one-block
+// kernel: a copy launch to or from host memory waits for free CUs and, to
+// host, for the L2 write-back, both slow beside the running profile kernel
+// (a 72-byte readback took 0.24 ms there); a kernel writing mapped memory does not.
+__global__ void copy_words_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+}  // namespace
+
 extern "C" {
 
 int karma_comm_id_bytes(void) { return NCCL_UNIQUE_ID_BYTES; }
@@ -102,10 +112,6 @@ int karma_comm_create(karma_ctx* ctx, const uint8_t* id, int world, int rank, ka
         rc = ctx_alloc(ctx, 16 * (size_t)world, &p);
         c->counts_dev = static_cast<int64_t*>(p);
     }
-    if (rc == KARMA_OK && hipHostMalloc(&c->pinned, c->scalar_bytes + 16 * (size_t)world, hipHostMallocDefault) != hipSuccess) {
-        set_error("hipHostMalloc of the comm staging buffer failed");
-        rc = KARMA_ERR_OOM;
-    }
     if (rc != KARMA_OK) {
         ncclCommDestroy(c->nc);
         ctx_free(ctx, c->scratch);
@@ -126,7 +132,6 @@ int karma_comm_destroy(karma_comm* c) {
         ctx_free(c->ctx, c->counts_dev);
     }
     if (c->nc) ncclCommDestroy(c->nc);
-    if (c->pinned) hipHostFree(c->pinned);
     delete c;
     return KARMA_OK;
 }
@@ -161,12 +166,19 @@ int karma_comm_allreduce_host(karma_comm* c, void* buf_host, int64_t count, int 
     KARMA_CHECK(buf_host && count >= 1 && (size_t)count * sz <= c->scalar_bytes, KARMA_ERR_ARG,
                 "karma_comm_allreduce_host: 1..%zu bytes of host scalars", c->scalar_bytes);
     const size_t bytes = (size_t)count * sz;
-    std::memcpy(c->pinned, buf_host, bytes);
-    KARMA_HIP(hipMemcpyAsync(c->scratch, c->pinned, bytes, hipMemcpyHostToDevice, c->ctx->stream));
+    const int words = (int)((bytes + 7) / 8);
+    void *hm = nullptr, *dm = nullptr;
+    KARMA_TRY(ctx_mapped(c->ctx, (size_t)words * 8, &hm, &dm));
+    std::memcpy(hm, buf_host, bytes);
+    hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream, static_cast<const uint64_t*>(dm),
+                       reinterpret_cast<uint64_t*>(c->scratch), words);
+    KARMA_HIP(hipGetLastError());
     KARMA_NCCL(ncclAllReduce(c->scratch, c->scratch, (size_t)count, t, o, c->nc, c->ctx->stream));
-    KARMA_HIP(hipMemcpyAsync(c->pinned, c->scratch, bytes, hipMemcpyDeviceToHost, c->ctx->stream));
+    hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream,
+                       reinterpret_cast<const uint64_t*>(c->scratch), static_cast<uint64_t*>(dm), words);
+    KARMA_HIP(hipGetLastError());
     KARMA_HIP(hipStreamSynchronize(c->ctx->stream));
-    std::memcpy(buf_host, c->pinned, bytes);
+    std::memcpy(buf_host, hm, bytes);
     return KARMA_OK;
 }
 
@@ -188,16 +200,22 @@ int karma_comm_exchange_counts(karma_comm* c, const int64_t* send_host, int64_t*
     KARMA_TRY(comm_begin(c));
     KARMA_CHECK(send_host && recv_host, KARMA_ERR_ARG, "karma_comm_exchange_counts: null argument");
     const int W = c->world;
-    int64_t* pin = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(c->pinned) + c->scalar_bytes);
+    void *hm = nullptr, *dm = nullptr;
+    KARMA_TRY(ctx_mapped(c->ctx, 16 * (size_t)W, &hm, &dm));
+    int64_t* pin = static_cast<int64_t*>(hm);
     std::memcpy(pin, send_host, 8 * (size_t)W);
-    KARMA_HIP(hipMemcpyAsync(c->counts_dev, pin, 8 * (size_t)W, hipMemcpyHostToDevice, c->ctx->stream));
+    hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream, static_cast<const uint64_t*>(dm),
+                       reinterpret_cast<uint64_t*>(c->counts_dev), W);
+    KARMA_HIP(hipGetLastError());
     KARMA_NCCL(ncclGroupStart());
     for (int r = 0; r < W; ++r) {
         KARMA_NCCL(ncclSend(c->counts_dev + r, 1, ncclInt64, r, c->nc, c->ctx->stream));
         KARMA_NCCL(ncclRecv(c->counts_dev + W + r, 1, ncclInt64, r, c->nc, c->ctx->stream));
     }
     KARMA_NCCL(ncclGroupEnd());
-    KARMA_HIP(hipMemcpyAsync(pin + W, c->counts_dev + W, 8 * (size_t)W, hipMemcpyDeviceToHost, c->ctx->stream));
+    hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream,
+                       reinterpret_cast<const uint64_t*>(c->counts_dev + W), static_cast<uint64_t*>(dm) + W, W);
+    KARMA_HIP(hipGetLastError());
     KARMA_HIP(hipStreamSynchronize(c->ctx->stream));
     std::memcpy(recv_host, pin + W, 8 * (size_t)W);
     return KARMA_OK;

@@ -131,3 +131,43 @@ def test_product_path_never_imports_torch():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "no-torch ok" in r.stdout
+
+
+class _OneRankGroup:
+    """The bootstrap group of a one-rank job (the unique id needs no exchange)."""
+
+    world, rank = 1, 0
+
+    def allgather(self, arr):
+        return [np.asarray(arr)]
+
+    def close(self):
+        pass
+
+
+def test_rccl_comm_world1_calls():
+    """The library's RCCL communicator at world size 1: every call the sharded
+    build makes (host-scalar reduces through mapped memory, the count exchange,
+    the all-to-all-v own slice, all-gathers) returns its input unchanged."""
+    from karma_amd.comm import RcclComm
+
+    ctx = _lib.Context(0)
+    comm = RcclComm(_OneRankGroup(), ctx)
+    try:
+        comm.barrier()
+        assert comm.max_float(2.5) == 2.5
+        assert comm.sum_int(7) == 7
+        src = np.arange(2 * 1000, dtype=np.int64)
+        buf = _lib.DevBuf.from_numpy(ctx, src)
+        out, recv = comm.alltoallv(buf, [src.size])
+        assert recv == [src.size]
+        np.testing.assert_array_equal(out.numpy(), src)
+        g = comm.allgather_fixed(buf)
+        np.testing.assert_array_equal(g.numpy(), src)
+        v = comm.allgather_var(_lib.DevBuf.from_numpy(ctx, src[:17]))
+        np.testing.assert_array_equal(v.numpy(), src[:17])
+        for b in (buf, out, g, v):
+            b.close()
+    finally:
+        comm.close()
+        ctx.close()
