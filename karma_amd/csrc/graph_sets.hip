@@ -1002,8 +1002,8 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
         }
         load(base + kCap);
         lds_barrier();
-        // bucket regions (pending + new, 8-aligned) and full-vector counts
-        for (int b = threadIdx.x; b < nb; b += kPT) cur[b] = 0;
+        // bucket regions (pending + new, 8-aligned), full-vector counts and
+        // the scatter cursors (region start + pending codes)
         if (wave == 0) {
             uint32_t c8 = 0, cq = 0;
             for (int b0 = 0; b0 < nb; b0 += 64) {
@@ -1013,6 +1013,7 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
                 if (b0 + lane < nb) {
                     toff[b0 + lane] = c8 + sx - r8;
                     qoff[b0 + lane] = cq + sy - q;
+                    cur[b0 + lane] = c8 + sx - r8 + pc[b0 + lane];
                 }
                 c8 += lane63(sx);
                 cq += lane63(sy);
@@ -1038,7 +1039,7 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
         for (int k = 0; k < kPer; ++k) {
             if (threadIdx.x + k * kPT < n) {
                 const uint32_t b = T::bucket(x[k], g);
-                s16[toff[b] + pc[b] + atomicAdd(&cur[b], 1u)] = T::value(x[k], g);
+                s16[atomicAdd(&cur[b], 1u)] = T::value(x[k], g);
             }
         }
         lds_barrier();
