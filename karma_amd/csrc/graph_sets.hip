@@ -58,6 +58,9 @@ constexpr int kNarrowB = 512, kNarrowBc = 128;
 #ifndef KARMA_PART_SUB
 #define KARMA_PART_SUB 1  // counter copies of the narrow code partition (1, 2 or 4; see partition_kernel)
 #endif
+#ifndef KARMA_REC_NT
+#define KARMA_REC_NT 1  // classify's record loads non-temporal (plain loads: classify 0.53 -> 0.58 ms)
+#endif
 #ifndef KARMA_CODE_AUX
 #define KARMA_CODE_AUX 0  // cache policy of classify's code stores (2, non-temporal: classify
                           // 0.53 -> 0.59 ms, the partition reading them 0.172 -> 0.165)
@@ -289,7 +292,10 @@ classify2_kernel(ClassArgs P) {
         if (t0 + kCIter <= hi) {
 #pragma unroll
             for (int u = 0; u < kCPer; ++u)
-                dst[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.rec + gb + 128 * u));
+                if (KARMA_REC_NT)
+                    dst[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.rec + gb + 128 * u));
+                else
+                    dst[u] = *reinterpret_cast<const u32x4*>(P.rec + gb + 128 * u);
         } else {
 #pragma unroll
             for (int u = 0; u < kCPer; ++u) {
