@@ -61,6 +61,14 @@ constexpr int kNarrowB = 512, kNarrowBc = 128;
 #ifndef KARMA_REC_NT
 #define KARMA_REC_NT 1  // classify's record loads non-temporal (plain loads: classify 0.53 -> 0.58 ms)
 #endif
+#ifndef KARMA_PART_LOAD_NT
+#define KARMA_PART_LOAD_NT 1  // the partition's loads of classify's codes non-temporal: they are read
+                              // once, and the runs it writes stay in the Infinity Cache for the reduce
+                              // (partition 0.173 -> 0.169 ms, reduce 0.087 -> 0.084)
+#endif
+#ifndef KARMA_RED_LOAD_NT
+#define KARMA_RED_LOAD_NT 0  // the reduces' run loads non-temporal (measured 0.087 -> 0.093 ms)
+#endif
 #ifndef KARMA_CODE_AUX
 #define KARMA_CODE_AUX 0  // cache policy of classify's code stores (2, non-temporal: classify
                           // 0.53 -> 0.59 ms, the partition reading them 0.172 -> 0.165)
@@ -792,7 +800,10 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
             const uint32_t gi = base + threadIdx.x + k * kPT;
             if (gi < items) {
                 while (lpre[lo + 1] <= gi) ++lo;  // list L: lpre[L] <= gi < lpre[L + 1]
-                v[k] = lists[(l_lo + lo) * list_cap + (gi - lpre[lo])];
+                if (KARMA_PART_LOAD_NT)
+                    v[k] = __builtin_nontemporal_load(&lists[(l_lo + lo) * list_cap + (gi - lpre[lo])]);
+                else
+                    v[k] = lists[(l_lo + lo) * list_cap + (gi - lpre[lo])];
             }
         }
     };
@@ -1119,7 +1130,7 @@ __device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int6
                     const int64_t o = readlane64(roff, rr);
                     if (j >= ex) off = o;
                 }
-                if (j < Tn) e[u] = data[off + j];
+                if (j < Tn) e[u] = KARMA_RED_LOAD_NT ? __builtin_nontemporal_load(&data[off + j]) : data[off + j];
             }
 #pragma unroll
             for (int u = 0; u < kWin; ++u)
