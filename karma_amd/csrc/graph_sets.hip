@@ -66,6 +66,11 @@ constexpr int kNarrowB = 512, kNarrowBc = 128;
                               // once, and the runs it writes stay in the Infinity Cache for the reduce
                               // (partition 0.173 -> 0.169 ms, reduce 0.087 -> 0.084)
 #endif
+#ifndef KARMA_APPEND_LOAD_NT
+#define KARMA_APPEND_LOAD_NT 1  // as KARMA_PART_LOAD_NT, for the append partition (weak-scaled
+                                // config 3: 0.277 -> 0.224 ms; its scattered run writes then
+                                // combine in the Infinity Cache instead of competing with the codes)
+#endif
 #ifndef KARMA_RED_LOAD_NT
 #define KARMA_RED_LOAD_NT 0  // the reduces' run loads non-temporal (measured 0.087 -> 0.093 ms)
 #endif
@@ -1006,7 +1011,8 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
         for (int k = 0; k < kPer; ++k) {
             const uint32_t gi = min(base + threadIdx.x + k * kPT, items - 1);
             while (lpre[lo + 1] <= gi) ++lo;
-            v[k] = lists[(l_lo + lo) * list_cap + (gi - lpre[lo])];
+            v[k] = KARMA_APPEND_LOAD_NT ? __builtin_nontemporal_load(&lists[(l_lo + lo) * list_cap + (gi - lpre[lo])])
+                                        : lists[(l_lo + lo) * list_cap + (gi - lpre[lo])];
         }
     };
     if (items > 0) load(0);
