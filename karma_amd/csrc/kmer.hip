@@ -478,6 +478,13 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 #define KARMA_PROF_ABLATE 0  // diagnostic builds only (tools/build_variant.sh): 1 rows only, 2 counting only,
                              // 3 rows only without the quotient divisions, 4 as 3 without the prefetch loads
 #endif
+#ifndef KARMA_ROW_AUX
+// cache policy of the profile's 16-byte row stores, as buffer stores (-1: global
+// stores, non-temporal per KARMA_PROF_NT).  18 = sc1 | nt: profile 0.361 -> 0.348 ms;
+// measured alongside: 2 (nt) 0.358, 3 (sc0 | nt) 0.357, 19 0.353, 16 (sc1) 0.355
+// with a slower step (1.30 vs 1.25 ms), 17 (sc0 | sc1) 0.354 with 1.28 ms
+#define KARMA_ROW_AUX 18
+#endif
 #ifndef KARMA_PROF_NT
 #define KARMA_PROF_NT 1  // profile rows written with non-temporal stores
 #endif
@@ -654,7 +661,21 @@ __device__ __forceinline__ void write_row_wave(double* __restrict__ row, uint32_
             d2 v;
             v.x = val(a);
             v.y = val(b);
+#if KARMA_ROW_AUX >= 0  // the row's 16-byte stores as buffer stores with this cache policy
+            {
+                typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+                const uint64_t u = (uint64_t)row;
+                const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+                    reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u)),
+                    0, (int)(M * 8), 0x00020000);
+                const u32x4_t w = {(uint32_t)__double2loint(v.x), (uint32_t)__double2hiint(v.x),
+                                   (uint32_t)__double2loint(v.y), (uint32_t)__double2hiint(v.y)};
+                __builtin_amdgcn_raw_buffer_store_b128(w, rr, (int)(j * 16), 0, KARMA_ROW_AUX);
+            }
+#else
             row_store(v, reinterpret_cast<d2*>(row) + j);
+#endif
         }
         if ((M & 1) && lane == 0) {
             const uint32_t a = C16 ? counts[M >> 1] & 0xFFFFu : counts[M - 1];
