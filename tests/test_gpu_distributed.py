@@ -171,3 +171,44 @@ def test_rccl_comm_world1_calls():
     finally:
         comm.close()
         ctx.close()
+
+
+def _free_port_pair():
+    import socket
+    for _ in range(50):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            p = s.getsockname()[1]
+        if p >= 65535:
+            continue
+        try:
+            with socket.socket() as s2:
+                s2.bind(("127.0.0.1", p + 1))  # hostgroup's bootstrap port (MASTER_PORT + 1)
+            return p
+        except OSError:
+            continue
+    raise RuntimeError("no free port pair")
+
+
+def test_bench_under_torch_distributed_run_two_ranks():
+    """The driver's multi-GPU launch (`python -m torch.distributed.run
+    --nproc-per-node N ... bench.py --gpus N`) rehearsed with 2 ranks on the
+    one device: the rank processes bootstrap through hostgroup (MASTER_PORT + 1),
+    exchange through the host-staged transport (RCCL refuses two ranks on one
+    device) and rank 0 prints exactly one JSON line with the whole-job value."""
+    import json
+    import os
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, KARMA_FORCE_DEVICE="0", KARMA_DIST_BACKEND="host")
+    port = _free_port_pair()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--config", "tiny"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=repo, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 2 and res["scaling"] == "weak"
+    assert res["value"] > 0 and res["ms_per_step"] > 0
