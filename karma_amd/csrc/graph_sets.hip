@@ -78,6 +78,12 @@ constexpr int kNarrowB = 512, kNarrowBc = 128;
 #define KARMA_CODE_AUX 0  // cache policy of classify's code stores (2, non-temporal: classify
                           // 0.53 -> 0.59 ms, the partition reading them 0.172 -> 0.165)
 #endif
+#ifndef KARMA_CR_SMAX
+#define KARMA_CR_SMAX 64  // code reduce: at most this many pieces per run
+#endif
+#ifndef KARMA_CR_ABLATE
+#define KARMA_CR_ABLATE 0  // diagnostic builds only: 1 = no LDS adds, 2 = no run stream
+#endif
 #ifndef KARMA_CG_SHIFT
 #define KARMA_CG_SHIFT 18  // a code bucket gets one reduce group per 2^18 records it may hold
 #endif
@@ -1172,17 +1178,20 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
     // rows hold one long run per bucket (code_append_kernel): split each into S
     // pieces so that every wave has runs to stream
     const int64_t R = f_hi - f_lo;
-    const int S = R > 0 ? (int)min<int64_t>(64, (2 * kCRT + R - 1) / R) : 1;
+    const int S = R > 0 ? (int)min<int64_t>(KARMA_CR_SMAX, (2 * kCRT + R - 1) / R) : 1;
     bool stop = false;
     // LDS slot of counter c = (m0_local << 3 | M): the low five bits XOR-ed with
     // m0_local >> 2, so that codes of one wave instruction spread over all 32
     // banks (unswizzled, the bank is (m0 & 3) << 3 | M, and M is mostly 0)
     auto slot = [](uint32_t c) { return c ^ ((c >> 5) & 31u); };
+    uint32_t sink = 0;  // KARMA_CR_ABLATE == 1 (diagnostic): loads kept, no LDS adds
     auto add = [&](uint32_t c) {
-        if (c != CodeStream::kPadV)
+        if (KARMA_CR_ABLATE == 1)
+            sink += c;
+        else if (c != CodeStream::kPadV)
             __hip_atomic_fetch_add(&h[slot(c)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    stream_runs(
+    if (KARMA_CR_ABLATE != 2) stream_runs(
         reinterpret_cast<const u32x4*>(cent), f_lo * S, f_hi * S, kCRT,
         [&](int64_t v, int64_t* beg, uint32_t* len) {
             const int64_t f = v / S;
@@ -1201,6 +1210,7 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
     __syncthreads();
     uint32_t* out = part_ch + (int64_t)blockIdx.x * hn;
     for (int i = threadIdx.x; i < hn; i += kCRT) out[i] = h[slot(i)];
+    if (KARMA_CR_ABLATE == 1 && sink == 0x9E3779B9u) out[0] = sink;
 }
 
 // ---- pair reduce --------------------------------------------------------------------
