@@ -81,6 +81,12 @@ constexpr int kNarrowB = 512, kNarrowBc = 128;
 #ifndef KARMA_CR_SMAX
 #define KARMA_CR_SMAX 64  // code reduce: at most this many pieces per run
 #endif
+#ifndef KARMA_CR_PIECES
+#define KARMA_CR_PIECES (2 * 1024)  // code reduce: run pieces per block to aim for
+#endif
+#ifndef KARMA_CR_PIPE
+#define KARMA_CR_PIPE 0  // code reduce: barrier-free run stream with the next batch's bounds prefetched
+#endif
 #ifndef KARMA_CR_ABLATE
 #define KARMA_CR_ABLATE 0  // diagnostic builds only: 1 = no LDS adds, 2 = no run stream
 #endif
@@ -1118,11 +1124,24 @@ template <typename Bounds, typename Count>
 __device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int64_t r_lo, int64_t r_hi, int threads,
                                             Bounds bounds, Count count, bool* stop) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // stop == nullptr: nothing stops the block early, so the waves run without
+    // a barrier per batch, and the next batch's run bounds are loaded before
+    // the current batch is streamed (their latency hides under its windows)
+    const bool pipe = KARMA_CR_PIPE && stop == nullptr;
+    int64_t nbeg = 0;
+    uint32_t nlen = 0;
+    if (pipe && r_lo + (int64_t)wave * 64 + lane < r_hi) bounds(r_lo + (int64_t)wave * 64 + lane, &nbeg, &nlen);
     for (int64_t r0 = r_lo + (int64_t)wave * 64; r0 - (int64_t)wave * 64 < r_hi; r0 += (int64_t)threads) {
         const int64_t r = r0 + lane;
         int64_t beg = 0;
         uint32_t len = 0;
-        if (r < r_hi) bounds(r, &beg, &len);
+        if (pipe) {
+            beg = nbeg, len = nlen;
+            nbeg = 0, nlen = 0;
+            if (r + threads < r_hi) bounds(r + threads, &nbeg, &nlen);
+        } else if (r < r_hi) {
+            bounds(r, &beg, &len);
+        }
         const uint32_t incl = wave_scan_incl(len);
         const uint32_t excl = incl - len;
         const int64_t roff = beg - (int64_t)excl;  // vector j of run r: data[roff + j]
@@ -1148,7 +1167,11 @@ __device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int6
             for (int u = 0; u < kWin; ++u)
                 if (j0 + 64u * u + lane < Tn) count(e[u]);
         }
-        if (__syncthreads_or(*stop)) return;
+        if (pipe) {
+            if (r0 + threads >= r_hi) break;  // this wave's last batch
+        } else if (__syncthreads_or(stop != nullptr && *stop)) {
+            return;
+        }
     }
 }
 
@@ -1178,8 +1201,7 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
     // rows hold one long run per bucket (code_append_kernel): split each into S
     // pieces so that every wave has runs to stream
     const int64_t R = f_hi - f_lo;
-    const int S = R > 0 ? (int)min<int64_t>(KARMA_CR_SMAX, (2 * kCRT + R - 1) / R) : 1;
-    bool stop = false;
+    const int S = R > 0 ? (int)max<int64_t>(1, min<int64_t>(KARMA_CR_SMAX, (KARMA_CR_PIECES + R - 1) / R)) : 1;
     // LDS slot of counter c = (m0_local << 3 | M): the low five bits XOR-ed with
     // m0_local >> 2, so that codes of one wave instruction spread over all 32
     // banks (unswizzled, the bank is (m0 & 3) << 3 | M, and M is mostly 0)
@@ -1206,7 +1228,7 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
             add(v.x & 0xFFFFu), add(v.x >> 16), add(v.y & 0xFFFFu), add(v.y >> 16);
             add(v.z & 0xFFFFu), add(v.z >> 16), add(v.w & 0xFFFFu), add(v.w >> 16);
         },
-        &stop);
+        nullptr);
     __syncthreads();
     uint32_t* out = part_ch + (int64_t)blockIdx.x * hn;
     for (int i = threadIdx.x; i < hn; i += kCRT) out[i] = h[slot(i)];
