@@ -38,9 +38,6 @@ sys.path.insert(0, REPO)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # kernels with an algorithmic-bytes figure: the roofline kernel is the slowest of these
 ROOFLINE_KERNELS = ("kmer_profile", "kmer_presence", "graph_classify", "graph_code_partition", "graph_code_reduce")
-# reference Python (karma/kmer.py:199-264 + read_graph.py:61-148, the path karma.py:197-240
-# runs) on config 3, measured in the survey container: ~300 s profile + 3.41 s graph
-REF_PY_CONFIG3_S = 300.0 + 3.41
 
 CONFIGS = {
     # name: (seed, contigs per GPU, fragments per GPU, paired, kmer)
@@ -61,12 +58,15 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling (BASELINE configs[3]): the config's contigs and fragments divided over "
-                         "the ranks (or over --emulate-ranks)")
+    ap.add_argument("--weak", action="store_true",
+                    help="headline = weak scaling (every rank a whole config-sized share of a W x larger problem); "
+                         "default strong (BASELINE configs[3]: the config divided over the ranks)")
+    ap.add_argument("--strong", action="store_true", help="(the default; kept for old command lines)")
+    ap.add_argument("--no-weak-leg", action="store_true",
+                    help="N > 1: skip the extra weak-scaling leg reported under \"weak\"")
     ap.add_argument("--emulate-ranks", type=int, default=1,
                     help="diagnostic: one process runs rank 0's compute of a W-rank problem (weak: global contig "
-                         "ids over W x the per-GPU contigs; --strong: 1/W of the config) with the exchange's local "
+                         "ids over W x the per-GPU contigs; strong: 1/W of the config) with the exchange's local "
                          "work (device split, merge of W sorted slices, totals) and no collectives; not the metric")
     ap.add_argument("--shuffle-contigs", action="store_true",
                     help="secondary number: contig ids randomly permuted (a FASTA without isoform adjacency; same "
@@ -74,8 +74,11 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=("full", "off"), default="full",
                     help="full: the oracle's OpenMP twin on the whole per-GPU workload (rank 0, N = 1)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end and eq-path legs")
-    return ap.parse_args()
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end, drop-in and eq-path legs")
+    ap.add_argument("--no-parity", action="store_true", help="skip the in-run digest check")
+    a = ap.parse_args()
+    a.strong = not a.weak
+    return a
 
 
 def log(*a):
@@ -115,6 +118,166 @@ def make_inputs(args, rank, world):
                 genes=genes, rec=rec, perm=perm)
 
 
+class Leg:
+    """One workload resident on this rank's GPU: inputs, ShardedBuild, device store and records."""
+
+    def __init__(self, args, ctx, comm, rank, world):
+        from karma_amd import _lib, engine
+        from karma_amd.distributed import ShardedBuild
+
+        t_gen = time.time()
+        self.args, self.comm, self.rank, self.world = args, comm, rank, world
+        self.inp = inp = make_inputs(args, rank, world)
+        self.A = len(inp["rec"])
+        log(f"[rank {rank}] {'strong' if args.strong else 'weak'}: generated {inp['n_loc']} contigs "
+            f"({int(inp['offs'][-1])} bases), {inp['f_loc']} fragments, {self.A} records in "
+            f"{time.time() - t_gen:.1f}s")
+        self.build = ShardedBuild(ctx, comm, engine.kmode_of(inp["kmer"]), inp["n_glob"], inp["c_lo"], inp["n_loc"],
+                                  emulate_ranks=inp["emu"])  # sets the library-owned main + side streams
+        self.store = engine.ContigStore(ctx, inp["blob"], inp["offs"], inp["key_len"])
+        self.rec_dev = _lib.DevBuf.from_numpy(ctx, inp["rec"].view(np.int64).reshape(-1))
+        ctx.sync()
+        self.packed_bytes = int(np.sum((np.diff(inp["offs"]) + 3) // 4))  # SURVEY §8(d): sum ceil(L/4)
+        self.ctxs = self.build.contexts()  # main context (+ the concurrent graph build's)
+
+    def step(self, keep=False, sequential=False):
+        return self.build.run(self.store, self.rec_dev.ptr, self.A, keep=keep, sequential=sequential)
+
+    def sync_all(self):
+        for c in self.ctxs:
+            c.sync()
+
+    def timed(self, steps, warmup, kernel_timing=True):
+        """W untimed steps, an optional per-kernel pass, then K steps bracketed by
+        barrier + device sync; returns (max-over-ranks seconds, last result,
+        per-kernel totals, dominant kernel, its live (ms, launches))."""
+        comm = self.comm
+        for _ in range(warmup):
+            self.step()
+        self.sync_all()
+        # Per-kernel breakdown, outside the timed region, with every launch timed
+        # and the profile on the main stream (sequential): kernels do not share the
+        # chip, so no launch is charged for time it spent queued behind another.
+        kern = {}
+        if kernel_timing:
+            for c in self.ctxs:
+                c.timing(True)
+                c.timing_reset()
+            for _ in range(steps):
+                self.step(sequential=True)
+            self.sync_all()
+            for c in self.ctxs:
+                for name, (ms, nl) in c.timing_read().items():
+                    prev = kern.get(name, (0.0, 0))
+                    kern[name] = (prev[0] + ms, prev[1] + nl)
+                c.timing(False)
+        dom = max((k for k in kern if k in ROOFLINE_KERNELS), key=lambda k: kern[k][0], default=None)
+        # timed region: the production order (profile on the side stream), with
+        # events only around the dominant kernel's launches (two per launch)
+        if dom:
+            for c in self.ctxs:
+                c.timing(True, dom)
+                c.timing_reset()
+        comm.barrier()
+        self.sync_all()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = self.step()
+        self.sync_all()
+        comm.barrier()
+        t1 = time.perf_counter()
+        dt = comm.max_float(t1 - t0)
+        dom_live = None
+        if dom:
+            for c in self.ctxs:
+                got = c.timing_read().get(dom)
+                if got:
+                    dom_live = got if dom_live is None else (dom_live[0] + got[0], dom_live[1] + got[1])
+                c.timing(False)
+        return dt, res, kern, dom, dom_live
+
+    def close(self):
+        self.build.close()
+        self.store.close()
+        self.rec_dev.close()
+
+
+def digest_key(args, world, emu):
+    """The tests/golden/digests.json entry this run's union of outputs must hash to, or None."""
+    if args.shuffle_contigs or emu > 1:
+        return None  # emulated ranks compute rank 0's share only; shuffled ids need the inverse relabelling
+    if world > 1 and not args.strong:
+        return None  # the weak global problem (W x config) has no oracle digest
+    return {"config2": "config2", "config3": "config3", "config5_1gpu": "config5_1gpu"}.get(args.config)
+
+
+def parity_check(leg, key):
+    """In-run parity (outside the timed region): one more step with its outputs
+    kept; every rank hashes its own profile rows, rank 0 gathers the row digests
+    (32 B per row), edges (a < b owned by the rank of a), column digest and
+    totals, and compares the union with tests/golden/digests.json[key] (the
+    oracle's digests; config 3's profile and edges are also the reference's own,
+    tests/golden/time_reference.py).  A multi-GPU run is thereby its own RCCL
+    parity test.  Returns the JSON object for the bench line (rank 0)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import digests as D
+    from karma_amd import engine
+
+    comm, inp = leg.comm, leg.inp
+    gold = D.load().get(key) if key else None
+    if gold is None:
+        return {"parity": None, "reason": f"no digests for {key or 'this workload'}"}
+    t0 = time.perf_counter()
+    res = leg.step(keep=True)
+    leg.sync_all()
+    M = int(res["M"])
+    prof = res["profile"].numpy()  # this rank's rows, D2H
+    rows = D.row_digests(prof)
+    del prof
+    cols = D.columns_digest(engine.decode_keys(res["columns"], engine.kmode_of(inp["kmer"])))
+    e = res["edges"]
+    meta = np.array([M, inp["c_lo"], inp["n_loc"], len(e.a)], np.int64)
+    g_meta = comm.allgather_host(meta)
+    g_rows = comm.allgather_host(np.frombuffer(rows, np.uint8))
+    g_cols = comm.allgather_host(np.frombuffer(cols.encode(), np.uint8))
+    g_a = comm.allgather_host(np.asarray(e.a, np.uint32))
+    g_b = comm.allgather_host(np.asarray(e.b, np.uint32))
+    g_w = comm.allgather_host(np.asarray(e.weight, np.float64))
+    g_s = comm.allgather_host(np.asarray(e.shared, np.int64))
+    g_t = comm.allgather_host(np.asarray(e.totals, np.int64))
+    if comm.rank != 0:
+        return None
+    order = np.argsort([int(m[1]) for m in g_meta], kind="stable")
+    mism = []
+    if any(int(m[0]) != gold["M"] for m in g_meta):
+        mism.append("M")
+    if any(bytes(c).decode() != gold["columns"] for c in g_cols):
+        mism.append("columns")
+    lo = 0
+    for r in order:  # the shards tile [0, N) in rank order
+        if int(g_meta[r][1]) != lo:
+            mism.append("shards")
+        lo += int(g_meta[r][2])
+    if lo != gold["N"]:
+        mism.append("N")
+    if "profile_rows" not in gold:
+        mism.append("profile_rows (absent from digests.json)")
+    elif D.profile_rows_digest(rows=b"".join(bytes(g_rows[r]) for r in order)) != gold["profile_rows"]:
+        mism.append("profile")
+    got = D.edge_digests(np.concatenate([g_a[r] for r in order]), np.concatenate([g_b[r] for r in order]),
+                         np.concatenate([g_w[r] for r in order]), np.concatenate([g_s[r] for r in order]),
+                         g_t[0])
+    for k in ("E", "ab", "weight", "shared", "totals"):
+        if got.get(k) != gold["edges"].get(k):
+            mism.append(f"edges.{k}")
+    if any(not np.array_equal(t, g_t[0]) for t in g_t):
+        mism.append("totals differ between ranks")
+    return {"parity": not mism, "against": f"tests/golden/digests.json[{key}]"
+            + (" (oracle; config 3 profile and edges also the reference's own)" if key == "config3" else " (oracle)"),
+            "checked": ["M", "columns", "profile_rows", "edges.ab", "edges.weight", "edges.shared", "edges.totals"],
+            "mismatch": mism, "edges": got["E"], "ranks": len(g_meta), "seconds": round(time.perf_counter() - t0, 2)}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -123,80 +286,22 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
-    from karma_amd import _lib, comm as comm_mod, engine
-    from karma_amd.distributed import ShardedBuild
+    from karma_amd import _lib, comm as comm_mod
 
     # KARMA_FORCE_DEVICE pins every rank to one device (multi-rank rehearsal on
     # a 1-GPU box together with KARMA_DIST_BACKEND=host); unset in real runs
     dev_index = int(os.environ.get("KARMA_FORCE_DEVICE", local_rank if world > 1 else 0))
     ctx = _lib.Context(dev_index)
     comm = comm_mod.create(ctx, world, rank)
+    build_info = _lib.build_info()
+    if build_info.get("defines") and not os.environ.get("KARMA_ALLOW_VARIANT"):
+        raise SystemExit(f"bench.py: libkarma_hip.so was built with non-default defines {build_info['defines']}; "
+                         f"rebuild with `make -C karma_amd/csrc` (KARMA_ALLOW_VARIANT=1 to time a variant)")
 
-    t_gen = time.time()
-    inp = make_inputs(args, rank, world)
-    A = len(inp["rec"])
+    leg = Leg(args, ctx, comm, rank, world)
+    inp, A = leg.inp, leg.A
     n_loc, f_loc = inp["n_loc"], inp["f_loc"]
-    log(f"[rank {rank}] generated {n_loc} contigs ({int(inp['offs'][-1])} bases), {f_loc} fragments, {A} records "
-        f"in {time.time() - t_gen:.1f}s")
-
-    build = ShardedBuild(ctx, comm, engine.kmode_of(inp["kmer"]), inp["n_glob"], inp["c_lo"], n_loc,
-                         emulate_ranks=inp["emu"])  # sets the library-owned main + side streams
-    store = engine.ContigStore(ctx, inp["blob"], inp["offs"], inp["key_len"])
-    rec_dev = _lib.DevBuf.from_numpy(ctx, inp["rec"].view(np.int64).reshape(-1))
-    ctx.sync()
-    packed_bytes = int(np.sum((np.diff(inp["offs"]) + 3) // 4))  # sum ceil(L/4)
-
-    def step(keep=False, sequential=False):
-        return build.run(store, rec_dev.ptr, A, keep=keep, sequential=sequential)
-
-    ctxs = build.contexts()  # main context (+ the concurrent graph build's)
-
-    def sync_all():
-        for c in ctxs:
-            c.sync()
-
-    for _ in range(args.warmup):
-        step()
-    sync_all()
-    # Per-kernel breakdown, outside the timed region, with every launch timed
-    # and the profile on the main stream (sequential): kernels do not share the
-    # chip, so no launch is charged for time it spent queued behind another.
-    kern = {}
-    if not args.no_timing:
-        for c in ctxs:
-            c.timing(True)
-            c.timing_reset()
-        for _ in range(args.steps):
-            step(sequential=True)
-        sync_all()
-        for c in ctxs:
-            for name, (ms, nl) in c.timing_read().items():
-                prev = kern.get(name, (0.0, 0))
-                kern[name] = (prev[0] + ms, prev[1] + nl)
-            c.timing(False)
-    dom = max((k for k in kern if k in ROOFLINE_KERNELS), key=lambda k: kern[k][0], default=None)
-    # timed region: the production order (profile on the side stream), with
-    # events only around the dominant kernel's launches (two per launch)
-    if dom:
-        for c in ctxs:
-            c.timing(True, dom)
-            c.timing_reset()
-    comm.barrier()
-    sync_all()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-    sync_all()
-    comm.barrier()
-    t1 = time.perf_counter()
-    dt = comm.max_float(t1 - t0)
-    dom_live = None
-    if dom:
-        for c in ctxs:
-            got = c.timing_read().get(dom)
-            if got:
-                dom_live = got if dom_live is None else (dom_live[0] + got[0], dom_live[1] + got[1])
-            c.timing(False)
+    dt, res, kern, dom, dom_live = leg.timed(args.steps, args.warmup, not args.no_timing)
     rec = inp["rec"]
     n_reads = int(np.count_nonzero(rec[1:, 0] != rec[:-1, 0])) + 1 if A else 0
 
@@ -206,8 +311,8 @@ def main():
     E = comm.sum_int(res["E_local"])
     # algorithmic bytes per launch; intermediates are diagnostic only
     per_kernel_bytes = {
-        "kmer_profile": packed_bytes + 8 * n_loc * M,
-        "kmer_presence": packed_bytes,
+        "kmer_profile": leg.packed_bytes + 8 * n_loc * M,
+        "kmer_presence": leg.packed_bytes,
         "graph_classify": 8 * A,  # the records, read once
     }
     intermediate_bytes = {
@@ -227,21 +332,40 @@ def main():
                 "traffic": traffic, "bytes_per_launch": b,
                 "intermediate_bytes_per_launch": intermediate_bytes.get(dom, 0),
                 "avg_launch_ms": round(ms / nl, 4), "launches": nl}
-    step_bytes = packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
+    step_bytes = leg.packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
     step_s = dt / args.steps
+    parity = None
+    if not args.no_parity:
+        parity = parity_check(leg, digest_key(args, world, inp["emu"]))
     extra = {}
     if rank == 0 and world == 1 and not args.no_e2e and inp["emu"] == 1 and not args.shuffle_contigs:
-        extra = end_to_end_legs(args, inp, ctx, build, store)
+        extra = end_to_end_legs(args, inp, ctx, leg.build, leg.store)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline != "off":
         cpu = cpu_baseline(inp)
-    build.close()
-    store.close()
-    rec_dev.close()
+    leg.close()
+    del leg
+
+    weak = None
+    if world > 1 and args.strong and not args.no_weak_leg:
+        # weak scaling as an extra key: every rank a whole config-sized share
+        import copy
+
+        wargs = copy.copy(args)
+        wargs.strong = False
+        wl = Leg(wargs, ctx, comm, rank, world)
+        wdt, wres, _, _, _ = wl.timed(args.steps, args.warmup, kernel_timing=False)
+        wunits = comm.sum_int(wl.inp["n_loc"] + wl.inp["f_loc"]) * args.steps
+        weak = {"value": round(wunits / wdt, 1), "unit": "(contigs+fragments)/s",
+                "ms_per_step": round(wdt / args.steps * 1e3, 3), "scaling": "weak",
+                "workload": f"{args.config} per rank: {wl.inp['n_loc']} contigs + {wl.inp['f_loc']} fragments on "
+                            f"each of {world} ranks (global {wl.inp['n_glob']} contigs / {wl.inp['f_glob']} "
+                            f"fragments)"}
+        wl.close()
 
     if rank == 0:
         emu = inp["emu"]
-        ref_py_units_s = (200_000 + 100_000_000) / REF_PY_CONFIG3_S
+        ref = reference_measured(args.config)
         line = {
             "metric": "contigs+reads/sec for k-mer vec + shared-read graph build; HBM GB/s vs roofline",
             "value": round(value, 1),
@@ -252,33 +376,53 @@ def main():
             "ms_per_step": round(step_s * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong" if args.strong else "weak",
-            # BASELINE.md publishes no number; this is the reference Python measured in
-            # the survey container on config 3, see vs_baseline_basis
-            "vs_baseline": round(value / ref_py_units_s, 1) if args.config == "config3" else None,
-            "vs_baseline_basis": (f"reference Python karma/kmer.py:199-264 + read_graph.py:61-148 on config 3 "
-                                  f"(BASELINE.md, survey container, 8 cores): {REF_PY_CONFIG3_S} s = "
-                                  f"{ref_py_units_s:.0f} units/s; not a published number"),
+            # BASELINE.md publishes no number for this metric
+            "vs_baseline": None,
             "dtype": "u32 keys / i64 counts / f64 div",
             "data": "synthetic (SplitMix64 generator, SURVEY.md §8(d))"
                     + (", contig ids shuffled" if args.shuffle_contigs else ""),
-            "config": {"workload": f"{args.config}{' strong' if args.strong else ''}: {n_loc} contigs (mean 800 bp) "
-                                   f"+ {f_loc} {'paired' if inp['paired'] else 'single-end'} fragments on rank 0 "
-                                   f"(global {inp['n_glob']} contigs / {inp['f_glob']} fragments), k={inp['kmer']}",
+            "config": {"workload": f"{args.config}{' strong' if args.strong else ' weak'}: {n_loc} contigs "
+                                   f"(mean 800 bp) + {f_loc} {'paired' if inp['paired'] else 'single-end'} "
+                                   f"fragments on rank 0 (global {inp['n_glob']} contigs / {inp['f_glob']} "
+                                   f"fragments), k={inp['kmer']}",
                        "contigs_rank0": n_loc, "fragments_rank0": f_loc, "records_rank0": A,
                        "columns_M": M, "edges": E, "parallelism": f"contig+fragment shards x{world}",
                        **({"emulated_ranks": emu, "global_contigs": inp["n_glob"]} if emu > 1 else {})},
+            "parity": parity["parity"] if parity else None,
+            "parity_detail": parity,
             "roofline": roof,
             "step": {"hbm_bytes_per_gpu": step_bytes, "achieved_GBs": round(step_bytes / step_s / 1e9, 1),
                      "frac": round(step_bytes / step_s / 1e9 / PEAK_HBM_GBS, 4),
                      "formula": "sum ceil(L/4) + 8*N*M + 8*A + 16*E + 8*N (SURVEY.md 8(d))"},
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in kern.items()},
             "kernels_ms_note": "sequential pass (profile on the main stream), every launch timed",
+            **({"weak": weak} if weak else {}),
             **extra,
             "cpu_baseline": cpu,
+            **({"vs_reference_measured": round(value / ref["units_per_s"], 1),
+                "reference_measured": ref} if ref and args.strong and emu == 1 else {}),
+            "build": build_info,
         }
         print(json.dumps(line), flush=True)
     comm.close()
     ctx.close()
+
+
+def reference_measured(config):
+    """The reference Python timed on this exact workload in the build container
+    (tests/golden/time_reference.py -> profiles/r03/reference_<config>.json):
+    read_fasta_file + __calc_kmer_profile + from_equivalence_classes."""
+    try:
+        with open(os.path.join(REPO, "profiles", "r03", f"reference_{config}.json")) as f:
+            r = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if "units_per_s" not in r:
+        return None
+    return {"units_per_s": r["units_per_s"], "seconds": r["total_s"],
+            "split_s": {k: r[k] for k in ("read_fasta_file_s", "calc_kmer_profile_s", "from_equivalence_classes_s")},
+            "threads": r["threads"], "host": "build container (8 vCPU Xeon), not the GPU box",
+            "source": f"profiles/r03/reference_{config}.json"}
 
 
 def pmc_traffic(args, world, kernel):
@@ -359,6 +503,80 @@ def end_to_end_legs(args, inp, ctx, build, store):
                       "members": int(len(members)), "edges": te[0][1],
                       "includes": "host eq arrays -> H2D -> sort/reduce -> weights -> edges D2H",
                       "value": round((n + inp["f_loc"]) / min(x[0] for x in te), 1)}
+    out["dropin"] = dropin_leg(inp)
+    return out
+
+
+def dropin_files(inp, fasta_path, eq_path):
+    """The workload as the files karma.py reads (karma.py:190, :236): a FASTA
+    with one sequence line per contig (keys ">ctg<i>") and the fragments as a
+    salmon eq_classes.txt (read_graph.py:75-82 format: n_txp, n_eq, n_txp
+    names, then "size<TAB>ids...<TAB>count" lines).  Also written by
+    tests/golden/time_reference.py, which times the reference on the same bytes."""
+    from karma_amd import engine
+
+    n, blob, offs, c_lo = inp["n_loc"], inp["blob"], inp["offs"], inp["c_lo"]
+    seqb = bytes(blob[: int(offs[-1])])
+    with open(fasta_path, "wb") as f:
+        f.write(b"".join(b">ctg%d\n%s\n" % (c_lo + i, seqb[int(offs[i]):int(offs[i + 1])]) for i in range(n)))
+    cls_off, mem, cnt = engine.synth_eq_classes(inp["seed"], inp["n_glob"], inp["f_lo"], inp["f_lo"] + inp["f_loc"],
+                                                inp["paired"], genes=inp["genes"])
+    ids = [str(x) for x in range(inp["n_glob"])]
+    memb = [ids[x] for x in mem.tolist()]
+    offl = cls_off.tolist()
+    lines = [f"{inp['n_glob']}\n{len(cnt)}\n"] + [f"ctg{i}\n" for i in range(inp["n_glob"])]
+    for c, k in enumerate(cnt.tolist()):
+        lo, hi = offl[c], offl[c + 1]
+        lines.append(f"{hi - lo}\t" + "\t".join(memb[lo:hi]) + f"\t{k}\n")
+    with open(eq_path, "w") as f:
+        f.write("".join(lines))
+    return len(cnt)
+
+
+def dropin_leg(inp, reps=2):
+    """The drop-in exactly as karma.py calls it, on files (karma.py:190, :197-210,
+    :240): karma_amd.fasta.read_fasta_file -> KmerClustering(...).
+    _KmerClustering__calc_kmer_profile() (a host float64 ndarray, kmer.py:199-264)
+    and ReadGraph.from_equivalence_classes(eq file, sequences) (an nx.Graph,
+    read_graph.py:61-148).  Best of `reps` after one warm call."""
+    import shutil
+    import tempfile
+
+    from karma_amd.fasta import read_fasta_file
+    from karma_amd.kmer import KmerClustering
+    from karma_amd.read_graph import ReadGraph
+
+    d = tempfile.mkdtemp(prefix="karma_dropin_")
+    try:
+        fa, eq = os.path.join(d, "contigs.fa"), os.path.join(d, "eq_classes.txt")
+        n_cls = dropin_files(inp, fa, eq)
+        best = None
+        for it in range(reps + 1):
+            t0 = time.perf_counter()
+            seqs = read_fasta_file(fa)
+            t1 = time.perf_counter()
+            prof = KmerClustering(seqs, d, inp["kmer"], 16)._KmerClustering__calc_kmer_profile()
+            t2 = time.perf_counter()
+            g = ReadGraph.from_equivalence_classes(eq, seqs)
+            t3 = time.perf_counter()
+            cur = (t3 - t0, t1 - t0, t2 - t1, t3 - t2, prof.shape, g.number_of_nodes(), g.number_of_edges())
+            del prof, g, seqs
+            if it and (best is None or cur[0] < best[0]):
+                best = cur
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    units = inp["n_loc"] + inp["f_loc"]
+    out = {"value": round(units / best[0], 1), "unit": "(contigs+fragments)/s", "seconds": round(best[0], 4),
+           "split_s": {"read_fasta_file": round(best[1], 4), "calc_kmer_profile": round(best[2], 4),
+                       "from_equivalence_classes": round(best[3], 4)},
+           "profile_shape": list(best[4]), "graph_nodes": best[5], "graph_edges": best[6], "eq_classes": n_cls,
+           "includes": "files on local disk -> FASTA parse -> profile as a host ndarray (H2D, kernels, D2H of "
+                       "8*N*M bytes) -> eq parse -> GPU graph -> nx.Graph in the reference's layout"}
+    ref = reference_measured("config3") if (inp["n_loc"], inp["f_loc"]) == (200_000, 100_000_000) else None
+    if ref:
+        out["reference_seconds"] = ref["seconds"]
+        out["speedup_vs_reference"] = round(ref["seconds"] / best[0], 1)
+        out["reference_split_s"] = ref["split_s"]
     return out
 
 

@@ -56,6 +56,10 @@ extern "C" {
 
 int karma_version(void);
 const char* karma_last_error(void);
+/* Build identity as a JSON object: {"arch", "defines" (extra -D flags of a
+ * variant build; "" for the shipped library), "src_sha256_16", "flags"}.
+ * bench.py prints it and refuses a non-default build. */
+const char* karma_build_info(void);
 int karma_device_count(int* n);
 
 /* ---- context: one device, one HIP stream --------------------------------- */

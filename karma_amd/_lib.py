@@ -152,7 +152,7 @@ _SIGS = {
     "karma_repr_f64_host": [_c_p, _i64, _c_p, _i64, _I64P],
 }
 
-EXPORTED = tuple(_SIGS) + ("karma_last_error", "karma_comm_id_bytes")
+EXPORTED = tuple(_SIGS) + ("karma_last_error", "karma_comm_id_bytes", "karma_build_info")
 
 
 class KarmaError(RuntimeError):
@@ -184,8 +184,20 @@ def load():
     lib.karma_last_error.restype = ctypes.c_char_p
     lib.karma_comm_id_bytes.argtypes = []
     lib.karma_comm_id_bytes.restype = ctypes.c_int
+    lib.karma_build_info.argtypes = []
+    lib.karma_build_info.restype = ctypes.c_char_p
     _LIB = lib
     return lib
+
+
+def build_info():
+    """The loaded library's build identity (karma_build_info): arch, extra -D
+    defines of a variant build ("" for the shipped library), source hash."""
+    import json
+
+    info = json.loads(load().karma_build_info().decode())
+    info["library"] = os.path.relpath(LIB_PATH, os.path.dirname(HERE))
+    return info
 
 
 def check(rc):

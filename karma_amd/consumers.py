@@ -21,6 +21,7 @@ computes.
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 
@@ -66,6 +67,11 @@ class NameTable:
 
 SMALL_VIEW = 1024  # nodes of a view copy served by one launch (karma_adj_view_summary)
 _TEXT_BUF = np.empty(1 << 20, np.uint8)  # edge_list bytes of one-launch view summaries
+# karma_adj_view_summary uses the context's one mapped host buffer (order,
+# status word, results) and _TEXT_BUF: one call at a time per process, so that
+# graphs on several threads (a ShardedBuild pool, a caller's workers) cannot
+# overwrite each other's inputs or results
+_SUMMARY_LOCK = threading.Lock()
 
 
 class DeviceAdj:
@@ -124,11 +130,12 @@ class DeviceAdj:
         done = ctypes.c_int(0)
         tl = _lib._i64(0)
         dn, do = names.device() if with_text else (None, None)
-        call("karma_adj_view_summary", self.h, ptr(order), k, dn, do, 1 if with_text else 0, ptr(deg), ptr(w),
-             ptr(_TEXT_BUF) if with_text else None, len(_TEXT_BUF), ctypes.byref(tl), ctypes.byref(done))
-        if not done.value:
-            return None
-        return deg, w, (_TEXT_BUF[:tl.value].tobytes() if with_text else None)
+        with _SUMMARY_LOCK:
+            call("karma_adj_view_summary", self.h, ptr(order), k, dn, do, 1 if with_text else 0, ptr(deg), ptr(w),
+                 ptr(_TEXT_BUF) if with_text else None, len(_TEXT_BUF), ctypes.byref(tl), ctypes.byref(done))
+            if not done.value:
+                return None
+            return deg, w, (_TEXT_BUF[:tl.value].tobytes() if with_text else None)
 
     def keep(self, mask):
         """G.remove_nodes_from(nodes at positions where mask == 0)."""

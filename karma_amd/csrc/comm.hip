@@ -14,6 +14,7 @@
 #include <cstring>
 #include <vector>
 
+#include "comm_group.h"
 #include "karma_internal.h"
 
 struct karma_comm {
@@ -62,11 +63,17 @@ int comm_begin(karma_comm* c) {
     return karma::ctx_begin(c->ctx);
 }
 
+
 }  // namespace
 
 using namespace karma;
 
 namespace {
+int group_rc(int rc, const NcclGroup& g) {
+    if (rc != KARMA_OK) set_error("%s", g.err);
+    return rc;
+}
+
 // Host scalars in and out through mapped host memory, moved by a one-block
 // kernel: a copy launch to or from host memory waits for free CUs and, to
 // host, for the L2 write-back, both slow beside the running profile kernel
@@ -207,12 +214,15 @@ int karma_comm_exchange_counts(karma_comm* c, const int64_t* send_host, int64_t*
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream, static_cast<const uint64_t*>(dm),
                        reinterpret_cast<uint64_t*>(c->counts_dev), W);
     KARMA_HIP(hipGetLastError());
-    KARMA_NCCL(ncclGroupStart());
-    for (int r = 0; r < W; ++r) {
-        KARMA_NCCL(ncclSend(c->counts_dev + r, 1, ncclInt64, r, c->nc, c->ctx->stream));
-        KARMA_NCCL(ncclRecv(c->counts_dev + W + r, 1, ncclInt64, r, c->nc, c->ctx->stream));
+    {
+        NcclGroup g;
+        KARMA_TRY(group_rc(g.start(), g));
+        for (int r = 0; r < W; ++r) {
+            KARMA_GROUP_ADD(g, ncclSend(c->counts_dev + r, 1, ncclInt64, r, c->nc, c->ctx->stream));
+            KARMA_GROUP_ADD(g, ncclRecv(c->counts_dev + W + r, 1, ncclInt64, r, c->nc, c->ctx->stream));
+        }
+        KARMA_TRY(group_rc(g.end(), g));
     }
-    KARMA_NCCL(ncclGroupEnd());
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream,
                        reinterpret_cast<const uint64_t*>(c->counts_dev + W), static_cast<uint64_t*>(dm) + W, W);
     KARMA_HIP(hipGetLastError());
@@ -224,26 +234,25 @@ int karma_comm_exchange_counts(karma_comm* c, const int64_t* send_host, int64_t*
 int karma_comm_alltoallv(karma_comm* c, const void* send_dev, const int64_t* send_off, void* recv_dev,
                          const int64_t* recv_off) {
     KARMA_TRY(comm_begin(c));
-    KARMA_CHECK(send_off && recv_off, KARMA_ERR_ARG, "karma_comm_alltoallv: null offsets");
     const int W = c->world;
-    for (int r = 0; r < W; ++r)
-        KARMA_CHECK(send_off[r + 1] >= send_off[r] && recv_off[r + 1] >= recv_off[r], KARMA_ERR_ARG,
-                    "karma_comm_alltoallv: offsets must not decrease");
-    KARMA_CHECK((send_dev || send_off[W] == 0) && (recv_dev || recv_off[W] == 0), KARMA_ERR_ARG,
-                "karma_comm_alltoallv: null buffer");
+    {
+        char msg[160];
+        KARMA_CHECK(alltoallv_args_ok(W, c->rank, send_dev, send_off, recv_dev, recv_off, msg, sizeof msg),
+                    KARMA_ERR_ARG, "karma_comm_alltoallv: %s", msg);
+    }
     const uint8_t* s = static_cast<const uint8_t*>(send_dev);
     uint8_t* d = static_cast<uint8_t*>(recv_dev);
-    KARMA_NCCL(ncclGroupStart());
-    for (int r = 0; r < W; ++r) {
-        const size_t sb = (size_t)(send_off[r + 1] - send_off[r]), rb = (size_t)(recv_off[r + 1] - recv_off[r]);
-        if (r == c->rank) {
-            KARMA_CHECK(sb == rb, KARMA_ERR_ARG, "karma_comm_alltoallv: own slice %zu != %zu bytes", sb, rb);
-            continue;
+    {
+        NcclGroup g;
+        KARMA_TRY(group_rc(g.start(), g));
+        for (int r = 0; r < W; ++r) {
+            if (r == c->rank) continue;
+            const size_t sb = (size_t)(send_off[r + 1] - send_off[r]), rb = (size_t)(recv_off[r + 1] - recv_off[r]);
+            if (sb) KARMA_GROUP_ADD(g, ncclSend(s + send_off[r], sb, ncclUint8, r, c->nc, c->ctx->stream));
+            if (rb) KARMA_GROUP_ADD(g, ncclRecv(d + recv_off[r], rb, ncclUint8, r, c->nc, c->ctx->stream));
         }
-        if (sb) KARMA_NCCL(ncclSend(s + send_off[r], sb, ncclUint8, r, c->nc, c->ctx->stream));
-        if (rb) KARMA_NCCL(ncclRecv(d + recv_off[r], rb, ncclUint8, r, c->nc, c->ctx->stream));
+        KARMA_TRY(group_rc(g.end(), g));
     }
-    KARMA_NCCL(ncclGroupEnd());
     const size_t own = (size_t)(send_off[c->rank + 1] - send_off[c->rank]);
     if (own)
         KARMA_HIP(hipMemcpyAsync(d + recv_off[c->rank], s + send_off[c->rank], own, hipMemcpyDeviceToDevice,

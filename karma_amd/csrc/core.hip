@@ -144,6 +144,21 @@ extern "C" {
 
 int karma_version(void) { return 1; }
 
+// The build's identity, for the bench line and the default-build check:
+// KARMA_BUILD_DEFINES holds the -D flags a variant build added on top of the
+// Makefile's (empty for the shipped library), KARMA_SRC_HASH the first 16 hex
+// digits of sha256 over the sources (Makefile).
+#ifndef KARMA_BUILD_DEFINES
+#define KARMA_BUILD_DEFINES "unknown (not built by karma_amd/csrc/Makefile)"
+#endif
+#ifndef KARMA_SRC_HASH
+#define KARMA_SRC_HASH "unknown"
+#endif
+const char* karma_build_info(void) {
+    return "{\"arch\": \"gfx950\", \"defines\": \"" KARMA_BUILD_DEFINES "\", \"src_sha256_16\": \"" KARMA_SRC_HASH
+           "\", \"flags\": \"-O3 -ffp-contract=off -fno-fast-math\"}";
+}
+
 const char* karma_last_error(void) { return g_err.c_str(); }
 
 int karma_device_count(int* n) {

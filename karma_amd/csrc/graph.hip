@@ -58,56 +58,6 @@ struct MinOp {
     __device__ __forceinline__ uint64_t operator()(const uint64_t& a, const uint64_t& b) const { return a < b ? a : b; }
 };
 
-// ---- eq classes -----------------------------------------------------------------
-__global__ void eq_totals_kernel(const int64_t* __restrict__ cls_off, const uint32_t* __restrict__ members,
-                                 const int64_t* __restrict__ counts, int64_t n_classes, uint32_t n_contigs,
-                                 unsigned long long* __restrict__ totals, int64_t* __restrict__ pair_cnt,
-                                 const uint8_t* __restrict__ skip, int* __restrict__ bad) {
-    int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_classes) return;
-    const int64_t s = cls_off[c], e = cls_off[c + 1], m = e - s;
-    const unsigned long long cnt = (unsigned long long)counts[c];
-    for (int64_t t = s; t < e; ++t) {
-        const uint32_t x = members[t];
-        if (x >= n_contigs) {
-            *bad = 1;
-            continue;
-        }
-        atomicAdd(&totals[x], cnt);  // two's complement: exact for negative counts too
-    }
-    pair_cnt[c] = (skip && skip[c]) ? 0 : m * (m - 1) / 2;
-}
-
-__global__ void eq_emit_kernel(const int64_t* __restrict__ cls_off, const uint32_t* __restrict__ members,
-                               const int64_t* __restrict__ counts, const int64_t* __restrict__ pair_off,
-                               int64_t n_classes, int64_t P, uint64_t* __restrict__ keys, int64_t* __restrict__ cnt_out) {
-    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P) return;
-    // class = last c with pair_off[c] <= p
-    int64_t lo = 0, hi = n_classes;
-    while (hi - lo > 1) {
-        int64_t mid = (lo + hi) >> 1;
-        if (pair_off[mid] <= p) lo = mid;
-        else hi = mid;
-    }
-    // skip empty classes that share the offset
-    int64_t c = lo;
-    const int64_t t = p - pair_off[c];
-    const int64_t s = cls_off[c], m = cls_off[c + 1] - s;
-    // combinations order: row i holds pairs (i, i+1..m-1); cum(i) = i*m - i*(i+1)/2
-    int64_t il = 0, ih = m - 1;
-    while (ih - il > 1) {
-        int64_t mid = (il + ih) >> 1;
-        if (mid * m - mid * (mid + 1) / 2 <= t) il = mid;
-        else ih = mid;
-    }
-    const int64_t i = il, j = i + 1 + (t - (i * m - i * (i + 1) / 2));
-    const uint32_t a = members[s + i], b = members[s + j];
-    const uint32_t lo2 = min(a, b), hi2 = max(a, b);
-    keys[p] = ((uint64_t)lo2 << 32) | hi2;
-    cnt_out[p] = counts[c];
-}
-
 // ---- finalize --------------------------------------------------------------------
 __global__ void diag_totals_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, int64_t n,
                                    int64_t* __restrict__ totals) {
@@ -254,14 +204,6 @@ __global__ void __launch_bounds__(kET) group_sum_kernel(const uint64_t* __restri
     co[pl.base + pl.rank] = c;
 }
 
-int scan_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
-    size_t tb = 0;
-    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, ctx->stream));
-    DevArray<uint8_t> tmp;
-    KARMA_TRY(tmp.alloc(ctx, tb));
-    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.ptr, tb, in, out, n, ctx->stream));
-    return KARMA_OK;
-}
 
 int grid1(int64_t n, int block = 256) { return (int)std::max<int64_t>(1, ceil_div(n, block)); }
 
@@ -633,72 +575,6 @@ int karma_graph_records(karma_ctx* ctx, const uint32_t* records, int64_t A, int6
     karma_graph_job* job = nullptr;
     KARMA_TRY(karma_graph_records_begin(ctx, records, A, N, flags, is_device, &job));
     return karma_graph_records_end(job, out);
-}
-
-int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
-                   const uint8_t* pair_skip, int64_t C, int64_t N, int is_device, karma_pairs** out) {
-    KARMA_TRY(ctx_begin(ctx));
-    KARMA_CHECK(out && cls_off && C >= 0 && N >= 0 && N < (int64_t(1) << 32), KARMA_ERR_ARG,
-                "karma_graph_eq: bad arguments");
-    int64_t n_mem = 0;
-    if (is_device) {
-        KARMA_HIP(hipMemcpyAsync(&n_mem, cls_off + C, 8, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    } else {
-        n_mem = cls_off[C];
-    }
-    DevArray<int64_t> d_off, d_cnt;
-    DevArray<uint32_t> d_mem;
-    DevArray<uint8_t> d_skip;
-    KARMA_TRY(d_off.alloc(ctx, C + 1));
-    KARMA_TRY(d_cnt.alloc(ctx, C));
-    KARMA_TRY(d_mem.alloc(ctx, n_mem));
-    KARMA_TRY(d_skip.alloc(ctx, C));
-    const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    KARMA_HIP(hipMemcpyAsync(d_off.ptr, cls_off, (C + 1) * 8, kind, ctx->stream));
-    if (C) KARMA_HIP(hipMemcpyAsync(d_cnt.ptr, counts, C * 8, kind, ctx->stream));
-    if (n_mem) KARMA_HIP(hipMemcpyAsync(d_mem.ptr, members, n_mem * 4, kind, ctx->stream));
-    if (C) {
-        if (pair_skip) KARMA_HIP(hipMemcpyAsync(d_skip.ptr, pair_skip, C, kind, ctx->stream));
-        else KARMA_HIP(hipMemsetAsync(d_skip.ptr, 0, C, ctx->stream));
-    }
-    auto* p = new karma_pairs();
-    p->ctx = ctx;
-    p->n_contigs = N;
-    std::unique_ptr<karma_pairs> guard(p);
-    KARMA_TRY(p->totals.alloc(ctx, N));
-    p->has_totals = true;
-    if (N) KARMA_HIP(hipMemsetAsync(p->totals.ptr, 0, N * 8, ctx->stream));
-    DevArray<int64_t> pc, poff;
-    DevArray<int> bad;
-    KARMA_TRY(pc.alloc(ctx, C + 1));
-    KARMA_TRY(poff.alloc(ctx, C + 1));
-    KARMA_TRY(bad.alloc(ctx, 1));
-    KARMA_HIP(hipMemsetAsync(bad.ptr, 0, 4, ctx->stream));
-    KARMA_HIP(hipMemsetAsync(pc.ptr + C, 0, 8, ctx->stream));
-    if (C)
-        KARMA_LAUNCH(ctx, "eq_totals", eq_totals_kernel, grid1(C), 256, 0, d_off.ptr, d_mem.ptr, d_cnt.ptr, C,
-                     (uint32_t)N, (unsigned long long*)p->totals.ptr, pc.ptr, d_skip.ptr, bad.ptr);
-    KARMA_TRY(scan_i64(ctx, pc.ptr, poff.ptr, C + 1));
-    int64_t P = 0;
-    int hbad = 0;
-    KARMA_HIP(hipMemcpyAsync(&P, poff.ptr + C, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipMemcpyAsync(&hbad, bad.ptr, 4, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    KARMA_CHECK(!hbad, KARMA_ERR_ARG, "eq class member index >= n_contigs");
-    DevArray<uint64_t> keys;
-    DevArray<int64_t> cnts;
-    KARMA_TRY(keys.alloc(ctx, P));
-    KARMA_TRY(cnts.alloc(ctx, P));
-    if (P)
-        KARMA_LAUNCH(ctx, "eq_emit", eq_emit_kernel, grid1(P), 256, 0, d_off.ptr, d_mem.ptr, d_cnt.ptr, poff.ptr, C,
-                     P, keys.ptr, cnts.ptr);
-    int key_bits = 32;
-    while (key_bits < 64 && (int64_t(1) << (key_bits - 32)) < N) ++key_bits;
-    KARMA_TRY(sort_reduce_pairs(ctx, keys.ptr, cnts.ptr, nullptr, P, key_bits, p->keys, p->counts, &p->first, &p->n));
-    p->has_first = true;
-    *out = guard.release();
-    return KARMA_OK;
 }
 
 int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, int64_t n, int is_device,

@@ -87,9 +87,6 @@ constexpr int kNarrowB = 512, kNarrowBc = 128;
 #ifndef KARMA_CR_PIPE
 #define KARMA_CR_PIPE 1  // code reduce: barrier-free run stream with the next batch's bounds prefetched (one GPU: 91 -> 75 us)
 #endif
-#ifndef KARMA_CR_ABLATE
-#define KARMA_CR_ABLATE 0  // diagnostic builds only: 1 = no LDS adds, 2 = no run stream
-#endif
 #ifndef KARMA_CG_SHIFT
 #define KARMA_CG_SHIFT 18  // a code bucket gets one reduce group per 2^18 records it may hold
 #endif
@@ -1206,14 +1203,11 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
     // m0_local >> 2, so that codes of one wave instruction spread over all 32
     // banks (unswizzled, the bank is (m0 & 3) << 3 | M, and M is mostly 0)
     auto slot = [](uint32_t c) { return c ^ ((c >> 5) & 31u); };
-    uint32_t sink = 0;  // KARMA_CR_ABLATE == 1 (diagnostic): loads kept, no LDS adds
     auto add = [&](uint32_t c) {
-        if (KARMA_CR_ABLATE == 1)
-            sink += c;
-        else if (c != CodeStream::kPadV)
+        if (c != CodeStream::kPadV)
             __hip_atomic_fetch_add(&h[slot(c)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    if (KARMA_CR_ABLATE != 2) stream_runs(
+    stream_runs(
         reinterpret_cast<const u32x4*>(cent), f_lo * S, f_hi * S, kCRT,
         [&](int64_t v, int64_t* beg, uint32_t* len) {
             const int64_t f = v / S;
@@ -1232,7 +1226,6 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
     __syncthreads();
     uint32_t* out = part_ch + (int64_t)blockIdx.x * hn;
     for (int i = threadIdx.x; i < hn; i += kCRT) out[i] = h[slot(i)];
-    if (KARMA_CR_ABLATE == 1 && sink == 0x9E3779B9u) out[0] = sink;
 }
 
 // ---- pair reduce --------------------------------------------------------------------

@@ -152,6 +152,10 @@ int sort_reduce_pairs(karma_ctx* ctx, const uint64_t* keys_in, const int64_t* co
                       int64_t n, int key_bits, DevArray<uint64_t>& keys_out, DevArray<int64_t>& counts_out,
                       DevArray<uint64_t>* first_out, int64_t* n_out);
 
+// Exclusive scan out[i] = in[0] + ... + in[i - 1], i < n, on ctx's stream
+// (hand-written, eq.hip).
+int scan_i64_device(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);
+
 }  // namespace karma
 
 struct karma_pairs {

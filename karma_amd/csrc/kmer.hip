@@ -474,10 +474,6 @@ constexpr int kWaveMaxM = 4096;
 #define KARMA_PROF_C16 1
 #endif
 typedef double d2 __attribute__((ext_vector_type(2)));
-#ifndef KARMA_PROF_ABLATE
-#define KARMA_PROF_ABLATE 0  // diagnostic builds only (tools/build_variant.sh): 1 rows only, 2 counting only,
-                             // 3 rows only without the quotient divisions, 4 as 3 without the prefetch loads
-#endif
 #ifndef KARMA_ROW_AUX
 // cache policy of the profile's 16-byte row stores, as buffer stores (-1: global
 // stores, non-temporal per KARMA_PROF_NT).  18 = sc1 | nt: profile 0.361 -> 0.348 ms;
@@ -631,11 +627,7 @@ __device__ __forceinline__ void write_row_wave(double* __restrict__ row, uint32_
                                                int32_t klen, int* __restrict__ err, double* __restrict__ lut,
                                                int lane) {
     const double len = (double)klen;
-#if KARMA_PROF_ABLATE >= 3  // diagnostic builds: no division for the table
-    lut[lane] = (double)lane;
-#else
     lut[lane] = lane ? (double)lane / len : 0.0;  // IEEE correctly rounded (kmer.py:120)
-#endif
     wave_lds_sync();
     auto val = [&](uint32_t a) {
         double v = lut[min(a, 63u)];
@@ -784,8 +776,7 @@ profile_wave_kernel(
         meta(c + stride, nxt);
         const int64_t L = cur.L;
         unsigned my = 0;
-        if (KARMA_PROF_ABLATE == 1 || KARMA_PROF_ABLATE >= 3) {  // diagnostic build: rows only, no counting
-        } else if (!cur.exc) {
+        if (!cur.exc) {
             count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
         } else {
             // a contig with exception bases: windows that touch one are keyed by
@@ -814,16 +805,11 @@ profile_wave_kernel(
                 }
             }, &st0);
         }
-        if (KARMA_PROF_ABLATE < 4 && c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
+        if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
         // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
         my = wave_total(my);
-#if KARMA_PROF_ABLATE == 2  // diagnostic build: counting only, no rows
-        if (lane == 0) row_tot[c] = (int64_t)my;
-        for (int j = lane; j < h_words; j += 64) counts[j] = 0;
-#else
         if (lane == 0) row_tot[c] = (int64_t)my;
         write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
-#endif
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         cur = nxt;

@@ -58,61 +58,129 @@ def _unpack(b: bytes) -> np.ndarray:
     return np.frombuffer(b[1 + n:], dtype=dt).copy()
 
 
+_HELLO = b"KRMA"
+
+
+def _is_local(addr):
+    return addr in ("127.0.0.1", "localhost", "::1", "0.0.0.0") or addr == socket.gethostname()
+
+
 class SocketGroup:
     """TCP star: rank 0 listens on (addr, port), the others connect.
 
     allgather: every rank sends its array to rank 0, which returns the list of
-    all of them to every rank.  Message sizes are whatever the arrays hold."""
+    all of them to every rank.  Message sizes are whatever the arrays hold.
 
-    def __init__(self, world, rank, addr="127.0.0.1", port=29600, timeout=300.0):
+    Port: `port` is tried first.  When it is taken and `handshake` names a file
+    (single-node jobs, from_env), rank 0 listens on a free port instead and
+    publishes it there (atomic rename); the other ranks re-read that file on
+    every connect attempt.  A connection is accepted only after a 4-byte hello
+    both ways, so a stale file or a foreign listener is retried, not trusted.
+    Without a handshake file a taken port fails at once, naming
+    KARMA_GROUP_PORT.  The other ranks give up after `timeout` seconds."""
+
+    def __init__(self, world, rank, addr="127.0.0.1", port=29600, timeout=120.0, handshake=None):
         self.world, self.rank = world, rank
         self.peers = {}
         self.sock = None
+        self.handshake = None
         if world == 1:
             return
         if rank == 0:
-            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
-            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-            srv.bind((addr, port))
-            srv.listen(world)
-            srv.settimeout(timeout)
-            try:
-                while len(self.peers) < world - 1:
-                    c, _ = srv.accept()
-                    c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    c.settimeout(None)
-                    (r,) = struct.unpack("<i", _recv_exact(c, 4))
-                    if not 0 < r < world or r in self.peers:
-                        c.close()
-                        raise ConnectionError(f"host group: unexpected rank {r}")
-                    self.peers[r] = c
-            finally:
-                srv.close()
+            self._serve(addr, port, timeout, handshake)
         else:
-            deadline = time.time() + timeout
-            while True:
+            self._connect(addr, port, timeout, handshake)
+
+    def _serve(self, addr, port, timeout, handshake):
+        srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        try:
+            srv.bind((addr, port))
+        except OSError as e:
+            if handshake is None:
+                srv.close()
+                raise OSError(e.errno, f"host group: rank 0 cannot listen on {addr}:{port} ({e.strerror}); "
+                                       f"set KARMA_GROUP_PORT to a free port") from e
+            srv.bind((addr, 0))
+        port = srv.getsockname()[1]
+        if handshake is not None:
+            tmp = f"{handshake}.{os.getpid()}.tmp"
+            with open(tmp, "w") as f:
+                f.write(str(port))
+            os.replace(tmp, handshake)
+            self.handshake = handshake
+        srv.listen(self.world)
+        srv.settimeout(timeout)
+        try:
+            while len(self.peers) < self.world - 1:
+                c, _ = srv.accept()
+                c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                c.settimeout(30.0)
                 try:
-                    s = socket.create_connection((addr, port), timeout=10)
-                    break
-                except OSError:
-                    if time.time() > deadline:
-                        raise
-                    time.sleep(0.05)
-            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            s.settimeout(None)
-            s.sendall(struct.pack("<i", rank))
-            self.sock = s
+                    hello = _recv_exact(c, 8)
+                except (OSError, ConnectionError):
+                    c.close()
+                    continue
+                (r,) = struct.unpack("<i", hello[4:])
+                if hello[:4] != _HELLO or not 0 < r < self.world or r in self.peers:
+                    c.close()
+                    continue
+                c.sendall(_HELLO)
+                c.settimeout(None)
+                self.peers[r] = c
+        finally:
+            srv.close()
+
+    def _connect(self, addr, port, timeout, handshake):
+        deadline = time.time() + timeout
+        while True:
+            p = port
+            if handshake is not None:
+                try:
+                    with open(handshake) as f:
+                        p = int(f.read().strip() or port)
+                except (OSError, ValueError):
+                    pass
+            try:
+                s = socket.create_connection((addr, p), timeout=5)
+                s.settimeout(10.0)
+                s.sendall(_HELLO + struct.pack("<i", self.rank))
+                if _recv_exact(s, 4) != _HELLO:
+                    raise ConnectionError("not a karma host group")
+                break
+            except (OSError, ConnectionError):
+                try:
+                    s.close()
+                except Exception:
+                    pass
+                if time.time() > deadline:
+                    raise TimeoutError(f"host group: rank {self.rank} could not reach rank 0 at {addr}:{p} within "
+                                       f"{timeout:.0f} s (KARMA_GROUP_PORT / KARMA_GROUP_TIMEOUT)")
+                time.sleep(0.05)
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        s.settimeout(None)
+        self.sock = s
 
     @classmethod
     def from_env(cls, world=None, rank=None):
         """Ranks started by a launcher (torchrun): RANK / WORLD_SIZE / MASTER_ADDR,
-        port KARMA_GROUP_PORT or MASTER_PORT + 1 (torchrun's own store holds
-        MASTER_PORT)."""
+        port KARMA_GROUP_PORT, else MASTER_PORT + 1 (torchrun's own store holds
+        MASTER_PORT) with a handshake file in the temp directory when the job is
+        on this node, so a taken port moves instead of stalling the job."""
+        import tempfile
+
         world = int(os.environ.get("WORLD_SIZE", "1")) if world is None else world
         rank = int(os.environ.get("RANK", "0")) if rank is None else rank
         addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-        port = int(os.environ.get("KARMA_GROUP_PORT") or int(os.environ.get("MASTER_PORT", "29500")) + 1)
-        return cls(world, rank, addr, port)
+        timeout = float(os.environ.get("KARMA_GROUP_TIMEOUT", "120"))
+        fixed = os.environ.get("KARMA_GROUP_PORT")
+        mport = int(os.environ.get("MASTER_PORT", "29500"))
+        port = int(fixed) if fixed else mport + 1
+        handshake = None
+        if not fixed and _is_local(addr):
+            run = os.environ.get("TORCHELASTIC_RUN_ID", "none")
+            handshake = os.path.join(tempfile.gettempdir(), f"karma_group_{run}_{mport}.port")
+        return cls(world, rank, addr, port, timeout=timeout, handshake=handshake)
 
     def allgather(self, arr) -> list:
         arr = np.asarray(arr)
@@ -145,6 +213,12 @@ class SocketGroup:
         for c in self.peers.values():
             c.close()
         self.peers = {}
+        if self.handshake is not None:
+            try:
+                os.remove(self.handshake)
+            except OSError:
+                pass
+            self.handshake = None
         if self.sock is not None:
             self.sock.close()
             self.sock = None

@@ -86,6 +86,51 @@ def _parse_eq_text(equivalence_class_file):
     return names, off, np.array(members, np.uint32), counts, skip
 
 
+def _copied_graph(cls, nodes, a, b, w):
+    """cls(incoming_graph_data=G) for the graph G the reference builds:
+        G = nx.Graph(); G.add_nodes_from(nodes)
+        for i: G.add_edge(nodes[a[i]], nodes[b[i]], weight=w[i])
+    built directly, without G.  nodes must be distinct and (a[i], b[i]) pairs
+    unique.  The copy is networkx's from_dict_of_dicts(G.adj): nodes in G's
+    order, then add_edges_from over (u, v) for u in G, v in G.adj[u].  So the
+    copy's adj[u] holds first the neighbours v placed before u (met while
+    walking v's list), by position, then the rest in G.adj[u] order, which is
+    add_edge order.  Every edge gets its own {"weight": w} dict, shared by both
+    directions, and every node an empty attribute dict, as in the copy."""
+    import gc
+
+    enabled = gc.isenabled()
+    gc.disable()  # ~2 x 200k new dicts: collector passes would cost ~30 %
+    try:
+        return _copied_graph_body(cls, nodes, a, b, w)
+    finally:
+        if enabled:
+            gc.enable()
+
+
+def _copied_graph_body(cls, nodes, a, b, w):
+    n = len(nodes)
+    a = np.asarray(a, np.int64)
+    b = np.asarray(b, np.int64)
+    lo, hi = np.minimum(a, b), np.maximum(a, b)
+    nm = np.empty(n, dtype=object)
+    nm[:] = nodes
+    adj = {x: {} for x in nodes}
+    dds = [{"weight": x} for x in np.asarray(w).tolist()]
+    # neighbours placed before u: per u, by position
+    o = np.lexsort((lo, hi))
+    o = o[lo[o] < hi[o]]
+    for u, v, i in zip(nm[hi[o]].tolist(), nm[lo[o]].tolist(), o.tolist()):
+        adj[u][v] = dds[i]
+    # the rest (and self-loops), in add_edge order
+    for u, v, d in zip(nm[lo].tolist(), nm[hi].tolist(), dds):
+        adj[u][v] = d
+    out = cls()
+    out._node = {x: {} for x in nodes}
+    out._adj = adj
+    return out
+
+
 def _invalidating(name):
     base = getattr(nx.Graph, name)
 
@@ -177,21 +222,28 @@ class ReadGraph(nx.Graph):
         edge with weight (s/|A| + s/|B|) / 2; computed on the GPU from the
         (read, contig) incidence instead of the O(N^2) pair loop."""
         logger.debug("Initial graph calculation.")
-        graph = nx.Graph()
         n = len(contigs)
-        if n >= 2:
-            rec, _ = contig_records(contigs)
-            e = _edges_or_zero_div(engine.graph_from_records, rec, n, grouped=False)
-            names = [c.name for c in contigs]
-            # combinations order: row 0 touches every contig, so nodes appear
-            # in list order; edges are added in (i, j) order = sorted order
-            graph.add_nodes_from(names)
-            for a, b, w in zip(e.a.tolist(), e.b.tolist(), e.weight.tolist()):
-                graph.add_edge(names[a], names[b], weight=w)
-        out = cls(incoming_graph_data=graph)
-        if n >= 2 and len(out) == n:  # distinct names: positions = list indices
-            out._mirror_spec = ("edges", names, e.a, e.b, e.weight)
-        return out
+        if n < 2:
+            return cls(incoming_graph_data=nx.Graph())
+        rec, _ = contig_records(contigs)
+        e = _edges_or_zero_div(engine.graph_from_records, rec, n, grouped=False)
+        names = [c.name for c in contigs]
+        # combinations order: row 0 touches every contig, so nodes appear
+        # in list order; edges are added in (i, j) order = sorted order
+        return cls._from_edge_list(names, e.a, e.b, e.weight)
+
+    @classmethod
+    def _from_edge_list(cls, names, a, b, w):
+        """The reference's add_nodes_from(names) + add_edge loop + cls(...) copy."""
+        if len(set(names)) == len(names):  # distinct names: positions = list indices
+            out = _copied_graph(cls, names, a, b, w)
+            out._mirror_spec = ("edges", list(names), a, b, np.asarray(w, np.float64))
+            return out
+        graph = nx.Graph()
+        graph.add_nodes_from(names)
+        for x, y, wt in zip(np.asarray(a).tolist(), np.asarray(b).tolist(), np.asarray(w).tolist()):
+            graph.add_edge(names[x], names[y], weight=wt)
+        return cls(incoming_graph_data=graph)
 
     @classmethod
     def from_sam(cls, sam, skip_headers: bool = True, threads: int = 0) -> "ReadGraph":
@@ -199,17 +251,11 @@ class ReadGraph(nx.Graph):
         grouped by RNAME in order of first appearance) without building Python
         readsets: the C++ reader's (read, contig) records go straight to the GPU."""
         rec, _ = load_sam_records(sam, skip_headers, threads)
-        graph = nx.Graph()
         names = rec.rnames
-        if len(names) >= 2:
-            e = _edges_or_zero_div(engine.graph_from_records, rec.records, len(names), grouped=False)
-            graph.add_nodes_from(names)
-            for a, b, w in zip(e.a.tolist(), e.b.tolist(), e.weight.tolist()):
-                graph.add_edge(names[a], names[b], weight=w)
-        out = cls(incoming_graph_data=graph)
-        if len(names) >= 2:
-            out._mirror_spec = ("edges", list(names), e.a, e.b, e.weight)
-        return out
+        if len(names) < 2:
+            return cls(incoming_graph_data=nx.Graph())
+        e = _edges_or_zero_div(engine.graph_from_records, rec.records, len(names), grouped=False)
+        return cls._from_edge_list(list(names), e.a, e.b, e.weight)
 
     def set_original_contigs(self, original_contigs: list) -> None:
         self.original_contigs = original_contigs
@@ -223,25 +269,25 @@ class ReadGraph(nx.Graph):
             e = None
         else:
             e = _edges_or_zero_div(engine.graph_from_eq, off, members, counts, skip, n)
-        weighted_graph = nx.Graph()
-        weighted_graph.add_nodes_from(names)
-        ea = eb = ew = np.zeros(0, np.uint32)
+        ea = eb = np.zeros(0, np.uint32)
+        ew = np.zeros(0, np.float64)
         if e is not None and len(e.a):
-            # the reference's intermediate graph yields edge (u, v) from its
-            # lower-index endpoint u, in first-insertion order (read_graph.py:120)
+            # the reference's intermediate graph (read_graph.py:96-131) gets edge
+            # (u, v) from its lower-index endpoint u, in first-insertion order
             order = np.lexsort((e.first, e.a))
             ea, eb, ew = e.a[order], e.b[order], e.weight[order]
-            for x, y, wt in zip(ea.tolist(), eb.tolist(), ew.tolist()):
-                weighted_graph.add_edge(names[x], names[y], weight=wt)
-        assert len(weighted_graph.nodes()) == n
+        # read_graph.py:136-143: FASTA names missing from the eq file become
+        # isolated nodes, in the order of this set difference (hash seed
+        # dependent, as in the reference); eq names are distinct (:93 assert)
+        eq_names = set(names)
         original_sequence_names = set([name.lstrip(">") for name in sequences_from_fasta.keys()])
-        for missing_node in original_sequence_names.difference(set(weighted_graph.nodes())):
-            weighted_graph.add_node(missing_node)
-        assert len(weighted_graph.nodes()) == len(sequences_from_fasta), (
+        nodes = list(names) + list(original_sequence_names.difference(eq_names))
+        assert len(nodes) == len(sequences_from_fasta), (
             "The read graph has not enough nodes. Maybe Salmon could couldn't add all contigs to a equivalence class")
-        out = cls(incoming_graph_data=weighted_graph)
-        # node order: the eq names (positions 0..n-1), then the FASTA-only nodes
-        out._mirror_spec = ("edges", list(out), ea, eb, np.asarray(ew, np.float64))
+        # cls(incoming_graph_data=weighted_graph) (read_graph.py:148), built
+        # directly in the layout that copy has
+        out = _copied_graph(cls, nodes, ea, eb, ew)
+        out._mirror_spec = ("edges", nodes, ea, eb, np.asarray(ew, np.float64))
         return out
 
     def update_graph(self, contigs: list) -> None:

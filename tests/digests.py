@@ -11,7 +11,13 @@ The encodings follow SURVEY.md §8(c) golden plan item (iii):
   totals    i64 per-contig fragment totals [n_contigs]   (read_graph.py:86-92)
   profile_blocks  sha256 of the concatenated sha256 digests of the profile's
             BLOCK_ROWS-row blocks (a checksum of checksums: hashed in parallel)
+  profile_rows    sha256 of the concatenated sha256 digests of the profile's
+            rows: independent of how the rows are sharded, so the ranks of a
+            multi-GPU run hash their own rows and rank 0 combines 32 B per row
+            (bench.py's in-run parity check)
 Large arrays are hashed in place (memoryview), so a 16 GB profile needs no copy.
+bench.py imports this module for its in-run parity check (hashing only; it
+never imports the oracle outside its cpu_baseline leg).
 """
 
 import hashlib
@@ -73,6 +79,29 @@ def columns_digest(cols):
 def profile_digest(prof):
     assert prof.dtype == np.float64 and prof.flags.c_contiguous
     return sha(prof)
+
+
+def row_digests(prof, threads=8):
+    """bytes: the sha256 digest of every row of a C-order float64 [n, M] array,
+    in row order (hashed on a thread pool; hashlib releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    assert prof.dtype == np.float64 and prof.flags.c_contiguous and prof.ndim == 2
+    n = prof.shape[0]
+    mv = memoryview(prof.reshape(n, -1)).cast("B")
+    row_b = prof.shape[1] * 8
+
+    def blk(lo):
+        hi = min(n, lo + BLOCK_ROWS)
+        return b"".join(hashlib.sha256(mv[i * row_b:(i + 1) * row_b]).digest() for i in range(lo, hi))
+
+    with ThreadPoolExecutor(threads) as pool:
+        return b"".join(pool.map(blk, range(0, n, BLOCK_ROWS)))
+
+
+def profile_rows_digest(prof=None, rows=None):
+    """sha256 over the per-row digests (of `prof`, or given as `rows` bytes)."""
+    return hashlib.sha256(row_digests(prof) if rows is None else rows).hexdigest()
 
 
 def edge_digests(a, b, weight, shared=None, totals=None):

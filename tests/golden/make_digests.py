@@ -75,17 +75,19 @@ def oracle_workload(name):
     # plus the digest of per-block digests (D.BLOCK_ROWS rows each), which the
     # GPU test can hash on several threads
     h = hashlib.sha256()
-    blocks = []
+    blocks, rows = [], []
     offs, key_len, n = inp["offs"], inp["key_len"], inp["n_loc"]
     for lo in range(0, n, D.BLOCK_ROWS):
         hi = min(n, lo + D.BLOCK_ROWS)
         blk = oracle.omp_kmer_profile_packed(inp["blob"], offs[lo:hi + 1], key_len[lo:hi], kmer, raw, M)
         h.update(memoryview(blk).cast("B"))
         blocks.append(hashlib.sha256(memoryview(blk).cast("B")).digest())
+        rows.append(D.row_digests(blk))
         del blk
     out = {"bench_args": D.WORKLOADS[name], "N": inp["n_loc"], "n_glob": n_glob, "c_lo": inp["c_lo"],
            "fragments": inp["f_loc"], "kmer": kmer, "M": int(M), "columns": D.columns_digest(cols),
-           "profile": h.hexdigest(), "profile_blocks": hashlib.sha256(b"".join(blocks)).hexdigest()}
+           "profile": h.hexdigest(), "profile_blocks": hashlib.sha256(b"".join(blocks)).hexdigest(),
+           "profile_rows": D.profile_rows_digest(rows=b"".join(rows))}
     t1 = time.time()
     rec = inp["rec"]
     starts = np.flatnonzero(np.r_[True, rec[1:, 0] != rec[:-1, 0]])

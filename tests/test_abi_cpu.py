@@ -67,3 +67,26 @@ def test_no_cpu_fallback_without_device():
     import pytest
     with pytest.raises(_lib.KarmaError):
         engine.kmer_profile({">a": "ACGTACGT"}, 5)
+
+
+def test_default_build_is_auditable():
+    # the shipped library adds no -D flags (a variant from tools/build_variant.sh
+    # records its flags and bench.py refuses it), and its source hash is the
+    # hash of the sources in the tree
+    import hashlib
+    import glob
+
+    info = _lib.build_info()
+    assert info["arch"] == "gfx950"
+    assert info["defines"] == ""
+    csrc = os.path.join(REPO, "karma_amd", "csrc")
+    srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))
+                  + glob.glob(os.path.join(csrc, "*.cpp")) + [os.path.join(REPO, "include", "karma.h")],
+                  key=lambda p: os.path.relpath(p, csrc))
+    h = hashlib.sha256()
+    for p in srcs:
+        h.update(open(p, "rb").read())
+    assert info["src_sha256_16"] == h.hexdigest()[:16], "libkarma_hip.so is stale: rebuild (make -C karma_amd/csrc)"
+    # no work-removing diagnostic switches in the product kernels
+    for p in srcs:
+        assert "ABLATE" not in open(p).read(), p

@@ -325,3 +325,46 @@ def test_host_comm_collectives(kind, tmp_path):
         assert np.array_equal(o["slices"], np.array([0, 1, 20, 21, 22, 23, 24], np.int64))
         assert o["recv"] == [r + 1] * world
         assert np.array_equal(o["a2a"], np.concatenate([np.full(r + 1, 100 * s + r) for s in range(world)]))
+
+
+def test_socket_group_moves_off_a_taken_port(tmp_path):
+    """MASTER_PORT + 1 held by a foreign listener: rank 0 listens on a free port
+    and publishes it through the handshake file; the others find it there.  The
+    foreign listener (no hello) is never taken for rank 0."""
+    import threading
+
+    base = free_port()
+    squat = socket.socket()
+    squat.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    squat.bind(("127.0.0.1", base))
+    squat.listen(8)
+    hs = str(tmp_path / "group.port")
+    world, outs = 3, [None] * 3
+
+    def t(r):
+        g = SocketGroup(world, r, "127.0.0.1", base, timeout=30, handshake=hs)
+        outs[r] = [int(x[0]) for x in g.allgather(np.array([10 + r]))]
+        g.close()
+
+    ts = [threading.Thread(target=t, args=(r,)) for r in range(world)]
+    for x in ts:
+        x.start()
+    for x in ts:
+        x.join(60)
+    squat.close()
+    assert outs == [[10, 11, 12]] * world
+    assert not os.path.exists(hs)  # rank 0 removes it at close
+
+
+def test_socket_group_taken_port_fails_fast_without_handshake():
+    base = free_port()
+    squat = socket.socket()
+    squat.bind(("127.0.0.1", base))
+    squat.listen(1)
+    import time as _t
+
+    t0 = _t.time()
+    with pytest.raises(OSError, match="KARMA_GROUP_PORT"):
+        SocketGroup(2, 0, "127.0.0.1", base, timeout=30)
+    assert _t.time() - t0 < 5
+    squat.close()

@@ -190,12 +190,11 @@ def _free_port_pair():
     raise RuntimeError("no free port pair")
 
 
-def test_bench_under_torch_distributed_run_two_ranks():
-    """The driver's multi-GPU launch (`python -m torch.distributed.run
-    --nproc-per-node N ... bench.py --gpus N`) rehearsed with 2 ranks on the
-    one device: the rank processes bootstrap through hostgroup (MASTER_PORT + 1),
-    exchange through the host-staged transport (RCCL refuses two ranks on one
-    device) and rank 0 prints exactly one JSON line with the whole-job value."""
+def _bench_two_ranks(*extra, timeout=240):
+    """bench.py under the driver's launch (`python -m torch.distributed.run
+    --nproc-per-node 2 ... bench.py --gpus 2`), both ranks on the one device:
+    bootstrap through hostgroup, exchange through the host-staged transport
+    (RCCL refuses two ranks on one device).  Returns the one JSON line."""
     import json
     import os
 
@@ -204,11 +203,34 @@ def test_bench_under_torch_distributed_run_two_ranks():
     port = _free_port_pair()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--config", "tiny"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=repo, env=env)
+           os.path.join(repo, "bench.py"), "--gpus", "2", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=repo, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
-    res = json.loads(lines[0])
-    assert res["n_gpus"] == 2 and res["steps"] == 2 and res["scaling"] == "weak"
+    return json.loads(lines[0])
+
+
+def test_bench_under_torch_distributed_run_two_ranks():
+    """Rank 0 prints exactly one JSON line: the strong headline (BASELINE
+    configs[3] shape) with the whole-job value, and the weak leg as an extra key."""
+    res = _bench_two_ranks("--steps", "2", "--warmup", "1", "--config", "tiny")
+    assert res["n_gpus"] == 2 and res["steps"] == 2 and res["scaling"] == "strong"
     assert res["value"] > 0 and res["ms_per_step"] > 0
+    assert res["weak"]["scaling"] == "weak" and res["weak"]["value"] > 0
+    assert res["config"]["contigs_rank0"] == 2500  # tiny's 5,000 contigs split 2 ways
+    assert res["build"]["defines"] == ""
+
+
+def test_bench_strong_config3_two_ranks_in_run_parity():
+    """The driver's N > 1 headline on BASELINE configs[3]'s workload split over
+    2 ranks: bench.py's in-run digest check (every rank hashes its profile rows,
+    rank 0 combines them with the ranks' edges and totals) must match
+    tests/golden/digests.json config3 -- the oracle's digests, which the
+    reference's own config-3 outputs also match."""
+    res = _bench_two_ranks("--steps", "1", "--warmup", "1", "--no-weak-leg", "--no-timing", "--cpu-baseline", "off",
+                           timeout=600)
+    assert res["scaling"] == "strong" and res["config"]["contigs_rank0"] == 100_000
+    d = res["parity_detail"]
+    assert res["parity"] is True, d
+    assert d["ranks"] == 2 and d["edges"] == 199_510 and d["mismatch"] == []

@@ -12,7 +12,11 @@ OUT=$REPO/karma_amd/variants
 B=$OUT/build_$NAME
 mkdir -p $B
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result -Wno-unused-value"
-for f in core kmer graph graph_sets consumers comm; do
+HASH=$(cat $(ls $SRC/*.hip $SRC/*.h $SRC/*.cpp $REPO/include/karma.h | sort) | sha256sum | cut -c1-16)
+# the variant's -D flags are recorded in karma_build_info() (bench.py refuses
+# a variant unless KARMA_ALLOW_VARIANT=1)
+/opt/rocm/bin/hipcc $FLAGS $EXTRA -DKARMA_BUILD_DEFINES="\"$EXTRA\"" -DKARMA_SRC_HASH="\"$HASH\"" -c $SRC/core.hip -o $B/core.o &
+for f in kmer graph graph_sets eq consumers comm; do
   /opt/rocm/bin/hipcc $FLAGS $EXTRA -c $SRC/$f.hip -o $B/$f.o &
 done
 wait
