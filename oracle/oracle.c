@@ -62,6 +62,7 @@ typedef void (*emit_fn)(void* ctx, const okey_t* k);
 static int64_t enum_kmers(const uint8_t* s, int64_t L, int kmode, emit_fn emit, void* ctx) {
     int64_t n = 0;
     okey_t k;
+    memset(&k, 0, sizeof k); /* bytes past len stay zero in the emitted keys */
     if (kmode == -1) {
         for (int64_t i = 0; i + 5 <= L; ++i) { /* kmer.py:72-73 */
             k.len = 5;
@@ -366,6 +367,45 @@ int oracle_threads(void) {
 #else
     return 1;
 #endif
+}
+
+/* oracle_kmer_columns over contigs in parallel: every thread keeps the sorted
+ * union of its contigs' k-mers, then the thread unions are merged (the CPU
+ * baseline's column table; same result as the scalar restatement). */
+int64_t oracle_omp_kmer_columns(const uint8_t* seq, const int64_t* offsets, int64_t n, int kmode, uint8_t* keys_out,
+                                int64_t cap) {
+    if (kmode == 0 || kmode > OK_MAXK || kmode < -1) return INT64_MIN;
+    int T = oracle_threads();
+    kvec_t* part = (kvec_t*)calloc((size_t)T, sizeof(kvec_t));
+#pragma omp parallel num_threads(T)
+    {
+        kvec_t* kv = &part[omp_get_thread_num()];
+        kvec_t one = {0, 0, 0};
+#pragma omp for schedule(dynamic, 256)
+        for (int64_t c = 0; c < n; ++c) {
+            one.n = 0;
+            enum_kmers(seq + offsets[c], offsets[c + 1] - offsets[c], kmode, kvec_push, &one);
+            int64_t m = sort_unique(one.v, one.n);
+            for (int64_t i = 0; i < m; ++i) kvec_push(kv, &one.v[i]);
+            if (kv->n > (1 << 20)) kv->n = sort_unique(kv->v, kv->n);
+        }
+        free(one.v);
+        kv->n = sort_unique(kv->v, kv->n);
+    }
+    kvec_t all = {0, 0, 0};
+    for (int t = 0; t < T; ++t) {
+        for (int64_t i = 0; i < part[t].n; ++i) kvec_push(&all, &part[t].v[i]);
+        free(part[t].v);
+    }
+    free(part);
+    int64_t M = sort_unique(all.v, all.n);
+    if (M > cap) {
+        free(all.v);
+        return -M;
+    }
+    memcpy(keys_out, all.v, (size_t)M * sizeof(okey_t));
+    free(all.v);
+    return M;
 }
 
 /* oracle_kmer_profile over rows in parallel (no counts_out). */

@@ -43,6 +43,8 @@ def lib():
         L.oracle_kmer_columns.argtypes = [ctypes.c_void_p, _i64p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                                           ctypes.c_int64]
         L.oracle_kmer_columns.restype = ctypes.c_int64
+        L.oracle_omp_kmer_columns.argtypes = L.oracle_kmer_columns.argtypes
+        L.oracle_omp_kmer_columns.restype = ctypes.c_int64
         L.oracle_kmer_profile.argtypes = [ctypes.c_void_p, _i64p, _i64p, ctypes.c_int64, ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_int64, _f64p, ctypes.c_void_p]
         L.oracle_kmer_profile.restype = ctypes.c_int
@@ -108,6 +110,23 @@ def kmer_columns(sequences, kmer_size):
         raw = np.zeros(cap * KEY_BYTES, dtype=np.uint8)
         M = L.oracle_kmer_columns(_p(blob, ctypes.c_void_p), _p(offs, _i64p), len(sequences), km,
                                   _p(raw, ctypes.c_void_p), cap)
+        if M == -(1 << 63):
+            raise ValueError(f"oracle supports 1 <= k <= 15 or '5p6', got {kmer_size!r}")
+        if M >= 0:
+            return raw, M
+        cap = -M
+
+
+def omp_kmer_columns_packed(blob, offs, kmer_size):
+    """kmer_columns of packed sequences on all host cores (oracle_omp_kmer_columns)."""
+    L = lib()
+    km = kmode_of(kmer_size)
+    offs = np.ascontiguousarray(offs, np.int64)
+    cap = 1 << 16
+    while True:
+        raw = np.zeros(cap * KEY_BYTES, dtype=np.uint8)
+        M = L.oracle_omp_kmer_columns(_p(blob, ctypes.c_void_p), _p(offs, _i64p), len(offs) - 1, km,
+                                      _p(raw, ctypes.c_void_p), cap)
         if M == -(1 << 63):
             raise ValueError(f"oracle supports 1 <= k <= 15 or '5p6', got {kmer_size!r}")
         if M >= 0:

@@ -133,3 +133,18 @@ def test_update_graph_hand(golden):
         g = oracle.update_graph(g, case["orig_names"], case["orig_sets"], case["new_names"], case["new_sets"])
         d = oracle.graph_dump(g)
         assert d == case["out"], name
+
+
+def test_omp_column_table_equals_scalar():
+    # the CPU baseline's parallel column table (oracle_omp_kmer_columns) is the
+    # scalar restatement's union, key for key, with non-ACGT bytes and every kmode
+    from collections import OrderedDict
+
+    from karma_amd import engine
+
+    blob, offs, _ = engine.synth_contigs(9, 3000, 1, 400, 50)
+    seqs = OrderedDict((f">c{i}", bytes(blob[offs[i]:offs[i + 1]]).decode("latin-1")) for i in range(3000))
+    for k in ("5p6", 1, 3, 5, 7, 8):
+        r1, m1 = oracle.kmer_columns(seqs, k)
+        r2, m2 = oracle.omp_kmer_columns_packed(blob, offs, k)
+        assert m1 == m2 and oracle.decode_keys(r1, m1) == oracle.decode_keys(r2, m2)
