@@ -226,7 +226,9 @@ int karma_pairs_merge_runs(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
                            int n_runs, int is_device, karma_pairs** out);
 /* The exchange's wire format: n x {i64 key, i64 count} interleaved in device
  * memory.  _get_kc writes the list in it (stream-ordered, not waited for);
- * _merge_runs_kc merges received runs of it. */
+ * _merge_runs_kc merges received runs of it (at most 64 runs: without a host
+ * synchronisation, equal keys of different runs left adjacent for the edge
+ * stage; accessors of the list sum them first). */
 int karma_pairs_get_kc(karma_pairs* p, int64_t* kc_dev);
 int karma_pairs_merge_runs_kc(karma_ctx* ctx, const int64_t* kc_dev, const int64_t* run_off, int n_runs,
                               karma_pairs** out);
@@ -243,6 +245,9 @@ int karma_pairs_device(karma_pairs* p, const uint64_t** keys, const int64_t** co
 int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* first, int is_device);
 /* Index of the first key with a >= bounds[r] for r = 0..nranks (host out; searched on the device). */
 int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts);
+/* karma_pairs_split and karma_pairs_get_kc in one launch (the exchange's send
+ * side): starts on the host when it returns, kc_dev (n x {key, count}) written. */
+int karma_pairs_split_kc(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts, int64_t* kc_dev);
 /* totals[c] = count of the diagonal pair (c, c) (readset sizes) for c in [0, n_contigs). */
 int karma_pairs_totals(karma_pairs* p, int64_t* totals_dev, int64_t n_contigs);
 
@@ -254,6 +259,18 @@ typedef struct karma_edges karma_edges;
  * list (diagonal in READS mode, eq totals in EQ mode). */
 int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64_t* totals_dev, int64_t n_contigs,
                            karma_edges** out, int64_t* n_edges);
+/* The same in two halves, for an all-gather of the totals in between (the
+ * sharded build: each owner's diagonal holds the readset sizes of the contigs
+ * it owns).  _begin takes the totals from the list (as totals_dev = NULL
+ * above), launches the edge count and returns the device totals array
+ * (int64[n_contigs], owned by the edges) for the caller to fill further;
+ * _end launches the weights and synchronises.  p must stay valid until _end.
+ * A list from karma_pairs_merge_runs_kc may hold equal adjacent keys (not yet
+ * summed): the edge stage sums them, and reports KARMA_ERR_UNSORTED for a
+ * merge input that was not sorted. */
+int karma_edges_begin(karma_ctx* ctx, karma_pairs* p, int mode, int64_t n_contigs, karma_edges** out,
+                      int64_t** totals_dev);
+int karma_edges_end(karma_edges* e, int64_t* n_edges);
 int karma_edges_destroy(karma_edges* e);
 /* Any output pointer may be NULL. first is only meaningful in EQ mode. */
 int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* shared, double* weight, uint64_t* first,

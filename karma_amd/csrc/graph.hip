@@ -32,6 +32,12 @@ struct karma_edges {
     DevArray<uint64_t> first;
     DevArray<int64_t> totals;
     bool has_first = false;
+    // between karma_edges_begin and _end: the pair list (caller-owned until
+    // _end), the per-block edge counts and the mode
+    const karma_pairs* src = nullptr;
+    DevArray<int64_t> blk;
+    int mode = 0;
+    bool open = false;
 };
 
 namespace {
@@ -59,13 +65,26 @@ struct MinOp {
 };
 
 // ---- finalize --------------------------------------------------------------------
+// A list may hold runs of equal adjacent keys (karma_pairs::dups): the first
+// element of a run stands for it, with the run's summed count.  On a sorted
+// unique list every run has one element.
+__device__ __forceinline__ bool group_head(const uint64_t* __restrict__ keys, int64_t i, uint64_t k) {
+    return i == 0 || keys[i - 1] != k;
+}
+__device__ __forceinline__ int64_t group_sum(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts,
+                                             int64_t n, int64_t i, uint64_t k) {
+    int64_t c = counts[i];
+    for (int64_t j = i + 1; j < n && keys[j] == k; ++j) c += counts[j];
+    return c;
+}
+
 __global__ void diag_totals_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, int64_t n,
                                    int64_t* __restrict__ totals) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
         const uint64_t k = keys[i];
         const uint32_t a = (uint32_t)(k >> 32), b = (uint32_t)k;
-        if (a == b) totals[a] = counts[i];
+        if (a == b && group_head(keys, i, k)) totals[a] = group_sum(keys, counts, n, i, k);
     }
 }
 
@@ -130,9 +149,11 @@ __global__ void __launch_bounds__(kET) edges_count_kernel(const uint64_t* __rest
     bool f = false;
     if (i < n) {
         const uint64_t k = keys[i];
-        const int64_t c = counts[i];
-        if (totals && (uint32_t)(k >> 32) == (uint32_t)k) totals[(uint32_t)k] = c;
-        f = edge_flag(k, c, mode);
+        if (group_head(keys, i, k)) {
+            const int64_t c = group_sum(keys, counts, n, i, k);
+            if (totals && (uint32_t)(k >> 32) == (uint32_t)k) totals[(uint32_t)k] = c;
+            f = edge_flag(k, c, mode);
+        }
     }
     const int cnt = __syncthreads_count(f);
     if (threadIdx.x == 0) blk_cnt[blockIdx.x] = cnt;
@@ -142,18 +163,23 @@ __global__ void __launch_bounds__(kET) edges_write_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, const uint64_t* __restrict__ first,
     int64_t n, int mode, const int64_t* __restrict__ totals, const int64_t* __restrict__ blk_cnt,
     uint32_t* __restrict__ ea, uint32_t* __restrict__ eb, int64_t* __restrict__ es, double* __restrict__ ew,
-    uint64_t* __restrict__ ef, int64_t* __restrict__ st) {
+    uint64_t* __restrict__ ef, int64_t* __restrict__ st, const int64_t* __restrict__ bad) {
     const int64_t i = (int64_t)blockIdx.x * kET + threadIdx.x;
     uint64_t k = 0;
     int64_t c = 0;
     bool f = false;
     if (i < n) {
         k = keys[i];
-        c = counts[i];
-        f = edge_flag(k, c, mode);
+        if (group_head(keys, i, k)) {
+            c = group_sum(keys, counts, n, i, k);
+            f = edge_flag(k, c, mode);
+        }
     }
     const BlockPlace pl = block_place(blk_cnt, f);
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) st[1] = pl.base + pl.total;  // the edge count
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        st[1] = pl.base + pl.total;  // the edge count
+        st[2] = bad ? *bad : 0;      // the order check of the merge that made the list
+    }
     if (!f) return;
     const int64_t o = pl.base + pl.rank;
     const uint32_t a = (uint32_t)(k >> 32), bb = (uint32_t)k;
@@ -235,6 +261,26 @@ __global__ void split_kernel(const uint64_t* __restrict__ keys, int64_t n, const
         else hi = mid;
     }
     starts[r] = lo;
+}
+
+// The exchange's split and wire format in one launch: block 0's first nb
+// threads search the owners' bounds (first key with a >= bounds[r]); every
+// thread interleaves (key, count) pairs.
+__global__ void split_kc_kernel(const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, int64_t n,
+                                const int64_t* __restrict__ bounds, int nb, int64_t* __restrict__ starts,
+                                longlong2* __restrict__ kc) {
+    if (blockIdx.x == 0 && (int)threadIdx.x < nb) {
+        const uint64_t lim = (uint64_t)bounds[threadIdx.x] << 32;
+        int64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (keys[mid] < lim) lo = mid + 1;
+            else hi = mid;
+        }
+        starts[threadIdx.x] = lo;
+    }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        kc[i] = make_longlong2((long long)keys[i], (long long)counts[i]);
 }
 
 // (key, count) pairs <-> separate key and count arrays (the exchange's wire format)
@@ -321,8 +367,10 @@ __device__ __forceinline__ int tile_run(const RunOffs& R, int nr, int64_t tile) 
 
 __global__ void __launch_bounds__(256) merge_bounds_kernel(const uint64_t* __restrict__ keys,
                                                            const longlong2* __restrict__ kc, RunOffs R, int nr,
-                                                           int64_t tiles, int64_t* __restrict__ wb) {
+                                                           int64_t tiles, int64_t* __restrict__ wb,
+                                                           int64_t* __restrict__ bad) {
     const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q == 0) *bad = 0;  // merge_rank_kernel (next on the stream) flags a descent inside a run
     if (q >= tiles * nr * 2) return;
     auto key_at = [&](int64_t i) -> uint64_t { return kc ? (uint64_t)kc[i].x : keys[i]; };
     const int64_t tile = q / (2 * nr);
@@ -601,6 +649,41 @@ int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* count
     return KARMA_OK;
 }
 
+// A list with runs of equal adjacent keys (karma_pairs::dups) to a sorted
+// unique one: group counts + group sums (two launches), one synchronisation,
+// and the order check of the merge that made it.
+static int compact_pairs(karma_pairs* p) {
+    if (!p->dups) return KARMA_OK;
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    const int64_t n = p->n;
+    DevArray<uint64_t> k;
+    DevArray<int64_t> c, nout;
+    KARMA_TRY(k.alloc(ctx, n));
+    KARMA_TRY(c.alloc(ctx, n));
+    KARMA_TRY(nout.alloc(ctx, 1));
+    KARMA_HIP(hipMemsetAsync(nout.ptr, 0, 8, ctx->stream));
+    if (n) {
+        const int64_t nb = ceil_div(n, kET);
+        DevArray<int64_t> blk;
+        KARMA_TRY(blk.alloc(ctx, nb));
+        KARMA_LAUNCH(ctx, "merge_groups", group_count_kernel, nb, kET, 0, p->keys.ptr, n, blk.ptr);
+        KARMA_LAUNCH(ctx, "merge_sum", group_sum_kernel, nb, kET, 0, p->keys.ptr, p->counts.ptr, n, blk.ptr, k.ptr,
+                     c.ptr, nout.ptr);
+    }
+    int64_t* hp = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, 16, reinterpret_cast<void**>(&hp)));
+    KARMA_HIP(hipMemcpyAsync(hp, nout.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipMemcpyAsync(hp + 1, p->bad.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    KARMA_CHECK(!hp[1], KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
+    p->keys.swap(k);
+    p->counts.swap(c);
+    p->n = hp[0];
+    p->dups = false;
+    return KARMA_OK;
+}
+
 static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, const int64_t* kc,
                            const int64_t* run_off, int n_runs, int is_device, karma_pairs** out) {
     KARMA_TRY(ctx_begin(ctx));
@@ -647,13 +730,31 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
             tiles += ceil_div(off[r + 1] - off[r], kMergeTile);
         }
         R.t[n_runs] = tiles;
+        const bool lazy = is_device != 0;
+        int64_t* badp = st + 1;
+        if (lazy) {
+            KARMA_TRY(p->bad.alloc(ctx, 1));
+            badp = p->bad.ptr;
+            if (!tiles) KARMA_HIP(hipMemsetAsync(badp, 0, 8, ctx->stream));
+        }
         if (tiles) {
             DevArray<int64_t> wb;
             KARMA_TRY(wb.alloc(ctx, tiles * n_runs * 2));
             KARMA_LAUNCH(ctx, "merge_bounds", merge_bounds_kernel, grid1(tiles * n_runs * 2), 256, 0, sk,
-                         reinterpret_cast<const longlong2*>(kc), R, n_runs, tiles, wb.ptr);
+                         reinterpret_cast<const longlong2*>(kc), R, n_runs, tiles, wb.ptr, badp);
             KARMA_LAUNCH(ctx, "merge_rank", merge_rank_kernel, tiles, 256, 0, sk, sc,
-                         reinterpret_cast<const longlong2*>(kc), R, n_runs, wb.ptr, kb[0].ptr, cb[0].ptr, st + 1);
+                         reinterpret_cast<const longlong2*>(kc), R, n_runs, wb.ptr, kb[0].ptr, cb[0].ptr, badp);
+        }
+        if (lazy) {
+            // merged order, equal keys adjacent: the edge stage sums the groups
+            // itself; other accessors compact first (compact_pairs).  No host
+            // synchronisation here.
+            p->keys.swap(kb[0]);
+            p->counts.swap(cb[0]);
+            p->n = n;
+            p->dups = true;
+            *out = guard.release();
+            return KARMA_OK;
         }
         sk = kb[0].ptr;
         sc = cb[0].ptr;
@@ -753,6 +854,8 @@ int karma_pairs_merge_runs_kc(karma_ctx* ctx, const int64_t* kc_dev, const int64
 }
 
 int karma_pairs_get_kc(karma_pairs* p, int64_t* kc_dev) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
+    KARMA_TRY(compact_pairs(p));
     KARMA_CHECK(p && (kc_dev || p->n == 0), KARMA_ERR_ARG, "karma_pairs_get_kc: bad arguments");
     KARMA_TRY(ctx_begin(p->ctx));
     if (p->n)
@@ -778,6 +881,8 @@ int karma_pairs_rebind(karma_pairs* p, karma_ctx* ctx) {
 }
 
 int karma_pairs_count(karma_pairs* p, int64_t* n) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
+    KARMA_TRY(compact_pairs(p));
     KARMA_CHECK(p && n, KARMA_ERR_ARG, "null argument");
     *n = p->n;
     return KARMA_OK;
@@ -785,12 +890,16 @@ int karma_pairs_count(karma_pairs* p, int64_t* n) {
 
 int karma_pairs_device(karma_pairs* p, const uint64_t** keys, const int64_t** counts) {
     KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
+    KARMA_TRY(compact_pairs(p));
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
     if (keys) *keys = p->keys.ptr;
     if (counts) *counts = p->counts.ptr;
     return KARMA_OK;
 }
 
 int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* first, int is_device) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
+    KARMA_TRY(compact_pairs(p));
     KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
     KARMA_TRY(ctx_begin(p->ctx));
     const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -804,6 +913,8 @@ int karma_pairs_get(karma_pairs* p, uint64_t* keys, int64_t* counts, uint64_t* f
 }
 
 int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts) {
+    KARMA_CHECK(p, KARMA_ERR_ARG, "null pairs");
+    KARMA_TRY(compact_pairs(p));
     KARMA_CHECK(p && bounds && starts && nranks >= 1, KARMA_ERR_ARG, "bad arguments");
     karma_ctx* ctx = p->ctx;
     KARMA_TRY(ctx_begin(ctx));
@@ -822,6 +933,26 @@ int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t
     return KARMA_OK;
 }
 
+int karma_pairs_split_kc(karma_pairs* p, const int64_t* bounds, int nranks, int64_t* starts, int64_t* kc_dev) {
+    KARMA_CHECK(p && bounds && starts && nranks >= 1 && nranks < 1024, KARMA_ERR_ARG, "bad arguments");
+    KARMA_TRY(compact_pairs(p));
+    KARMA_CHECK(kc_dev || p->n == 0, KARMA_ERR_ARG, "karma_pairs_split_kc: null wire buffer");
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    const int nb = nranks + 1;
+    void *hb = nullptr, *db = nullptr;
+    KARMA_TRY(ctx_mapped(ctx, 2 * nb * 8, &hb, &db));
+    int64_t* h = static_cast<int64_t*>(hb);
+    int64_t* d = static_cast<int64_t*>(db);
+    std::memcpy(h, bounds, nb * 8);
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>(1, ceil_div(p->n, 256)), 4096);
+    KARMA_LAUNCH(ctx, "pairs_split_kc", split_kc_kernel, grid, std::max(256, ((nb + 63) / 64) * 64), 0, p->keys.ptr,
+                 p->counts.ptr, p->n, d, nb, d + nb, reinterpret_cast<longlong2*>(kc_dev));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    std::memcpy(starts, h + nb, nb * 8);
+    return KARMA_OK;
+}
+
 int karma_pairs_totals(karma_pairs* p, int64_t* totals_dev, int64_t N) {
     KARMA_CHECK(p && totals_dev && N >= 0, KARMA_ERR_ARG, "bad arguments");
     karma_ctx* ctx = p->ctx;
@@ -833,19 +964,26 @@ int karma_pairs_totals(karma_pairs* p, int64_t* totals_dev, int64_t N) {
     return KARMA_OK;
 }
 
-int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64_t* totals_dev, int64_t N,
-                           karma_edges** out, int64_t* n_edges) {
+// The edge stage in two halves.  _begin sets the totals (the caller's, the eq
+// totals, or zeros that the count kernel fills with the list's diagonal) and
+// launches the count kernel; _end launches the write kernel and synchronises.
+// Between the two the caller may all-gather the totals (the owners' readset
+// sizes, karma_edges_begin's totals_dev).
+static int edges_begin_impl(karma_ctx* ctx, karma_pairs* p, int mode, const int64_t* totals_dev, int64_t N,
+                            karma_edges** out) {
     KARMA_TRY(ctx_begin(ctx));
-    KARMA_CHECK(p && out && n_edges && N >= 0, KARMA_ERR_ARG, "karma_edges_from_pairs: bad arguments");
+    KARMA_CHECK(p && out && N >= 0, KARMA_ERR_ARG, "karma_edges: bad arguments");
     KARMA_CHECK(mode == KARMA_MODE_READS || mode == KARMA_MODE_EQ, KARMA_ERR_ARG, "bad mode");
+    KARMA_CHECK(!p->dups || !p->has_first, KARMA_ERR_STATE, "karma_edges: an eq list with unsummed groups");
     auto* e = new karma_edges();
     e->ctx = ctx;
     e->n_contigs = N;
+    e->src = p;
+    e->mode = mode;
     std::unique_ptr<karma_edges> guard(e);
     KARMA_TRY(e->totals.alloc(ctx, N));
-    const int64_t* tot = totals_dev;
     bool diag_here = false;
-    if (!tot) {
+    if (!totals_dev) {
         if (mode == KARMA_MODE_EQ) {
             KARMA_CHECK(p->has_totals && p->n_contigs == N, KARMA_ERR_STATE, "eq pair list without totals");
             if (N) KARMA_HIP(hipMemcpyAsync(e->totals.ptr, p->totals.ptr, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
@@ -854,16 +992,30 @@ int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64
             diag_here = true;
         }
     } else if (N) {
-        KARMA_HIP(hipMemcpyAsync(e->totals.ptr, tot, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(e->totals.ptr, totals_dev, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
     }
     const int64_t n = p->n;
-    DevArray<int64_t> blk;
-    const int64_t nb = std::max<int64_t>(1, ceil_div(n, kET));
-    KARMA_TRY(blk.alloc(ctx, nb));
-    // st (mapped host memory, written by the last kernel): 0 zero-division flag, 1 edge count
+    KARMA_TRY(e->blk.alloc(ctx, std::max<int64_t>(1, ceil_div(n, kET))));
+    if (n)
+        KARMA_LAUNCH(ctx, "edge_count", edges_count_kernel, ceil_div(n, kET), kET, 0, p->keys.ptr, p->counts.ptr, n,
+                     mode, diag_here ? e->totals.ptr : (int64_t*)nullptr, e->blk.ptr);
+    e->open = true;
+    *out = guard.release();
+    return KARMA_OK;
+}
+
+static int edges_end_impl(karma_edges* e, int64_t* n_edges) {
+    KARMA_CHECK(e && e->open && n_edges, KARMA_ERR_STATE, "karma_edges_end: no open edge stage");
+    karma_ctx* ctx = e->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    const karma_pairs* p = e->src;
+    e->open = false;
+    const int64_t n = p->n;
+    // st (mapped host memory, written by the write kernel): 0 zero-division
+    // flag, 1 edge count, 2 the list's merge order check
     void *hst = nullptr, *dst_ = nullptr;
-    KARMA_TRY(ctx_mapped(ctx, 16, &hst, &dst_));
-    std::memset(hst, 0, 16);
+    KARMA_TRY(ctx_mapped(ctx, 24, &hst, &dst_));
+    std::memset(hst, 0, 24);
     int64_t* const st = static_cast<int64_t*>(dst_);
     // edges <= pairs: written before the count is known on the host
     KARMA_TRY(e->a.alloc(ctx, n));
@@ -872,23 +1024,41 @@ int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64
     KARMA_TRY(e->w.alloc(ctx, n));
     e->has_first = p->has_first;
     if (e->has_first) KARMA_TRY(e->first.alloc(ctx, n));
-    if (n) {
-        KARMA_LAUNCH(ctx, "edge_count", edges_count_kernel, nb, kET, 0, p->keys.ptr, p->counts.ptr, n, mode,
-                     diag_here ? e->totals.ptr : (int64_t*)nullptr, blk.ptr);
-        KARMA_LAUNCH(ctx, "edge_weights", edges_write_kernel, nb, kET, 0, p->keys.ptr, p->counts.ptr,
-                     p->has_first ? p->first.ptr : (const uint64_t*)nullptr, n, mode, e->totals.ptr, blk.ptr,
-                     e->a.ptr, e->b.ptr, e->s.ptr, e->w.ptr, e->has_first ? e->first.ptr : (uint64_t*)nullptr,
-                     st);
-    }
+    if (n)
+        KARMA_LAUNCH(ctx, "edge_weights", edges_write_kernel, ceil_div(n, kET), kET, 0, p->keys.ptr, p->counts.ptr,
+                     p->has_first ? p->first.ptr : (const uint64_t*)nullptr, n, e->mode, e->totals.ptr, e->blk.ptr,
+                     e->a.ptr, e->b.ptr, e->s.ptr, e->w.ptr, e->has_first ? e->first.ptr : (uint64_t*)nullptr, st,
+                     p->dups ? (const int64_t*)p->bad.ptr : (const int64_t*)nullptr);
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    e->blk.release();
+    e->src = nullptr;
     const volatile int64_t* hs = static_cast<const volatile int64_t*>(hst);
+    KARMA_CHECK(!hs[2], KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
     KARMA_CHECK(!(int)hs[0], KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
-    const int64_t E = hs[1];
-    e->E = E;
-    *n_edges = E;
+    e->E = hs[1];
+    *n_edges = e->E;
+    return KARMA_OK;
+}
+
+int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64_t* totals_dev, int64_t N,
+                           karma_edges** out, int64_t* n_edges) {
+    KARMA_CHECK(out && n_edges, KARMA_ERR_ARG, "karma_edges_from_pairs: bad arguments");
+    karma_edges* e = nullptr;
+    KARMA_TRY(edges_begin_impl(ctx, p, mode, totals_dev, N, &e));
+    std::unique_ptr<karma_edges> guard(e);
+    KARMA_TRY(edges_end_impl(e, n_edges));
     *out = guard.release();
     return KARMA_OK;
 }
+
+int karma_edges_begin(karma_ctx* ctx, karma_pairs* p, int mode, int64_t N, karma_edges** out, int64_t** totals_dev) {
+    KARMA_CHECK(out && totals_dev, KARMA_ERR_ARG, "karma_edges_begin: bad arguments");
+    KARMA_TRY(edges_begin_impl(ctx, p, mode, nullptr, N, out));
+    *totals_dev = (*out)->totals.ptr;
+    return KARMA_OK;
+}
+
+int karma_edges_end(karma_edges* e, int64_t* n_edges) { return edges_end_impl(e, n_edges); }
 
 int karma_edges_destroy(karma_edges* e) {
     if (!e) return KARMA_OK;

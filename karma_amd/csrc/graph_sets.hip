@@ -1586,25 +1586,21 @@ __global__ void fill_ones_i64_kernel(int64_t* __restrict__ v, int64_t n) {
     if (i < n) v[i] = 1;
 }
 
-__global__ void assemble2_kernel(const uint64_t* const* __restrict__ src_k, const int64_t* const* __restrict__ src_c,
-                                 const int64_t* __restrict__ n_per, const int64_t* __restrict__ dst_off,
-                                 uint64_t* __restrict__ keys, int64_t* __restrict__ counts) {
+// Bucket b's sorted list lies at base + b * stride (final_kernel's slots), or,
+// for a bucket that overflowed the LDS tables, at the generic path's arrays
+// (src_k[b] / src_c[b] non-null: the overflow path only)
+__global__ void assemble2_kernel(const uint64_t* __restrict__ base_k, const int64_t* __restrict__ base_c,
+                                 int64_t stride, const uint64_t* const* __restrict__ src_k,
+                                 const int64_t* const* __restrict__ src_c, const int64_t* __restrict__ n_per,
+                                 const int64_t* __restrict__ dst_off, uint64_t* __restrict__ keys,
+                                 int64_t* __restrict__ counts) {
     const int64_t b = blockIdx.x;
     const int64_t n = n_per[b], d = dst_off[b];
-    const uint64_t* sk = src_k[b];
-    const int64_t* sc = src_c[b];
+    const uint64_t* sk = src_k && src_k[b] ? src_k[b] : base_k + b * stride;
+    const int64_t* sc = src_c && src_c[b] ? src_c[b] : base_c + b * stride;
     for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
         keys[d + t] = sk[t];
         counts[d + t] = sc[t];
-    }
-}
-
-__global__ void fill_ptrs2_kernel(const uint64_t* base_k, const int64_t* base_c, int64_t n, int64_t stride,
-                                  const uint64_t** pk, const int64_t** pc) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < n) {
-        pk[b] = base_k + b * stride;
-        pc[b] = base_c + b * stride;
     }
 }
 
@@ -2165,18 +2161,20 @@ int SetsJob::finish(karma_pairs* out) {
         std::fprintf(stderr, "[karma] general reads %llu, big reads %u, pair flushes %u\n", (unsigned long long)tot,
                      n_big, hc[2]);
     }
-    DevArray<const uint64_t*> pk;
+    DevArray<const uint64_t*> pk;  // per-bucket list overrides (overflowed buckets only)
     DevArray<const int64_t*> pc;
-    KARMA_TRY(pk.alloc(ctx, B));
-    KARMA_TRY(pc.alloc(ctx, B));
-    KARMA_LAUNCH(ctx, "bucket_ptrs", fill_ptrs2_kernel, grid_n(B), 256, 0, slot_k.ptr, slot_c.ptr, (int64_t)B,
-                 (int64_t)kSlotCap, pk.ptr, pc.ptr);
     std::vector<std::unique_ptr<DevArray<uint64_t>>> keep_k;
     std::vector<std::unique_ptr<DevArray<int64_t>>> keep_c;
     const int64_t widen_threads = std::max<int64_t>(hc[2], (int64_t(8) << g.bw) + 24);
     bool any_ovf = false;
     for (int b = 0; b < B; ++b) {
         if (!hovf[b]) continue;
+        if (!any_ovf) {
+            KARMA_TRY(pk.alloc(ctx, B));
+            KARMA_TRY(pc.alloc(ctx, B));
+            KARMA_HIP(hipMemsetAsync(pk.ptr, 0, B * sizeof(void*), ctx->stream));
+            KARMA_HIP(hipMemsetAsync(pc.ptr, 0, B * sizeof(void*), ctx->stream));
+        }
         any_ovf = true;
         // generic path for a bucket whose distinct pairs exceed the LDS tables
         DevArray<unsigned long long> np;
@@ -2215,7 +2213,8 @@ int SetsJob::finish(karma_pairs* out) {
     DevArray<int64_t> mc;
     KARMA_TRY(mk.alloc(ctx, U));
     KARMA_TRY(mc.alloc(ctx, U));
-    KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, pk.ptr, pc.ptr, n_per, dst, mk.ptr, mc.ptr);
+    KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, slot_k.ptr, slot_c.ptr, (int64_t)kSlotCap,
+                 pk.ptr, pc.ptr, n_per, dst, mk.ptr, mc.ptr);
     if (!relabeled) return finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out);
     KARMA_TRY(finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out, remap_map.ptr));
     // back to the original ids, sorted again (keys stay unique: the map is a bijection)

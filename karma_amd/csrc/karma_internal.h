@@ -168,6 +168,12 @@ struct karma_pairs {
     karma::DevArray<int64_t> totals;   // eq path only
     bool has_first = false;
     bool has_totals = false;
+    // An owner's merge of received runs may leave equal keys adjacent (dups):
+    // the edge stage and the totals sum such groups themselves; every other
+    // accessor compacts the list first (graph.hip compact_pairs).  bad: the
+    // merge's order check (device flag), read at the next synchronisation.
+    bool dups = false;
+    karma::DevArray<int64_t> bad;
 };
 
 namespace karma {

@@ -135,11 +135,11 @@ class HipOps:
 
     def pairs_kc_split(self, pairs, bounds):
         """The list as interleaved (key, count) int64 pairs (2n, the exchange's
-        wire format, written on the device) and the owners' start offsets."""
-        starts = pairs.split(bounds)
+        wire format, written on the device) and the owners' start offsets: one
+        launch (karma_pairs_split_kc)."""
         n = pairs.count()
         kc = DevBuf(self.ctx, (2 * n,), np.int64)
-        pairs.get_kc(kc.ptr if n else None)
+        starts = pairs.split_kc(bounds, kc.ptr if n else None)
         return kc, starts
 
     def merge_kc(self, kc, runs):
@@ -153,6 +153,16 @@ class HipOps:
 
     def edges(self, pairs, n_contigs, totals=None):
         return pairs.edges(_lib.KARMA_MODE_READS, n_contigs, totals.ptr if totals is not None else None)
+
+    def edges_begin(self, pairs, n_contigs):
+        """The edge stage's first half (karma_edges_begin): the list's diagonal
+        counts land in the returned totals buffer (a view owned by the edges),
+        which the caller all-gathers before edges_end."""
+        e, tp = pairs.edges_begin(_lib.KARMA_MODE_READS, n_contigs)
+        return e, DevBuf(self.ctx, (n_contigs,), np.int64, _ptr=tp, _owner=e)
+
+    def edges_end(self, e):
+        return e.end()
 
     def edge_count(self, edges):
         return edges.E
@@ -312,8 +322,15 @@ class ShardedBuild:
                 merged = ops.merge_kc(kc, np.diff(starts).tolist())
             # the owner's merged list holds the diagonal (a, a) of every a it owns:
             # complete readset sizes for its slice, gathered to every rank
-            tot = comm.allgather_slices_(ops.totals(merged, self.n_glob), self.bounds)
-            edges = ops.edges(merged, self.n_glob, tot)
+            if hasattr(ops, "edges_begin"):
+                # two halves around the all-gather: the edge count kernel writes
+                # the diagonal into the edges' own totals, gathered in place
+                eh, tot = ops.edges_begin(merged, self.n_glob)
+                comm.allgather_slices_(tot, self.bounds)
+                edges = ops.edges_end(eh)
+            else:
+                tot = comm.allgather_slices_(ops.totals(merged, self.n_glob), self.bounds)
+                edges = ops.edges(merged, self.n_glob, tot)
             ops.close(local)
             final_pairs = merged
         else:

@@ -358,6 +358,25 @@ class Pairs:
         call("karma_pairs_split", self.h, ptr(bounds), len(bounds) - 1, ptr(starts))
         return starts
 
+    def split_kc(self, bounds, kc_dev_ptr):
+        """split(bounds) and get_kc(kc_dev_ptr) in one launch (karma_pairs_split_kc)."""
+        bounds = np.ascontiguousarray(bounds, np.int64)
+        starts = np.zeros(len(bounds), np.int64)
+        call("karma_pairs_split_kc", self.h, ptr(bounds), len(bounds) - 1, ptr(starts),
+             ctypes.c_void_p(kc_dev_ptr) if kc_dev_ptr else None)
+        return starts
+
+    def edges_begin(self, mode, n_contigs):
+        """First half of edges() (karma_edges_begin): returns the open Edges and the
+        device address of its int64[n_contigs] totals, for an all-gather before
+        Edges.end() computes the weights."""
+        h = ctypes.c_void_p()
+        tp = ctypes.c_void_p()
+        call("karma_edges_begin", self.ctx.h, self.h, mode, n_contigs, ctypes.byref(h), ctypes.byref(tp))
+        e = Edges(self.ctx, h, -1, n_contigs)
+        e._pairs = self  # the list stays alive until end()
+        return e, tp.value
+
     def totals_device(self, dst_dev_ptr, n_contigs):
         call("karma_pairs_totals", self.h, ctypes.c_void_p(dst_dev_ptr), n_contigs)
 
@@ -396,6 +415,14 @@ class EdgeArrays:
 class Edges:
     def __init__(self, ctx, h, E, n_contigs):
         self.ctx, self.h, self.E, self.n_contigs = ctx, h, E, n_contigs
+
+    def end(self):
+        """Second half of Pairs.edges_begin (karma_edges_end): weights, edge count."""
+        E = ctypes.c_int64()
+        call("karma_edges_end", self.h, ctypes.byref(E))
+        self.E = E.value
+        self._pairs = None
+        return self
 
     def get(self) -> EdgeArrays:
         E = self.E

@@ -392,6 +392,58 @@ def test_merge_runs_and_split(seed, n_runs, n):
         bad[off[r]], bad[off[r] + 1] = keys[off[r] + 1] + np.uint64(1), keys[off[r]]  # a descent inside a run
         with pytest.raises(_lib.KarmaError):
             engine.Pairs.merge(ctx, bad, counts, runs=lens.tolist())
+        # the device wire-format merge checks order at its next synchronisation:
+        # the accessor's compaction, or the edge stage (which sums the groups itself)
+        kcb = np.stack([bad.view(np.int64), counts], 1).copy()
+        dev = ctypes.c_void_p()
+        _lib.call("karma_dev_alloc", ctx.h, kcb.nbytes, ctypes.byref(dev))
+        try:
+            _lib.call("karma_memcpy", ctx.h, dev, _lib.ptr(kcb), kcb.nbytes, 0)
+            for use in ("get", "edges"):
+                p = engine.Pairs.merge_runs_kc(ctx, dev.value, lens.tolist())
+                with pytest.raises(_lib.KarmaError) as ei:
+                    if use == "get":
+                        p.get()
+                    else:
+                        e, _ = p.edges_begin(_lib.KARMA_MODE_READS, n_contigs)
+                        e.end()
+                assert ei.value.code == _lib.KARMA_ERR_UNSORTED
+                p.close()
+        finally:
+            _lib.load().karma_dev_free(ctx.h, dev)
+
+
+def test_edges_of_unsummed_merge_equal_compacted():
+    # a merged list with equal keys left adjacent (merge_runs_kc) gives the
+    # same edges and totals as its compacted form, in one call or two halves
+    import ctypes
+    rng = np.random.default_rng(77)
+    n_contigs, W = 3000, 5
+    runs = []
+    for _ in range(W):
+        a = rng.integers(0, n_contigs, 40_000, dtype=np.uint64)
+        b = np.minimum(a + rng.integers(0, 6, 40_000, dtype=np.uint64), n_contigs - 1)
+        u = np.unique((a << np.uint64(32)) | b)
+        runs.append(np.stack([u.view(np.int64), rng.integers(1, 50, len(u))], 1))
+    kc = np.concatenate(runs).copy()
+    ctx = _lib.default_context()
+    dev = ctypes.c_void_p()
+    _lib.call("karma_dev_alloc", ctx.h, kc.nbytes, ctypes.byref(dev))
+    try:
+        _lib.call("karma_memcpy", ctx.h, dev, _lib.ptr(kc), kc.nbytes, 0)
+        lens = [len(r) for r in runs]
+        p1 = engine.Pairs.merge_runs_kc(ctx, dev.value, lens)
+        e1, _ = p1.edges_begin(_lib.KARMA_MODE_READS, n_contigs)
+        g1 = e1.end().get()
+        p2 = engine.Pairs.merge_runs_kc(ctx, dev.value, lens)
+        assert p2.count() < len(kc)  # compacted: the equal keys were summed
+        g2 = p2.edges(_lib.KARMA_MODE_READS, n_contigs).get()
+        for f in ("a", "b", "shared", "totals"):
+            assert np.array_equal(getattr(g1, f), getattr(g2, f)), f
+        assert np.array_equal(g1.weight.view(np.uint64), g2.weight.view(np.uint64))
+        assert len(g1.a) > 1000
+    finally:
+        _lib.load().karma_dev_free(ctx.h, dev)
 
 
 def test_graph_records_split_call():
