@@ -128,6 +128,11 @@ int karma_comm_exchange_counts(karma_comm* c, const int64_t* send_host, int64_t*
  * recv_dev[recv_off[me], ...); offsets are host arrays of world + 1 entries. */
 int karma_comm_alltoallv(karma_comm* c, const void* send_dev, const int64_t* send_off, void* recv_dev,
                          const int64_t* recv_off);
+/* The same for a list held as two arrays of equal element size (keys and
+ * counts): part a and part b of each slice go as two grouped sends, so the
+ * sender needs no interleaved copy.  Offsets (bytes) apply to both parts. */
+int karma_comm_alltoallv_kv(karma_comm* c, const void* send_a, const void* send_b, const int64_t* send_off,
+                            void* recv_a, void* recv_b, const int64_t* recv_off);
 
 /* ---- contig store (device-resident, 2-bit packed + exception mask) -------- */
 typedef struct karma_contigs karma_contigs;
@@ -172,6 +177,11 @@ int karma_kmer_columns(karma_kmer_plan* p, uint64_t* keys_host);
 /* Dense float64 profile, row r = contig r of the store, stride ld >= M:
  * out[r*ld + col] = count / key_len[r] (kmer.py:120, :231-233), zeros written. */
 int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_device);
+/* Rows [row_lo, row_hi) of the same profile: row r of out is contig row_lo + r
+ * (SURVEY.md §8(e) streaming: a profile larger than host or device memory is
+ * produced and copied out one row block at a time; host output synchronises). */
+int karma_kmer_profile_rows(karma_kmer_plan* p, int64_t row_lo, int64_t row_hi, double* out, int64_t ld,
+                            int out_is_device);
 /* karma_kmer_profile into device memory, launched on `side` (a hipStream_t)
  * after everything already enqueued on the context's stream -- or, while a
  * karma_graph_records_begin job is open, after that job's classify kernel and

@@ -75,6 +75,7 @@ _SIGS = {
     "karma_comm_allgather": [_c_p, _c_p, _c_p, _i64],
     "karma_comm_exchange_counts": [_c_p, _c_p, _c_p],
     "karma_comm_alltoallv": [_c_p, _c_p, _c_p, _c_p, _c_p],
+    "karma_comm_alltoallv_kv": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
     "karma_contigs_create": [_c_p, _c_p, _c_p, _c_p, _i64, _i32, _PP],
     "karma_contigs_destroy": [_c_p],
     "karma_contigs_info": [_c_p, _I64P, _I64P, _I64P, _I64P],
@@ -92,6 +93,7 @@ _SIGS = {
     "karma_kmer_plan_finalize_wait": [_c_p, _I64P],
     "karma_kmer_columns": [_c_p, _c_p],
     "karma_kmer_profile": [_c_p, _c_p, _i64, _i32],
+    "karma_kmer_profile_rows": [_c_p, _i64, _i64, _c_p, _i64, _i32],
     "karma_kmer_profile_side": [_c_p, _c_p, _i64, _c_p],
     "karma_ctx_join": [_c_p, _c_p],
     "karma_ctx_set_side_headroom": [_c_p, _i32],

@@ -59,6 +59,9 @@ class SoloComm:
     def alltoallv(self, buf, send_counts):
         return buf, [int(x) for x in send_counts]
 
+    def alltoallv_kv(self, a, b, send_counts):
+        return a, b, [int(x) for x in send_counts]
+
     def close(self):
         pass
 
@@ -127,6 +130,11 @@ class HostComm:
             recv.append(n)
         out = np.concatenate(pieces) if pieces else h[:0]
         return _like(buf, out.astype(h.dtype, copy=False)), recv
+
+    def alltoallv_kv(self, a, b, send_counts):
+        ra, recv = self.alltoallv(a, send_counts)
+        rb, _ = self.alltoallv(b, send_counts)
+        return ra, rb, recv
 
     def close(self):
         self.group.close()
@@ -224,6 +232,24 @@ class RcclComm:
         out = DevBuf(self.ctx, (int(rc.sum()),), buf.dtype)
         call("karma_comm_alltoallv", self.h, ctypes.c_void_p(buf.ptr), ptr(soff), ctypes.c_void_p(out.ptr), ptr(roff))
         return out, [int(x) for x in rc]
+
+    def alltoallv_kv(self, a, b, send_counts):
+        """alltoallv of a list held as two arrays of one element size (keys and
+        counts): two grouped sends per peer, no interleaved copy."""
+        assert a.dtype.itemsize == b.dtype.itemsize and a.size == b.size
+        isz = a.dtype.itemsize
+        sc = np.ascontiguousarray(send_counts, np.int64)
+        rc = np.zeros(self.world, np.int64)
+        call("karma_comm_exchange_counts", self.h, ptr(sc), ptr(rc))
+        soff = np.zeros(self.world + 1, np.int64)
+        roff = np.zeros(self.world + 1, np.int64)
+        np.cumsum(sc * isz, out=soff[1:])
+        np.cumsum(rc * isz, out=roff[1:])
+        ra = DevBuf(self.ctx, (int(rc.sum()),), a.dtype)
+        rb = DevBuf(self.ctx, (int(rc.sum()),), b.dtype)
+        call("karma_comm_alltoallv_kv", self.h, ctypes.c_void_p(a.ptr), ctypes.c_void_p(b.ptr), ptr(soff),
+             ctypes.c_void_p(ra.ptr), ctypes.c_void_p(rb.ptr), ptr(roff))
+        return ra, rb, [int(x) for x in rc]
 
     def close(self):
         if getattr(self, "h", None):

@@ -260,4 +260,44 @@ int karma_comm_alltoallv(karma_comm* c, const void* send_dev, const int64_t* sen
     return KARMA_OK;
 }
 
+int karma_comm_alltoallv_kv(karma_comm* c, const void* send_a, const void* send_b, const int64_t* send_off,
+                            void* recv_a, void* recv_b, const int64_t* recv_off) {
+    KARMA_TRY(comm_begin(c));
+    const int W = c->world;
+    {
+        char msg[160];
+        KARMA_CHECK(alltoallv_args_ok(W, c->rank, send_a, send_off, recv_a, recv_off, msg, sizeof msg) &&
+                        alltoallv_args_ok(W, c->rank, send_b, send_off, recv_b, recv_off, msg, sizeof msg),
+                    KARMA_ERR_ARG, "karma_comm_alltoallv_kv: %s", msg);
+    }
+    const uint8_t *sa = static_cast<const uint8_t*>(send_a), *sb_ = static_cast<const uint8_t*>(send_b);
+    uint8_t *da = static_cast<uint8_t*>(recv_a), *db = static_cast<uint8_t*>(recv_b);
+    {
+        // per peer: part a, then part b, in the same order on both sides
+        NcclGroup g;
+        KARMA_TRY(group_rc(g.start(), g));
+        for (int r = 0; r < W; ++r) {
+            if (r == c->rank) continue;
+            const size_t sn = (size_t)(send_off[r + 1] - send_off[r]), rn = (size_t)(recv_off[r + 1] - recv_off[r]);
+            if (sn) {
+                KARMA_GROUP_ADD(g, ncclSend(sa + send_off[r], sn, ncclUint8, r, c->nc, c->ctx->stream));
+                KARMA_GROUP_ADD(g, ncclSend(sb_ + send_off[r], sn, ncclUint8, r, c->nc, c->ctx->stream));
+            }
+            if (rn) {
+                KARMA_GROUP_ADD(g, ncclRecv(da + recv_off[r], rn, ncclUint8, r, c->nc, c->ctx->stream));
+                KARMA_GROUP_ADD(g, ncclRecv(db + recv_off[r], rn, ncclUint8, r, c->nc, c->ctx->stream));
+            }
+        }
+        KARMA_TRY(group_rc(g.end(), g));
+    }
+    const size_t own = (size_t)(send_off[c->rank + 1] - send_off[c->rank]);
+    if (own) {
+        KARMA_HIP(hipMemcpyAsync(da + recv_off[c->rank], sa + send_off[c->rank], own, hipMemcpyDeviceToDevice,
+                                 c->ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(db + recv_off[c->rank], sb_ + send_off[c->rank], own, hipMemcpyDeviceToDevice,
+                                 c->ctx->stream));
+    }
+    return KARMA_OK;
+}
+
 }  // extern "C"

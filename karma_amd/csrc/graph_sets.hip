@@ -1607,12 +1607,7 @@ __global__ void assemble2_kernel(const uint64_t* __restrict__ base_k, const int6
 int grid_n(int64_t n, int block = 256) { return (int)std::max<int64_t>(1, ceil_div(n, block)); }
 
 int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
-    size_t tb = 0;
-    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, ctx->stream));
-    DevArray<uint8_t> tmp;
-    KARMA_TRY(tmp.alloc(ctx, tb));
-    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.ptr, tb, in, out, n, ctx->stream));
-    return KARMA_OK;
+    return karma::scan_i64_device(ctx, in, out, n);  // hand-written (eq.hip): one launch up to 4096 items
 }
 
 
@@ -1770,9 +1765,13 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
 constexpr int kRelabelProbes = 256;
 
 __global__ void __launch_bounds__(kRelabelProbes) relabel_probe_kernel(const uint2* __restrict__ rec, int64_t A,
-                                                                       uint32_t N, unsigned* __restrict__ relabel) {
+                                                                       uint32_t N, unsigned* __restrict__ relabel,
+                                                                       uint64_t* __restrict__ zero, int64_t n_zero) {
     __shared__ unsigned wide;
     if (threadIdx.x == 0) wide = 0;
+    // the job's control block (flags, counters, per-bucket sizes; relabel is
+    // one of its words) is cleared here: no memset launch ahead of the probe
+    for (int64_t i = threadIdx.x; i < n_zero; i += kRelabelProbes) zero[i] = 0;
     __syncthreads();
     // a window of 32 records from an even position, loaded at once (16 B each)
     constexpr int kW = 32;
@@ -2002,7 +2001,8 @@ int SetsJob::launch() {
     KARMA_TRY(pent.alloc(ctx, pscap + 8));
     KARMA_TRY(pf_base.alloc(ctx, max_pflush));
     KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
-    KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk) * 8, ctx->stream));
+    const bool probe = A > 0 && !relabeled;  // the probe kernel clears the control block
+    if (!probe) KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk) * 8, ctx->stream));
     if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
     if (KARMA_MARK_AT == 3 && attempt == 0 && !relabeled) {  // side-stream work may start beside classify
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
@@ -2031,7 +2031,7 @@ int SetsJob::launch() {
             // a probe of the reads decides: when many span more than 4 contig
             // ids, this pass is skipped and a relabelled rerun follows
             KARMA_LAUNCH(ctx, "relabel_probe", relabel_probe_kernel, 1, kRelabelProbes, 0, rec, A, (uint32_t)N,
-                         counters + 3);
+                         counters + 3, reinterpret_cast<uint64_t*>(ctrl.ptr), (int64_t)(ctrl_words + 2 * n_pblk));
             C.skip = counters + 3;
         }
         KARMA_TRY(classify(0, n_chunks));

@@ -1233,16 +1233,26 @@ int karma_kmer_row_totals(karma_kmer_plan* p, int64_t* dst) {
     return KARMA_OK;
 }
 
-int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_device) {
+// Rows [lo, hi) of the profile: the per-contig arrays are passed shifted by lo
+// (packed words and raw bytes are addressed through them), so row r of `out`
+// is contig lo + r.
+static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out, int64_t ld, int out_is_device) {
     KARMA_CHECK(p && p->M >= 0, KARMA_ERR_STATE, "karma_kmer_profile before finalize");
     karma_ctx* ctx = p->ctx;
     karma_contigs* c = p->store;
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(ld >= p->M, KARMA_ERR_ARG, "ld (%lld) < M (%lld)", (long long)ld, (long long)p->M);
-    const int64_t n = c->n, M = p->M;
+    KARMA_CHECK(0 <= lo && lo <= hi && hi <= c->n, KARMA_ERR_ARG, "rows [%lld, %lld) outside [0, %lld)",
+                (long long)lo, (long long)hi, (long long)c->n);
+    const int64_t n = hi - lo, M = p->M;
     if (n == 0) return KARMA_OK;
+    int64_t* const row_tot = p->row_tot.ptr + lo;
+    const uint8_t* const has_exc = c->has_exc.ptr + lo;
+    const int64_t* const woff = c->woff.ptr + lo;
+    const int64_t* const off = c->off + lo;
+    const int32_t* const keylen = c->keylen + lo;
     // row totals first: with M == 0 every row is all-zero (kmer.py:250-258)
-    KARMA_HIP(hipMemsetAsync(p->row_tot.ptr, 0, n * 8, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(row_tot, 0, n * 8, ctx->stream));
     if (M == 0) return KARMA_OK;
     KARMA_CHECK(out, KARMA_ERR_ARG, "null out");
     KARMA_CHECK(c->zero_key_maxlen < p->kmin, KARMA_ERR_ZERO_DIV,
@@ -1271,9 +1281,9 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
         const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_wave_kernel<P56, C16>), kPBlock, \
                                      lds, ceil_div(n, kPBlock / 64));                                            \
         KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16>), g_, kPBlock, lds, c->packed.ptr,      \
-                     c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len,        \
+                     c->mask.ptr, has_exc, woff, off, c->raw, keylen, n, k, with_len,                            \
                      p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err,       \
-                     (int)p->S, p->row_tot.ptr);                                                                 \
+                     (int)p->S, row_tot);                                                                        \
     } while (0)
         if (p56) {
             if (c16) KARMA_WAVE_LAUNCH(true, true);
@@ -1291,9 +1301,9 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
         const size_t lds = lds_ok ? M * 4 : 0;
 #define KARMA_PROFILE_LAUNCH(P56, LDS)                                                                           \
     KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, LDS>), grid, kPBlock, lds, c->packed.ptr, c->mask.ptr, \
-                 c->has_exc.ptr, c->woff.ptr, c->off, c->raw, c->keylen, n, k, with_len, p->col_of_ord.ptr,      \
+                 has_exc, woff, off, c->raw, keylen, n, k, with_len, p->col_of_ord.ptr,                          \
                  p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err, (int)p->S,      \
-                 p->row_tot.ptr)
+                 row_tot)
         if (p->kmode == KARMA_KMER_5P6) {
             if (lds_ok) KARMA_PROFILE_LAUNCH(true, true);
             else KARMA_PROFILE_LAUNCH(true, false);
@@ -1308,6 +1318,16 @@ int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_d
         KARMA_HIP(hipStreamSynchronize(ctx->stream));
     }
     return KARMA_OK;
+}
+
+int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_device) {
+    KARMA_CHECK(p && p->store, KARMA_ERR_STATE, "karma_kmer_profile: null plan");
+    return profile_rows(p, 0, p->store->n, out, ld, out_is_device);
+}
+
+int karma_kmer_profile_rows(karma_kmer_plan* p, int64_t row_lo, int64_t row_hi, double* out, int64_t ld,
+                            int out_is_device) {
+    return profile_rows(p, row_lo, row_hi, out, ld, out_is_device);
 }
 
 int karma_kmer_profile_side(karma_kmer_plan* p, double* out_dev, int64_t ld, void* side) {

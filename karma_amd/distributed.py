@@ -142,6 +142,22 @@ class HipOps:
         starts = pairs.split_kc(bounds, kc.ptr if n else None)
         return kc, starts
 
+    def pairs_kv(self, pairs, bounds):
+        """The owners' start offsets (karma_pairs_split: device searches) and the
+        list's own key and count arrays as device buffers (no copy): the
+        exchange sends each owner's slice of both (RcclComm.alltoallv_kv)."""
+        starts = pairs.split(bounds)
+        k, c = pairs.device_ptrs()
+        n = pairs.count()
+        return (DevBuf(self.ctx, (n,), np.uint64, _ptr=k, _owner=pairs),
+                DevBuf(self.ctx, (n,), np.int64, _ptr=c, _owner=pairs), starts)
+
+    def merge_kv(self, keys, counts, runs):
+        """The owner's list from received runs of keys and counts (each sorted):
+        one ranking pass, no host synchronisation (karma_pairs_merge_runs)."""
+        return self.engine.Pairs.merge(self.ctx, keys.ptr if keys.size else None,
+                                       counts.ptr if counts.size else None, device=True, n=keys.size, runs=runs)
+
     def merge_kc(self, kc, runs):
         """The owner's list from the senders' slices of interleaved pairs (runs: their lengths, each sorted)."""
         return self.engine.Pairs.merge_runs_kc(self.ctx, kc.ptr if kc.size else None, runs)
@@ -311,14 +327,24 @@ class ShardedBuild:
             stats["entries"] = ops.entries(local)
             stats["pairs_local"] = ops.pair_count(local)
         if comm.world > 1 or self.emulate:
-            if comm.world > 1:
+            bounds = self.bounds if comm.world > 1 else np.linspace(0, self.n_glob, self.emulate + 1).astype(np.int64)
+            if hasattr(ops, "pairs_kv"):
+                # the list's keys and counts, each owner's slice of both in one
+                # grouped all-to-all-v; the owner merges one sorted run per sender
+                keys, counts, starts = ops.pairs_kv(local, bounds)
+                if comm.world > 1:
+                    rk, rc, recv = comm.alltoallv_kv(keys, counts, np.diff(starts))
+                    merged = ops.merge_kv(rk, rc, recv)
+                else:  # emulation: this rank's own W slices stand in for the W received ones
+                    merged = ops.merge_kv(keys, counts, np.diff(starts).tolist())
+            elif comm.world > 1:
                 # one all-to-all-v of interleaved (key, count) int64 pairs; the
                 # owner receives one sorted slice per sender and merges them
                 kc, starts = ops.pairs_kc_split(local, self.bounds)
                 recv_kc, recv = comm.alltoallv(kc, 2 * np.diff(starts))
                 merged = ops.merge_kc(recv_kc, [r // 2 for r in recv])
             else:  # emulation: this rank's own W slices stand in for the W received ones
-                kc, starts = ops.pairs_kc_split(local, np.linspace(0, self.n_glob, self.emulate + 1).astype(np.int64))
+                kc, starts = ops.pairs_kc_split(local, bounds)
                 merged = ops.merge_kc(kc, np.diff(starts).tolist())
             # the owner's merged list holds the diagonal (a, a) of every a it owns:
             # complete readset sizes for its slice, gathered to every rank

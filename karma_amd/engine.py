@@ -160,6 +160,13 @@ class KmerPlan:
             call("karma_kmer_profile", self.h, ptr(out), self.M, 0)
         return out
 
+    def profile_rows(self, lo, hi, out):
+        """Rows [lo, hi) into a host float64 array of hi - lo rows (C order,
+        row stride = its second dimension >= M)."""
+        assert out.dtype == np.float64 and out.flags.c_contiguous and out.shape[0] == hi - lo
+        if hi > lo:
+            call("karma_kmer_profile_rows", self.h, lo, hi, ptr(out), out.shape[1], 0)
+
     def profile_device(self, dst_dev_ptr, ld=None):
         call("karma_kmer_profile", self.h, ctypes.c_void_p(dst_dev_ptr), ld or self.M, 1)
 
@@ -178,10 +185,17 @@ class KmerPlan:
         self.close()
 
 
-def kmer_profile(sequences, kmer_size, ctx=None):
+BLOCK_BYTES = 4 << 30  # row blocks of a streamed profile (device buffer and D2H unit)
+
+
+def kmer_profile(sequences, kmer_size, ctx=None, out=None, block_bytes=None):
     """Full single-device k-mer profile of an OrderedDict (kmer.py:199-233).
 
-    Returns (profile float64[N, M], columns list[str], row_totals int64[N])."""
+    out: None (a new array), or a caller float64[N, M] C-order array -- a
+    numpy.memmap for a profile larger than host memory -- that is filled one
+    row block (~block_bytes) at a time (SURVEY.md §8(e) streaming).  Its shape
+    must be (N, M); M is the column count the sequences give (kmer_columns).
+    Returns (profile, columns list[str], row_totals int64[N])."""
     ctx = ctx or _lib.default_context()
     kmode = kmode_of(kmer_size)
     packed = getattr(sequences, "karma_packed", None)  # fasta.FastaDict straight from the C++ reader
@@ -190,15 +204,80 @@ def kmer_profile(sequences, kmer_size, ctx=None):
     try:
         plan = KmerPlan(ctx, store, kmode)
         try:
-            plan.finalize()
+            M = plan.finalize()
             cols = decode_keys(plan.columns(), kmode)
-            prof = plan.profile_host()
+            n = store.n
+            big = n * M * 8 > (block_bytes or BLOCK_BYTES)
+            if out is None and not big:
+                prof = plan.profile_host()
+            else:
+                if out is None:
+                    out = np.empty((n, M), np.float64)
+                if out.shape != (n, M) or out.dtype != np.float64 or not out.flags.c_contiguous:
+                    raise ValueError(f"out must be a C-order float64 array of shape {(n, M)}")
+                for lo, hi, blk in _row_blocks(plan, n, M, block_bytes):
+                    out[lo:hi] = blk
+                prof = out
             tot = plan.row_totals()
         finally:
             plan.close()
     finally:
         store.close()
     return prof, cols, tot
+
+
+def _row_blocks(plan, n, M, block_bytes=None, ring=1):
+    """(lo, hi, block) over the profile's rows; blocks are host arrays reused
+    round-robin from a ring of `ring` (a consumer may hold ring - 1 of them)."""
+    rows = max(1, min(n, (block_bytes or BLOCK_BYTES) // max(1, 8 * M)))
+    bufs = [np.empty((rows, M), np.float64) for _ in range(max(1, ring))]
+    for i, lo in enumerate(range(0, n, rows)):
+        hi = min(n, lo + rows)
+        blk = bufs[i % len(bufs)][: hi - lo]
+        plan.profile_rows(lo, hi, blk)  # M == 0: the row totals only
+        yield lo, hi, blk
+
+
+def kmer_profile_blocks(sequences, kmer_size, block_rows, ctx=None, ring=1):
+    """The profile as a stream of (lo, hi, rows float64[hi - lo, M]) row blocks
+    and the column list: (columns, generator).  Block arrays are reused from a
+    ring of `ring` buffers: a consumer may keep the last ring - 1 blocks while
+    it advances (e.g. hash them on a thread pool).  Nothing of size N x M
+    exists on the host or the device at once (SURVEY.md §8(e) C5 streaming)."""
+    ctx = ctx or _lib.default_context()
+    kmode = kmode_of(kmer_size)
+    packed = getattr(sequences, "karma_packed", None)
+    blob, offs, key_len = packed if packed is not None else encode_sequences(sequences)
+    store = ContigStore(ctx, blob, offs, key_len)
+    plan = KmerPlan(ctx, store, kmode)
+    M = plan.finalize()
+    cols = decode_keys(plan.columns(), kmode)
+
+    def gen():
+        try:
+            yield from _row_blocks(plan, store.n, M, block_rows * max(1, 8 * M), ring)
+        finally:
+            plan.close()
+            store.close()
+
+    return cols, gen()
+
+
+def kmer_columns_count(sequences, kmer_size, ctx=None):
+    """M: the number of columns (present k-mers) of the sequences' profile."""
+    ctx = ctx or _lib.default_context()
+    kmode = kmode_of(kmer_size)
+    packed = getattr(sequences, "karma_packed", None)
+    blob, offs, key_len = packed if packed is not None else encode_sequences(sequences)
+    store = ContigStore(ctx, blob, offs, key_len)
+    try:
+        plan = KmerPlan(ctx, store, kmode)
+        try:
+            return plan.finalize()
+        finally:
+            plan.close()
+    finally:
+        store.close()
 
 
 def kmer_profile_device(sequences, kmer_size, ctx=None):

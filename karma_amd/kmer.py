@@ -45,11 +45,21 @@ class KmerClustering:
             (unlabeled if label == -1 else labeled).append(members)
         return labeled, unlabeled
 
-    def __calc_kmer_profile(self):
+    def __calc_kmer_profile(self, out=None):
         """kmer.py:199-264 on the GPU.  Same return value, side effects
         (self.kmers, self.sorted_kmer_set) and failure modes (ZeroDivisionError
-        for a zero-length key, logger.error + exit(1) for an all-zero row)."""
-        return self.__profile(engine.kmer_profile)
+        for a zero-length key, logger.error + exit(1) for an all-zero row).
+
+        out (an addition; the reference has no such argument): a caller
+        float64[N, M] C-order array or numpy.memmap that the profile fills one
+        row block at a time and that is returned -- config 5's 131 GB profile
+        need not exist in host memory as a fresh array.  M is the column count
+        (KmerClustering.columns_count)."""
+        return self.__profile(lambda seqs, k: engine.kmer_profile(seqs, k, out=out))
+
+    def columns_count(self):
+        """M, the column count __calc_kmer_profile will have (to size `out`)."""
+        return engine.kmer_columns_count(self.sequences, self.kmer_size)
 
     def calc_kmer_profile_device(self):
         """The same profile left in HBM for a GPU consumer (SURVEY.md §8(f) row 4,

@@ -25,4 +25,4 @@ def test_comm_sources_use_the_guarded_group():
     # no bare ncclGroupStart/End (and so no early return inside a group) in comm.hip
     src = open(os.path.join(CSRC, "comm.hip")).read()
     assert "ncclGroupStart" not in src and "ncclGroupEnd" not in src
-    assert src.count("NcclGroup g;") == 2
+    assert src.count("NcclGroup g;") == 3  # count exchange, alltoallv, alltoallv_kv

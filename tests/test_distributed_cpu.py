@@ -150,6 +150,14 @@ class OracleOps:
         kc = np.asarray(kc, np.int64).reshape(-1, 2)
         return self.merge(kc[:, 0].copy(), kc[:, 1].copy(), runs)
 
+    # the production exchange: keys and counts as two arrays (alltoallv_kv)
+    def pairs_kv(self, pairs, bounds):
+        starts = np.searchsorted(pairs["keys"], np.asarray(bounds, np.uint64) << np.uint64(32))
+        return pairs["keys"].view(np.int64), pairs["counts"], starts
+
+    def merge_kv(self, keys, counts, runs):
+        return self.merge(np.asarray(keys, np.int64).copy(), np.asarray(counts, np.int64).copy(), list(runs))
+
     def merge(self, keys, counts, runs):
         k = keys.view(np.uint64)
         # the contract of karma_pairs_merge_runs: one sorted slice per sender
@@ -298,6 +306,8 @@ def test_host_comm_collectives(kind, tmp_path):
         out["slices"] = c.allgather_slices_(buf, bounds).copy()
         send = np.concatenate([np.full(r + 1, 100 * rank + r, np.int64) for r in range(world)])
         out["a2a"], out["recv"] = c.alltoallv(send, [r + 1 for r in range(world)])
+        ka, kb, out["recv_kv"] = c.alltoallv_kv(send, -send, [r + 1 for r in range(world)])
+        out["kv_ok"] = bool(np.array_equal(ka, out["a2a"]) and np.array_equal(kb, -out["a2a"]))
         c.barrier()
         return out
 
@@ -324,6 +334,7 @@ def test_host_comm_collectives(kind, tmp_path):
         assert np.array_equal(o["var"], np.array([0, 0, 1], np.int64))
         assert np.array_equal(o["slices"], np.array([0, 1, 20, 21, 22, 23, 24], np.int64))
         assert o["recv"] == [r + 1] * world
+        assert o["recv_kv"] == o["recv"] and o["kv_ok"]
         assert np.array_equal(o["a2a"], np.concatenate([np.full(r + 1, 100 * s + r) for s in range(world)]))
 
 

@@ -102,3 +102,64 @@ def test_dlpack_zero_copy_into_torch_consumer():
         pytest.skip("torch not importable")
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert p.stdout.startswith("ok")
+
+
+def test_streamed_profile_into_memmap(tmp_path):
+    """SURVEY.md §8(e) C5 streaming: the host profile filled one row block at a
+    time into a caller's numpy.memmap (KmerClustering.__calc_kmer_profile(out=)),
+    bit-identical to the one-piece profile and the oracle."""
+    from collections import OrderedDict
+
+    from karma_amd import engine
+    from karma_amd.kmer import KmerClustering
+    from oracle import oracle
+
+    blob, offs, key_len = engine.synth_contigs(31, 3000, 20, 900, 40)
+    seqs = OrderedDict((f">c{i}", bytes(blob[offs[i]:offs[i + 1]]).decode("latin-1")) for i in range(3000))
+    for k in ("5p6", 7):
+        whole, cols, tot = engine.kmer_profile(seqs, k)
+        mm = np.lib.format.open_memmap(str(tmp_path / f"p{k}.npy"), mode="w+", dtype=np.float64, shape=whole.shape)
+        got, cols2, tot2 = engine.kmer_profile(seqs, k, out=mm, block_bytes=whole.shape[1] * 8 * 701)
+        assert got is mm and cols2 == cols and np.array_equal(tot2, tot)
+        assert np.array_equal(np.asarray(mm).view(np.uint64), whole.view(np.uint64))
+        oprof, ocols, _ = oracle.calc_kmer_profile(seqs, k)
+        assert ocols == cols and np.array_equal(whole.view(np.uint64), oprof.view(np.uint64))
+    kc = KmerClustering(seqs, str(tmp_path), "5p6", 4)
+    out = np.lib.format.open_memmap(str(tmp_path / "kc.npy"), mode="w+", dtype=np.float64,
+                                    shape=(3000, kc.columns_count()))
+    res = kc._KmerClustering__calc_kmer_profile(out=out)
+    assert res is out and len(kc.kmers) == out.shape[1]
+    ref = KmerClustering(seqs, str(tmp_path), "5p6", 4)._KmerClustering__calc_kmer_profile()
+    assert np.array_equal(np.asarray(out).view(np.uint64), ref.view(np.uint64))
+
+
+def test_config5_profile_streamed_in_row_blocks():
+    """BASELINE configs[4] (1M contigs, k = 7, a 131 GB profile) streamed to the
+    host in 8192-row blocks (1 GB each, a ring of 12 host buffers, blocks hashed
+    on a thread pool): the block digests equal the oracle's (tests/golden/
+    digests.json config5_1gpu).  Device memory holds one block, not the profile."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+
+    import digests as D
+    from karma_amd import engine
+
+    g = D.load()["config5_1gpu"]
+    assert g["N"] == 1_000_000 and g["kmer"] == 7
+    packed = engine.synth_contigs(5, g["N"], 400, 800, 0)  # bench.make_inputs' contigs of config5_1gpu
+
+    class Packed(dict):  # the store's input as is (FastaDict-style), no Python strings
+        karma_packed = packed
+
+    ring = 12
+    cols, blocks = engine.kmer_profile_blocks(Packed(), 7, D.BLOCK_ROWS, ring=ring)
+    assert len(cols) == g["M"] and D.columns_digest(cols) == g["columns"]
+    digs, pend = [], []
+    with ThreadPoolExecutor(ring - 2) as pool:
+        for lo, hi, blk in blocks:
+            pend.append(pool.submit(lambda m: hashlib.sha256(m).digest(), memoryview(blk).cast("B")))
+            while len(pend) > ring - 2:  # a block is hashed before its buffer comes round again
+                digs.append(pend.pop(0).result())
+        digs += [f.result() for f in pend]
+    assert len(digs) == -(-g["N"] // D.BLOCK_ROWS)
+    assert hashlib.sha256(b"".join(digs)).hexdigest() == g["profile_blocks"]
