@@ -162,6 +162,13 @@ def test_rccl_comm_world1_calls():
         out, recv = comm.alltoallv(buf, [src.size])
         assert recv == [src.size]
         np.testing.assert_array_equal(out.numpy(), src)
+        neg = _lib.DevBuf.from_numpy(ctx, -src)
+        ka, kb, recv2 = comm.alltoallv_kv(buf, neg, [src.size])
+        assert recv2 == [src.size]
+        np.testing.assert_array_equal(ka.numpy(), src)
+        np.testing.assert_array_equal(kb.numpy(), -src)
+        for b in (neg, ka, kb):
+            b.close()
         g = comm.allgather_fixed(buf)
         np.testing.assert_array_equal(g.numpy(), src)
         v = comm.allgather_var(_lib.DevBuf.from_numpy(ctx, src[:17]))
