@@ -718,7 +718,8 @@ profile_wave_kernel(
     const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
     const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
     const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
-    double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot) {
+    double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
+    int64_t exc0) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     // wave index in an SGPR: contig offsets and lengths load with scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
@@ -762,8 +763,11 @@ profile_wave_kernel(
             m.klen = keylen[cc];
             // the flag byte from its dword by a scalar load (a byte load is a
             // vector load, whose wait also drains the previous row's stores)
-            const uint32_t hw = reinterpret_cast<const uint32_t*>(has_exc)[cc >> 2];
-            m.exc = ((hw >> (8 * (cc & 3))) & 0xFFu) != 0;
+            // (has_exc is the store's whole array, dword-aligned: contig cc of
+            // these rows is entry exc0 + cc)
+            const int64_t ce = exc0 + cc;
+            const uint32_t hw = reinterpret_cast<const uint32_t*>(has_exc)[ce >> 2];
+            m.exc = ((hw >> (8 * (ce & 3))) & 0xFFu) != 0;
         }
     };
     const int64_t stride = (int64_t)gridDim.x * wpb;
@@ -1281,9 +1285,9 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_wave_kernel<P56, C16>), kPBlock, \
                                      lds, ceil_div(n, kPBlock / 64));                                            \
         KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16>), g_, kPBlock, lds, c->packed.ptr,      \
-                     c->mask.ptr, has_exc, woff, off, c->raw, keylen, n, k, with_len,                            \
+                     c->mask.ptr, c->has_exc.ptr, woff, off, c->raw, keylen, n, k, with_len,                     \
                      p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err,       \
-                     (int)p->S, row_tot);                                                                        \
+                     (int)p->S, row_tot, lo);                                                                    \
     } while (0)
         if (p56) {
             if (c16) KARMA_WAVE_LAUNCH(true, true);

@@ -264,6 +264,12 @@ class ReadGraph(nx.Graph):
     def from_equivalence_classes(cls, equivalence_class_file: str, sequences_from_fasta: dict) -> "ReadGraph":
         """read_graph.py:61-148 with the pair sums and weights on the GPU."""
         names, off, members, counts, skip = parse_eq_classes(equivalence_class_file)
+        return cls._from_eq_arrays(names, off, members, counts, skip, sequences_from_fasta)
+
+    @classmethod
+    def _from_eq_arrays(cls, names, off, members, counts, skip, sequences_from_fasta):
+        """from_equivalence_classes after the parse (read_graph.py:86-148): eq
+        names, class offsets/members/counts and the size-token-"1" flags."""
         n = len(names)
         if n == 0:
             e = None

@@ -405,3 +405,40 @@ def omp_graph_reads(grp_off, members, n_nodes):
             break
         cap = -E
     return dict(a=ea[:E], b=eb[:E], shared=es[:E], weight=ew[:E], totals=totals[:n_nodes], zero_div=bool(zd.value))
+
+
+def calc_connections(a, b, w, sub, rank, weight_cutoff=0):
+    """karma.py:103-118 (calc_connections_between_mcl_subclusters) restated for
+    large graphs: instead of walking product(nodes_A, nodes_B) with has_edge for
+    every pair of subclusters (O(N^2)), every edge (a, b, w) between two
+    subclusters is placed at its position in that walk -- pair (i, j), i < j the
+    subcluster indices in dict order, then (rank of the i-side node in nodes_A,
+    rank of the j-side node in nodes_B) -- and each pair's running sum is
+    accumulated left to right from 0 in Python floats, counting the edges after
+    which it exceeds the cutoff (the reference appends [A, B] once per such
+    edge).  sub[node] = subcluster index or -1, rank[node] = position in its
+    subcluster.  Returns a list of (i, j, count) in combinations order."""
+    a = np.asarray(a, np.int64)
+    b = np.asarray(b, np.int64)
+    sa, sb = np.asarray(sub)[a], np.asarray(sub)[b]
+    keep = (sa >= 0) & (sb >= 0) & (sa != sb)
+    a, b, w, sa, sb = a[keep], b[keep], np.asarray(w, np.float64)[keep], sa[keep], sb[keep]
+    lo_is_a = sa < sb
+    i = np.where(lo_is_a, sa, sb)
+    j = np.where(lo_is_a, sb, sa)
+    ri = np.where(lo_is_a, np.asarray(rank)[a], np.asarray(rank)[b])
+    rj = np.where(lo_is_a, np.asarray(rank)[b], np.asarray(rank)[a])
+    o = np.lexsort((rj, ri, j, i))
+    out = []
+    cur, weight, over = None, 0, 0
+    for x, y, wt in zip(i[o].tolist(), j[o].tolist(), w[o].tolist()):
+        if (x, y) != cur:
+            if cur is not None and over:
+                out.append((cur[0], cur[1], over))
+            cur, weight, over = (x, y), 0, 0
+        weight += wt
+        if weight > weight_cutoff:
+            over += 1
+    if cur is not None and over:
+        out.append((cur[0], cur[1], over))
+    return out

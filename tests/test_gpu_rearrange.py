@@ -119,3 +119,55 @@ def test_rearrange_hand_graph_and_partition_check():
     with pytest.raises(ValueError):
         subs = lookup([[["a", "b"], ["b"]]])
         rearrange.calc_connections_between_mcl_subclusters(subs, 0, full_graph=h)
+
+
+def test_rearrange_config5_scale():
+    """BASELINE configs[4] --rearrange leg (karma.py:409-437) at config-5 size: the
+    graph of config 5's 1M contigs, from 25M of its fragments as salmon eq
+    classes through the drop-in's eq constructor (the path karma.py:240 calls),
+    ~250k MCL-like subclusters (2-8 contigs, some mixing genes); the connection
+    list of karma.py:103-118 at three cutoffs equals the large-graph
+    restatement oracle.calc_connections (pinned on the CPU against the
+    reference's goldens and its own walk, tests/test_rearrange_oracle_cpu.py),
+    computed from the oracle's own eq graph."""
+    import numpy as np
+
+    from karma_amd import engine
+    from oracle import oracle
+
+    n = 1_000_000
+    genes = engine.synth_genes(5, n)
+    off, mem, cnt = engine.synth_eq_classes(5, n, 0, 25_000_000, True, genes=genes)
+    skip = (np.diff(off) == 1).astype(np.uint8)
+    names = [f"ctg{i}" for i in range(n)]
+    g = ReadGraph._from_eq_arrays(names, off, mem, cnt, skip, dict.fromkeys((">" + x for x in names), ""))
+    og = oracle.graph_groups(off, mem, cnt, skip, n, dedup=False)
+    assert g.number_of_edges() == len(og["a"]) > 500_000
+    rng = random.Random(55)
+    order = list(range(n))
+    for i in range(0, n - 1, 2):  # a fifth of neighbouring pairs swapped: subclusters that mix genes
+        if rng.random() < 0.2:
+            order[i], order[i + 1] = order[i + 1], order[i]
+    nest, i = [], 0
+    while i < n:
+        k = rng.randint(2, 8)
+        cl = order[i:i + k]
+        i += k
+        cut = rng.randint(1, len(cl))
+        nest.append([[names[x] for x in cl[:cut]]] + ([[names[x] for x in cl[cut:]]] if cl[cut:] else []))
+    subs = lookup(nest)
+    keys = list(subs)
+    sub = np.full(n, -1, np.int64)
+    rank = np.zeros(n, np.int64)
+    for si, key in enumerate(keys):
+        for r, node in enumerate(subs[key]["mcl_subcluster"]):
+            x = int(node[3:])
+            sub[x], rank[x] = si, r
+    assert len(keys) > 200_000
+    for cutoff in (0, 0.2, 1.0):
+        got = rearrange.calc_connections_between_mcl_subclusters(subs, cutoff, full_graph=g)
+        want = []
+        for a, b, c in oracle.calc_connections(og["a"], og["b"], og["weight"], sub, rank, cutoff):
+            want.extend([keys[a], keys[b]] for _ in range(c))
+        assert got == want, cutoff
+        assert len(want) > (1000 if cutoff < 1 else 0)
