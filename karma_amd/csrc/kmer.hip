@@ -1255,8 +1255,10 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
     const int64_t* const woff = c->woff.ptr + lo;
     const int64_t* const off = c->off + lo;
     const int32_t* const keylen = c->keylen + lo;
-    // row totals first: with M == 0 every row is all-zero (kmer.py:250-258)
-    KARMA_HIP(hipMemsetAsync(row_tot, 0, n * 8, ctx->stream));
+    const bool wave = M <= kWaveMaxM && p->S <= 8192;
+    // row totals: with M == 0 every row is all-zero (kmer.py:250-258); the
+    // block kernel adds to them; the wave kernel writes every row's total
+    if (M == 0 || !wave) KARMA_HIP(hipMemsetAsync(row_tot, 0, n * 8, ctx->stream));
     if (M == 0) return KARMA_OK;
     KARMA_CHECK(out, KARMA_ERR_ARG, "null out");
     KARMA_CHECK(c->zero_key_maxlen < p->kmin, KARMA_ERR_ZERO_DIV,
@@ -1268,10 +1270,11 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         if ((rc = dev_out.alloc(ctx, (size_t)n * ld))) return rc;
         dst = dev_out.ptr;
     }
+    // a kernel-side flag for a zero-length key's row with k-mers; the host
+    // check above (zero_key_maxlen) is the error path, so the flag is never
+    // read and not cleared per launch
     int* const err = p->err.ptr;  // no temporaries: the launch may run on a side stream
-    KARMA_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
     bool with_len = p->kmode != 8;
-    const bool wave = M <= kWaveMaxM && p->S <= 8192;
     const int k = p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode;
     if (wave) {
         // one round of resident blocks, each wave striding over contigs; u16
