@@ -218,6 +218,12 @@ typedef struct karma_graph_job karma_graph_job;
 int karma_graph_records_begin(karma_ctx* ctx, const uint32_t* records, int64_t n_records, int64_t n_contigs,
                               int flags, int is_device, karma_graph_job** job);
 int karma_graph_records_end(karma_graph_job* job, karma_pairs** out);
+/* Owner bounds (nranks + 1 contig ids) of the exchange that will split the
+ * next records job's list on this context: the job finds each owner's start
+ * on the device as it builds the list, and karma_pairs_split with the same
+ * bounds then answers without a launch or a synchronisation.  Applies to one
+ * job; at most 64 ranks. */
+int karma_graph_split_hint(karma_ctx* ctx, const int64_t* bounds, int nranks);
 /* Salmon eq classes (read_graph.py:75-114): cls_off[n_classes+1] into members
  * (contig indices as listed, duplicates kept), counts[n_classes], pair_skip[c]=1
  * when the eq_size token is "1" (read_graph.py:102).  Totals (read_graph.py:86-92)

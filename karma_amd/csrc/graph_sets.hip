@@ -1380,12 +1380,21 @@ __device__ __forceinline__ uint32_t code_count(const uint32_t* __restrict__ part
 // HF hash slots: one group's list (n_pg = 1, < kHashR keys) fits 4096, and the
 // block then takes 68 KB of LDS (2 blocks per CU for the many small buckets of
 // a large n_contigs); several groups' lists are merged in 8192.
+// Owner bounds of an exchange (karma_graph_split_hint): the final kernel of the
+// bucket holding bound r writes the number of its keys with a < bounds[r].
+constexpr int kMaxSplit = 65;  // 64 ranks
+struct SplitArgs {
+    int n;
+    int64_t b[kMaxSplit];
+    int64_t* out;  // per bound: keys of its bucket below it
+};
+
 template <int HF>
 __global__ void __launch_bounds__(kFT) final_kernel(
     int n_pg, int n_cg, int bw, int bbits, int dbits, int bwc, const uint32_t* __restrict__ part_band,
     const uint32_t* __restrict__ part_ch, const uint32_t* __restrict__ part_keys,
     const uint32_t* __restrict__ part_cnt, const int* __restrict__ part_n, uint64_t* __restrict__ out_keys,
-    int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n, uint8_t* __restrict__ overflow) {
+    int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n, uint8_t* __restrict__ overflow, SplitArgs split) {
     __shared__ uint32_t bsum[kBand];
     __shared__ uint32_t rowpos[(kBand >> 3) + 1];  // nonzero band slots before row a_local (D = 8 on this path)
     __shared__ uint32_t hkeys[HF];
@@ -1511,6 +1520,22 @@ __global__ void __launch_bounds__(kFT) final_kernel(
         oc[pos] = hvals[j];
     }
     if (threadIdx.x == 0) out_n[bucket] = nb + nh;
+    if (split.n) {
+        __syncthreads();  // the bucket's list, written above by this block
+        const int64_t total = nb + nh, c_lo = (int64_t)bucket << bw, c_hi = c_lo + (int64_t(1) << bw);
+        for (int r = threadIdx.x; r < split.n; r += kFT) {
+            const int64_t bd = split.b[r];
+            if (bd < c_lo || bd >= c_hi) continue;
+            const uint64_t lim = (uint64_t)bd << 32;
+            int64_t lo = 0, hi = total;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (ok[mid] < lim) lo = mid + 1;
+                else hi = mid;
+            }
+            split.out[r] = lo;
+        }
+    }
 }
 
 // ---- overflow fallback: every pair of one bucket as (key, count), generic sort ----
@@ -1889,6 +1914,8 @@ struct SetsJob {
     // | pairs per bucket[B+1] | their exclusive scan[B+1] | overflow[B]
     int64_t ctrl_words = 0;
     DevArray<int64_t> ctrl;
+    std::vector<int64_t> split_b;  // owner bounds (karma_graph_split_hint), found by the final kernel
+    int64_t* split_loc = nullptr;   // in the control block: per bound, keys of its bucket below it
     int* flags = nullptr;
     unsigned* counters = nullptr;
     int64_t* n_per = nullptr;
@@ -1944,7 +1971,7 @@ int SetsJob::setup() {
     KARMA_TRY(n_gen.alloc(ctx, n_chunks));
     KARMA_TRY(n_pl.alloc(ctx, n_chunks));
     KARMA_TRY(big_list.alloc(ctx, A / (kMaxFast + 1) + 1));
-    ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8);
+    ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8) + (int64_t)split_b.size();
     // one allocation (and one memset per attempt) for the control block and
     // the per-partition-block item counts behind it
     KARMA_TRY(ctrl.alloc(ctx, ctrl_words + 2 * n_pblk));
@@ -1954,6 +1981,7 @@ int SetsJob::setup() {
     n_per = ctrl.ptr + 6;
     dst = n_per + (B + 1);
     ovf = reinterpret_cast<uint8_t*>(dst + (B + 1));
+    split_loc = dst + (B + 1) + ceil_div(B, 8);
     void* hpin = nullptr;
     KARMA_TRY(ctx_job_pinned(ctx, ctrl_words * 8, &hpin));
     hctrl = static_cast<const int64_t*>(hpin);
@@ -2085,14 +2113,18 @@ int SetsJob::launch() {
                      n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
     KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
                  g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
+    SplitArgs sa{};
+    sa.n = (int)split_b.size();
+    for (int r = 0; r < sa.n; ++r) sa.b[r] = split_b[r];
+    sa.out = split_loc;
     if (n_pg == 1)
         KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashR>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits,
                      g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
-                     ovf);
+                     ovf, sa);
     else
         KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashF>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits,
                      g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
-                     ovf);
+                     ovf, sa);
     KARMA_TRY(scan_excl_i64(ctx, n_per, dst, B + 1));
     KARMA_HIP(hipMemcpyAsync(const_cast<int64_t*>(hctrl), ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost,
                              ctx->stream));
@@ -2215,7 +2247,21 @@ int SetsJob::finish(karma_pairs* out) {
     KARMA_TRY(mc.alloc(ctx, U));
     KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, slot_k.ptr, slot_c.ptr, (int64_t)kSlotCap,
                  pk.ptr, pc.ptr, n_per, dst, mk.ptr, mc.ptr);
-    if (!relabeled) return finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out);
+    if (!relabeled) {
+        KARMA_TRY(finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out));
+        if (!split_b.empty() && !any_ovf && n_big == 0) {
+            // the owners' slice starts, from the final kernel's in-bucket counts
+            const int64_t* h_dst = hctrl + 6 + (B + 1);
+            const int64_t* h_loc = h_dst + (B + 1) + ceil_div(B, 8);
+            out->split_bounds = split_b;
+            out->split_starts.resize(split_b.size());
+            for (size_t r = 0; r < split_b.size(); ++r) {
+                const int64_t b = split_b[r] >> g.bw;
+                out->split_starts[r] = split_b[r] <= 0 ? 0 : (b < B ? h_dst[b] + h_loc[r] : U);
+            }
+        }
+        return KARMA_OK;
+    }
     KARMA_TRY(finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out, remap_map.ptr));
     // back to the original ids, sorted again (keys stay unique: the map is a bijection)
     if (out->n) KARMA_LAUNCH(ctx, "relabel_back", relabel_back_kernel, grid_n(out->n), 256, 0, out->keys.ptr, out->n,
@@ -2240,6 +2286,8 @@ int sets_begin(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob**
     j->rec = rec;
     j->A = A;
     j->N = N;
+    if (!ctx->split_bounds.empty() && (int)ctx->split_bounds.size() <= kMaxSplit) j->split_b = ctx->split_bounds;
+    ctx->split_bounds.clear();  // one job
     KARMA_TRY(j->setup());
     const int rc = j->launch();
     if (rc) {

@@ -85,6 +85,9 @@ struct karma_ctx {
     void* mapped = nullptr;
     void* mapped_dev = nullptr;
     size_t mapped_bytes = 0;
+    // owner bounds for the next records graph job (karma_graph_split_hint): its
+    // final kernel also finds where each owner's slice starts (no split launch)
+    std::vector<int64_t> split_bounds;
 };
 
 namespace karma {
@@ -174,6 +177,9 @@ struct karma_pairs {
     // merge's order check (device flag), read at the next synchronisation.
     bool dups = false;
     karma::DevArray<int64_t> bad;
+    // karma_pairs_split's answer for split_bounds, found by the records job
+    // that built the list (empty: search on demand)
+    std::vector<int64_t> split_bounds, split_starts;
 };
 
 namespace karma {

@@ -123,8 +123,9 @@ class HipOps:
         pairs.rebind(self.ctx)
         return pairs
 
-    def graph_begin(self, records, n_records, n_contigs):
-        return self.engine.Pairs.from_records_begin(self.ctx, n_contigs, records, n_records)
+    def graph_begin(self, records, n_records, n_contigs, split_bounds=None):
+        return self.engine.Pairs.from_records_begin(self.ctx, n_contigs, records, n_records,
+                                                    split_bounds=split_bounds)
 
     def graph_end(self, job):
         return job.end()
@@ -233,6 +234,7 @@ class ShardedBuild:
             self.gops = HipOps(self.gctx, make_current=False)
             self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="karma-graph")
         bounds = np.zeros(comm.world + 1, np.int64)
+        self.split_bounds = None  # the exchange's owner bounds (None: no exchange)
         if comm.world > 1:
             allb = [b.tolist() for b in comm.allgather_host(np.array([c_lo, c_lo + n_loc], np.int64))]
             for r in range(comm.world):
@@ -242,6 +244,10 @@ class ShardedBuild:
         else:
             bounds[1] = n_glob
         self.bounds = bounds
+        if comm.world > 1:
+            self.split_bounds = bounds
+        elif self.emulate:
+            self.split_bounds = np.linspace(0, n_glob, self.emulate + 1).astype(np.int64)
 
     def contexts(self):
         """The karma contexts this build launches on (per-kernel timing)."""
@@ -269,6 +275,12 @@ class ShardedBuild:
             if side:
                 ops.join()
 
+    def _graph_begin(self, records, n_records):
+        """The records job, told the exchange's owner bounds when there is one."""
+        if self.split_bounds is not None:
+            return self.ops.graph_begin(records, n_records, self.n_glob, split_bounds=self.split_bounds)
+        return self.ops.graph_begin(records, n_records, self.n_glob)
+
     def _run(self, store, records, n_records, keep, side):
         ops, comm = self.ops, self.comm
         fut = None
@@ -283,7 +295,7 @@ class ShardedBuild:
             early = side and comm.world == 1 and hasattr(ops, "kmer_plan_side")
             job = None
             if early:
-                job = ops.graph_begin(records, n_records, self.n_glob)  # ---- read_graph.py:19-50 ----
+                job = self._graph_begin(records, n_records)  # ---- read_graph.py:19-50 ----
                 try:
                     plan = ops.kmer_plan_side(store, self.kmode)
                 except BaseException:
@@ -302,7 +314,7 @@ class ShardedBuild:
                 # and the profile (side stream) starts after the graph's kernels
                 if not early:
                     ops.finalize_async(plan)
-                    job = ops.graph_begin(records, n_records, self.n_glob)  # ---- read_graph.py:19-50 ----
+                    job = self._graph_begin(records, n_records)  # ---- read_graph.py:19-50 ----
                 try:
                     M = ops.finalize_wait(plan)
                     if self._prof is None or tuple(self._prof.shape) != (self.n_loc, M):
@@ -327,7 +339,7 @@ class ShardedBuild:
             stats["entries"] = ops.entries(local)
             stats["pairs_local"] = ops.pair_count(local)
         if comm.world > 1 or self.emulate:
-            bounds = self.bounds if comm.world > 1 else np.linspace(0, self.n_glob, self.emulate + 1).astype(np.int64)
+            bounds = self.split_bounds
             if hasattr(ops, "pairs_kv"):
                 # the list's keys and counts, each owner's slice of both in one
                 # grouped all-to-all-v; the owner merges one sorted run per sender

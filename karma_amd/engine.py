@@ -349,9 +349,13 @@ class Pairs:
         return cls(ctx, h)
 
     @classmethod
-    def from_records_begin(cls, ctx, n_contigs, device_ptr, n_records, grouped=True):
+    def from_records_begin(cls, ctx, n_contigs, device_ptr, n_records, grouped=True, split_bounds=None):
         """First half of from_records on device records (karma_graph_records_begin):
-        the pipeline is enqueued up to its host synchronisation; .end() finishes."""
+        the pipeline is enqueued up to its host synchronisation; .end() finishes.
+        split_bounds: owner bounds the list will be split at (karma_graph_split_hint)."""
+        if split_bounds is not None:
+            b = np.ascontiguousarray(split_bounds, np.int64)
+            call("karma_graph_split_hint", ctx.h, ptr(b), len(b) - 1)
         h = ctypes.c_void_p()
         flags = _lib.KARMA_REC_SORTED if grouped else _lib.KARMA_REC_UNSORTED
         call("karma_graph_records_begin", ctx.h, ctypes.c_void_p(device_ptr), n_records, n_contigs, flags, 1,

@@ -471,5 +471,15 @@ def test_graph_records_split_call():
         job2 = engine.Pairs.from_records_begin(ctx, n, dev.value, A)  # the context is free again
         k2, c2, _ = job2.end().get()
         assert np.array_equal(k0, k2) and np.array_equal(c0, c2)
+        # owner bounds given up front (karma_graph_split_hint): the final kernel's
+        # starts equal a search of the finished list, also for bounds off the
+        # bucket grid, at 0 and at n; other bounds still search
+        for bounds in ([0, 1000, 2000, n], [0, 1, 1024, 1025, 2047, 2999, n], [0, n]):
+            job3 = engine.Pairs.from_records_begin(ctx, n, dev.value, A, split_bounds=bounds)
+            p3 = job3.end()
+            want = np.searchsorted(k0, np.array(bounds, np.uint64) << np.uint64(32))
+            assert np.array_equal(p3.split(bounds), want)
+            assert np.array_equal(p3.split([0, 1500, n]), np.searchsorted(k0, np.array([0, 1500, n], np.uint64) << np.uint64(32)))
+            p3.close()
     finally:
         _lib.load().karma_dev_free(ctx.h, dev)
