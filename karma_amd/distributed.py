@@ -57,14 +57,20 @@ class HipOps:
     def kmer_plan(self, store, kmode):
         return self.engine.KmerPlan(self.ctx, store, kmode)
 
-    def kmer_plan_side(self, store, kmode):
-        """The presence pass and the column table enqueued on the side stream
-        (no exchange between them on one rank), so that the graph's kernels on
-        the main stream start at once, beside them; finalize_wait() waits for
-        the column table alone."""
+    def kmer_plan_side(self, store, kmode, comm=None):
+        """The presence pass and the column table enqueued on the side stream,
+        so that the graph's kernels on the main stream start at once, beside
+        them; finalize_wait() waits for the column table alone.  With a
+        communicator of several ranks the column set's exchange runs there too
+        (presence all-gather and OR-merge, exception keys all-gather; their
+        host synchronisations wait for the side stream only), issued in the
+        same order on every rank."""
         self.ctx.set_stream(self.side)
         try:
             plan = self.engine.KmerPlan(self.ctx, store, kmode)
+            if comm is not None and comm.world > 1:
+                self.presence_merge(plan, comm.allgather_fixed(self.presence_words(plan)), comm.world)
+                self.set_exceptions(plan, comm.allgather_var(self.exceptions(plan)))
             plan.finalize_async()
         finally:
             self.ctx.set_stream(self.stream)
@@ -289,21 +295,21 @@ class ShardedBuild:
         local = None
         try:
             # ---- k-mer profile (kmer.py:199-233) ----
-            # one rank with a side stream: the graph's kernels are enqueued
-            # first, then the presence pass and the column table on the side
-            # stream, beside them (no exchange between presence and columns)
-            early = side and comm.world == 1 and hasattr(ops, "kmer_plan_side")
+            # with a side stream: the graph's kernels are enqueued first, then
+            # the presence pass, the column set's exchange (several ranks) and
+            # the column table on the side stream, beside them
+            early = side and hasattr(ops, "kmer_plan_side")
             job = None
             if early:
                 job = self._graph_begin(records, n_records)  # ---- read_graph.py:19-50 ----
                 try:
-                    plan = ops.kmer_plan_side(store, self.kmode)
+                    plan = ops.kmer_plan_side(store, self.kmode, comm)
                 except BaseException:
                     ops.graph_end(job)
                     raise
             else:
                 plan = ops.kmer_plan(store, self.kmode)
-            if comm.world > 1:
+            if comm.world > 1 and not early:
                 # column set = global union: OR of every rank's presence bitmap,
                 # union of every rank's exception keys (kmer.py:146-179)
                 ops.presence_merge(plan, comm.allgather_fixed(ops.presence_words(plan)), comm.world)
