@@ -1897,6 +1897,16 @@ __global__ void relabel_back_kernel(uint64_t* __restrict__ keys, int64_t n, cons
 #ifndef KARMA_MARK_AT
 #define KARMA_MARK_AT 0
 #endif
+// where side-stream work (the k-mer profile) may start, see SetsJob::launch;
+// KARMA_MARK_AT in the environment overrides the default (scheduling only:
+// every position runs the same kernels)
+int mark_at() {
+    static const int at = [] {
+        const char* e = std::getenv("KARMA_MARK_AT");
+        return e ? std::atoi(e) : KARMA_MARK_AT;
+    }();
+    return at;
+}
 struct SetsJob {
     karma_ctx* ctx = nullptr;
     const uint2* rec = nullptr;
@@ -2032,7 +2042,7 @@ int SetsJob::launch() {
     const bool probe = A > 0 && !relabeled;  // the probe kernel clears the control block
     if (!probe) KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk) * 8, ctx->stream));
     if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
-    if (KARMA_MARK_AT == 3 && attempt == 0 && !relabeled) {  // side-stream work may start beside classify
+    if (mark_at() == 3 && attempt == 0 && !relabeled) {  // side-stream work may start beside classify
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
         KARMA_HIP(hipEventRecord(ctx->mark_ev, ctx->stream));
         ctx->mark_set = true;
@@ -2071,7 +2081,7 @@ int SetsJob::launch() {
     // 2 stretches the profile to 0.60 ms beside the reduce (1.43 vs 1.35);
     // 3 stretches classify 0.54 -> 0.74 ms (1.35 vs 1.25): HBM is already full
     auto mark = [&](int at) -> int {
-        if (KARMA_MARK_AT != at || attempt != 0) return KARMA_OK;
+        if (mark_at() != at || attempt != 0) return KARMA_OK;
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
         KARMA_HIP(hipEventRecord(ctx->mark_ev, ctx->stream));
         ctx->mark_set = true;
@@ -2105,6 +2115,7 @@ int SetsJob::launch() {
         KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
                      g.Bc, g.bwc, n_cg, part_ch.ptr);
     }
+    KARMA_TRY(mark(4));  // after the code reduce: beside the pair kernels and the final kernel
     if (wide_p)
         KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStreamWide>, n_pblk, kPT, 0, plist.ptr, pcap,
                      n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
