@@ -241,3 +241,88 @@ def test_bench_strong_config3_two_ranks_in_run_parity():
     d = res["parity_detail"]
     assert res["parity"] is True, d
     assert d["ranks"] == 2 and d["edges"] == 199_510 and d["mismatch"] == []
+
+
+_RCCL_RANK = r"""
+import os, sys
+sys.path.insert(0, os.environ["KARMA_REPO"])
+import numpy as np
+from karma_amd import _lib, engine, comm as comm_mod
+from karma_amd.distributed import ShardedBuild
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+sizes = [int(x) for x in os.environ["KARMA_SHARDS"].split(",")]
+n_glob, c_lo, n_loc = sum(sizes), sum(sizes[:rank]), sizes[rank]
+F = int(os.environ["KARMA_FRAGS"])
+ctx = _lib.Context(rank)
+comm = comm_mod.create(ctx, world, rank, backend="rccl")
+blob, offs, key_len = engine.synth_contigs(29, n_loc, 30, 900, 300, first=c_lo)
+genes = engine.synth_genes(29, n_glob)
+f_lo, f_hi = F * rank // world, F * (rank + 1) // world
+rec = engine.synth_records(29, n_glob, f_lo, f_hi, True, genes=genes)
+build = ShardedBuild(ctx, comm, -1, n_glob, c_lo, n_loc)
+store = engine.ContigStore(ctx, blob, offs, key_len)
+rec_dev = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))
+res = build.run(store, rec_dev.ptr, len(rec), keep=True)
+e = res["edges"]
+np.savez(os.path.join(os.environ["KARMA_OUT"], f"rank{rank}.npz"), profile=res["profile"].numpy(),
+         cols=res["columns"], a=e.a, b=e.b, w=e.weight, tot=e.totals)
+build.close(); store.close(); rec_dev.close(); comm.close(); ctx.close()
+"""
+
+
+def test_rccl_ranks_on_separate_devices_match_oracle(tmp_path):
+    """The library's RCCL communicator across real ranks (one process and one
+    GPU each): unequal contig shards (the padded all-gather of the exception
+    keys and the non-in-place totals all-gather), the grouped key/count
+    all-to-all-v, the owners' merge; the union must equal the single-process
+    oracle bit for bit.  Needs >= 2 GPUs: skipped on a one-GPU box (there the
+    driver's multi-GPU bench runs the same exchange with its in-run parity
+    check)."""
+    import ctypes
+    import os
+
+    n = ctypes.c_int(0)
+    _lib.load().karma_device_count(ctypes.byref(n))
+    if n.value < 2:
+        pytest.skip("needs >= 2 GPUs")
+    world = min(n.value, 4)
+    sizes = [700 + 131 * r for r in range(world)]
+    frags = 50_000 * world
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _free_port_pair()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), KARMA_REPO=repo, KARMA_OUT=str(tmp_path),
+                   KARMA_SHARDS=",".join(map(str, sizes)), KARMA_FRAGS=str(frags))
+        procs.append(subprocess.Popen([sys.executable, "-c", _RCCL_RANK], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    for p in procs:
+        out, err = p.communicate(timeout=300)
+        assert p.returncode == 0, err[-3000:]
+    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    n_glob = sum(sizes)
+    seqs, recs = OrderedDict(), []
+    genes = engine.synth_genes(29, n_glob)
+    lo = 0
+    for r in range(world):
+        blob, offs, _ = engine.synth_contigs(29, sizes[r], 30, 900, 300, first=lo)
+        for i in range(sizes[r]):
+            seqs[f">ctg{lo + i}"] = bytes(blob[offs[i]:offs[i + 1]]).decode()
+        lo += sizes[r]
+        recs.append(engine.synth_records(29, n_glob, frags * r // world, frags * (r + 1) // world, True, genes=genes))
+    prof, cols, _ = oracle.calc_kmer_profile(seqs, "5p6")
+    for p in parts:
+        assert engine.decode_keys(p["cols"], -1) == cols
+    got = np.concatenate([p["profile"] for p in parts])
+    assert np.array_equal(got.view(np.uint64), prof.view(np.uint64))
+    rec = np.concatenate(recs).astype(np.int64)
+    st = np.flatnonzero(np.r_[True, rec[1:, 0] != rec[:-1, 0]])
+    o = oracle.graph_groups(np.r_[st, len(rec)], rec[:, 1], None, None, n_glob, dedup=True)
+    a = np.concatenate([p["a"] for p in parts])
+    b = np.concatenate([p["b"] for p in parts])
+    w = np.concatenate([p["w"] for p in parts])
+    assert np.array_equal(a, o["a"]) and np.array_equal(b, o["b"])
+    assert np.array_equal(w.view(np.uint64), o["weight"].view(np.uint64))
+    for p in parts:
+        assert np.array_equal(p["tot"], o["totals"])
