@@ -55,9 +55,6 @@ constexpr int kMaxBc = 512;           // code buckets
 // partition LDS is sized by the bucket count: the narrow variants (<= 512 pair
 // and <= 128 code buckets, n_contigs <= 2^19) keep 3 code-partition blocks per CU
 constexpr int kNarrowB = 512, kNarrowBc = 128;
-#ifndef KARMA_PART_SUB
-#define KARMA_PART_SUB 1  // counter copies of the narrow code partition (1, 2 or 4; see partition_kernel)
-#endif
 #ifndef KARMA_REC_NT
 #define KARMA_REC_NT 1  // classify's record loads non-temporal (plain loads: classify 0.53 -> 0.58 ms)
 #endif
@@ -651,8 +648,9 @@ struct CodeStreamT {
     static constexpr int kCap = 8192;   // codes per flush (32 KB of LDS)
     static constexpr int kPad = 8;      // 16 B of u16
     static constexpr int kMaxNb = NB;
-    static constexpr int kSub = NB <= 128 ? KARMA_PART_SUB : 1;  // partition counter copies (LDS)
     static constexpr D kPadV = 0xFFFF;  // codes are < 2^15
+    // 3 blocks of 8 waves per CU (<= 85 VGPRs) for the narrow variant
+    static constexpr int kMinWaves = NB <= 128 ? 6 : 1;
     __device__ static int nb(const Geo& g) { return g.Bc; }
     __device__ static uint32_t bucket(S s, const Geo& g) { return (s & 0xFFFFFFu) >> g.bwc; }
     __device__ static D value(S s, const Geo& g) {
@@ -668,8 +666,8 @@ struct PairStreamT {
     static constexpr int kCap = 4096;
     static constexpr int kPad = 4;
     static constexpr int kMaxNb = NB;
-    static constexpr int kSub = 1;
     static constexpr D kPadV = kEmpty;  // pair keys are < 2^31
+    static constexpr int kMinWaves = 1;
     __device__ static int nb(const Geo& g) { return g.B; }
     __device__ static uint32_t bucket(S s, const Geo& g) { return (uint32_t)(s >> 32) >> g.bw; }
     __device__ static D value(S s, const Geo& g) {
@@ -719,7 +717,8 @@ __device__ __forceinline__ void part_need(uint64_t items, int cap, int nb, int p
 }
 
 template <class T>
-__global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __restrict__ lists, int64_t list_cap,
+__global__ void __launch_bounds__(kPT) __attribute__((amdgpu_waves_per_eu(T::kMinWaves)))
+partition_kernel(const typename T::S* __restrict__ lists, int64_t list_cap,
                                                          const uint32_t* __restrict__ list_n, int64_t n_lists,
                                                          int per_block, Geo g, typename T::D* __restrict__ out,
                                                          RunDir dir) {
@@ -730,19 +729,14 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
     constexpr int kCopyIt = (kVMax + kPT - 1) / kPT;
     __shared__ S buf[T::kCap];
     __shared__ D sorted[T::kCap + T::kMaxNb * (T::kPad - 1)];
-    // Per-bucket counters, optionally in kSub copies (lane l using copy
-    // l % kSub, so lanes of one wave instruction that hit the same bucket hit
-    // kSub different words).  The flush's scan turns the counts into scatter
-    // cursors (cur), writes the runs' padding and clears the counts, so one
-    // set of each serves every fill (double-buffered counts, a separate base
-    // table and a pad pass took 0.176-0.184 ms; this layout 0.172-0.174).
-    // Copies cost LDS: 2 or 4 copies leave 2 blocks per CU instead of 3
-    // (0.204 and 0.173 ms), so one copy is the default.
-    constexpr int kSub = T::kSub;
-    constexpr int kHS = T::kMaxNb + (kSub > 1 ? 4 : 0);  // words per copy (LDS: 3 blocks per CU need <= 53 KB)
-    __shared__ uint32_t hist[kSub * kHS];
+    // Per-bucket counters.  Each item's add returns its rank among the fill's
+    // items of its bucket, kept in registers; the flush's scan turns the
+    // counts into run offsets (toff), writes the runs' padding and clears the
+    // counts, and the scatter is a plain LDS store at toff[b] + rank (round 3:
+    // one LDS atomic per item instead of two; the cursor adds had repeated
+    // the count adds' same-address conflicts).
+    __shared__ uint32_t hist[T::kMaxNb];
     __shared__ uint32_t toff[T::kMaxNb + 1];
-    __shared__ uint32_t cur[kSub * kHS];  // copy q of bucket b scatters to cur[q * kHS + b]++
     __shared__ uint32_t lpre[kMaxListsPerBlock + 1];
     __shared__ int64_t red_s[2][kPT / 64];
     const int nb = T::nb(g);
@@ -779,8 +773,7 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
         }
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int sub = (lane & (kSub - 1)) * kHS;  // this thread's copy
-    for (int b = threadIdx.x; b < kSub * kHS; b += kPT) hist[b] = 0;
+    for (int b = threadIdx.x; b < T::kMaxNb; b += kPT) hist[b] = 0;
 
     // the block's lists as one concatenated range: prefix of their lengths
     const int64_t l_lo = (int64_t)blockIdx.x * per_block;
@@ -832,12 +825,14 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
 #define PART_ITEM(k) buf[threadIdx.x + (k) * kPT]
     for (uint32_t base = 0; base < items; base += T::kCap) {
         const uint32_t n = min(items - base, (uint32_t)T::kCap);
-        uint32_t* const h = hist;
+        uint32_t rk[(kPer + 1) / 2];  // ranks within the bucket, two 16-bit ranks per register
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const uint32_t i = threadIdx.x + k * kPT;
             PART_ITEM(k) = v[k];
-            if (i < n) atomicAdd(&h[sub + T::bucket(v[k], g)], 1u);
+            const uint32_t r = i < n ? atomicAdd(&hist[T::bucket(v[k], g)], 1u) : 0u;
+            if (k & 1) rk[k >> 1] |= r << 16;
+            else rk[k >> 1] = r;
         }
         load(base + T::kCap);  // the next fill's loads overlap this flush
         // ---- flush: counting sort of buf by bucket into padded runs ----
@@ -846,24 +841,14 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
             uint32_t c2 = 0;
             for (int b0 = 0; b0 < nb; b0 += 64) {
                 const int bb = b0 + lane;
-                uint32_t cnt[kSub], tot = 0;
-#pragma unroll
-                for (int q = 0; q < kSub; ++q) {
-                    cnt[q] = bb < nb ? h[q * kHS + bb] : 0u;
-                    if (bb < nb) h[q * kHS + bb] = 0;  // counted: clear for the next fill
-                    tot += cnt[q];
-                }
-                const uint32_t val = (tot + (T::kPad - 1)) & ~(uint32_t)(T::kPad - 1);
+                const uint32_t cnt = bb < nb ? hist[bb] : 0u;
+                if (bb < nb) hist[bb] = 0;  // counted: clear for the next fill
+                const uint32_t val = (cnt + (T::kPad - 1)) & ~(uint32_t)(T::kPad - 1);
                 const uint32_t x = wave_scan_incl(val);
                 if (bb < nb) {
-                    uint32_t o = c2 + x - val;
+                    const uint32_t o = c2 + x - val;
                     toff[bb] = o;
-#pragma unroll
-                    for (int q = 0; q < kSub; ++q) {
-                        cur[q * kHS + bb] = o;
-                        o += cnt[q];
-                    }
-                    for (uint32_t i = o; i < c2 + x; ++i) sorted[i] = T::kPadV;  // the run's padding
+                    for (uint32_t i = o + cnt; i < c2 + x; ++i) sorted[i] = T::kPadV;  // the run's padding
                 }
                 c2 += lane63(x);
             }
@@ -882,8 +867,8 @@ __global__ void __launch_bounds__(kPT) partition_kernel(const typename T::S* __r
             for (int k = 0; k < kPer; ++k) {
                 if (threadIdx.x + k * kPT < n) {
                     const S it = PART_ITEM(k);
-                    const uint32_t b = T::bucket(it, g);
-                    sorted[atomicAdd(&cur[sub + b], 1u)] = T::value(it, g);
+                    const uint32_t r = (rk[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    sorted[toff[T::bucket(it, g)] + r] = T::value(it, g);
                 }
             }
 #undef PART_ITEM
