@@ -1015,11 +1015,14 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
     for (uint32_t base = 0; base < items; base += kCap, parity ^= 1) {
         const uint32_t n = min(items - base, (uint32_t)kCap);
         uint32_t* h = hist[parity];
+        uint32_t rk[(kPer + 1) / 2];  // ranks within the bucket (as in partition_kernel), two per register
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
             const uint32_t i = threadIdx.x + k * kPT;
             x[k] = v[k];
-            if (i < n) atomicAdd(&h[T::bucket(x[k], g)], 1u);
+            const uint32_t r = i < n ? atomicAdd(&h[T::bucket(x[k], g)], 1u) : 0u;
+            if (k & 1) rk[k >> 1] |= r << 16;
+            else rk[k >> 1] = r;
         }
         load(base + kCap);
         lds_barrier();
@@ -1060,7 +1063,7 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
         for (int k = 0; k < kPer; ++k) {
             if (threadIdx.x + k * kPT < n) {
                 const uint32_t b = T::bucket(x[k], g);
-                s16[atomicAdd(&cur[b], 1u)] = T::value(x[k], g);
+                s16[cur[b] + ((rk[k >> 1] >> (16 * (k & 1))) & 0xFFFFu)] = T::value(x[k], g);
             }
         }
         lds_barrier();
