@@ -83,24 +83,45 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
     return x;
 }
 
-// Bitonic sort of (key, val) pairs in LDS, n a power of two.
+// Bitonic sort of (key, val) pairs in LDS, n a power of two.  Thread t
+// compares elements i = 2t - (t mod stride) and i + stride, so for strides
+// <= 64 the lanes of one wave touch only their own 128 elements
+// ([2 * t0, 2 * t0 + 128) for the wave's first t0): those steps need the
+// wave's LDS ordering only, and block barriers are left to the strides >= 128
+// (a 1024-key sort: 6 block barriers instead of 55).
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ void lds_bitonic(uint32_t* keys, uint32_t* vals, int n) {
-    for (int size = 2; size <= n; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < n / 2; t += blockDim.x) {
-                const int i = 2 * t - (t & (stride - 1));
-                const int j = i + stride;
-                const bool up = (i & size) == 0;
-                const uint32_t ki = keys[i], kj = keys[j];
-                if ((ki > kj) == up) {
-                    keys[i] = kj;
-                    keys[j] = ki;
-                    const uint32_t v = vals[i];
-                    vals[i] = vals[j];
-                    vals[j] = v;
-                }
+    auto step = [&](int size, int stride) {
+        for (int t = threadIdx.x; t < n / 2; t += blockDim.x) {
+            const int i = 2 * t - (t & (stride - 1));
+            const int j = i + stride;
+            const bool up = (i & size) == 0;
+            const uint32_t ki = keys[i], kj = keys[j];
+            if ((ki > kj) == up) {
+                keys[i] = kj;
+                keys[j] = ki;
+                const uint32_t v = vals[i];
+                vals[i] = vals[j];
+                vals[j] = v;
             }
+        }
+    };
+    for (int size = 2; size <= n; size <<= 1) {
+        int stride = size >> 1;
+        for (; stride >= 128; stride >>= 1) {
+            step(size, stride);
             __syncthreads();
         }
+        for (; stride > 0; stride >>= 1) {
+            step(size, stride);
+            wave_lds_order();
+        }
+        if (size >= 128) __syncthreads();  // the next size starts with a cross-wave stride
     }
+    __syncthreads();
 }

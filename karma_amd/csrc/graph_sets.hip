@@ -1409,18 +1409,33 @@ __global__ void __launch_bounds__(kFT) final_kernel(
     // (m0 + i, m0 + j), i <= j, of its contigs; this bucket takes the pairs
     // with m0 + i inside it, from codes with m0 in [start - 3, end)
     if (n_cg > 0) {
-        const int first = bucket > 0 ? -24 : 0;  // 3 contigs x 8 codes before the bucket
-        for (int i = first + (int)threadIdx.x; i < (8 << bw); i += kFT) {
-            const uint32_t k = code_count(part_ch, n_cg, bwc, (bucket << (bw + 3)) + i);
-            if (!k) continue;
-            const int m0l = i >> 3;  // may be -3..-1
-            const uint32_t bits = 1u | ((uint32_t)i & 7u) << 1;
+        // a thread per first contig m0 (its 8 codes M = 0..7 as two 16-byte
+        // loads per group, every group's loads in flight together); the codes'
+        // pairs are summed in registers, then at most 10 LDS atomics per m0
+        // (code M: contigs m0 + i for the set bits i of 1 | M << 1)
+        const int hn = 8 << bwc;
+        for (int m0l = (bucket > 0 ? -3 : 0) + (int)threadIdx.x; m0l < (1 << bw); m0l += kFT) {
+            const int64_t gi = ((int64_t)bucket << (bw + 3)) + 8 * (int64_t)m0l;  // code (m0, 0)
+            const uint4* src = reinterpret_cast<const uint4*>(part_ch + (gi >> (bwc + 3)) * n_cg * hn + (gi & (hn - 1)));
+            uint32_t k[8] = {};
+            for (int g = 0; g < n_cg; ++g) {
+                const uint4 a = src[(int64_t)g * (hn >> 2)], b = src[(int64_t)g * (hn >> 2) + 1];
+                k[0] += a.x, k[1] += a.y, k[2] += a.z, k[3] += a.w;
+                k[4] += b.x, k[5] += b.y, k[6] += b.z, k[7] += b.w;
+            }
 #pragma unroll
             for (int i1 = 0; i1 < 4; ++i1) {
-                if (!(bits >> i1 & 1u) || m0l + i1 < 0 || m0l + i1 >= (1 << bw)) continue;
+                if (m0l + i1 < 0 || m0l + i1 >= (1 << bw)) continue;
 #pragma unroll
-                for (int j1 = i1; j1 < 4; ++j1)
-                    if (bits >> j1 & 1u) atomicAdd(&bsum[(m0l + i1) << dbits | (j1 - i1)], k);
+                for (int j1 = i1; j1 < 4; ++j1) {
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int M = 0; M < 8; ++M) {
+                        const uint32_t bits = 1u | (uint32_t)M << 1;
+                        if ((bits >> i1 & 1u) && (bits >> j1 & 1u)) acc += k[M];
+                    }
+                    if (acc) atomicAdd(&bsum[(m0l + i1) << dbits | (j1 - i1)], acc);
+                }
             }
         }
         __syncthreads();
