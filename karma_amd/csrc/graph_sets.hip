@@ -1377,20 +1377,76 @@ struct SplitArgs {
     int64_t* out;  // per bound: keys of its bucket below it
 };
 
+// The buckets' lists back to back in one array: block b's offset is the sum
+// of the lists of blocks < b, found by a decoupled look-back (one wave): the
+// block publishes its own size at once (kLbAgg), reads its predecessors' words
+// 64 at a time from the nearest down, and stops at the first that carries an
+// inclusive prefix (kLbPre); block 0 (and the virtual block -1) carry one.
+// Predecessors were dispatched first and publish before they wait, so every
+// wave's spin ends.
+constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 2ull << 62, kLbVal = kLbAgg - 1;
+
+__device__ int64_t lookback_offset(uint64_t* lb, int b, int64_t total, int lane) {
+    if (b == 0) {
+        if (lane == 0) __hip_atomic_store(&lb[0], kLbPre | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(&lb[b], kLbAgg | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t excl = 0;
+    for (int top = b - 1;; top -= 64) {
+        const int idx = top - lane;  // lane 0: the nearest predecessor
+        uint64_t v;
+        unsigned long long pre, none;
+        for (;;) {
+            v = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
+            pre = __ballot((v & ~kLbVal) == kLbPre);
+            none = __ballot((v & ~kLbVal) == 0);
+            const unsigned long long need = pre ? (pre & (~pre + 1)) * 2 - 1 : ~0ull;  // lanes up to the first prefix
+            if (!(none & need)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const int first = pre ? __ffsll((long long)pre) - 1 : 64;
+        int64_t x = lane <= first ? (int64_t)(v & kLbVal) : 0;
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        excl += x;
+        if (pre) break;
+    }
+    if (lane == 0)
+        __hip_atomic_store(&lb[b], kLbPre | (uint64_t)(excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 template <int HF>
 __global__ void __launch_bounds__(kFT) final_kernel(
     int n_pg, int n_cg, int bw, int bbits, int dbits, int bwc, const uint32_t* __restrict__ part_band,
     const uint32_t* __restrict__ part_ch, const uint32_t* __restrict__ part_keys,
     const uint32_t* __restrict__ part_cnt, const int* __restrict__ part_n, uint64_t* __restrict__ out_keys,
-    int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n, uint8_t* __restrict__ overflow, SplitArgs split) {
+    int64_t* __restrict__ out_counts, int64_t* __restrict__ out_n, uint8_t* __restrict__ overflow, SplitArgs split,
+    uint64_t* __restrict__ lb, int64_t* __restrict__ out_off) {
     __shared__ uint32_t bsum[kBand];
     __shared__ uint32_t rowpos[(kBand >> 3) + 1];  // nonzero band slots before row a_local (D = 8 on this path)
     __shared__ uint32_t hkeys[HF];
     __shared__ uint32_t hvals[HF];
     __shared__ uint32_t wsum[kFT / 64];
     __shared__ int nuniq, cnt;
+    __shared__ int64_t base;
     const int bucket = blockIdx.x;
-    if (overflow[bucket]) return;  // generic path
+    // a bucket on the generic path (overflow) takes no room in the array: the
+    // host rebuilds the list from the per-bucket sources (SetsJob::finish)
+    auto skip = [&]() {
+        if (threadIdx.x < 64) {
+            const int64_t o = lookback_offset(lb, bucket, 0, (int)threadIdx.x);
+            if (threadIdx.x == 0) {
+                out_off[bucket] = o;
+                out_n[bucket] = 0;
+                if (bucket == (int)gridDim.x - 1) out_off[bucket + 1] = o;
+            }
+        }
+    };
+    if (overflow[bucket]) {  // generic path
+        skip();
+        return;
+    }
     HTab<HF, kFT> t{hkeys, hvals, &nuniq};
     const int band_n = dbits >= 0 ? (1 << (bw + dbits)) : 0;
     // one group (HF == kHashR): its list is already unique, copied as is
@@ -1457,6 +1513,7 @@ __global__ void __launch_bounds__(kFT) final_kernel(
                 full |= !t.insert(part_keys[sl * kHashR + i], part_cnt[sl * kHashR + i]);
             if (__syncthreads_or(full)) {
                 if (threadIdx.x == 0) overflow[bucket] = 1;
+                skip();
                 return;
             }
         }
@@ -1489,10 +1546,19 @@ __global__ void __launch_bounds__(kFT) final_kernel(
         run += w < wave ? c : 0u;
         nb += c;
     }
+    if (wave == 0) {
+        const int64_t o = lookback_offset(lb, bucket, (int64_t)nb + nh, lane);
+        if (lane == 0) {
+            base = o;
+            out_off[bucket] = o;
+            if (bucket == (int)gridDim.x - 1) out_off[bucket + 1] = o + nb + nh;  // the list's length
+        }
+    }
+    __syncthreads();
     const uint32_t bmask = (1u << bbits) - 1u;
     const uint64_t abase = (uint64_t)bucket << bw;
-    uint64_t* ok = out_keys + (int64_t)bucket * kSlotCap;
-    int64_t* oc = out_counts + (int64_t)bucket * kSlotCap;
+    uint64_t* ok = out_keys + base;
+    int64_t* oc = out_counts + base;
     for (int e0 = seg0; e0 < seg1; e0 += 64) {
         const int i = e0 + lane;
         const uint32_t c = bsum[i];
@@ -1614,18 +1680,19 @@ __global__ void fill_ones_i64_kernel(int64_t* __restrict__ v, int64_t n) {
     if (i < n) v[i] = 1;
 }
 
-// Bucket b's sorted list lies at base + b * stride (final_kernel's slots), or,
+// Bucket b's sorted list lies at base + src_off[b] (final_kernel's array), or,
 // for a bucket that overflowed the LDS tables, at the generic path's arrays
-// (src_k[b] / src_c[b] non-null: the overflow path only)
+// (src_k[b] / src_c[b] non-null).  Only after an overflow: otherwise the final
+// kernel's array is the list.
 __global__ void assemble2_kernel(const uint64_t* __restrict__ base_k, const int64_t* __restrict__ base_c,
-                                 int64_t stride, const uint64_t* const* __restrict__ src_k,
+                                 const int64_t* __restrict__ src_off, const uint64_t* const* __restrict__ src_k,
                                  const int64_t* const* __restrict__ src_c, const int64_t* __restrict__ n_per,
                                  const int64_t* __restrict__ dst_off, uint64_t* __restrict__ keys,
                                  int64_t* __restrict__ counts) {
     const int64_t b = blockIdx.x;
     const int64_t n = n_per[b], d = dst_off[b];
-    const uint64_t* sk = src_k && src_k[b] ? src_k[b] : base_k + b * stride;
-    const int64_t* sc = src_c && src_c[b] ? src_c[b] : base_c + b * stride;
+    const uint64_t* sk = src_k && src_k[b] ? src_k[b] : base_k + src_off[b];
+    const int64_t* sc = src_c && src_c[b] ? src_c[b] : base_c + src_off[b];
     for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
         keys[d + t] = sk[t];
         counts[d + t] = sc[t];
@@ -1932,6 +1999,7 @@ struct SetsJob {
     int* flags = nullptr;
     unsigned* counters = nullptr;
     int64_t* n_per = nullptr;
+    uint64_t* lb = nullptr;  // the final kernel's look-back words (zeroed with the control block)
     int64_t* dst = nullptr;
     uint8_t* ovf = nullptr;
     const int64_t* hctrl = nullptr;  // pinned copy of the control block
@@ -1987,8 +2055,9 @@ int SetsJob::setup() {
     ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8) + (int64_t)split_b.size();
     // one allocation (and one memset per attempt) for the control block and
     // the per-partition-block item counts behind it
-    KARMA_TRY(ctrl.alloc(ctx, ctrl_words + 2 * n_pblk));
+    KARMA_TRY(ctrl.alloc(ctx, ctrl_words + 2 * n_pblk + B));
     blk_items = reinterpret_cast<unsigned long long*>(ctrl.ptr + ctrl_words);
+    lb = reinterpret_cast<uint64_t*>(ctrl.ptr + ctrl_words + 2 * n_pblk);
     flags = reinterpret_cast<int*>(ctrl.ptr);
     counters = reinterpret_cast<unsigned*>(ctrl.ptr + 2);
     n_per = ctrl.ptr + 6;
@@ -2043,7 +2112,7 @@ int SetsJob::launch() {
     KARMA_TRY(pf_base.alloc(ctx, max_pflush));
     KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
     const bool probe = A > 0 && !relabeled;  // the probe kernel clears the control block
-    if (!probe) KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk) * 8, ctx->stream));
+    if (!probe) KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk + B) * 8, ctx->stream));
     if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
     if (mark_at() == 3 && attempt == 0 && !relabeled) {  // side-stream work may start beside classify
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
@@ -2072,7 +2141,7 @@ int SetsJob::launch() {
             // a probe of the reads decides: when many span more than 4 contig
             // ids, this pass is skipped and a relabelled rerun follows
             KARMA_LAUNCH(ctx, "relabel_probe", relabel_probe_kernel, 1, kRelabelProbes, 0, rec, A, (uint32_t)N,
-                         counters + 3, reinterpret_cast<uint64_t*>(ctrl.ptr), (int64_t)(ctrl_words + 2 * n_pblk));
+                         counters + 3, reinterpret_cast<uint64_t*>(ctrl.ptr), (int64_t)(ctrl_words + 2 * n_pblk + B));
             C.skip = counters + 3;
         }
         KARMA_TRY(classify(0, n_chunks));
@@ -2134,12 +2203,11 @@ int SetsJob::launch() {
     if (n_pg == 1)
         KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashR>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits,
                      g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
-                     ovf, sa);
+                     ovf, sa, lb, dst);
     else
         KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashF>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits,
                      g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
-                     ovf, sa);
-    KARMA_TRY(scan_excl_i64(ctx, n_per, dst, B + 1));
+                     ovf, sa, lb, dst);
     KARMA_HIP(hipMemcpyAsync(const_cast<int64_t*>(hctrl), ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost,
                              ctx->stream));
     return KARMA_OK;
@@ -2209,6 +2277,7 @@ int SetsJob::finish(karma_pairs* out) {
     }
     DevArray<const uint64_t*> pk;  // per-bucket list overrides (overflowed buckets only)
     DevArray<const int64_t*> pc;
+    DevArray<int64_t> src_off;     // where the final kernel put each other bucket's list
     std::vector<std::unique_ptr<DevArray<uint64_t>>> keep_k;
     std::vector<std::unique_ptr<DevArray<int64_t>>> keep_c;
     const int64_t widen_threads = std::max<int64_t>(hc[2], (int64_t(8) << g.bw) + 24);
@@ -2218,6 +2287,8 @@ int SetsJob::finish(karma_pairs* out) {
         if (!any_ovf) {
             KARMA_TRY(pk.alloc(ctx, B));
             KARMA_TRY(pc.alloc(ctx, B));
+            KARMA_TRY(src_off.alloc(ctx, B));
+            KARMA_HIP(hipMemcpyAsync(src_off.ptr, dst, B * 8, hipMemcpyDeviceToDevice, ctx->stream));
             KARMA_HIP(hipMemsetAsync(pk.ptr, 0, B * sizeof(void*), ctx->stream));
             KARMA_HIP(hipMemsetAsync(pc.ptr, 0, B * sizeof(void*), ctx->stream));
         }
@@ -2257,10 +2328,17 @@ int SetsJob::finish(karma_pairs* out) {
     }
     DevArray<uint64_t> mk;
     DevArray<int64_t> mc;
-    KARMA_TRY(mk.alloc(ctx, U));
-    KARMA_TRY(mc.alloc(ctx, U));
-    KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, slot_k.ptr, slot_c.ptr, (int64_t)kSlotCap,
-                 pk.ptr, pc.ptr, n_per, dst, mk.ptr, mc.ptr);
+    if (any_ovf) {
+        KARMA_TRY(mk.alloc(ctx, U));
+        KARMA_TRY(mc.alloc(ctx, U));
+        KARMA_LAUNCH(ctx, "bucket_assemble", assemble2_kernel, B, 256, 0, slot_k.ptr, slot_c.ptr, src_off.ptr,
+                     pk.ptr, pc.ptr, n_per, dst, mk.ptr, mc.ptr);
+    } else {
+        // the final kernel wrote the buckets' lists back to back: the list as is
+        // (its arrays hold B x kSlotCap entries, the first U of them used)
+        mk.swap(slot_k);
+        mc.swap(slot_c);
+    }
     if (!relabeled) {
         KARMA_TRY(finish_pairs(ctx, rec, A, N, big_list.ptr, n_big, mk, mc, U, out));
         if (!split_b.empty() && !any_ovf && n_big == 0) {
