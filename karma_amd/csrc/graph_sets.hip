@@ -146,13 +146,18 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
     return x;
 }
+// inclusive max over lanes 0..l (values >= -1)
+__device__ __forceinline__ int wave_max_incl(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xF, 0xF, false));  // row_shr:1
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xF, 0xF, false));  // row_shr:2
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xF, 0xF, false));  // row_shr:4
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xF, 0xF, false));  // row_shr:8
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return x;
+}
 __device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
 
-__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 
 // ---- classify -------------------------------------------------------------------
 constexpr int kCW = 256;                // classify threads per block (4 independent waves)
@@ -1105,10 +1110,12 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
 // lanes' run table, and kWin windows are in flight before they are counted.
 constexpr int kWin = 16;
 
+// slots: 64 ints of LDS per wave of the block.
 template <typename Bounds, typename Count>
 __device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int64_t r_lo, int64_t r_hi, int threads,
-                                            Bounds bounds, Count count, bool* stop) {
+                                            Bounds bounds, Count count, bool* stop, int* slots) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int* const wslot = slots + wave * 64;
     // stop == nullptr: nothing stops the block early, so the waves run without
     // a barrier per batch, and the next batch's run bounds are loaded before
     // the current batch is streamed (their latency hides under its windows)
@@ -1131,21 +1138,25 @@ __device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int6
         const uint32_t excl = incl - len;
         const int64_t roff = beg - (int64_t)excl;  // vector j of run r: data[roff + j]
         const uint32_t Tn = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        int rlo = 0;
+        // the run (lane) holding vector j of a window: each run starting inside
+        // the window writes its lane to the window slot of its first vector,
+        // then a max-scan over the slots (seeded with the run that covers the
+        // previous window's last vector) gives every lane its run
+        int carry = -1;
         for (uint32_t j0 = 0; j0 < Tn; j0 += 64u * kWin) {
             u32x4 e[kWin];
 #pragma unroll
             for (int u = 0; u < kWin; ++u) {
                 const uint32_t w0 = j0 + 64u * u, j = w0 + lane;
                 if (w0 >= Tn) continue;  // uniform
-                while (rlo < 63 && (uint32_t)__builtin_amdgcn_readlane((int)incl, rlo) <= w0) ++rlo;
-                int64_t off = 0;
-                for (int rr = rlo; rr < 64; ++rr) {
-                    const uint32_t ex = (uint32_t)__builtin_amdgcn_readlane((int)excl, rr);
-                    if (ex >= w0 + 64u) break;
-                    const int64_t o = readlane64(roff, rr);
-                    if (j >= ex) off = o;
-                }
+                wslot[lane] = -1;
+                wave_lds_order();
+                if (len && excl >= w0 && excl < w0 + 64u) wslot[excl - w0] = lane;
+                wave_lds_order();
+                const int rr = wave_max_incl(max(wslot[lane], carry));
+                carry = __builtin_amdgcn_readlane(rr, 63);
+                const int64_t off = (int64_t)(((uint64_t)(uint32_t)__shfl((int)((uint64_t)roff >> 32), rr) << 32) |
+                                              (uint32_t)__shfl((int)(uint32_t)roff, rr));
                 if (j < Tn) e[u] = KARMA_RED_LOAD_NT ? __builtin_nontemporal_load(&data[off + j]) : data[off + j];
             }
 #pragma unroll
@@ -1177,6 +1188,7 @@ constexpr int kHistMax = 1 << (kMaxBwCompact + 2 + 3);  // 32768 counters (128 K
 __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __restrict__ cent, RunDir dir, int Bc,
                                                            int bwc, int n_cg, uint32_t* __restrict__ part_ch) {
     __shared__ uint32_t h[kHistMax];
+    __shared__ int slots[kCRT];
     const int bucket = blockIdx.x / n_cg, grp = blockIdx.x % n_cg;
     const int hn = 1 << (bwc + 3);
     for (int i = threadIdx.x; i < hn; i += kCRT) h[i] = 0;
@@ -1210,7 +1222,7 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
             add(v.x & 0xFFFFu), add(v.x >> 16), add(v.y & 0xFFFFu), add(v.y >> 16);
             add(v.z & 0xFFFFu), add(v.z >> 16), add(v.w & 0xFFFFu), add(v.w >> 16);
         },
-        nullptr);
+        nullptr, slots);
     __syncthreads();
     uint32_t* out = part_ch + (int64_t)blockIdx.x * hn;
     for (int i = threadIdx.x; i < hn; i += kCRT) out[i] = h[slot(i)];
@@ -1296,6 +1308,7 @@ __global__ void __launch_bounds__(kRT) pair_reduce_kernel(const uint32_t* __rest
     __shared__ uint32_t hkeys[kHashR];
     __shared__ uint32_t hvals[kHashR];
     __shared__ int nuniq, cnt, ovf;
+    __shared__ int slots[kRT];
     HTab<kHashR, kRT> t{hkeys, hvals, &nuniq};
     const int bucket = blockIdx.x / n_pg, grp = blockIdx.x % n_pg;
     const int band_n = dbits >= 0 ? (1 << (bw + dbits)) : 0;
@@ -1332,7 +1345,7 @@ __global__ void __launch_bounds__(kRT) pair_reduce_kernel(const uint32_t* __rest
             add(v.x), add(v.y), add(v.z), add(v.w);
             if (nuniq > kHashR - kHashR / 8) full = true;  // early out: the bucket goes generic
         },
-        &full);
+        &full, slots);
     if (full) ovf = 1;
     __syncthreads();
     if (ovf) {
