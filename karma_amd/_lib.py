@@ -213,8 +213,11 @@ def check(rc):
     return rc
 
 
-# diagnostic: per-entry-point host time (KARMA_CALL_TIMES=1; tools/host_profile.py)
-CALL_TIMES = {} if os.environ.get("KARMA_CALL_TIMES") == "1" else None
+# diagnostic: per-entry-point host time (KARMA_CALL_TIMES=1; tools/host_profile.py),
+# and with KARMA_CALL_TIMES=seq every call's (name, start, end) in CALL_SEQ
+# (tools/host_timeline.py)
+CALL_TIMES = {} if os.environ.get("KARMA_CALL_TIMES") in ("1", "seq") else None
+CALL_SEQ = [] if os.environ.get("KARMA_CALL_TIMES") == "seq" else None
 
 
 def call(name, *args):
@@ -226,9 +229,11 @@ def call(name, *args):
     try:
         return check(getattr(load(), name)(*args))
     finally:
-        dt = time.perf_counter() - t0
+        t1 = time.perf_counter()
         n, tot = CALL_TIMES.get(name, (0, 0.0))
-        CALL_TIMES[name] = (n + 1, tot + dt)
+        CALL_TIMES[name] = (n + 1, tot + t1 - t0)
+        if CALL_SEQ is not None:
+            CALL_SEQ.append((name, t0, t1))
 
 
 def ptr(a):
@@ -327,10 +332,15 @@ class DevBuf:
 
     def __init__(self, ctx, shape, dtype, _ptr=None, _owner=None):
         self.ctx = ctx
-        self.shape = (int(shape),) if np.isscalar(shape) else tuple(int(x) for x in shape)
+        # plain Python arithmetic: a buffer is made per exchange step, where
+        # numpy's scalar helpers cost microseconds each
+        self.shape = tuple(int(x) for x in shape) if isinstance(shape, (tuple, list)) else (int(shape),)
         self.dtype = np.dtype(dtype)
-        self.size = int(np.prod(self.shape)) if self.shape else 1
-        self.nbytes = self.size * self.dtype.itemsize
+        size = 1
+        for x in self.shape:
+            size *= x
+        self.size = size
+        self.nbytes = size * self.dtype.itemsize
         self._owner = _owner
         if _ptr is not None:
             self.ptr = _ptr

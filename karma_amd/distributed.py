@@ -358,7 +358,8 @@ class ShardedBuild:
                     rk, rc, recv = comm.alltoallv_kv(keys, counts, np.diff(starts))
                     merged = ops.merge_kv(rk, rc, recv)
                 else:  # emulation: this rank's own W slices stand in for the W received ones
-                    merged = ops.merge_kv(keys, counts, np.diff(starts).tolist())
+                    st = starts.tolist()
+                    merged = ops.merge_kv(keys, counts, [b - a for a, b in zip(st, st[1:])])
             elif comm.world > 1:
                 # one all-to-all-v of interleaved (key, count) int64 pairs; the
                 # owner receives one sorted slice per sender and merges them

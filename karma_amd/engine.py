@@ -8,6 +8,7 @@ read_graph.py, contig.py) call these functions.
 from __future__ import annotations
 
 import ctypes
+import itertools
 from dataclasses import dataclass
 
 import numpy as np
@@ -395,17 +396,19 @@ class Pairs:
         merge tree instead of a full sort."""
         h = ctypes.c_void_p()
         if runs is not None:
+            if device:
+                # the run offsets as a ctypes array (no numpy on this per-step path)
+                off = (ctypes.c_int64 * (len(runs) + 1))(0, *itertools.accumulate(int(r) for r in runs))
+                assert n is None or n == off[len(runs)], "run lengths do not add up to n"
+                call("karma_pairs_merge_runs", ctx.h, ctypes.c_void_p(keys) if keys else None,
+                     ctypes.c_void_p(counts) if counts else None, off, len(runs), 1, ctypes.byref(h))
+                return cls(ctx, h)
             off = np.zeros(len(runs) + 1, np.int64)
             np.cumsum(np.asarray(runs, np.int64), out=off[1:])
-            if device:
-                assert n is None or n == off[-1], "run lengths do not add up to n"
-                call("karma_pairs_merge_runs", ctx.h, ctypes.c_void_p(keys) if keys else None,
-                     ctypes.c_void_p(counts) if counts else None, ptr(off), len(runs), 1, ctypes.byref(h))
-            else:
-                keys = np.ascontiguousarray(keys, np.uint64)
-                counts = np.ascontiguousarray(counts, np.int64)
-                call("karma_pairs_merge_runs", ctx.h, ptr(keys) if len(keys) else None,
-                     ptr(counts) if len(counts) else None, ptr(off), len(runs), 0, ctypes.byref(h))
+            keys = np.ascontiguousarray(keys, np.uint64)
+            counts = np.ascontiguousarray(counts, np.int64)
+            call("karma_pairs_merge_runs", ctx.h, ptr(keys) if len(keys) else None,
+                 ptr(counts) if len(counts) else None, ptr(off), len(runs), 0, ctypes.byref(h))
             return cls(ctx, h)
         if device:
             call("karma_pairs_merge", ctx.h, ctypes.c_void_p(keys) if keys else None,
