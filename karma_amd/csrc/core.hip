@@ -101,9 +101,16 @@ int ctx_job_pinned(karma_ctx* ctx, size_t bytes, void** out) {
 }
 
 int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int64_t work) {
+    const auto key = std::make_pair(kernel, std::make_pair(block, lds));
+    auto it = ctx->occupancy.find(key);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
-        per_cu = 1;
+    if (it != ctx->occupancy.end()) {
+        per_cu = it->second;
+    } else {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        ctx->occupancy.emplace(key, per_cu);
+    }
     per_cu = std::max(1, per_cu - ctx->grid_headroom);
     return (int)std::max<int64_t>(1, std::min<int64_t>(work, (int64_t)per_cu * ctx->cu_count));
 }

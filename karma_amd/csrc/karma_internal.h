@@ -88,6 +88,9 @@ struct karma_ctx {
     // owner bounds for the next records graph job (karma_graph_split_hint): its
     // final kernel also finds where each owner's slice starts (no split launch)
     std::vector<int64_t> split_bounds;
+    // resident blocks per CU by (kernel, block size, dynamic LDS): the occupancy
+    // query costs host microseconds and is asked on every call of a step
+    std::map<std::pair<const void*, std::pair<int, size_t>>, int> occupancy;
 };
 
 namespace karma {
