@@ -1603,19 +1603,22 @@ __global__ void __launch_bounds__(kFT) final_kernel(
     }
     if (threadIdx.x == 0) out_n[bucket] = nb + nh;
     if (split.n) {
-        __syncthreads();  // the bucket's list, written above by this block
-        const int64_t total = nb + nh, c_lo = (int64_t)bucket << bw, c_hi = c_lo + (int64_t(1) << bw);
+        // keys of this bucket with a below the bound: the band's nonzero slots
+        // in the rows before it (rowpos) plus the hash keys before its row
+        // (sorted in LDS), no search over the list just written
+        const int64_t c_lo = (int64_t)bucket << bw, c_hi = c_lo + (int64_t(1) << bw);
         for (int r = threadIdx.x; r < split.n; r += kFT) {
             const int64_t bd = split.b[r];
             if (bd < c_lo || bd >= c_hi) continue;
-            const uint64_t lim = (uint64_t)bd << 32;
-            int64_t lo = 0, hi = total;
+            const uint32_t al = (uint32_t)(bd - c_lo);
+            const uint32_t lim = al << bbits;
+            int lo = 0, hi = nh;
             while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (ok[mid] < lim) lo = mid + 1;
+                const int mid = (lo + hi) >> 1;
+                if (hkeys[mid] < lim) lo = mid + 1;
                 else hi = mid;
             }
-            split.out[r] = lo;
+            split.out[r] = (int64_t)(band_n ? rowpos[al] : 0u) + lo;
         }
     }
 }
