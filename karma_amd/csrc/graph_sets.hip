@@ -1981,7 +1981,7 @@ __global__ void relabel_back_kernel(uint64_t* __restrict__ keys, int64_t n, cons
 // assembles.  Between the two the host may enqueue unrelated work (the k-mer
 // profile on a side stream).
 #ifndef KARMA_MARK_AT
-#define KARMA_MARK_AT 0
+#define KARMA_MARK_AT 5
 #endif
 // where side-stream work (the k-mer profile) may start, see SetsJob::launch;
 // KARMA_MARK_AT in the environment overrides the default (scheduling only:
@@ -2162,9 +2162,11 @@ int SetsJob::launch() {
         }
         KARMA_TRY(classify(0, n_chunks));
     }
-    // where side-stream work (the k-mer profile) may start: 0 = after the whole
-    // pipeline (default), 1 = after classify, 2 = after the code partition,
-    // 3 = at once (beside classify).
+    // where side-stream work (the k-mer profile) may start: 5 = after the final
+    // kernel, beside the control-block readback (default; 0.283 against 0.291
+    // ms for the 8-rank strong preview, equal on one GPU, profiles/r03/ab_mark5/),
+    // 0 = after the whole pipeline, 1 = after classify, 2 = after the code
+    // partition, 3 = at once (beside classify), 4 = after the code reduce.
     // Measured: 1 slows the code partition 0.19 -> 0.5 ms (1.46 vs 1.37 ms/step);
     // 2 stretches the profile to 0.60 ms beside the reduce (1.43 vs 1.35);
     // 3 stretches classify 0.54 -> 0.74 ms (1.35 vs 1.25): HBM is already full
@@ -2224,6 +2226,7 @@ int SetsJob::launch() {
         KARMA_LAUNCH(ctx, "graph_bucket_final", final_kernel<kHashF>, B, kFT, 0, n_pg, n_cg, g.bw, g.bbits, g.dbits,
                      g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
                      ovf, sa, lb, dst);
+    KARMA_TRY(mark(5));  // after the final kernel, before the control-block readback
     KARMA_HIP(hipMemcpyAsync(const_cast<int64_t*>(hctrl), ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost,
                              ctx->stream));
     return KARMA_OK;
