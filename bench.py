@@ -140,8 +140,8 @@ class Leg:
         self.packed_bytes = int(np.sum((np.diff(inp["offs"]) + 3) // 4))  # sum ceil(L/4)
         self.ctxs = self.build.contexts()  # main context (+ the concurrent graph build's)
 
-    def step(self, keep=False, sequential=False):
-        return self.build.run(self.store, self.rec_dev.ptr, self.A, keep=keep, sequential=sequential)
+    def step(self, keep=False, sequential=False, count=True):
+        return self.build.run(self.store, self.rec_dev.ptr, self.A, keep=keep, sequential=sequential, count=count)
 
     def sync_all(self):
         for c in self.ctxs:
@@ -181,8 +181,12 @@ class Leg:
         comm.barrier()
         self.sync_all()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            res = self.step()
+        # with an exchange, the owner's edge count of a step is read back only
+        # in the last step (ShardedBuild.run count=False): the other steps end
+        # without waiting for their last kernels, as in a stream of batches;
+        # every kernel still runs, and the device sync below waits for all
+        for i in range(steps):
+            res = self.step(count=i == steps - 1)
         self.sync_all()
         comm.barrier()
         t1 = time.perf_counter()

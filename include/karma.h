@@ -287,6 +287,10 @@ int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64
 int karma_edges_begin(karma_ctx* ctx, karma_pairs* p, int mode, int64_t n_contigs, karma_edges** out,
                       int64_t** totals_dev);
 int karma_edges_end(karma_edges* e, int64_t* n_edges);
+/* n_edges = NULL: _end launches the weights and returns at once; the edge
+ * count, and the zero-total and merge-order errors, come with the first
+ * karma_edges_count / _get / _totals (one synchronisation there). */
+int karma_edges_count(karma_edges* e, int64_t* n_edges);
 int karma_edges_destroy(karma_edges* e);
 /* Any output pointer may be NULL. first is only meaningful in EQ mode. */
 int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* shared, double* weight, uint64_t* first,

@@ -117,6 +117,7 @@ _SIGS = {
     "karma_edges_from_pairs": [_c_p, _c_p, _i32, _c_p, _i64, _PP, _I64P],
     "karma_edges_begin": [_c_p, _c_p, _i32, _i64, _PP, _PP],
     "karma_edges_end": [_c_p, _I64P],
+    "karma_edges_count": [_c_p, _I64P],
     "karma_pairs_split_kc": [_c_p, _c_p, _i32, _c_p, _c_p],
     "karma_edges_destroy": [_c_p],
     "karma_edges_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _i32],

@@ -38,6 +38,11 @@ struct karma_edges {
     DevArray<int64_t> blk;
     int mode = 0;
     bool open = false;
+    // karma_edges_end without a count: the write kernel's status words
+    // (zero-total flag, edge count, merge order flag) wait in blk past the
+    // per-block counts until the first read of the edges
+    bool pending = false;
+    int64_t n_blk = 0;
 };
 
 namespace {
@@ -144,8 +149,10 @@ __device__ __forceinline__ bool edge_flag(uint64_t k, int64_t c, int mode) {
 
 __global__ void __launch_bounds__(kET) edges_count_kernel(const uint64_t* __restrict__ keys,
                                                           const int64_t* __restrict__ counts, int64_t n, int mode,
-                                                          int64_t* __restrict__ totals, int64_t* __restrict__ blk_cnt) {
+                                                          int64_t* __restrict__ totals, int64_t* __restrict__ blk_cnt,
+                                                          int64_t* __restrict__ st) {
     const int64_t i = (int64_t)blockIdx.x * kET + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 3) st[threadIdx.x] = 0;  // the write kernel's status words
     bool f = false;
     if (i < n) {
         const uint64_t k = keys[i];
@@ -1042,22 +1049,62 @@ static int edges_begin_impl(karma_ctx* ctx, karma_pairs* p, int mode, const int6
         KARMA_HIP(hipMemcpyAsync(e->totals.ptr, totals_dev, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
     }
     const int64_t n = p->n;
-    KARMA_TRY(e->blk.alloc(ctx, std::max<int64_t>(1, ceil_div(n, kET))));
+    e->n_blk = std::max<int64_t>(1, ceil_div(n, kET));
+    KARMA_TRY(e->blk.alloc(ctx, e->n_blk + 3));
     if (n)
         KARMA_LAUNCH(ctx, "edge_count", edges_count_kernel, ceil_div(n, kET), kET, 0, p->keys.ptr, p->counts.ptr, n,
-                     mode, diag_here ? e->totals.ptr : (int64_t*)nullptr, e->blk.ptr);
+                     mode, diag_here ? e->totals.ptr : (int64_t*)nullptr, e->blk.ptr, e->blk.ptr + e->n_blk);
+    else
+        KARMA_HIP(hipMemsetAsync(e->blk.ptr + e->n_blk, 0, 3 * 8, ctx->stream));
     e->open = true;
     *out = guard.release();
     return KARMA_OK;
 }
 
+// The deferred half of karma_edges_end (n_edges = NULL): the status words
+// from device memory, one synchronisation, the same checks.
+static int edges_resolve(karma_edges* e) {
+    if (!e->pending) return KARMA_OK;
+    karma_ctx* ctx = e->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    void* hpin = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, 24, &hpin));
+    KARMA_HIP(hipMemcpyAsync(hpin, e->blk.ptr + e->n_blk, 24, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    e->pending = false;
+    e->blk.release();
+    const int64_t* hs = static_cast<const int64_t*>(hpin);
+    KARMA_CHECK(!hs[2], KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
+    KARMA_CHECK(!(int)hs[0], KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
+    e->E = hs[1];
+    return KARMA_OK;
+}
+
 static int edges_end_impl(karma_edges* e, int64_t* n_edges) {
-    KARMA_CHECK(e && e->open && n_edges, KARMA_ERR_STATE, "karma_edges_end: no open edge stage");
+    KARMA_CHECK(e && e->open, KARMA_ERR_STATE, "karma_edges_end: no open edge stage");
     karma_ctx* ctx = e->ctx;
     KARMA_TRY(ctx_begin(ctx));
     const karma_pairs* p = e->src;
     e->open = false;
     const int64_t n = p->n;
+    if (!n_edges) {  // deferred: the write kernel's status words stay on the device
+        KARMA_TRY(e->a.alloc(ctx, n));
+        KARMA_TRY(e->b.alloc(ctx, n));
+        KARMA_TRY(e->s.alloc(ctx, n));
+        KARMA_TRY(e->w.alloc(ctx, n));
+        e->has_first = p->has_first;
+        if (e->has_first) KARMA_TRY(e->first.alloc(ctx, n));
+        if (n)
+            KARMA_LAUNCH(ctx, "edge_weights", edges_write_kernel, ceil_div(n, kET), kET, 0, p->keys.ptr, p->counts.ptr,
+                         p->has_first ? p->first.ptr : (const uint64_t*)nullptr, n, e->mode, e->totals.ptr,
+                         e->blk.ptr, e->a.ptr, e->b.ptr, e->s.ptr, e->w.ptr,
+                         e->has_first ? e->first.ptr : (uint64_t*)nullptr, e->blk.ptr + e->n_blk,
+                         p->dups ? (const int64_t*)p->bad.ptr : (const int64_t*)nullptr);
+        e->src = nullptr;
+        e->pending = true;
+        e->E = -1;
+        return KARMA_OK;
+    }
     // st (mapped host memory, written by the write kernel): 0 zero-division
     // flag, 1 edge count, 2 the list's merge order check
     void *hst = nullptr, *dst_ = nullptr;
@@ -1107,6 +1154,13 @@ int karma_edges_begin(karma_ctx* ctx, karma_pairs* p, int mode, int64_t N, karma
 
 int karma_edges_end(karma_edges* e, int64_t* n_edges) { return edges_end_impl(e, n_edges); }
 
+int karma_edges_count(karma_edges* e, int64_t* n_edges) {
+    KARMA_CHECK(e && n_edges && !e->open, KARMA_ERR_STATE, "karma_edges_count: no finished edge stage");
+    KARMA_TRY(edges_resolve(e));
+    *n_edges = e->E;
+    return KARMA_OK;
+}
+
 int karma_edges_destroy(karma_edges* e) {
     if (!e) return KARMA_OK;
     hipSetDevice(e->ctx->device);
@@ -1117,6 +1171,7 @@ int karma_edges_destroy(karma_edges* e) {
 int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, double* w, uint64_t* first, int is_device) {
     KARMA_CHECK(e, KARMA_ERR_ARG, "null edges");
     KARMA_TRY(ctx_begin(e->ctx));
+    KARMA_TRY(edges_resolve(e));
     const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     hipStream_t st = e->ctx->stream;
     if (e->E) {
@@ -1133,6 +1188,7 @@ int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, double
 int karma_edges_totals(karma_edges* e, int64_t* totals, int is_device) {
     KARMA_CHECK(e && (totals || !e->n_contigs), KARMA_ERR_ARG, "bad arguments");
     KARMA_TRY(ctx_begin(e->ctx));
+    KARMA_TRY(edges_resolve(e));
     if (e->n_contigs)
         KARMA_HIP(hipMemcpyAsync(totals, e->totals.ptr, e->n_contigs * 8,
                                  is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->ctx->stream));

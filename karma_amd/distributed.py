@@ -184,8 +184,10 @@ class HipOps:
         e, tp = pairs.edges_begin(_lib.KARMA_MODE_READS, n_contigs)
         return e, DevBuf(self.ctx, (n_contigs,), np.int64, _ptr=tp, _owner=e)
 
-    def edges_end(self, e):
-        return e.end()
+    def edges_end(self, e, count=True):
+        """count=False: the weights launched, the edge count read when first
+        used (no synchronisation in the step)."""
+        return e.end(count)
 
     def edge_count(self, edges):
         return edges.E
@@ -259,10 +261,13 @@ class ShardedBuild:
         """The karma contexts this build launches on (per-kernel timing)."""
         return [c for c in (self.ops.ctx if hasattr(self.ops, "ctx") else None, self.gctx) if c is not None]
 
-    def run(self, store, records, n_records, keep=False, sequential=False):
+    def run(self, store, records, n_records, keep=False, sequential=False, count=True):
         """One step.  sequential=True keeps the profile on the main stream (no
         side stream): slower, but every kernel has the chip to itself, which is
-        what a per-kernel timing pass wants."""
+        what a per-kernel timing pass wants.  count=False (a step of a stream
+        of identical steps; with an exchange only): the owner's edge count is
+        not read back, so the step ends without waiting for its last kernels,
+        and stats["E_local"] is None."""
         ops = self.ops
         # Default order (one stream pair): k-mer columns, then the graph's
         # kernels alone on the chip (classify .. final), then the profile on
@@ -276,7 +281,7 @@ class ShardedBuild:
             # exchange, a block slot per CU stays free for its collectives
             ops.ctx.set_side_headroom(1 if self.comm.world > 1 or self.emulate else 0)
         try:
-            return self._run(store, records, n_records, keep, side)
+            return self._run(store, records, n_records, keep, side, count or keep)
         finally:
             if side:
                 ops.join()
@@ -287,7 +292,7 @@ class ShardedBuild:
             return self.ops.graph_begin(records, n_records, self.n_glob, split_bounds=self.split_bounds)
         return self.ops.graph_begin(records, n_records, self.n_glob)
 
-    def _run(self, store, records, n_records, keep, side):
+    def _run(self, store, records, n_records, keep, side, count=True):
         ops, comm = self.ops, self.comm
         fut = None
         if self._pool is not None:  # ---- shared-read graph, concurrent (read_graph.py:19-50) ----
@@ -376,7 +381,7 @@ class ShardedBuild:
                 # the diagonal into the edges' own totals, gathered in place
                 eh, tot = ops.edges_begin(merged, self.n_glob)
                 comm.allgather_slices_(tot, self.bounds)
-                edges = ops.edges_end(eh)
+                edges = ops.edges_end(eh) if count else ops.edges_end(eh, count=False)
             else:
                 tot = comm.allgather_slices_(ops.totals(merged, self.n_glob), self.bounds)
                 edges = ops.edges(merged, self.n_glob, tot)
@@ -385,7 +390,7 @@ class ShardedBuild:
         else:
             edges = ops.edges(local, self.n_glob)
             final_pairs = local
-        stats["E_local"] = ops.edge_count(edges)
+        stats["E_local"] = ops.edge_count(edges) if count else None
         if keep:
             stats["profile"] = self._prof
             stats["edges"] = ops.edge_arrays(edges)

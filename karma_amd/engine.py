@@ -500,13 +500,28 @@ class EdgeArrays:
 
 class Edges:
     def __init__(self, ctx, h, E, n_contigs):
-        self.ctx, self.h, self.E, self.n_contigs = ctx, h, E, n_contigs
+        self.ctx, self.h, self._E, self.n_contigs = ctx, h, E, n_contigs
 
-    def end(self):
-        """Second half of Pairs.edges_begin (karma_edges_end): weights, edge count."""
-        E = ctypes.c_int64()
-        call("karma_edges_end", self.h, ctypes.byref(E))
-        self.E = E.value
+    @property
+    def E(self):
+        """Edge count; after end(count=False) its first read synchronises and
+        reports the edge stage's errors (karma_edges_count)."""
+        if self._E is None:
+            E = ctypes.c_int64()
+            call("karma_edges_count", self.h, ctypes.byref(E))
+            self._E = E.value
+        return self._E
+
+    def end(self, count=True):
+        """Second half of Pairs.edges_begin (karma_edges_end): weights, and the
+        edge count (count=False: launched only; E is read when first used)."""
+        if count:
+            E = ctypes.c_int64()
+            call("karma_edges_end", self.h, ctypes.byref(E))
+            self._E = E.value
+        else:
+            call("karma_edges_end", self.h, None)
+            self._E = None
         self._pairs = None
         return self
 

@@ -399,14 +399,18 @@ def test_merge_runs_and_split(seed, n_runs, n):
         _lib.call("karma_dev_alloc", ctx.h, kcb.nbytes, ctypes.byref(dev))
         try:
             _lib.call("karma_memcpy", ctx.h, dev, _lib.ptr(kcb), kcb.nbytes, 0)
-            for use in ("get", "edges"):
+            for use in ("get", "edges", "edges_deferred"):
                 p = engine.Pairs.merge_runs_kc(ctx, dev.value, lens.tolist())
                 with pytest.raises(_lib.KarmaError) as ei:
                     if use == "get":
                         p.get()
-                    else:
+                    elif use == "edges":
                         e, _ = p.edges_begin(_lib.KARMA_MODE_READS, n_contigs)
                         e.end()
+                    else:  # end without the count: the error comes with the first read
+                        e, _ = p.edges_begin(_lib.KARMA_MODE_READS, n_contigs)
+                        e.end(count=False)
+                        e.E
                 assert ei.value.code == _lib.KARMA_ERR_UNSORTED
                 p.close()
         finally:
@@ -435,6 +439,15 @@ def test_edges_of_unsummed_merge_equal_compacted():
         p1 = engine.Pairs.merge_runs_kc(ctx, dev.value, lens)
         e1, _ = p1.edges_begin(_lib.KARMA_MODE_READS, n_contigs)
         g1 = e1.end().get()
+        # the same with the count deferred to the first read
+        p3 = engine.Pairs.merge_runs_kc(ctx, dev.value, lens)
+        e3, _ = p3.edges_begin(_lib.KARMA_MODE_READS, n_contigs)
+        e3.end(count=False)
+        g3 = e3.get()
+        assert e3.E == e1.E == len(g3.a)
+        for f in ("a", "b", "shared", "totals"):
+            assert np.array_equal(getattr(g1, f), getattr(g3, f)), f
+        assert np.array_equal(g1.weight.view(np.uint64), g3.weight.view(np.uint64))
         p2 = engine.Pairs.merge_runs_kc(ctx, dev.value, lens)
         assert p2.count() < len(kc)  # compacted: the equal keys were summed
         g2 = p2.edges(_lib.KARMA_MODE_READS, n_contigs).get()
