@@ -216,6 +216,12 @@ int karma_ctx_destroy(karma_ctx* ctx) {
         hipEventDestroy(l.stop);
     }
     for (auto e : ctx->event_pool) hipEventDestroy(e);
+    if (ctx->fork_stream) {
+        hipStreamSynchronize(ctx->fork_stream);
+        hipStreamDestroy(ctx->fork_stream);
+    }
+    if (ctx->fork_a) hipEventDestroy(ctx->fork_a);
+    if (ctx->fork_b) hipEventDestroy(ctx->fork_b);
     if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
     if (ctx->pinned) hipHostFree(ctx->pinned);
     if (ctx->job_pinned) hipHostFree(ctx->job_pinned);

@@ -1986,6 +1986,26 @@ __global__ void relabel_back_kernel(uint64_t* __restrict__ keys, int64_t n, cons
 // where side-stream work (the k-mer profile) may start, see SetsJob::launch;
 // KARMA_MARK_AT in the environment overrides the default (scheduling only:
 // every position runs the same kernels)
+// the general-read branch on the context's fork stream beside the code branch
+// (KARMA_FORK=0 in the environment: both branches in order on one stream;
+// scheduling only, the same kernels run)
+bool fork_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("KARMA_FORK");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return on;
+}
+int ctx_fork(karma_ctx* ctx) {
+    if (!ctx->fork_stream) {
+        int lo = 0, hi = 0;
+        KARMA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        KARMA_HIP(hipStreamCreateWithPriority(&ctx->fork_stream, hipStreamNonBlocking, hi));
+        KARMA_HIP(hipEventCreateWithFlags(&ctx->fork_a, hipEventDisableTiming));
+        KARMA_HIP(hipEventCreateWithFlags(&ctx->fork_b, hipEventDisableTiming));
+    }
+    return KARMA_OK;
+}
 int mark_at() {
     static const int at = [] {
         const char* e = std::getenv("KARMA_MARK_AT");
@@ -2182,11 +2202,37 @@ int SetsJob::launch() {
         KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
     }
-    KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
-                 codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items + n_pblk, lpb, flags,
-                 relabeled ? (const uint32_t*)remap_map.ptr : nullptr, (const unsigned*)(counters + 3));
     const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items};
     pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items + n_pblk};
+    // Two independent branches after classify, joined by the final kernel:
+    // general reads -> pair lists -> pair partition -> pair reduce, and the
+    // code partition -> code reduce.  The first (three short kernels) runs on
+    // the context's fork stream beside the second.
+    hipStream_t const main_stream = ctx->stream;
+    const bool fork = fork_on();
+    if (fork) {
+        KARMA_TRY(ctx_fork(ctx));
+        KARMA_HIP(hipEventRecord(ctx->fork_a, main_stream));
+        KARMA_HIP(hipStreamWaitEvent(ctx->fork_stream, ctx->fork_a, 0));
+        ctx->stream = ctx->fork_stream;
+    }
+    int rc_pair = [&]() -> int {
+        KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
+                     codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items + n_pblk, lpb, flags,
+                     relabeled ? (const uint32_t*)remap_map.ptr : nullptr, (const unsigned*)(counters + 3));
+        if (wide_p)
+            KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStreamWide>, n_pblk, kPT, 0, plist.ptr,
+                         pcap, n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
+        else
+            KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
+                         n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
+        KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
+                     g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
+        if (fork) KARMA_HIP(hipEventRecord(ctx->fork_b, ctx->fork_stream));
+        return KARMA_OK;
+    }();
+    ctx->stream = main_stream;
+    KARMA_TRY(rc_pair);
     if (g.Bc > 0) {
         uint16_t* const trash = cent.ptr + (ccap + 7) / 8 * 8;
         if (append && wide_c)
@@ -2205,15 +2251,8 @@ int SetsJob::launch() {
         KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
                      g.Bc, g.bwc, n_cg, part_ch.ptr);
     }
-    KARMA_TRY(mark(4));  // after the code reduce: beside the pair kernels and the final kernel
-    if (wide_p)
-        KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStreamWide>, n_pblk, kPT, 0, plist.ptr, pcap,
-                     n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
-    else
-        KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStream>, n_pblk, kPT, 0, plist.ptr, pcap,
-                     n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
-    KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
-                 g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
+    KARMA_TRY(mark(4));  // after the code reduce: beside the final kernel
+    if (fork) KARMA_HIP(hipStreamWaitEvent(main_stream, ctx->fork_b, 0));
     SplitArgs sa{};
     sa.n = (int)split_b.size();
     for (int r = 0; r < sa.n; ++r) sa.b[r] = split_b[r];

@@ -91,6 +91,11 @@ struct karma_ctx {
     // resident blocks per CU by (kernel, block size, dynamic LDS): the occupancy
     // query costs host microseconds and is asked on every call of a step
     std::map<std::pair<const void*, std::pair<int, size_t>>, int> occupancy;
+    // a records graph job's second branch (general reads' pairs: general,
+    // pair partition, pair reduce) runs here beside the code branch, forked
+    // after classify and joined before the final kernel (SetsJob::launch)
+    hipStream_t fork_stream = nullptr;
+    hipEvent_t fork_a = nullptr, fork_b = nullptr;
 };
 
 namespace karma {
