@@ -2209,7 +2209,9 @@ int SetsJob::launch() {
     // code partition -> code reduce.  The first (three short kernels) runs on
     // the context's fork stream beside the second.
     hipStream_t const main_stream = ctx->stream;
-    const bool fork = fork_on();
+    // (not while every launch is timed: the per-kernel pass wants each kernel
+    // alone on the chip)
+    const bool fork = fork_on() && !(ctx->timing && ctx->timing_only.empty());
     if (fork) {
         KARMA_TRY(ctx_fork(ctx));
         KARMA_HIP(hipEventRecord(ctx->fork_a, main_stream));
