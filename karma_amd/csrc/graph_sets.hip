@@ -163,14 +163,14 @@ __device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__buil
 constexpr int kCW = 256;                // classify threads per block (4 independent waves)
 constexpr int kCIter = 512;             // records per wave step (8 per lane)
 constexpr int kCPer = kCIter / 128;     // 16-byte units per lane per step
-constexpr int64_t kCChunk = 8192;       // records per wave chunk (16 steps)
+constexpr int64_t kCChunk = 8192;       // records per wave chunk (16 steps; chunk_records may halve it)
 
 struct ClassArgs {
     const uint2* rec;
     int64_t A;
     uint32_t N;
     int compact;
-    uint32_t* codes;    // chunk c: [c * kCChunk, +n_codes[c]) codes, general starts from the end down
+    uint32_t* codes;    // chunk c: [c * chunk, +n_codes[c]) codes, general starts from the end down
     uint32_t* n_codes;  // per chunk
     uint32_t* n_gen;    // per chunk
     unsigned long long* blk_items;  // per partition block (lists_per_block chunks): codes
@@ -183,6 +183,7 @@ struct ClassArgs {
     const uint32_t* remap;  // contig relabelling (classify2_kernel<.., REMAP>), new id by old id
     int64_t c0;             // first chunk of this launch
     const unsigned* skip;   // set: leave the chunks empty (a relabelled rerun follows)
+    int64_t chunk;          // records per chunk (chunk_records)
 };
 
 // lanes below this one with their bit set in a wave mask
@@ -277,7 +278,7 @@ classify2_kernel(ClassArgs P) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
-    const int64_t c_lo = chunk * kCChunk;
+    const int64_t c_lo = chunk * P.chunk;
     if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
     if (P.skip && *P.skip) {  // the sample chunks asked for a relabelled rerun
         if (lane == 0) {
@@ -286,14 +287,14 @@ classify2_kernel(ClassArgs P) {
         }
         return;
     }
-    const int64_t c_hi = min(P.A, c_lo + kCChunk);
+    const int64_t c_hi = min(P.A, c_lo + P.chunk);
     uint32_t* out = P.codes + c_lo;
     // the chunk's region as a buffer resource built from wave-uniform values
     const uint64_t out_u = (uint64_t)out;
     const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(out_u >> 32)) << 32) |
                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)out_u)),
-        0, kCChunk * 4, 0x00020000);
+        0, (int)(P.chunk * 4), 0x00020000);
     // transpose buffer: lane l's 8 records in row l (4 units of 16 bytes), the
     // unit index XOR-ed with (l >> 2) & 3: conflict-free for the 16-byte stores
     // (8-lane groups, banks mod 32) and for the row reads (16-lane groups,
@@ -412,7 +413,7 @@ classify2_kernel(ClassArgs P) {
                 } else {
                     const uint64_t g = e & ~big & ~ok;
                     if (g) {
-                        if (in_mask(g)) out[kCChunk - 1 - (ng + rank_below(g))] = pos;
+                        if (in_mask(g)) out[P.chunk - 1 - (ng + rank_below(g))] = pos;
                         ng += __popcll(g);
                     }
                     const uint64_t bg = e & big;
@@ -551,7 +552,7 @@ classify2_kernel(ClassArgs P) {
             else if (ok) {
                 out[nc] = code;
                 if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
-            } else out[kCChunk - 1 - ng] = ct_pos;
+            } else out[P.chunk - 1 - ng] = ct_pos;
         }
         nc += ok ? 1u : 0u;
         ng += !big && !ok ? 1u : 0u;
@@ -588,7 +589,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
                                                        unsigned long long* __restrict__ blk_items,
                                                        int lists_per_block, int* __restrict__ flags,
                                                        const uint32_t* __restrict__ remap,
-                                                       const unsigned* __restrict__ relabel) {
+                                                       const unsigned* __restrict__ relabel, int64_t chunk_len) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t chunk = (int64_t)blockIdx.x * (kGW / 64) + wave;
     if (chunk >= n_chunks) return;
@@ -596,7 +597,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
     const uint32_t ng = relabel && *relabel ? 0u : n_gen[chunk];
     uint32_t np = 0;
     uint64_t* out = pairs + chunk * pcap;
-    const int64_t c_lo = chunk * kCChunk;
+    const int64_t c_lo = chunk * chunk_len;
     bool full = false;
     for (uint32_t kb = 0; kb < ng; kb += 64) {
         const uint32_t k = kb + lane;
@@ -605,7 +606,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
 #pragma unroll
         for (int t = 0; t < kMaxFast; ++t) rs.keep[t] = false;
         if (k < ng) {
-            const int64_t s = c_lo + codes[c_lo + kCChunk - 1 - k];
+            const int64_t s = c_lo + codes[c_lo + chunk_len - 1 - k];
             const uint32_t rid = rec[s].x;
             bool v = true;
 #pragma unroll
@@ -1824,12 +1825,12 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         if (A > 0) {
             ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags,
-                        nullptr,   0,         0,       nullptr, 0, nullptr};
+                        nullptr,   0,         0,       nullptr, 0, nullptr, kCChunk};
             KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false>), ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags,
-                     (const uint32_t*)nullptr, (const unsigned*)nullptr);
+                     (const uint32_t*)nullptr, (const unsigned*)nullptr, kCChunk);
         KARMA_LAUNCH(ctx, "widen_counts", widen_counts_kernel, grid_n(n_chunks + 1), 256, 0, n_pl.ptr, n_chunks,
                      widths.ptr);
         KARMA_TRY(scan_excl_i64(ctx, widths.ptr, off.ptr, n_chunks + 1));
@@ -1879,11 +1880,18 @@ __global__ void __launch_bounds__(kRelabelProbes) relabel_probe_kernel(const uin
                                                                        uint32_t N, unsigned* __restrict__ relabel,
                                                                        uint64_t* __restrict__ zero, int64_t n_zero) {
     __shared__ unsigned wide;
-    if (threadIdx.x == 0) wide = 0;
     // the job's control block (flags, counters, per-bucket sizes; relabel is
-    // one of its words) is cleared here: no memset launch ahead of the probe
-    for (int64_t i = threadIdx.x; i < n_zero; i += kRelabelProbes) zero[i] = 0;
-    __syncthreads();
+    // one of its words) is cleared here: no memset launch ahead of the probe.
+    // Thread 0 clears the word holding the relabel flag and sets the flag, so
+    // the barriers order LDS only (no wait for the clearing stores)
+    const int64_t rw = (int64_t)(reinterpret_cast<uintptr_t>(relabel) - reinterpret_cast<uintptr_t>(zero)) / 8;
+    if (threadIdx.x == 0) {
+        wide = 0;
+        zero[rw] = 0;
+    }
+    for (int64_t i = threadIdx.x; i < n_zero; i += kRelabelProbes)
+        if (i != rw) zero[i] = 0;
+    lds_barrier();
     // a window of 32 records from an even position, loaded at once (16 B each)
     constexpr int kW = 32;
     const int64_t p = (A * (int64_t)threadIdx.x / kRelabelProbes) & ~int64_t(1);
@@ -1911,7 +1919,7 @@ __global__ void __launch_bounds__(kRelabelProbes) relabel_probe_kernel(const uin
             if (mx - mn > 3u && mx < N) atomicAdd(&wide, 1u);
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0 && wide * 8 > kRelabelProbes) *relabel = 1;
 }
 
@@ -2006,6 +2014,17 @@ int ctx_fork(karma_ctx* ctx) {
     }
     return KARMA_OK;
 }
+// Records per classify chunk (one wave each, 4 waves per SIMD resident).  A
+// launch of few chunks per wave slot ends in a partial round: 38.6M records
+// (config 3 over 8 ranks) are 4,711 chunks of 8192 on 4,096 slots.  Half-size
+// chunks while 8192-record chunks would fill fewer than 4 rounds: classify
+// 0.0755 -> 0.070 ms there, 0.139 -> 0.128 ms at 4 ranks; at config 3 on one
+// GPU (9.2 rounds) 8192 stays, 4096 measured 0.536 -> 0.549 ms
+// (profiles/r03/ab_chunk/).
+int64_t chunk_records(const karma_ctx* ctx, int64_t A) {
+    const int64_t slots = (int64_t)ctx->cu_count * 16;
+    return ceil_div(A, kCChunk) < 4 * slots ? kCChunk / 2 : kCChunk;
+}
 int mark_at() {
     static const int at = [] {
         const char* e = std::getenv("KARMA_MARK_AT");
@@ -2020,6 +2039,7 @@ struct SetsJob {
     Geo g{};
     int B = 0;
     int64_t n_chunks = 0;
+    int64_t chunk = kCChunk;  // records per classify chunk (chunk_records)
     bool wide_c = false, wide_p = false, append = false;
     int lpb = 0;
     int64_t n_pblk = 0;
@@ -2069,7 +2089,8 @@ struct SetsJob {
 int SetsJob::setup() {
     KARMA_TRY(make_geo(N, &g));
     B = g.B;
-    n_chunks = std::max<int64_t>(1, ceil_div(A, kCChunk));
+    chunk = chunk_records(ctx, A);
+    n_chunks = std::max<int64_t>(1, ceil_div(A, chunk));
     // partition: one round of resident blocks, each taking consecutive chunk lists
     wide_c = g.Bc > kNarrowBc;
     wide_p = B > kNarrowB;
@@ -2083,11 +2104,12 @@ int SetsJob::setup() {
     const int resident = resident_grid(ctx, code_part, kPT, 0, int64_t(1) << 30);
     lpb = (int)std::min<int64_t>(kMaxListsPerBlock, ceil_div(n_chunks, resident));
     n_pblk = ceil_div(n_chunks, lpb);
-    KARMA_TRY(codes.alloc(ctx, n_chunks * kCChunk));
+    KARMA_TRY(codes.alloc(ctx, n_chunks * chunk));
     KARMA_TRY(n_codes.alloc(ctx, n_chunks));
     KARMA_TRY(n_gen.alloc(ctx, n_chunks));
     KARMA_TRY(n_pl.alloc(ctx, n_chunks));
     KARMA_TRY(big_list.alloc(ctx, A / (kMaxFast + 1) + 1));
+    pcap = chunk / 8;
     ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8) + (int64_t)split_b.size();
     // one allocation (and one memset per attempt) for the control block and
     // the per-partition-block item counts behind it
@@ -2158,7 +2180,8 @@ int SetsJob::launch() {
     if (A > 0) {
         ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
                     n_gen.ptr, blk_items, lpb, big_list.ptr, counters, flags,
-                    append ? blk_hist.ptr : nullptr, g.bwc, g.Bc, relabeled ? remap_map.ptr : nullptr, 0, nullptr};
+                    append ? blk_hist.ptr : nullptr, g.bwc, g.Bc, relabeled ? remap_map.ptr : nullptr, 0, nullptr,
+                    chunk};
         auto classify = [&](int64_t c_from, int64_t c_to) -> int {
             C.c0 = c_from;
             const int64_t cg = ceil_div(c_to - c_from, kCW / 64);
@@ -2221,7 +2244,7 @@ int SetsJob::launch() {
     int rc_pair = [&]() -> int {
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items + n_pblk, lpb, flags,
-                     relabeled ? (const uint32_t*)remap_map.ptr : nullptr, (const unsigned*)(counters + 3));
+                     relabeled ? (const uint32_t*)remap_map.ptr : nullptr, (const unsigned*)(counters + 3), chunk);
         if (wide_p)
             KARMA_LAUNCH(ctx, "graph_pair_partition", partition_kernel<PairStreamWide>, n_pblk, kPT, 0, plist.ptr,
                          pcap, n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
@@ -2238,16 +2261,16 @@ int SetsJob::launch() {
     if (g.Bc > 0) {
         uint16_t* const trash = cent.ptr + (ccap + 7) / 8 * 8;
         if (append && wide_c)
-            KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kMaxBc>, n_pblk, kPT, 0, codes.ptr, kCChunk,
+            KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kMaxBc>, n_pblk, kPT, 0, codes.ptr, chunk,
                          n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
         else if (append)
             KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kNarrowBc>, n_pblk, kPT, 0, codes.ptr,
-                         kCChunk, n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
+                         chunk, n_codes.ptr, n_chunks, lpb, g, blk_hist.ptr, cent.ptr, trash, cdir, flags + 3);
         else if (wide_c)
             KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStreamWide>, n_pblk, kPT, 0, codes.ptr,
-                         kCChunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
+                         chunk, n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
         else
-            KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr, kCChunk,
+            KARMA_LAUNCH(ctx, "graph_code_partition", partition_kernel<CodeStream>, n_pblk, kPT, 0, codes.ptr, chunk,
                          n_codes.ptr, n_chunks, lpb, g, cent.ptr, cdir);
         KARMA_TRY(mark(2));
         KARMA_LAUNCH(ctx, "graph_code_reduce", code_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, cent.ptr, cdir,
@@ -2323,7 +2346,7 @@ int SetsJob::finish(karma_pairs* out) {
         if (!hf[2]) break;
         KARMA_CHECK(attempt == 0, KARMA_ERR_STATE, "pair list capacity exceeded twice");
         attempt = 1;
-        pcap = kCChunk * 9 / 2;  // every read with <= 8 records fits
+        pcap = chunk * 9 / 2;  // every read with <= 8 records fits
         KARMA_TRY(launch());
     }
     const unsigned n_big = hc[0];
