@@ -433,8 +433,10 @@ def pmc_traffic(args, world, kernel):
     """HBM bytes per launch of `kernel` from a rocprofv3 PMC run of THIS
     workload (profiles/pmc_traffic.json, written by tools/pmc_traffic.py and
     keyed by workload), else None."""
-    key = f"{args.config}{'_strong' if args.strong else ''}{'_shuffled' if args.shuffle_contigs else ''}" \
-          f"_n{world * max(1, args.emulate_ranks)}"
+    ranks = world * max(1, args.emulate_ranks)
+    # strong and weak are one workload on one rank (the table's config3_n1)
+    key = f"{args.config}{'_strong' if args.strong and ranks > 1 else ''}" \
+          f"{'_shuffled' if args.shuffle_contigs else ''}_n{ranks}"
     try:
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
             return json.load(f).get(key, {}).get(kernel)
