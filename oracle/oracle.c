@@ -372,33 +372,71 @@ int oracle_threads(void) {
 /* oracle_kmer_columns over contigs in parallel: every thread keeps the sorted
  * union of its contigs' k-mers, then the thread unions are merged (the CPU
  * baseline's column table; same result as the scalar restatement). */
+/* Per-thread exact set of k-mer keys (open addressing over the 16-byte keys;
+ * bytes past len are zero in every emitted key, so whole-key equality is
+ * str equality).  The OpenMP twin collects the union with it instead of
+ * sorting each contig's k-mers: the set stays a few thousand keys, so an
+ * insert is a probe of an L1-resident table. */
+typedef struct {
+    okey_t* slot;
+    uint8_t* used;
+    int64_t cap, n;
+} kset_t;
+
+static uint64_t okey_hash(const okey_t* k) {
+    uint64_t a, b;
+    memcpy(&a, k, 8);
+    memcpy(&b, (const uint8_t*)k + 8, 8);
+    uint64_t h = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+    return h ^ (h >> 31);
+}
+
+static void kset_insert(kset_t* s, const okey_t* k) {
+    uint64_t i = okey_hash(k) & (uint64_t)(s->cap - 1);
+    while (s->used[i]) {
+        if (!memcmp(&s->slot[i], k, sizeof *k)) return;
+        i = (i + 1) & (uint64_t)(s->cap - 1);
+    }
+    s->used[i] = 1;
+    s->slot[i] = *k;
+    s->n++;
+}
+
+static void kset_add(void* ctx, const okey_t* k) {
+    kset_t* s = (kset_t*)ctx;
+    if (2 * (s->n + 1) > s->cap) { /* grow: rehash into twice the slots */
+        kset_t t = {0, 0, s->cap ? 2 * s->cap : 4096, 0};
+        t.slot = (okey_t*)malloc((size_t)t.cap * sizeof(okey_t));
+        t.used = (uint8_t*)calloc((size_t)t.cap, 1);
+        for (int64_t i = 0; i < s->cap; ++i)
+            if (s->used[i]) kset_insert(&t, &s->slot[i]);
+        free(s->slot);
+        free(s->used);
+        *s = t;
+    }
+    kset_insert(s, k);
+}
+
 int64_t oracle_omp_kmer_columns(const uint8_t* seq, const int64_t* offsets, int64_t n, int kmode, uint8_t* keys_out,
                                 int64_t cap) {
     if (kmode == 0 || kmode > OK_MAXK || kmode < -1) return INT64_MIN;
     int T = oracle_threads();
-    kvec_t* part = (kvec_t*)calloc((size_t)T, sizeof(kvec_t));
+    kset_t* part = (kset_t*)calloc((size_t)T, sizeof(kset_t));
 #pragma omp parallel num_threads(T)
     {
-        kvec_t* kv = &part[omp_get_thread_num()];
-        kvec_t one = {0, 0, 0};
+        kset_t* ks = &part[omp_get_thread_num()];
 #pragma omp for schedule(dynamic, 256)
-        for (int64_t c = 0; c < n; ++c) {
-            one.n = 0;
-            enum_kmers(seq + offsets[c], offsets[c + 1] - offsets[c], kmode, kvec_push, &one);
-            int64_t m = sort_unique(one.v, one.n);
-            for (int64_t i = 0; i < m; ++i) kvec_push(kv, &one.v[i]);
-            if (kv->n > (1 << 20)) kv->n = sort_unique(kv->v, kv->n);
-        }
-        free(one.v);
-        kv->n = sort_unique(kv->v, kv->n);
+        for (int64_t c = 0; c < n; ++c) enum_kmers(seq + offsets[c], offsets[c + 1] - offsets[c], kmode, kset_add, ks);
     }
     kvec_t all = {0, 0, 0};
     for (int t = 0; t < T; ++t) {
-        for (int64_t i = 0; i < part[t].n; ++i) kvec_push(&all, &part[t].v[i]);
-        free(part[t].v);
+        for (int64_t i = 0; i < part[t].cap; ++i)
+            if (part[t].used[i]) kvec_push(&all, &part[t].slot[i]);
+        free(part[t].slot);
+        free(part[t].used);
     }
     free(part);
-    int64_t M = sort_unique(all.v, all.n);
+    int64_t M = sort_unique(all.v, all.n); /* sorted() of the union, kmer.py:172 */
     if (M > cap) {
         free(all.v);
         return -M;
