@@ -2021,7 +2021,13 @@ int ctx_fork(karma_ctx* ctx) {
 // 0.0755 -> 0.070 ms there, 0.139 -> 0.128 ms at 4 ranks; at config 3 on one
 // GPU (9.2 rounds) 8192 stays, 4096 measured 0.536 -> 0.549 ms
 // (profiles/r03/ab_chunk/).
+// KARMA_CHUNK=4096|8192 in the environment pins the size (tests run both
+// sizes on the same small inputs; read per call).
 int64_t chunk_records(const karma_ctx* ctx, int64_t A) {
+    if (const char* e = std::getenv("KARMA_CHUNK")) {
+        const int64_t c = std::atoll(e);
+        if (c == kCChunk || c == kCChunk / 2) return c;
+    }
     const int64_t slots = (int64_t)ctx->cu_count * 16;
     return ceil_div(A, kCChunk) < 4 * slots ? kCChunk / 2 : kCChunk;
 }

@@ -496,3 +496,25 @@ def test_graph_records_split_call():
             p3.close()
     finally:
         _lib.load().karma_dev_free(ctx.h, dev)
+
+
+@pytest.mark.parametrize("chunk", ["4096", "8192"])
+def test_records_both_chunk_sizes(chunk, monkeypatch):
+    """Classify's chunk size follows the launch size (graph_sets.hip
+    chunk_records): inputs below ~134M records take 4096-record chunks, config
+    3 and 5 take 8192.  KARMA_CHUNK pins either size so both run the small
+    cases: reads across chunk boundaries, reads of > 8 records, a bucket
+    overflow beside compact reads, and the relabelled rerun."""
+    monkeypatch.setenv("KARMA_CHUNK", chunk)
+    check_records(engine.synth_records(2, 20_000, 0, 400_000, True), 20_000)
+    check_records(engine.synth_records(13, 1_600_000, 0, 1_500_000, True), 1_600_000)
+    rng = np.random.default_rng(2)
+    rows = []
+    for r in range(3000):
+        lo = int(rng.integers(0, 1000))
+        for c in rng.integers(lo, lo + 200, int(rng.choice([1, 2, 3, 9, 17, 40]))):
+            rows.append((r, int(c)))
+    check_records(np.array(rows, np.uint32), 1200)
+    rec = np.ascontiguousarray(engine.synth_records(21, 20_000, 0, 400_000, True))
+    rec[:, 1] = np.random.default_rng(3).permutation(20_000).astype(np.uint32)[rec[:, 1]]
+    check_records(rec, 20_000)
