@@ -192,7 +192,8 @@ int karma_kmer_profile_side(karma_kmer_plan* plan, double* out_dev, int64_t ld, 
 /* The context's stream waits (on the device) for the work enqueued on `side`. */
 int karma_ctx_join(karma_ctx* ctx, void* side);
 /* Block slots per CU the side-stream profile's grid leaves free for the main
- * stream (default 1: room for RCCL kernels beside it; 0 on one GPU). */
+ * stream (default 0: the profile's 3 blocks per CU take the chip; a free slot
+ * measured slower). */
 int karma_ctx_set_side_headroom(karma_ctx* ctx, int blocks_per_cu);
 /* Number of k-mer occurrences per contig (0 => the all-zero row of kmer.py:250-258). */
 int karma_kmer_row_totals(karma_kmer_plan* p, int64_t* dst_host);

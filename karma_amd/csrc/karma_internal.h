@@ -76,7 +76,7 @@ struct karma_ctx {
     bool job_open = false;
     hipEvent_t side_ev = nullptr;  // main -> side stream ordering (karma_kmer_profile_side)
     int grid_headroom = 0;         // blocks per CU resident_grid leaves free (a side-stream launch)
-    int side_headroom = 1;         // grid_headroom of karma_kmer_profile_side (karma_ctx_set_side_headroom)
+    int side_headroom = 0;         // grid_headroom of karma_kmer_profile_side (karma_ctx_set_side_headroom)
     hipEvent_t mark_ev = nullptr;  // recorded by an open graph job after its classify kernel
     bool mark_set = false;
     int64_t* fin_pinned = nullptr;  // M of an in-flight karma_kmer_plan_finalize_async

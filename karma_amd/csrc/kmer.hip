@@ -708,9 +708,12 @@ __host__ __device__ constexpr int64_t hist_words(int64_t M, bool c16) {
 __host__ __device__ constexpr int64_t tab_entries(bool p56, uint32_t S) { return p56 ? 1088 : (int64_t)S; }
 
 template <bool P56, bool C16>
-// 8 waves per SIMD (4 blocks per CU with u16 counters)
+// 6 waves per SIMD (3 blocks per CU): fewer rows written at once write faster
+// than 8 waves (4 blocks) do, and the counting still hides under the writes:
+// profile 0.345-0.355 -> 0.335-0.337 ms at config 3 (round 3,
+// profiles/r03/ab_profwaves/; 7 waves: 0.407, 5: 0.497, 4: 0.499 ms)
 #ifndef KARMA_PROF_WAVES
-#define KARMA_PROF_WAVES 8
+#define KARMA_PROF_WAVES 6
 #endif
 __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(KARMA_PROF_WAVES, KARMA_PROF_WAVES)))
 profile_wave_kernel(

@@ -276,10 +276,14 @@ class ShardedBuild:
         # before anything uses the plan or the profile.
         side = self._pool is None and hasattr(ops, "graph_begin") and not sequential
         if side:
-            # one GPU: nothing but short kernels share the chip with the profile,
-            # which then takes all of it (1.35 vs 1.36-1.39 ms/step); with an
-            # exchange, a block slot per CU stays free for its collectives
-            ops.ctx.set_side_headroom(1 if self.comm.world > 1 or self.emulate else 0)
+            # the profile's one-round grid takes the whole chip (3 blocks per
+            # CU at 6 waves per SIMD); the exchange's kernels and collectives
+            # queue behind its blocks.  Leaving a block slot free for them
+            # (round 2's default with an exchange) halves the profile's blocks
+            # now: 8-rank strong preview 0.244 (none free) vs 0.256 ms, weak
+            # 1.35-1.37 vs 1.40-1.42 ms (profiles/r03/ab_headroom/)
+            hr = os.environ.get("KARMA_SIDE_HEADROOM")  # measurement override (blocks per CU)
+            ops.ctx.set_side_headroom(int(hr) if hr else 0)
         try:
             return self._run(store, records, n_records, keep, side, count or keep)
         finally:
