@@ -147,18 +147,39 @@ __device__ __forceinline__ bool edge_flag(uint64_t k, int64_t c, int mode) {
     return c != 0 && !(diag && mode == KARMA_MODE_READS);
 }
 
+// With totals (n_tot entries, n >= 1) the kernel writes every entry itself, so
+// no memset precedes it: the diagonal group of contig a writes its sum, and
+// the first key of each contig a zeroes a when it is not the diagonal and the
+// contigs between the previous contig and a; the grid zeroes those before the
+// first contig and after the last (the keys are sorted by a, and (a, a) is
+// the smallest key of a).
 __global__ void __launch_bounds__(kET) edges_count_kernel(const uint64_t* __restrict__ keys,
                                                           const int64_t* __restrict__ counts, int64_t n, int mode,
-                                                          int64_t* __restrict__ totals, int64_t* __restrict__ blk_cnt,
-                                                          int64_t* __restrict__ st) {
+                                                          int64_t* __restrict__ totals, int64_t n_tot,
+                                                          int64_t* __restrict__ blk_cnt, int64_t* __restrict__ st) {
     const int64_t i = (int64_t)blockIdx.x * kET + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < 3) st[threadIdx.x] = 0;  // the write kernel's status words
+    if (totals) {
+        const int64_t a_first = (int64_t)(keys[0] >> 32), a_last = (int64_t)(keys[n - 1] >> 32);
+        const int64_t stride = (int64_t)gridDim.x * kET;
+        for (int64_t c = i; c < min(a_first, n_tot); c += stride) totals[c] = 0;
+        for (int64_t c = a_last + 1 + i; c < n_tot; c += stride) totals[c] = 0;
+    }
     bool f = false;
     if (i < n) {
         const uint64_t k = keys[i];
+        const uint32_t a = (uint32_t)(k >> 32);
+        const bool in_tot = totals && (int64_t)a < n_tot;
+        if (in_tot && i > 0) {
+            const uint32_t pa = (uint32_t)(keys[i - 1] >> 32);
+            for (uint32_t c = pa + 1; c < a; ++c) totals[c] = 0;  // contigs without keys (none when pa == a)
+            if (pa != a && a != (uint32_t)k) totals[a] = 0;
+        } else if (in_tot && a != (uint32_t)k) {
+            totals[a] = 0;  // the first contig has no diagonal
+        }
         if (group_head(keys, i, k)) {
             const int64_t c = group_sum(keys, counts, n, i, k);
-            if (totals && (uint32_t)(k >> 32) == (uint32_t)k) totals[(uint32_t)k] = c;
+            if (in_tot && a == (uint32_t)k) totals[a] = c;
             f = edge_flag(k, c, mode);
         }
     }
@@ -1041,8 +1062,8 @@ static int edges_begin_impl(karma_ctx* ctx, karma_pairs* p, int mode, const int6
         if (mode == KARMA_MODE_EQ) {
             KARMA_CHECK(p->has_totals && p->n_contigs == N, KARMA_ERR_STATE, "eq pair list without totals");
             if (N) KARMA_HIP(hipMemcpyAsync(e->totals.ptr, p->totals.ptr, N * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        } else {  // the diagonal counts, written by the edge count kernel
-            if (N) KARMA_HIP(hipMemsetAsync(e->totals.ptr, 0, N * 8, ctx->stream));
+        } else {  // the diagonal counts, written by the edge count kernel (with the zeros when the list is not empty)
+            if (N && !p->n) KARMA_HIP(hipMemsetAsync(e->totals.ptr, 0, N * 8, ctx->stream));
             diag_here = true;
         }
     } else if (N) {
@@ -1053,7 +1074,7 @@ static int edges_begin_impl(karma_ctx* ctx, karma_pairs* p, int mode, const int6
     KARMA_TRY(e->blk.alloc(ctx, e->n_blk + 3));
     if (n)
         KARMA_LAUNCH(ctx, "edge_count", edges_count_kernel, ceil_div(n, kET), kET, 0, p->keys.ptr, p->counts.ptr, n,
-                     mode, diag_here ? e->totals.ptr : (int64_t*)nullptr, e->blk.ptr, e->blk.ptr + e->n_blk);
+                     mode, diag_here ? e->totals.ptr : (int64_t*)nullptr, N, e->blk.ptr, e->blk.ptr + e->n_blk);
     else
         KARMA_HIP(hipMemsetAsync(e->blk.ptr + e->n_blk, 0, 3 * 8, ctx->stream));
     e->open = true;
