@@ -1887,7 +1887,7 @@ __global__ void __launch_bounds__(kRelabelProbes) relabel_probe_kernel(const uin
     const int64_t rw = (int64_t)(reinterpret_cast<uintptr_t>(relabel) - reinterpret_cast<uintptr_t>(zero)) / 8;
     if (threadIdx.x == 0) {
         wide = 0;
-        zero[rw] = 0;
+        if (rw >= 0 && rw < n_zero) zero[rw] = 0;
     }
     for (int64_t i = threadIdx.x; i < n_zero; i += kRelabelProbes)
         if (i != rw) zero[i] = 0;
