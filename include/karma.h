@@ -61,6 +61,9 @@ const char* karma_last_error(void);
  * bench.py prints it and refuses a non-default build. */
 const char* karma_build_info(void);
 int karma_device_count(int* n);
+/* Layout of a context's mapped host region (diagnostic; no device needed):
+ * one fixed slot per user, offsets[s] / bytes[s] for s < min(cap, *n). */
+int karma_mapped_slots(int64_t* offsets, int64_t* bytes, int cap, int* n);
 
 /* ---- context: one device, one HIP stream --------------------------------- */
 typedef struct karma_ctx karma_ctx;
@@ -112,6 +115,13 @@ typedef struct karma_comm karma_comm;
 int karma_comm_id_bytes(void);
 int karma_comm_unique_id(uint8_t* id);
 int karma_comm_create(karma_ctx* ctx, const uint8_t* id, int world, int rank, karma_comm** out);
+/* The same with flags.  KARMA_COMM_SIDE: a second communicator over the same
+ * ranks (its own unique id) for collectives enqueued on a side stream.  One
+ * communicator's operations must be issued in the same order on every rank; a
+ * job with collectives on two streams gives each stream its own communicator,
+ * so the two orders never interleave differently across ranks. */
+#define KARMA_COMM_SIDE 1
+int karma_comm_create_ex(karma_ctx* ctx, const uint8_t* id, int world, int rank, int flags, karma_comm** out);
 int karma_comm_destroy(karma_comm* c);
 int karma_comm_info(karma_comm* c, int* world, int* rank);
 /* In place on device memory, stream-ordered. */

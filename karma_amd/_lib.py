@@ -29,6 +29,7 @@ KARMA_ERR_COMM = -9
 
 KARMA_DT_U8, KARMA_DT_I32, KARMA_DT_I64, KARMA_DT_U64, KARMA_DT_F64 = 0, 1, 2, 3, 4
 KARMA_OP_SUM, KARMA_OP_MAX, KARMA_OP_MIN = 0, 1, 2
+KARMA_COMM_SIDE = 1
 _DTYPE_CODE = {np.dtype(np.uint8): KARMA_DT_U8, np.dtype(np.int32): KARMA_DT_I32, np.dtype(np.int64): KARMA_DT_I64,
                np.dtype(np.uint64): KARMA_DT_U64, np.dtype(np.float64): KARMA_DT_F64}
 
@@ -67,6 +68,8 @@ _SIGS = {
     "karma_stream_sync": [_c_p, _c_p],
     "karma_comm_unique_id": [_c_p],
     "karma_comm_create": [_c_p, _c_p, _i32, _i32, _PP],
+    "karma_comm_create_ex": [_c_p, _c_p, _i32, _i32, _i32, _PP],
+    "karma_mapped_slots": [_c_p, _c_p, _i32, ctypes.POINTER(ctypes.c_int)],
     "karma_comm_destroy": [_c_p],
     "karma_comm_info": [_c_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
     "karma_comm_allreduce": [_c_p, _c_p, _i64, _i32, _i32],

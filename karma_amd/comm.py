@@ -141,18 +141,38 @@ class HostComm:
 
 
 class RcclComm:
-    """The library's RCCL communicator on one device (karma_comm_*)."""
+    """The library's RCCL communicator on one device (karma_comm_*).
 
-    def __init__(self, group, ctx):
+    With several ranks it holds two communicators over the same ranks: this
+    one for the main stream and `side` (KARMA_COMM_SIDE, its own unique id) for
+    the column set's exchange on the side stream.  One communicator's
+    operations must be issued in the same order on every rank; with one per
+    stream, how the two streams interleave on a rank cannot matter."""
+
+    def __init__(self, group, ctx, with_side=True):
         self.group, self.world, self.rank, self.ctx = group, group.world, group.rank, ctx
         lib = _lib.load()
-        uid = np.zeros(lib.karma_comm_id_bytes(), np.uint8)
+        nb = lib.karma_comm_id_bytes()
+        nid = 2 if with_side and self.world > 1 else 1
+        uid = np.zeros(nid * nb, np.uint8)
         if self.rank == 0:
-            call("karma_comm_unique_id", ptr(uid))
+            for i in range(nid):
+                call("karma_comm_unique_id", ctypes.c_void_p(uid.ctypes.data + i * nb))
         uid = np.ascontiguousarray(self.group.allgather(uid)[0])
+        self.h = self._create(uid[:nb], 0)
+        self.side, self._side_of = self, None
+        if nid == 2:
+            s = RcclComm.__new__(RcclComm)
+            s.group, s.world, s.rank, s.ctx = group, self.world, self.rank, ctx
+            s.h = self._create(uid[nb:], _lib.KARMA_COMM_SIDE)
+            s.side, s._side_of = s, self
+            self.side = s
+
+    def _create(self, uid, flags):
         h = ctypes.c_void_p()
-        call("karma_comm_create", ctx.h, ptr(uid), self.world, self.rank, ctypes.byref(h))
-        self.h = h
+        call("karma_comm_create_ex", self.ctx.h, ptr(np.ascontiguousarray(uid)), self.world, self.rank, flags,
+             ctypes.byref(h))
+        return h
 
     # -- host scalars --
     def _reduce_host(self, arr, op):
@@ -252,10 +272,14 @@ class RcclComm:
         return ra, rb, [int(x) for x in rc]
 
     def close(self):
+        if self.side is not self:
+            self.side.close()
+            self.side = self
         if getattr(self, "h", None):
             _lib.load().karma_comm_destroy(self.h)
             self.h = None
-        self.group.close()
+        if self._side_of is None:  # the side communicator shares the main one's group
+            self.group.close()
 
 
 def create(ctx=None, world=None, rank=None, backend=None):

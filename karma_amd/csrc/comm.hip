@@ -25,6 +25,9 @@ struct karma_comm {
     int32_t* scratch = nullptr;     // device: barrier word / host-scalar staging (scalar_bytes; host side:
                                     // the context's mapped buffer, ctx_mapped)
     int64_t* counts_dev = nullptr;  // device: all-to-all count exchange (2 * world int64)
+    // the context's mapped slot for host scalars: a side-stream communicator
+    // (KARMA_COMM_SIDE) has its own, so its scalars never alias the main one's
+    int scalar_slot = karma::kMapCommScalar;
 };
 
 namespace {
@@ -95,16 +98,19 @@ int karma_comm_unique_id(uint8_t* id) {
     return KARMA_OK;
 }
 
-int karma_comm_create(karma_ctx* ctx, const uint8_t* id, int world, int rank, karma_comm** out) {
+int karma_comm_create_ex(karma_ctx* ctx, const uint8_t* id, int world, int rank, int flags, karma_comm** out) {
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(id && out && world >= 1 && rank >= 0 && rank < world, KARMA_ERR_ARG,
                 "karma_comm_create: bad arguments (world %d, rank %d)", world, rank);
+    KARMA_CHECK(world <= 1024, KARMA_ERR_ARG, "karma_comm_create: world %d above 1024", world);
+    KARMA_CHECK((flags & ~KARMA_COMM_SIDE) == 0, KARMA_ERR_ARG, "karma_comm_create: unknown flags %d", flags);
     ncclUniqueId u;
     std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
     auto* c = new karma_comm();
     c->ctx = ctx;
     c->world = world;
     c->rank = rank;
+    c->scalar_slot = (flags & KARMA_COMM_SIDE) ? kMapSideScalar : kMapCommScalar;
     ncclResult_t r = ncclCommInitRank(&c->nc, world, u, rank);
     if (r != ncclSuccess) {
         set_error("ncclCommInitRank(world %d, rank %d): %s", world, rank, ncclGetErrorString(r));
@@ -128,6 +134,10 @@ int karma_comm_create(karma_ctx* ctx, const uint8_t* id, int world, int rank, ka
     }
     *out = c;
     return KARMA_OK;
+}
+
+int karma_comm_create(karma_ctx* ctx, const uint8_t* id, int world, int rank, karma_comm** out) {
+    return karma_comm_create_ex(ctx, id, world, rank, 0, out);
 }
 
 int karma_comm_destroy(karma_comm* c) {
@@ -175,7 +185,7 @@ int karma_comm_allreduce_host(karma_comm* c, void* buf_host, int64_t count, int 
     const size_t bytes = (size_t)count * sz;
     const int words = (int)((bytes + 7) / 8);
     void *hm = nullptr, *dm = nullptr;
-    KARMA_TRY(ctx_mapped(c->ctx, (size_t)words * 8, &hm, &dm));
+    KARMA_TRY(ctx_mapped(c->ctx, c->scalar_slot, (size_t)words * 8, &hm, &dm));
     std::memcpy(hm, buf_host, bytes);
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream, static_cast<const uint64_t*>(dm),
                        reinterpret_cast<uint64_t*>(c->scratch), words);
@@ -208,7 +218,7 @@ int karma_comm_exchange_counts(karma_comm* c, const int64_t* send_host, int64_t*
     KARMA_CHECK(send_host && recv_host, KARMA_ERR_ARG, "karma_comm_exchange_counts: null argument");
     const int W = c->world;
     void *hm = nullptr, *dm = nullptr;
-    KARMA_TRY(ctx_mapped(c->ctx, 16 * (size_t)W, &hm, &dm));
+    KARMA_TRY(ctx_mapped(c->ctx, kMapCommCounts, 16 * (size_t)W, &hm, &dm));
     int64_t* pin = static_cast<int64_t*>(hm);
     std::memcpy(pin, send_host, 8 * (size_t)W);
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream, static_cast<const uint64_t*>(dm),

@@ -762,7 +762,7 @@ int karma_adj_view_summary(karma_adj* src, const int64_t* order, int64_t k, cons
     constexpr int64_t kMapped = 1 << 20;
     const int64_t cap = with_text ? std::max<int64_t>(0, std::min<int64_t>(text_cap, kMapped - o_text - 16)) : 0;
     void *hbuf = nullptr, *dbuf = nullptr;
-    KARMA_TRY(ctx_mapped(ctx, kMapped, &hbuf, &dbuf));
+    KARMA_TRY(ctx_mapped(ctx, kMapConsumers, kMapped, &hbuf, &dbuf));
     uint8_t* hb = static_cast<uint8_t*>(hbuf);
     uint8_t* db = static_cast<uint8_t*>(dbuf);
     std::memcpy(hb, order, 8 * k);

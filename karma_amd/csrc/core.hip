@@ -128,18 +128,39 @@ int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out) {
     return KARMA_OK;
 }
 
-int ctx_mapped(karma_ctx* ctx, size_t bytes, void** host, void** dev) {
-    if (ctx->mapped_bytes < bytes) {
-        if (ctx->mapped) KARMA_HIP(hipHostFree(ctx->mapped));
-        ctx->mapped = ctx->mapped_dev = nullptr;
-        ctx->mapped_bytes = 0;
-        const size_t want = std::max<size_t>(bytes, 256 * 1024);
-        KARMA_HIP(hipHostMalloc(&ctx->mapped, want, hipHostMallocMapped | hipHostMallocCoherent));
-        ctx->mapped_bytes = want;
+// Slot capacities (bytes, multiples of 256); offsets are their prefix sums.
+static constexpr int64_t kMapCap[kMapSlots] = {
+    int64_t(1) << 20,  // consumers
+    8 * 1024,          // comm scalars: world <= 1024
+    16 * 1024,         // comm counts: world <= 1024
+    16 * 1024 + 256,   // split: nranks <= 1023
+    256,               // merge status
+    256,               // edge status
+    4096,              // step status
+    8 * 1024,          // side communicator scalars
+};
+
+int64_t mapped_slot_bytes(int slot) { return slot >= 0 && slot < kMapSlots ? kMapCap[slot] : 0; }
+
+int64_t mapped_slot_offset(int slot) {
+    int64_t o = 0;
+    for (int s = 0; s < slot && s < kMapSlots; ++s) o += kMapCap[s];
+    return o;
+}
+
+int ctx_mapped(karma_ctx* ctx, int slot, size_t bytes, void** host, void** dev) {
+    KARMA_CHECK(slot >= 0 && slot < kMapSlots, KARMA_ERR_ARG, "mapped slot %d out of range", slot);
+    KARMA_CHECK((int64_t)bytes <= kMapCap[slot], KARMA_ERR_ARG, "mapped slot %d holds %lld bytes, %zu asked", slot,
+                (long long)kMapCap[slot], bytes);
+    if (!ctx->mapped) {  // allocated once, freed with the context
+        const size_t total = (size_t)mapped_slot_offset(kMapSlots);
+        KARMA_HIP(hipHostMalloc(&ctx->mapped, total, hipHostMallocMapped | hipHostMallocCoherent));
+        ctx->mapped_bytes = total;
         KARMA_HIP(hipHostGetDevicePointer(&ctx->mapped_dev, ctx->mapped, 0));
     }
-    *host = ctx->mapped;
-    *dev = ctx->mapped_dev;
+    const int64_t o = mapped_slot_offset(slot);
+    *host = static_cast<uint8_t*>(ctx->mapped) + o;
+    *dev = static_cast<uint8_t*>(ctx->mapped_dev) + o;
     return KARMA_OK;
 }
 
@@ -167,6 +188,16 @@ const char* karma_build_info(void) {
 }
 
 const char* karma_last_error(void) { return g_err.c_str(); }
+
+int karma_mapped_slots(int64_t* offsets, int64_t* bytes, int cap, int* n) {
+    KARMA_CHECK(n && (cap <= 0 || (offsets && bytes)), KARMA_ERR_ARG, "karma_mapped_slots: bad arguments");
+    for (int s = 0; s < kMapSlots && s < cap; ++s) {
+        offsets[s] = mapped_slot_offset(s);
+        bytes[s] = mapped_slot_bytes(s);
+    }
+    *n = kMapSlots;
+    return KARMA_OK;
+}
 
 int karma_device_count(int* n) {
     KARMA_CHECK(n, KARMA_ERR_ARG, "null out");

@@ -170,10 +170,13 @@ __global__ void __launch_bounds__(kET) edges_count_kernel(const uint64_t* __rest
         const uint64_t k = keys[i];
         const uint32_t a = (uint32_t)(k >> 32);
         const bool in_tot = totals && (int64_t)a < n_tot;
-        if (in_tot && i > 0) {
+        if (totals && i > 0) {
             const uint32_t pa = (uint32_t)(keys[i - 1] >> 32);
-            for (uint32_t c = pa + 1; c < a; ++c) totals[c] = 0;  // contigs without keys (none when pa == a)
-            if (pa != a && a != (uint32_t)k) totals[a] = 0;
+            // contigs without keys between the previous contig and this one
+            // (none when pa == a), up to n_tot also when a itself is past it
+            const uint32_t lim = (int64_t)a < n_tot ? a : (uint32_t)n_tot;
+            for (uint32_t c = pa + 1; c < lim; ++c) totals[c] = 0;
+            if (in_tot && pa != a && a != (uint32_t)k) totals[a] = 0;
         } else if (in_tot && a != (uint32_t)k) {
             totals[a] = 0;  // the first contig has no diagonal
         }
@@ -777,7 +780,7 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
     // st (mapped host memory, written by the kernels): [0] unique keys
     // (ReduceByKey's run count), [1] order violation
     void *hst = nullptr, *dst_ = nullptr;
-    KARMA_TRY(ctx_mapped(ctx, 16, &hst, &dst_));
+    KARMA_TRY(ctx_mapped(ctx, kMapMerge, 16, &hst, &dst_));
     std::memset(hst, 0, 16);
     int64_t* const st = static_cast<int64_t*>(dst_);
     void* hpin = nullptr;
@@ -998,7 +1001,7 @@ int karma_pairs_split(karma_pairs* p, const int64_t* bounds, int nranks, int64_t
     // for free CUs, 0.24 ms in the 8-rank emulation)
     const int nb = nranks + 1;
     void *hb = nullptr, *db = nullptr;
-    KARMA_TRY(ctx_mapped(ctx, 2 * nb * 8, &hb, &db));
+    KARMA_TRY(ctx_mapped(ctx, kMapSplit, 2 * nb * 8, &hb, &db));
     int64_t* h = static_cast<int64_t*>(hb);
     int64_t* d = static_cast<int64_t*>(db);
     std::memcpy(h, bounds, nb * 8);
@@ -1016,7 +1019,7 @@ int karma_pairs_split_kc(karma_pairs* p, const int64_t* bounds, int nranks, int6
     KARMA_TRY(ctx_begin(ctx));
     const int nb = nranks + 1;
     void *hb = nullptr, *db = nullptr;
-    KARMA_TRY(ctx_mapped(ctx, 2 * nb * 8, &hb, &db));
+    KARMA_TRY(ctx_mapped(ctx, kMapSplit, 2 * nb * 8, &hb, &db));
     int64_t* h = static_cast<int64_t*>(hb);
     int64_t* d = static_cast<int64_t*>(db);
     std::memcpy(h, bounds, nb * 8);
@@ -1129,7 +1132,7 @@ static int edges_end_impl(karma_edges* e, int64_t* n_edges) {
     // st (mapped host memory, written by the write kernel): 0 zero-division
     // flag, 1 edge count, 2 the list's merge order check
     void *hst = nullptr, *dst_ = nullptr;
-    KARMA_TRY(ctx_mapped(ctx, 24, &hst, &dst_));
+    KARMA_TRY(ctx_mapped(ctx, kMapEdges, 24, &hst, &dst_));
     std::memset(hst, 0, 24);
     int64_t* const st = static_cast<int64_t*>(dst_);
     // edges <= pairs: written before the count is known on the host

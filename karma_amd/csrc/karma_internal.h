@@ -108,8 +108,26 @@ int ctx_begin(karma_ctx* ctx);  // hipSetDevice
 int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int64_t work);
 // Pinned host scratch of >= bytes (valid until the next call on this ctx).
 int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out);
-// Mapped coherent pinned scratch of >= bytes: host and device addresses.
-int ctx_mapped(karma_ctx* ctx, size_t bytes, void** host, void** dev);
+// Mapped coherent pinned host memory that kernels read and write directly.
+// One region per context, allocated once and freed only with the context, cut
+// into fixed per-user slots, so two users never alias (a side-stream
+// collective's scalars beside a main-stream status word, say) and no address
+// handed out is ever freed while a stream may still use it.
+enum MappedSlot : int {
+    kMapConsumers = 0,  // karma_adj_view_summary inputs and results (1 MiB)
+    kMapCommScalar,     // karma_comm_allreduce_host: host scalars (8 x world)
+    kMapCommCounts,     // karma_comm_exchange_counts: sent and received counts (16 x world)
+    kMapSplit,          // karma_pairs_split{,_kc}: bounds and starts (2 x (nranks + 1) x 8)
+    kMapMerge,          // karma_pairs_merge_runs: unique-key count, order flag
+    kMapEdges,          // karma_edges_end: zero-division flag, edge count, order flag
+    kMapStep,           // karma_step: per-step status words (deferred checks)
+    kMapSideScalar,     // the side-stream communicator's host scalars (8 x world)
+    kMapSlots
+};
+// Byte offset and capacity of each slot (karma_ctx_mapped_layout exposes them).
+int64_t mapped_slot_offset(int slot);
+int64_t mapped_slot_bytes(int slot);
+int ctx_mapped(karma_ctx* ctx, int slot, size_t bytes, void** host, void** dev);
 // Pinned scratch owned by the open split graph call (valid until its _end).
 int ctx_job_pinned(karma_ctx* ctx, size_t bytes, void** out);
 // Wrap a launch with HIP events when timing is on.

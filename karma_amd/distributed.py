@@ -69,8 +69,11 @@ class HipOps:
         try:
             plan = self.engine.KmerPlan(self.ctx, store, kmode)
             if comm is not None and comm.world > 1:
-                self.presence_merge(plan, comm.allgather_fixed(self.presence_words(plan)), comm.world)
-                self.set_exceptions(plan, comm.allgather_var(self.exceptions(plan)))
+                # the side stream's own communicator (RcclComm.side): never the
+                # main stream's, whose operations interleave differently per rank
+                sc = getattr(comm, "side", comm)
+                self.presence_merge(plan, sc.allgather_fixed(self.presence_words(plan)), comm.world)
+                self.set_exceptions(plan, sc.allgather_var(self.exceptions(plan)))
             plan.finalize_async()
         finally:
             self.ctx.set_stream(self.stream)

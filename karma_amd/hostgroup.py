@@ -121,10 +121,16 @@ class SocketGroup:
                 except (OSError, ConnectionError):
                     c.close()
                     continue
-                (r,) = struct.unpack("<i", hello[4:])
-                if hello[:4] != _HELLO or not 0 < r < self.world or r in self.peers:
+                if hello[:4] != _HELLO:  # not a karma rank (a stale dialler, a port scan): ignored
                     c.close()
                     continue
+                (r,) = struct.unpack("<i", hello[4:])
+                if not 0 < r < self.world or r in self.peers:
+                    # a karma rank with a rank this job cannot hold: a misconfigured
+                    # launch (two processes with one RANK, or WORLD_SIZE disagreeing)
+                    c.close()
+                    what = "a duplicate" if r in self.peers else f"out of range for world size {self.world}"
+                    raise ConnectionError(f"host group: a rank connected as rank {r}, {what}")
                 c.sendall(_HELLO)
                 c.settimeout(None)
                 self.peers[r] = c
@@ -177,7 +183,10 @@ class SocketGroup:
         mport = int(os.environ.get("MASTER_PORT", "29500"))
         port = int(fixed) if fixed else mport + 1
         handshake = None
-        if not fixed and _is_local(addr):
+        # the port fallback publishes the new port in a local file: only when
+        # every rank runs on this node (a remote rank could not read it)
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        if not fixed and _is_local(addr) and local_world == world:
             run = os.environ.get("TORCHELASTIC_RUN_ID", "none")
             handshake = os.path.join(tempfile.gettempdir(), f"karma_group_{run}_{mport}.port")
         return cls(world, rank, addr, port, timeout=timeout, handshake=handshake)

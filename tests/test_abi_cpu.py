@@ -90,3 +90,23 @@ def test_default_build_is_auditable():
     # no work-removing diagnostic switches in the product kernels
     for p in srcs:
         assert "ABLATE" not in open(p).read(), p
+
+
+def test_mapped_slots_are_distinct():
+    """A context's mapped host region is cut into fixed per-user slots (the
+    comm scalars, the count exchange, the split, the merge and edge status
+    words, the consumers, the step status): none overlaps another, every one is
+    aligned, and the region never has to grow (core.hip ctx_mapped)."""
+    n = ctypes.c_int(0)
+    off = np.zeros(32, np.int64)
+    nb = np.zeros(32, np.int64)
+    _lib.call("karma_mapped_slots", _lib.ptr(off), _lib.ptr(nb), 32, ctypes.byref(n))
+    k = n.value
+    assert k >= 7
+    spans = sorted((int(o), int(o + b)) for o, b in zip(off[:k], nb[:k]))
+    assert all(b > 0 for b in nb[:k])
+    assert all(o % 256 == 0 for o in off[:k])
+    for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+        assert a1 <= b0, "mapped slots overlap"
+    # the users that may run on different streams at once have their own slots
+    assert len(set(off[:k].tolist())) == k

@@ -379,3 +379,61 @@ def test_socket_group_taken_port_fails_fast_without_handshake():
         SocketGroup(2, 0, "127.0.0.1", base, timeout=30)
     assert _t.time() - t0 < 5
     squat.close()
+
+
+def test_socket_group_duplicate_rank_fails_fast():
+    """Two processes launched with the same RANK: rank 0 names the duplicate at
+    once instead of waiting out the connect timeout (a valid hello with a rank
+    the job already holds, or one outside the world size)."""
+    import struct
+    import threading
+    import time as _t
+
+    from karma_amd.hostgroup import _HELLO
+
+    port = free_port()
+    err = []
+
+    def serve():
+        try:
+            SocketGroup(3, 0, "127.0.0.1", port, timeout=30)
+        except ConnectionError as e:
+            err.append(str(e))
+
+    t = threading.Thread(target=serve)
+    t0 = _t.time()
+    t.start()
+    socks = []
+    for r in (1, 1):  # the second hello repeats rank 1
+        while True:
+            try:
+                s = socket.create_connection(("127.0.0.1", port), timeout=5)
+                break
+            except OSError:
+                _t.sleep(0.05)
+        s.sendall(_HELLO + struct.pack("<i", r))
+        socks.append(s)
+    t.join(20)
+    for s in socks:
+        s.close()
+    assert err and "duplicate" in err[0] and "rank 1" in err[0]
+    assert _t.time() - t0 < 10
+
+
+def test_socket_group_port_fallback_only_for_single_node(monkeypatch):
+    """The handshake file (rank 0's fallback port) is local: a job whose ranks
+    are not all on this node keeps the fixed port (LOCAL_WORLD_SIZE < WORLD_SIZE)."""
+    seen = {}
+
+    def fake_init(self, world, rank, addr="127.0.0.1", port=29600, timeout=120.0, handshake=None):
+        seen["handshake"] = handshake
+
+    monkeypatch.setattr(SocketGroup, "__init__", fake_init)
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.delenv("KARMA_GROUP_PORT", raising=False)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    SocketGroup.from_env(8, 1)
+    assert seen["handshake"] is None
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    SocketGroup.from_env(8, 1)
+    assert seen["handshake"] is not None
