@@ -144,8 +144,7 @@ class Leg:
         return self.build.run(self.store, self.rec_dev.ptr, self.A, keep=keep, sequential=sequential, count=count)
 
     def sync_all(self):
-        for c in self.ctxs:
-            c.sync()
+        self.build.sync()  # every enqueued step, deferred checks included, and the contexts
 
     def timed(self, steps, warmup, kernel_timing=True):
         """W untimed steps, an optional per-kernel pass, then K steps bracketed by
@@ -178,19 +177,31 @@ class Leg:
             for c in self.ctxs:
                 c.timing(True, dom)
                 c.timing_reset()
+        from karma_amd import _lib
+
         comm.barrier()
         self.sync_all()
+        calls0 = _lib.api_calls()
+        host = 0.0
         t0 = time.perf_counter()
-        # with an exchange, the owner's edge count of a step is read back only
-        # in the last step (ShardedBuild.run count=False): the other steps end
-        # without waiting for their last kernels, as in a stream of batches;
-        # every kernel still runs, and the device sync below waits for all
+        # a stream of batches: the outputs of every step but the last are not
+        # read (ShardedBuild.run count=False), so in one process a step returns
+        # without waiting for anything (karma_step's deferred path: its checks
+        # arrive through mapped memory, a step needing the general path runs
+        # again synchronously) and with an exchange the owner's edge count is
+        # not read back; every kernel still runs, and the sync below waits for
+        # all of them and checks every step
         for i in range(steps):
+            h0 = time.perf_counter()
             res = self.step(count=i == steps - 1)
+            host += time.perf_counter() - h0
         self.sync_all()
         comm.barrier()
         t1 = time.perf_counter()
         dt = comm.max_float(t1 - t0)
+        self.host_us_per_step = host / steps * 1e6
+        self.api_calls_per_step = (_lib.api_calls() - calls0) / steps
+        self.step_info = self.build.native.info().tolist() if self.build.native is not None else None
         dom_live = None
         if dom:
             for c in self.ctxs:
@@ -337,6 +348,12 @@ def main():
                 "intermediate_bytes_per_launch": intermediate_bytes.get(dom, 0),
                 "avg_launch_ms": round(ms / nl, 4), "launches": nl}
     step_bytes = leg.packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
+    host_us, api_calls = leg.host_us_per_step, leg.api_calls_per_step
+    si = leg.step_info
+    step_driver = ({"native": True, "deferred_steps": si[5], "synchronous_steps": si[4], "rerun_steps": si[6],
+                    "note": "karma_step (csrc/step.hip): one C ABI call per step; host_us_per_step is the time "
+                            "inside those calls, api_calls_per_step the HIP/RCCL calls they made"}
+                   if si else {"native": False})
     step_s = dt / args.steps
     parity = None
     if not args.no_parity:
@@ -398,6 +415,9 @@ def main():
             "step": {"hbm_bytes_per_gpu": step_bytes, "achieved_GBs": round(step_bytes / step_s / 1e9, 1),
                      "frac": round(step_bytes / step_s / 1e9 / PEAK_HBM_GBS, 4),
                      "formula": "sum ceil(L/4) + 8*N*M + 8*A + 16*E + 8*N (SURVEY.md 8(d))"},
+            "host_us_per_step": round(host_us, 1),
+            "api_calls_per_step": round(api_calls, 1),
+            "step_driver": step_driver,
             "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in kern.items()},
             "kernels_ms_note": "sequential pass (profile on the main stream), every launch timed",
             **({"weak": weak} if weak else {}),

@@ -64,6 +64,10 @@ int karma_device_count(int* n);
 /* Layout of a context's mapped host region (diagnostic; no device needed):
  * one fixed slot per user, offsets[s] / bytes[s] for s < min(cap, *n). */
 int karma_mapped_slots(int64_t* offsets, int64_t* bytes, int cap, int* n);
+/* HIP runtime (and RCCL) calls this thread has made through the library that
+ * enqueue work, wait, or manage streams, events and memory (launches, copies,
+ * memsets, event records, stream waits, synchronisations, collectives). */
+int karma_api_calls(uint64_t* n);
 
 /* ---- context: one device, one HIP stream --------------------------------- */
 typedef struct karma_ctx karma_ctx;
@@ -307,6 +311,49 @@ int karma_edges_destroy(karma_edges* e);
 int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* shared, double* weight, uint64_t* first,
                     int is_device);
 int karma_edges_totals(karma_edges* e, int64_t* totals, int is_device);
+
+/* ---- one rank's step of the sharded build ---------------
+ * The whole hot path of one batch on this rank as one call: the records job
+ * (read_graph.py:19-50 via Contig readsets, contig.py:4-35) on a main stream,
+ * the k-mer column table and dense profile (kmer.py:146-264) on a side stream,
+ * and, with several owners, the owners' split, the key/count all-to-all-v, the
+ * owner's merge and the edge stage around the totals all-gather.  Replaces the
+ * Python per-step sequence of karma_amd/distributed.py (which stays for the
+ * host-staged rehearsal transport).
+ * comm: the main-stream communicator (NULL or world 1: one process);
+ * side_comm: the column-set exchange's communicator (KARMA_COMM_SIDE; NULL: comm).
+ * bounds[nranks + 1]: owner contig ranges; this rank's store holds
+ * [bounds[rank], bounds[rank + 1]).  One process with nranks > 1 emulates
+ * rank `rank` of an nranks-rank job (the exchange's local work, no collectives).
+ * The step owns two streams; inputs stay on the device (records: n x {u32 read,
+ * u32 contig}, grouped by read). */
+typedef struct karma_step karma_step;
+#define KARMA_STEP_KEEP 1       /* outputs kept for karma_step_profile / _columns / _edges */
+#define KARMA_STEP_SEQUENTIAL 2 /* every kernel on the main stream (per-kernel timing) */
+#define KARMA_STEP_DEFER 4      /* outputs not read: one process returns without waiting for anything (the
+                                 * step's checks arrive through mapped memory and are read <= 2 steps later;
+                                 * a step needing the general path runs again synchronously); with several
+                                 * ranks the edge count is not read back.  Inputs must stay valid until the
+                                 * next non-deferred step or karma_step_sync. */
+int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, int kmode, int64_t n_glob,
+                      const int64_t* bounds, int nranks, int rank, karma_step** out);
+/* info (may be NULL): [0] M, [1] local edges (-1: not read), [2] local pair list
+ * size, [3] its summed counts (the last two with KARMA_STEP_KEEP, else -1). */
+int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records_dev, int64_t n_records, int flags,
+                   int64_t* info);
+/* Waits for every enqueued step and checks the deferred ones. */
+int karma_step_sync(karma_step* s);
+/* [M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending] (first n). */
+int karma_step_info(karma_step* s, int64_t* info, int n);
+/* Outputs (valid until the next run).  _profile: the newest step's profile
+ * (device, rows x M dense f64; a deferred step's once karma_step_sync has read
+ * its column count).  _columns and _edges: the last KARMA_STEP_KEEP step's
+ * column keys and edges (owned by the step: read with karma_edges_get /
+ * _totals, never destroyed). */
+int karma_step_profile(karma_step* s, double** dev, int64_t* rows, int64_t* M);
+int karma_step_columns(karma_step* s, uint64_t* keys_host);
+int karma_step_edges(karma_step* s, karma_edges** e);
+int karma_step_destroy(karma_step* s);
 
 /* ---- synthetic inputs (spec in karma_amd/synth.py) ------- */
 int karma_synth_contig_lengths(uint64_t seed, int64_t n, int32_t len_min, int32_t len_span, int64_t* lengths);

@@ -38,6 +38,7 @@ KARMA_REC_SORTED = 0
 KARMA_REC_UNSORTED = 1
 KARMA_MODE_READS = 0
 KARMA_MODE_EQ = 1
+KARMA_STEP_KEEP, KARMA_STEP_SEQUENTIAL, KARMA_STEP_DEFER = 1, 2, 4
 
 _c_p = ctypes.c_void_p
 _i64 = ctypes.c_int64
@@ -125,6 +126,15 @@ _SIGS = {
     "karma_edges_destroy": [_c_p],
     "karma_edges_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _i32],
     "karma_edges_totals": [_c_p, _c_p, _i32],
+    "karma_api_calls": [_c_p],
+    "karma_step_create": [_c_p, _c_p, _c_p, _i32, _i64, _c_p, _i32, _i32, _PP],
+    "karma_step_run": [_c_p, _c_p, _c_p, _i64, _i32, _c_p],
+    "karma_step_sync": [_c_p],
+    "karma_step_info": [_c_p, _c_p, _i32],
+    "karma_step_profile": [_c_p, _PP, _I64P, _I64P],
+    "karma_step_columns": [_c_p, _c_p],
+    "karma_step_edges": [_c_p, _PP],
+    "karma_step_destroy": [_c_p],
     "karma_synth_contig_lengths": [_u64, _i64, _i32, _i32, _c_p],
     "karma_synth_contig_bases": [_u64, _c_p, _i64, _i32, _c_p],
     "karma_synth_n_genes": [_u64, _i64, _i32, _I64P],
@@ -401,6 +411,13 @@ class DevBuf:
             self.close()
         except Exception:
             pass
+
+
+def api_calls():
+    """HIP runtime (and RCCL) calls this thread has made through the library (karma_api_calls)."""
+    n = ctypes.c_uint64(0)
+    call("karma_api_calls", ctypes.byref(n))
+    return n.value
 
 
 def dtype_code(dtype):

@@ -34,6 +34,7 @@ namespace {
 
 #define KARMA_NCCL(expr)                                                                                \
     do {                                                                                                \
+        ++::karma::t_hip_calls;                                                                         \
         ncclResult_t _r = (expr);                                                                       \
         if (_r != ncclSuccess) {                                                                        \
             ::karma::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr, ncclGetErrorString(_r));    \
@@ -187,10 +188,12 @@ int karma_comm_allreduce_host(karma_comm* c, void* buf_host, int64_t count, int 
     void *hm = nullptr, *dm = nullptr;
     KARMA_TRY(ctx_mapped(c->ctx, c->scalar_slot, (size_t)words * 8, &hm, &dm));
     std::memcpy(hm, buf_host, bytes);
+    ++t_hip_calls;
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream, static_cast<const uint64_t*>(dm),
                        reinterpret_cast<uint64_t*>(c->scratch), words);
     KARMA_HIP(hipGetLastError());
     KARMA_NCCL(ncclAllReduce(c->scratch, c->scratch, (size_t)count, t, o, c->nc, c->ctx->stream));
+    ++t_hip_calls;
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream,
                        reinterpret_cast<const uint64_t*>(c->scratch), static_cast<uint64_t*>(dm), words);
     KARMA_HIP(hipGetLastError());
@@ -221,6 +224,7 @@ int karma_comm_exchange_counts(karma_comm* c, const int64_t* send_host, int64_t*
     KARMA_TRY(ctx_mapped(c->ctx, kMapCommCounts, 16 * (size_t)W, &hm, &dm));
     int64_t* pin = static_cast<int64_t*>(hm);
     std::memcpy(pin, send_host, 8 * (size_t)W);
+    ++t_hip_calls;
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream, static_cast<const uint64_t*>(dm),
                        reinterpret_cast<uint64_t*>(c->counts_dev), W);
     KARMA_HIP(hipGetLastError());
@@ -233,6 +237,7 @@ int karma_comm_exchange_counts(karma_comm* c, const int64_t* send_host, int64_t*
         }
         KARMA_TRY(group_rc(g.end(), g));
     }
+    ++t_hip_calls;
     hipLaunchKernelGGL(copy_words_kernel, dim3(1), dim3(64), 0, c->ctx->stream,
                        reinterpret_cast<const uint64_t*>(c->counts_dev + W), static_cast<uint64_t*>(dm) + W, W);
     KARMA_HIP(hipGetLastError());

@@ -29,7 +29,6 @@
 // and the --rearrange aggregation (karma.py:103-118):
 //   karma_adj_cross_sums  per subcluster pair (A, B), A < B, the edge weights
 //                         between them summed in product(nodes_A, nodes_B) order.
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -578,12 +577,7 @@ __global__ void __launch_bounds__(kSumT) view_summary_kernel(
 }
 
 int scan_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
-    size_t tb = 0;
-    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, ctx->stream));
-    DevArray<uint8_t> tmp;
-    KARMA_TRY(tmp.alloc(ctx, tb ? tb : 1));
-    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.ptr, tb, in, out, n, ctx->stream));
-    return KARMA_OK;
+    return scan_excl_i64(ctx, in, out, n);  // one look-back launch (sort.hip)
 }
 
 int read_i64(karma_ctx* ctx, const int64_t* dev, int64_t* host) {
@@ -658,15 +652,7 @@ int karma_adj_from_edges(karma_ctx* ctx, int64_t n, const uint32_t* ids, const u
         KARMA_LAUNCH(ctx, "adj_edge_entries", edge_entries_kernel, grid_of(n_edges), 256, 0, da.ptr, db.ptr, n_edges,
                      slot.ptr, key.ptr, val.ptr, bad.ptr, (uint32_t)n);
     KARMA_TRY(check_flag(ctx, bad.ptr, "edge endpoint >= n"));
-    if (m) {
-        size_t tb = 0;
-        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.ptr, key2.ptr, val.ptr, val2.ptr, (int)m, 0, 64,
-                                                     ctx->stream));
-        DevArray<uint8_t> tmp;
-        KARMA_TRY(tmp.alloc(ctx, tb ? tb : 1));
-        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, key.ptr, key2.ptr, val.ptr, val2.ptr, (int)m, 0, 64,
-                                                     ctx->stream));
-    }
+    if (m) KARMA_TRY(radix_sort_u64(ctx, key.ptr, val.ptr, m, 64, key2.ptr, val2.ptr));  // stable (sort.hip)
     KARMA_TRY(cnt.alloc(ctx, n + 1));
     KARMA_HIP(hipMemsetAsync(cnt.ptr, 0, (n + 1) * 8, ctx->stream));
     KARMA_TRY(g->nbr.alloc(ctx, m ? m : 1));
@@ -975,19 +961,10 @@ int karma_adj_cross_sums(karma_adj* g, const int32_t* sub, const int32_t* rank, 
     KARMA_LAUNCH(ctx, "adj_cross_fill", cross_fill_kernel, grid_of(n), 256, 0, g->off.ptr, g->nbr.ptr, g->w.ptr, n,
                  dsub.ptr, drank.ptr, start.ptr, pk.ptr, ik.ptr, ew.ptr);
     KARMA_LAUNCH(ctx, "adj_iota", iota_u32_kernel, grid_of(m), 256, 0, idx.ptr, m);
-    // LSD: by the in-pair key, then stably by (A, B)
-    size_t tb = 0, tb2 = 0;
-    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ik.ptr, k1.ptr, idx.ptr, idx2.ptr, (int)m, 0, 64,
-                                                 ctx->stream));
-    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, k2.ptr, k1.ptr, idx2.ptr, idx3.ptr, (int)m, 0, 64,
-                                                 ctx->stream));
-    DevArray<uint8_t> tmp;
-    KARMA_TRY(tmp.alloc(ctx, std::max<size_t>(1, std::max(tb, tb2))));
-    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, ik.ptr, k1.ptr, idx.ptr, idx2.ptr, (int)m, 0, 64,
-                                                 ctx->stream));
+    // LSD: by the in-pair key, then stably by (A, B) (the library's radix sort, sort.hip)
+    KARMA_TRY(radix_sort_u64(ctx, ik.ptr, idx.ptr, m, 64, k1.ptr, idx2.ptr));
     KARMA_LAUNCH(ctx, "adj_cross_gather", gather_u64_kernel, grid_of(m), 256, 0, idx2.ptr, m, pk.ptr, k2.ptr);
-    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb2, k2.ptr, k1.ptr, idx2.ptr, idx3.ptr, (int)m, 0, 64,
-                                                 ctx->stream));
+    KARMA_TRY(radix_sort_u64(ctx, k2.ptr, idx2.ptr, m, 64, k1.ptr, idx3.ptr));
     DevArray<int64_t> head, seg;
     KARMA_TRY(head.alloc(ctx, m + 1));
     KARMA_TRY(seg.alloc(ctx, m + 1));

@@ -8,6 +8,7 @@
 namespace karma {
 
 static thread_local std::string g_err;
+thread_local uint64_t t_hip_calls = 0;
 
 void set_error(const char* fmt, ...) {
     char buf[1024];
@@ -188,6 +189,12 @@ const char* karma_build_info(void) {
 }
 
 const char* karma_last_error(void) { return g_err.c_str(); }
+
+int karma_api_calls(uint64_t* n) {
+    KARMA_CHECK(n, KARMA_ERR_ARG, "null out");
+    *n = t_hip_calls;
+    return KARMA_OK;
+}
 
 int karma_mapped_slots(int64_t* offsets, int64_t* bytes, int cap, int* n) {
     KARMA_CHECK(n && (cap <= 0 || (offsets && bytes)), KARMA_ERR_ARG, "karma_mapped_slots: bad arguments");

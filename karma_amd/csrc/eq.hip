@@ -10,7 +10,7 @@
 //   1. eq_count    one thread per class (a block per class above kSmallM
 //                  members): totals (u64 atomics), the class's pair count,
 //                  and per contig a the number of pairs whose lower id is a;
-//   2. two exclusive scans (hand-written, scan_i64_device): class pair
+//   2. two exclusive scans (single-launch look-back, sort.hip): class pair
 //      offsets (first-emission indices) and contig segment offsets;
 //   3. eq_scatter  the same walk writes every pair into the segment of its
 //                  lower contig: a counting sort by a, no comparisons;
@@ -37,7 +37,6 @@ constexpr int64_t kSmallM = 32;  // classes above this size: a block each
 constexpr int kRT = 512;         // seg_reduce threads
 constexpr int kSeg = 2048;       // target entries per seg_reduce block
 constexpr int kSegCap = 2 * kSeg;  // LDS capacity of one block's run (runs snap to segment starts)
-constexpr int kScanT = 256, kScanItems = 16, kScanTile = kScanT * kScanItems;
 
 // pair t (combinations order) of a class of m members -> (i, j), i < j:
 // row i holds (i, i+1..m-1); pairs before row i: i*m - i*(i+1)/2
@@ -341,61 +340,6 @@ __global__ void __launch_bounds__(kRT) seg_compact_kernel(const int64_t* __restr
     }
 }
 
-// ---- exclusive scan (n items, int64 out) ---------------------------------------------
-template <typename T>
-__global__ void __launch_bounds__(kScanT) scan_tile_sums_kernel(const T* __restrict__ in, int64_t n,
-                                                                int64_t* __restrict__ sums) {
-    __shared__ int64_t lds_w[kScanT / 64];
-    const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
-    int64_t v = 0;
-    for (int i = 0; i < kScanItems; ++i) {
-        const int64_t p = t0 + (int64_t)i * kScanT + threadIdx.x;
-        if (p < n) v += (int64_t)in[p];
-    }
-    int64_t tot;
-    block_scan_excl<kScanT>(v, lds_w, &tot);
-    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
-}
-
-// one block: exclusive scan of the tile sums in place
-__global__ void __launch_bounds__(kScanT) scan_tops_kernel(int64_t* __restrict__ sums, int64_t n_tiles) {
-    __shared__ int64_t lds_w[kScanT / 64];
-    int64_t carry = 0;
-    for (int64_t c0 = 0; c0 < n_tiles; c0 += kScanT) {
-        const int64_t p = c0 + threadIdx.x;
-        const int64_t v = p < n_tiles ? sums[p] : 0;
-        int64_t tot;
-        const int64_t x = block_scan_excl<kScanT>(v, lds_w, &tot);
-        if (p < n_tiles) sums[p] = carry + x;
-        carry += tot;
-    }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(kScanT) scan_apply_kernel(const T* __restrict__ in, int64_t n,
-                                                            const int64_t* __restrict__ sums,
-                                                            int64_t* __restrict__ out) {
-    __shared__ int64_t lds_w[kScanT / 64];
-    const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
-    // thread t holds items t0 + t * kScanItems .. + kScanItems - 1 (contiguous)
-    int64_t v[kScanItems];
-    int64_t s = 0;
-#pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        const int64_t p = t0 + (int64_t)threadIdx.x * kScanItems + i;
-        v[i] = p < n ? (int64_t)in[p] : 0;
-        s += v[i];
-    }
-    int64_t tot;
-    int64_t x = block_scan_excl<kScanT>(s, lds_w, &tot) + (sums ? sums[blockIdx.x] : 0);
-#pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        const int64_t p = t0 + (int64_t)threadIdx.x * kScanItems + i;
-        if (p < n) out[p] = x;
-        x += v[i];
-    }
-}
-
 int grid_of(int64_t n, int block) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(karma::ceil_div(n, block), 1 << 20));
 }
@@ -404,27 +348,15 @@ int grid_of(int64_t n, int block) {
 
 namespace karma {
 
-// out[i] = in[0] + ... + in[i - 1] for i < n (hand-written: one launch up to
-// kScanTile items, three above)
-template <typename T>
-int scan_excl_device(karma_ctx* ctx, const T* in, int64_t* out, int64_t n, DevArray<int64_t>& sums) {
-    if (n <= 0) return KARMA_OK;
-    const int64_t tiles = ceil_div(n, kScanTile);
-    if (tiles == 1) {
-        KARMA_LAUNCH(ctx, "scan", scan_apply_kernel<T>, 1, kScanT, 0, in, n, (const int64_t*)nullptr, out);
-        return KARMA_OK;
-    }
-    KARMA_TRY(sums.alloc(ctx, tiles));
-    KARMA_LAUNCH(ctx, "scan", scan_tile_sums_kernel<T>, tiles, kScanT, 0, in, n, sums.ptr);
-    KARMA_LAUNCH(ctx, "scan", scan_tops_kernel, 1, kScanT, 0, sums.ptr, tiles);
-    KARMA_LAUNCH(ctx, "scan", scan_apply_kernel<T>, tiles, kScanT, 0, in, n, (const int64_t*)sums.ptr, out);
-    return KARMA_OK;
+// out[i] = in[0] + ... + in[i - 1] for i < n: the single-launch look-back
+// scans of sort.hip
+int scan_excl_device(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, DevArray<int64_t>&) {
+    return scan_excl_i64(ctx, in, out, n);
+}
+int scan_excl_device(karma_ctx* ctx, const uint32_t* in, int64_t* out, int64_t n, DevArray<int64_t>&) {
+    return scan_excl_u32(ctx, in, out, n);
 }
 
-int scan_i64_device(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
-    DevArray<int64_t> sums;
-    return scan_excl_device(ctx, in, out, n, sums);
-}
 
 }  // namespace karma
 

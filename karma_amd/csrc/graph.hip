@@ -11,9 +11,6 @@
 // pipeline (the hot one) is graph_sets.hip.  The diagonal (a, a) of a pair
 // list counts |readset(a)| (the normaliser), so one mechanism yields both the
 // shared counts and the totals.
-#include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_merge.hpp>
-
 #include <algorithm>
 #include <cstring>
 #include <memory>
@@ -49,26 +46,6 @@ namespace {
 
 
 // ---- generic sort + reduce (low-volume paths) ----------------------------------
-__global__ void iota_kernel(uint32_t* __restrict__ v, int64_t n) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) v[i] = (uint32_t)i;
-}
-
-__global__ void gather_kernel(const uint32_t* __restrict__ idx, const int64_t* __restrict__ c_in,
-                              const uint64_t* __restrict__ f_in, int64_t n, int64_t* __restrict__ c_out,
-                              uint64_t* __restrict__ f_out) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const uint32_t j = idx[i];
-        c_out[i] = c_in ? c_in[j] : 1;
-        if (f_out) f_out[i] = f_in ? f_in[j] : (uint64_t)j;
-    }
-}
-
-struct MinOp {
-    __device__ __forceinline__ uint64_t operator()(const uint64_t& a, const uint64_t& b) const { return a < b ? a : b; }
-};
-
 // ---- finalize --------------------------------------------------------------------
 // A list may hold runs of equal adjacent keys (karma_pairs::dups): the first
 // element of a run stands for it, with the run's summed count.  On a sorted
@@ -330,23 +307,6 @@ __global__ void deinterleave_kc_kernel(const longlong2* __restrict__ kc, int64_t
     }
 }
 
-// keys sorted within each run [off[r], off[r + 1]): a descent is allowed only
-// where a run starts
-__global__ void runs_check_kernel(const uint64_t* __restrict__ k, int64_t n, const int64_t* __restrict__ off, int nr,
-                                  int64_t* __restrict__ bad) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (k[i] <= k[i + 1]) continue;
-        int lo = 0, hi = nr;  // off[lo] <= i + 1 < off[hi]
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (off[mid] <= i + 1) lo = mid;
-            else hi = mid;
-        }
-        if (off[lo] != i + 1) *bad = 1;
-    }
-}
-
-
 // ---- owner merge of W sorted runs: one ranking pass ------------------------------
 // Element j of run r (key k) lands at j + sum over the other runs s of the
 // number of their elements that precede it: < k for s > r, <= k for s < r
@@ -536,52 +496,26 @@ int sort_reduce_pairs(karma_ctx* ctx, const uint64_t* keys_in, const int64_t* co
         *n_out = 0;
         return KARMA_OK;
     }
+    // the library's radix sort (sort.hip) with the input positions as values,
+    // then one reduce-by-key pass through that permutation
     DevArray<uint64_t> ks;
-    DevArray<uint32_t> idx, idx_s;
-    DevArray<int64_t> cs;
-    DevArray<uint64_t> fs;
+    DevArray<uint32_t> perm;
     KARMA_TRY(ks.alloc(ctx, n));
-    KARMA_TRY(idx.alloc(ctx, n));
-    KARMA_TRY(idx_s.alloc(ctx, n));
-    KARMA_TRY(cs.alloc(ctx, n));
-    if (first_out) KARMA_TRY(fs.alloc(ctx, n));
-    KARMA_LAUNCH(ctx, "iota", iota_kernel, grid1(n), 256, 0, idx.ptr, n);
-    size_t tb = 0;
-    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys_in, ks.ptr, idx.ptr, idx_s.ptr, (int)n, 0, key_bits,
-                                                 ctx->stream));
-    DevArray<uint8_t> tmp;
-    KARMA_TRY(tmp.alloc(ctx, tb));
-    KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, keys_in, ks.ptr, idx.ptr, idx_s.ptr, (int)n, 0, key_bits,
-                                                 ctx->stream));
-    KARMA_LAUNCH(ctx, "gather", gather_kernel, grid1(n), 256, 0, idx_s.ptr, counts_in, first_in, n, cs.ptr,
-                 first_out ? fs.ptr : (uint64_t*)nullptr);
-    DevArray<uint64_t> uk;
+    KARMA_TRY(perm.alloc(ctx, n));
+    KARMA_TRY(radix_sort_u64(ctx, keys_in, nullptr, n, key_bits, ks.ptr, perm.ptr));
+    DevArray<uint64_t> uk, uf;
     DevArray<int64_t> uc, nruns;
     KARMA_TRY(uk.alloc(ctx, n));
     KARMA_TRY(uc.alloc(ctx, n));
+    if (first_out) KARMA_TRY(uf.alloc(ctx, n));
     KARMA_TRY(nruns.alloc(ctx, 1));
-    size_t tb2 = 0;
-    KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb2, ks.ptr, uk.ptr, cs.ptr, uc.ptr, nruns.ptr,
-                                                hipcub::Sum(), (int)n, ctx->stream));
-    DevArray<uint8_t> tmp2;
-    KARMA_TRY(tmp2.alloc(ctx, tb2));
-    KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(tmp2.ptr, tb2, ks.ptr, uk.ptr, cs.ptr, uc.ptr, nruns.ptr,
-                                                hipcub::Sum(), (int)n, ctx->stream));
-    DevArray<uint64_t> uf, uk2;
-    if (first_out) {
-        KARMA_TRY(uf.alloc(ctx, n));
-        KARMA_TRY(uk2.alloc(ctx, n));
-        size_t tb3 = 0;
-        KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb3, ks.ptr, uk2.ptr, fs.ptr, uf.ptr, nruns.ptr, MinOp(),
-                                                    (int)n, ctx->stream));
-        DevArray<uint8_t> tmp3;
-        KARMA_TRY(tmp3.alloc(ctx, tb3));
-        KARMA_HIP(hipcub::DeviceReduce::ReduceByKey(tmp3.ptr, tb3, ks.ptr, uk2.ptr, fs.ptr, uf.ptr, nruns.ptr,
-                                                    MinOp(), (int)n, ctx->stream));
-    }
-    int64_t U = 0;
-    KARMA_HIP(hipMemcpyAsync(&U, nruns.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_TRY(reduce_sorted(ctx, ks.ptr, perm.ptr, counts_in, first_in, n, uk.ptr, uc.ptr,
+                            first_out ? uf.ptr : nullptr, nruns.ptr));
+    int64_t* hp = nullptr;
+    KARMA_TRY(ctx_pinned(ctx, 8, reinterpret_cast<void**>(&hp)));
+    KARMA_HIP(hipMemcpyAsync(hp, nruns.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    const int64_t U = *hp;
     KARMA_TRY(keys_out.alloc(ctx, U));
     KARMA_TRY(counts_out.alloc(ctx, U));
     KARMA_HIP(hipMemcpyAsync(keys_out.ptr, uk.ptr, U * 8, hipMemcpyDeviceToDevice, ctx->stream));
@@ -633,13 +567,8 @@ int karma_graph_records_begin(karma_ctx* ctx, const uint32_t* records, int64_t A
         if ((rc = rid.alloc(ctx, A)) || (rc = cid.alloc(ctx, A)) || (rc = rid2.alloc(ctx, A)) ||
             (rc = cid2.alloc(ctx, A))) return rc;
         KARMA_LAUNCH(ctx, "deinterleave", deinterleave_kernel, grid1(A), 256, 0, own.ptr, A, rid.ptr, cid.ptr);
-        size_t tb = 0;
-        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, rid.ptr, rid2.ptr, cid.ptr, cid2.ptr, (int)A, 0, 32,
-                                                     ctx->stream));
-        DevArray<uint8_t> tmp;
-        if ((rc = tmp.alloc(ctx, tb))) return rc;
-        KARMA_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.ptr, tb, rid.ptr, rid2.ptr, cid.ptr, cid2.ptr, (int)A, 0, 32,
-                                                     ctx->stream));
+        // grouped by read: the library's radix sort on the read ids (sort.hip)
+        if ((rc = radix_sort_u32(ctx, rid.ptr, cid.ptr, A, 32, rid2.ptr, cid2.ptr))) return rc;
         KARMA_LAUNCH(ctx, "interleave", interleave_kernel, grid1(A), 256, 0, rid2.ptr, cid2.ptr, A, own.ptr);
     }
     if (reinterpret_cast<uintptr_t>(rec) & 15) {  // the set pipeline streams 16-byte loads
@@ -783,8 +712,6 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
     KARMA_TRY(ctx_mapped(ctx, kMapMerge, 16, &hst, &dst_));
     std::memset(hst, 0, 16);
     int64_t* const st = static_cast<int64_t*>(dst_);
-    void* hpin = nullptr;
-    KARMA_TRY(ctx_pinned(ctx, std::max<size_t>(16, (n_runs + 1) * 8), &hpin));
     if (n_runs <= kMergeMaxRuns) {
         // one ranking pass into merged order (reads the interleaved wire format directly)
         RunOffs R{};
@@ -826,6 +753,8 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
         sk = kb[0].ptr;
         sc = cb[0].ptr;
     } else {
+        // more than kMergeMaxRuns runs: the ranking merge on groups of up to
+        // kMergeMaxRuns consecutive runs, level by level, ping-pong buffers
         if (kc && n) {  // interleaved device input: split once into the merge's first buffers
             KARMA_TRY(kb[1].alloc(ctx, n));
             KARMA_TRY(cb[1].alloc(ctx, n));
@@ -834,61 +763,49 @@ static int merge_runs_impl(karma_ctx* ctx, const uint64_t* keys, const int64_t* 
             sk = kb[1].ptr;
             sc = cb[1].ptr;
         }
-        DevArray<int64_t> doff;
-        KARMA_TRY(doff.alloc(ctx, n_runs + 1));
-        std::memcpy(hpin, off.data(), (n_runs + 1) * 8);
-        KARMA_HIP(hipMemcpyAsync(doff.ptr, hpin, (n_runs + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-        if (n > 1)
-            KARMA_LAUNCH(ctx, "runs_check", runs_check_kernel, std::min<int64_t>(grid1(n), 4096), 256, 0, sk, n, doff.ptr,
-                         n_runs, st + 1);
-        // pairwise merge tree over the runs (rocprim merge path), ping-pong buffers
-        if (n_runs > 1 && n) {
-            size_t need = 0;
-            for (std::vector<int64_t> o = off; o.size() > 2;) {  // plan: the largest temporary
-                std::vector<int64_t> next{0};
-                for (size_t j = 0; j + 1 < o.size(); j += 2) {
-                    if (j + 2 < o.size() && o[j + 1] > o[j] && o[j + 2] > o[j + 1]) {
-                        size_t tb = 0;
-                        KARMA_HIP(rocprim::merge(nullptr, tb, sk, sk, (uint64_t*)nullptr, sc, sc, (int64_t*)nullptr,
-                                                 (size_t)(o[j + 1] - o[j]), (size_t)(o[j + 2] - o[j + 1]),
-                                                 rocprim::less<uint64_t>(), ctx->stream));
-                        need = std::max(need, tb);
-                    }
-                    next.push_back(o[std::min(j + 2, o.size() - 1)]);
+        KARMA_TRY(kb[0].alloc(ctx, n));
+        KARMA_TRY(cb[0].alloc(ctx, n));
+        if (!kb[1].ptr) {
+            KARMA_TRY(kb[1].alloc(ctx, n));
+            KARMA_TRY(cb[1].alloc(ctx, n));
+        }
+        DevArray<int64_t> scratch;  // merge_bounds_kernel clears its flag word: a throwaway one here
+        KARMA_TRY(scratch.alloc(ctx, 1));
+        int dst = 0;
+        for (std::vector<int64_t> o = off; o.size() > 2; dst ^= 1) {
+            const int nr_all = (int)o.size() - 1;
+            std::vector<int64_t> next{0};
+            for (int g0 = 0; g0 < nr_all; g0 += kMergeMaxRuns) {
+                const int g1 = std::min(nr_all, g0 + kMergeMaxRuns);
+                const int64_t base = o[g0], len = o[g1] - base;
+                next.push_back(o[g1]);
+                if (!len) continue;
+                if (g1 - g0 == 1) {  // a lone run: carried over
+                    KARMA_HIP(hipMemcpyAsync(kb[dst].ptr + base, sk + base, len * 8, hipMemcpyDeviceToDevice,
+                                             ctx->stream));
+                    KARMA_HIP(hipMemcpyAsync(cb[dst].ptr + base, sc + base, len * 8, hipMemcpyDeviceToDevice,
+                                             ctx->stream));
+                    continue;
                 }
-                o.swap(next);
-            }
-            DevArray<uint8_t> tmp;
-            KARMA_TRY(tmp.alloc(ctx, std::max<size_t>(need, 1)));
-            KARMA_TRY(kb[0].alloc(ctx, n));
-            KARMA_TRY(cb[0].alloc(ctx, n));
-            if (!kb[1].ptr) {
-                KARMA_TRY(kb[1].alloc(ctx, n));
-                KARMA_TRY(cb[1].alloc(ctx, n));
-            }
-            int dst = 0;
-            for (std::vector<int64_t> o = off; o.size() > 2; dst ^= 1) {
-                std::vector<int64_t> next{0};
-                for (size_t j = 0; j + 1 < o.size(); j += 2) {
-                    const int64_t a0 = o[j], a1 = o[j + 1];
-                    const int64_t a2 = j + 2 < o.size() ? o[j + 2] : a1;
-                    if (a1 > a0 && a2 > a1) {  // two non-empty runs (an empty merge would launch an empty grid)
-                        size_t tb = need;
-                        KARMA_HIP(rocprim::merge(tmp.ptr, tb, sk + a0, sk + a1, kb[dst].ptr + a0, sc + a0, sc + a1,
-                                                 cb[dst].ptr + a0, (size_t)(a1 - a0), (size_t)(a2 - a1),
-                                                 rocprim::less<uint64_t>(), ctx->stream));
-                    } else if (a2 > a0) {  // one run (odd one out, or its partner is empty): carried over
-                        KARMA_HIP(hipMemcpyAsync(kb[dst].ptr + a0, sk + a0, (a2 - a0) * 8, hipMemcpyDeviceToDevice,
-                                                 ctx->stream));
-                        KARMA_HIP(hipMemcpyAsync(cb[dst].ptr + a0, sc + a0, (a2 - a0) * 8, hipMemcpyDeviceToDevice,
-                                                 ctx->stream));
-                    }
-                    next.push_back(o[std::min(j + 2, o.size() - 1)]);
+                RunOffs R{};
+                const int nr = g1 - g0;
+                int64_t tiles = 0;
+                for (int r = 0; r <= nr; ++r) R.o[r] = o[g0 + r] - base;
+                for (int r = 0; r < nr; ++r) {
+                    R.t[r] = tiles;
+                    tiles += ceil_div(R.o[r + 1] - R.o[r], kMergeTile);
                 }
-                o.swap(next);
-                sk = kb[dst].ptr;
-                sc = cb[dst].ptr;
+                R.t[nr] = tiles;
+                DevArray<int64_t> wb;
+                KARMA_TRY(wb.alloc(ctx, tiles * nr * 2));
+                KARMA_LAUNCH(ctx, "merge_bounds", merge_bounds_kernel, ceil_div(tiles * nr * 2, 256 / kMG), 256, 0,
+                             sk + base, (const longlong2*)nullptr, R, nr, tiles, wb.ptr, scratch.ptr);
+                KARMA_LAUNCH(ctx, "merge_rank", merge_rank_kernel, tiles, 256, 0, sk + base, sc + base,
+                             (const longlong2*)nullptr, R, nr, wb.ptr, kb[dst].ptr + base, cb[dst].ptr + base, st + 1);
             }
+            o.swap(next);
+            sk = kb[dst].ptr;
+            sc = cb[dst].ptr;
         }
     }
     // equal keys (from different runs, or repeated in one) are now adjacent
@@ -1158,6 +1075,21 @@ static int edges_end_impl(karma_edges* e, int64_t* n_edges) {
     return KARMA_OK;
 }
 
+}  // extern "C"
+
+namespace karma {
+// karma_step: the device address of a pending edge stage's three status words
+// (zero-total flag, edge count, merge order), which the caller copies out in
+// stream order and checks later; the edges are then no longer pending.
+const int64_t* edges_take_pending(karma_edges* e) {
+    if (!e || !e->pending) return nullptr;
+    e->pending = false;
+    return e->blk.ptr + e->n_blk;
+}
+}  // namespace karma
+
+extern "C" {
+
 int karma_edges_from_pairs(karma_ctx* ctx, karma_pairs* p, int mode, const int64_t* totals_dev, int64_t N,
                            karma_edges** out, int64_t* n_edges) {
     KARMA_CHECK(out && n_edges, KARMA_ERR_ARG, "karma_edges_from_pairs: bad arguments");
@@ -1185,11 +1117,19 @@ int karma_edges_count(karma_edges* e, int64_t* n_edges) {
     return KARMA_OK;
 }
 
+// An edge stage still pending (karma_edges_end without a count) has its
+// zero-total and merge-order words unread: they are read here (one wait) and
+// an error is reported on stderr and returned, not dropped.
 int karma_edges_destroy(karma_edges* e) {
     if (!e) return KARMA_OK;
     hipSetDevice(e->ctx->device);
+    int rc = KARMA_OK;
+    if (e->pending) {
+        rc = edges_resolve(e);
+        if (rc) std::fprintf(stderr, "karma_edges_destroy: a deferred edge stage reported: %s\n", karma_last_error());
+    }
     delete e;
-    return KARMA_OK;
+    return rc;
 }
 
 int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, double* w, uint64_t* first, int is_device) {

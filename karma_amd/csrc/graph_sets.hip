@@ -32,7 +32,6 @@
 //   big reads   (> 8 records): separate generic path, merged at the end.
 // Device-side counters size every grid-stride loop, so the common path has
 // one host synchronisation (flags, overflow, output size) at the end.
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -1718,9 +1717,6 @@ __global__ void assemble2_kernel(const uint64_t* __restrict__ base_k, const int6
 
 int grid_n(int64_t n, int block = 256) { return (int)std::max<int64_t>(1, ceil_div(n, block)); }
 
-int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
-    return karma::scan_i64_device(ctx, in, out, n);  // hand-written (eq.hip): one launch up to 4096 items
-}
 
 
 }  // namespace
@@ -2083,6 +2079,7 @@ struct SetsJob {
     DevArray<int64_t> slot_c;
     RunDir pdir{};
     int attempt = 0;
+    bool deferred = false;                  // no control-block readback (sets_begin_deferred)
     bool relabeled = false;                 // a relabelled rerun (see relabel_probe_kernel)
     DevArray<uint32_t> remap_map, remap_inv;  // new id by old id, old id by new id
 
@@ -2128,9 +2125,11 @@ int SetsJob::setup() {
     dst = n_per + (B + 1);
     ovf = reinterpret_cast<uint8_t*>(dst + (B + 1));
     split_loc = dst + (B + 1) + ceil_div(B, 8);
-    void* hpin = nullptr;
-    KARMA_TRY(ctx_job_pinned(ctx, ctrl_words * 8, &hpin));
-    hctrl = static_cast<const int64_t*>(hpin);
+    if (!deferred) {
+        void* hpin = nullptr;
+        KARMA_TRY(ctx_job_pinned(ctx, ctrl_words * 8, &hpin));
+        hctrl = static_cast<const int64_t*>(hpin);
+    }
     // code stream: <= one code per record + < 8 padding codes per run; a block
     // flushes only a full buffer, and once at its end
     max_cflush = n_pblk + ceil_div(A, CodeStream::kCap) + 1;
@@ -2297,8 +2296,9 @@ int SetsJob::launch() {
                      g.bwc, part_b.ptr, part_ch.ptr, part_k.ptr, part_c.ptr, part_n.ptr, slot_k.ptr, slot_c.ptr, n_per,
                      ovf, sa, lb, dst);
     KARMA_TRY(mark(5));  // after the final kernel, before the control-block readback
-    KARMA_HIP(hipMemcpyAsync(const_cast<int64_t*>(hctrl), ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost,
-                             ctx->stream));
+    if (!deferred)
+        KARMA_HIP(hipMemcpyAsync(const_cast<int64_t*>(hctrl), ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost,
+                                 ctx->stream));
     return KARMA_OK;
 }
 
@@ -2493,6 +2493,46 @@ void sets_free(SetsJob* job) {
     job->ctx->mark_set = false;
     hipStreamSynchronize(job->ctx->stream);  // its kernels may still use the scratch
     delete job;
+}
+
+int sets_begin_deferred(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job, SetsDeferred* v) {
+    KARMA_CHECK(N <= kMaxCompactN, KARMA_ERR_ARG, "sets_begin: n_contigs above the compact path");
+    KARMA_CHECK(!ctx->job_open, KARMA_ERR_STATE, "a split graph call is already open on this context");
+    std::unique_ptr<SetsJob> j(new SetsJob());
+    j->ctx = ctx;
+    j->rec = rec;
+    j->A = A;
+    j->N = N;
+    j->deferred = true;
+    if (!ctx->split_bounds.empty() && (int)ctx->split_bounds.size() <= kMaxSplit) j->split_b = ctx->split_bounds;
+    ctx->split_bounds.clear();  // one job
+    KARMA_TRY(j->setup());
+    const int rc = j->launch();
+    if (rc) {
+        ctx->mark_set = false;
+        return rc;
+    }
+    v->keys = j->slot_k.ptr;
+    v->counts = j->slot_c.ptr;
+    v->cap = (int64_t)j->B * kSlotCap;
+    v->dst = j->dst;
+    v->split_loc = j->split_loc;
+    v->split_b = j->split_b;
+    v->B = j->B;
+    v->bw = j->g.bw;
+    v->flags = j->flags;
+    v->counters = j->counters;
+    v->ovf = j->ovf;
+    ctx->job_open = true;
+    *job = j.release();
+    return KARMA_OK;
+}
+
+void sets_release(SetsJob* job) {
+    if (!job) return;
+    job->ctx->job_open = false;
+    job->ctx->mark_set = false;
+    delete job;  // its buffers go back to the main stream's cache: later work there is ordered after its kernels
 }
 
 int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {

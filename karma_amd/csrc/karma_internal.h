@@ -16,8 +16,19 @@ namespace karma {
 
 void set_error(const char* fmt, ...);
 
+// HIP runtime calls made on this thread that enqueue work, wait, or manage
+// streams/events/memory (launches, copies, memsets, event records, stream
+// waits, synchronisations): karma_api_calls, the bench's api_calls_per_step.
+// hipGetLastError and hipSetDevice (no queue traffic) are not counted.
+extern thread_local uint64_t t_hip_calls;
+constexpr bool counted_call(const char* e) {
+    return !((e[0] == 'h' && e[1] == 'i' && e[2] == 'p' && e[3] == 'G' && e[4] == 'e' && e[5] == 't' && e[6] == 'L') ||
+             (e[0] == 'h' && e[1] == 'i' && e[2] == 'p' && e[3] == 'S' && e[4] == 'e' && e[5] == 't' && e[6] == 'D'));
+}
+
 #define KARMA_HIP(expr)                                                                     \
     do {                                                                                    \
+        if (::karma::counted_call(#expr)) ++::karma::t_hip_calls;                           \
         hipError_t _e = (expr);                                                             \
         if (_e != hipSuccess) {                                                             \
             ::karma::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
@@ -168,6 +179,7 @@ struct DevArray {
     do {                                                                                \
         hipEvent_t _stop = nullptr;                                                     \
         ::karma::timing_start((ctx), (name), &_stop);                                   \
+        ++::karma::t_hip_calls;                                                         \
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), (shmem), (ctx)->stream, __VA_ARGS__); \
         ::karma::timing_stop((ctx), _stop);                                             \
         KARMA_HIP(hipGetLastError());                                                   \
@@ -181,9 +193,28 @@ int sort_reduce_pairs(karma_ctx* ctx, const uint64_t* keys_in, const int64_t* co
                       int64_t n, int key_bits, DevArray<uint64_t>& keys_out, DevArray<int64_t>& counts_out,
                       DevArray<uint64_t>* first_out, int64_t* n_out);
 
-// Exclusive scan out[i] = in[0] + ... + in[i - 1], i < n, on ctx's stream
-// (hand-written, eq.hip).
-int scan_i64_device(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);
+// sort.hip: the library's own single-launch look-back scans, stable LSD radix
+// sorts (u32 values move with the keys; vin == NULL: the input positions;
+// vout == NULL: keys only) and the reduce-by-key of a sorted array (counts
+// summed and the smallest "first" per group, both read through perm when given;
+// cin == NULL counts 1 each, fin == NULL takes the position itself; uc / uf
+// may be NULL; the group count lands in *n_out_dev on the device).
+int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);
+int scan_excl_u32(karma_ctx* ctx, const uint32_t* in, int64_t* out, int64_t n);
+int radix_sort_u64(karma_ctx* ctx, const uint64_t* kin, const uint32_t* vin, int64_t n, int key_bits,
+                   uint64_t* kout, uint32_t* vout);
+int radix_sort_u32(karma_ctx* ctx, const uint32_t* kin, const uint32_t* vin, int64_t n, int key_bits,
+                   uint32_t* kout, uint32_t* vout);
+int reduce_sorted(karma_ctx* ctx, const uint64_t* keys, const uint32_t* perm, const int64_t* cin,
+                  const uint64_t* fin, int64_t n, uint64_t* uk, int64_t* uc, uint64_t* uf, int64_t* n_out_dev);
+
+// k-mer plan internals for karma_step (kmer.hip)
+int64_t kmer_m_cap(const karma_kmer_plan* p);
+int kmer_finalize_device(karma_kmer_plan* p, int64_t* m_out);
+int kmer_profile_device_m(karma_kmer_plan* p, double* out_dev, const int64_t* m_dev);
+int kmer_set_m(karma_kmer_plan* p, int64_t M);
+// graph.hip: a pending edge stage's status words (see karma_edges_end), handed over
+const int64_t* edges_take_pending(karma_edges* e);
 
 }  // namespace karma
 
@@ -220,4 +251,22 @@ int64_t sets_max_contigs();
 int sets_begin(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job);
 int sets_end(SetsJob* job, karma_pairs* out);  // frees the job
 void sets_free(SetsJob* job);
+// A records job launched without its control-block readback (karma_step's
+// deferred steps): nothing waits for it; the list and the words that say
+// whether the common path held stay on the device.
+struct SetsDeferred {
+    const uint64_t* keys = nullptr;  // the final kernel's list: sorted unique keys ...
+    const int64_t* counts = nullptr;  // ... and counts, dst[B] of them
+    int64_t cap = 0;                  // capacity of keys / counts
+    const int64_t* dst = nullptr;     // per-bucket list offsets (B + 1; dst[B] = list length)
+    const int64_t* split_loc = nullptr;  // per split bound: keys of its bucket below it
+    std::vector<int64_t> split_b;     // the split bounds (host)
+    int B = 0, bw = 0;
+    const int* flags = nullptr;       // [0] unsorted, [1] contig range, [2] pair capacity, [3] partition check
+    const unsigned* counters = nullptr;  // [0] big reads, [3] relabel vote
+    const uint8_t* ovf = nullptr;     // per bucket: overflowed the LDS tables (generic path needed)
+};
+int sets_begin_deferred(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job, SetsDeferred* view);
+// Frees a deferred job's buffers to the allocator (stream-ordered; no wait).
+void sets_release(SetsJob* job);
 }  // namespace karma

@@ -17,7 +17,6 @@
 // Ordinals: k-mer code for integer k (4^k values); for "5p6" the 5-mer q has
 // ordinal 5q and the 6-mer (q, x) ordinal 5q + 1 + x, so ordinal order equals
 // Python str order (a proper prefix sorts first).
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
@@ -69,7 +68,33 @@ struct karma_kmer_plan {
     }
 };
 
+namespace karma {
+// The most columns a plan can have: every reachable ACGT ordinal (4^k, or for
+// 5p6 the 1024 5-mers and the 64 palindromic 6-mers) plus its exception keys.
+int64_t kmer_m_cap(const karma_kmer_plan* p) {
+    return (p->kmode == KARMA_KMER_5P6 ? 1088 : (int64_t)p->S) + p->n_exc;
+}
+}  // namespace karma
+
 namespace {
+
+// Sorted unique copy of n u64 keys (the exception k-mers; low volume): the
+// library's radix sort and reduce-by-key (sort.hip), one wait for the count.
+int sort_unique_keys(karma_ctx* ctx, const uint64_t* src, int64_t n, DevArray<uint64_t>& out, int64_t* n_out) {
+    DevArray<uint64_t> sorted, uniq;
+    DevArray<int64_t> nsel;
+    int rc;
+    if ((rc = sorted.alloc(ctx, n)) || (rc = uniq.alloc(ctx, n)) || (rc = nsel.alloc(ctx, 1))) return rc;
+    KARMA_TRY(radix_sort_u64(ctx, src, nullptr, n, 64, sorted.ptr, nullptr));
+    KARMA_TRY(reduce_sorted(ctx, sorted.ptr, nullptr, nullptr, nullptr, n, uniq.ptr, nullptr, nullptr, nsel.ptr));
+    int64_t nu = 0;
+    KARMA_HIP(hipMemcpyAsync(&nu, nsel.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    if ((rc = out.alloc(ctx, nu))) return rc;
+    KARMA_HIP(hipMemcpyAsync(out.ptr, uniq.ptr, nu * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    *n_out = nu;
+    return KARMA_OK;
+}
 
 constexpr int kBlock = 256;
 constexpr int kPBlock = 512;  // profile: 8 waves share one LDS column table
@@ -722,13 +747,19 @@ profile_wave_kernel(
     const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
     const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
     double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
-    int64_t exc0) {
+    int64_t exc0, const int64_t* __restrict__ m_dev) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     // wave index in an SGPR: contig offsets and lengths load with scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
     const int t_pad = (int)((tab_entries(P56, S) + 7) & ~7);
+    // LDS is laid out for M; with m_dev (the column table's count, not read
+    // back to the host first) M is its capacity and the rows are dense
     const int h_words = (int)hist_words(M, C16);
+    if (m_dev) {
+        M = *m_dev;
+        ld = M;
+    }
     uint32_t* counts = lds + t_pad / 2 + wave * (h_words + kProfWin);
     uint32_t* win = counts + h_words;
     uint16_t* mbuf = reinterpret_cast<uint16_t*>(win + 80);
@@ -833,10 +864,15 @@ __global__ void __launch_bounds__(kPBlock) profile_kernel(
     const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
     const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
     double* __restrict__ out, int64_t ld, uint32_t* __restrict__ scratch, int* __restrict__ err, int S,
-    int64_t* __restrict__ row_tot) {
+    int64_t* __restrict__ row_tot, const int64_t* __restrict__ m_dev) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_counts[];
     {
+        // scratch rows are M apart (the capacity when m_dev gives the count)
         uint32_t* counts = LDS_COUNTS ? lds_counts : scratch + (int64_t)blockIdx.x * M;
+        if (m_dev) {
+            M = *m_dev;
+            ld = M;
+        }
         for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
             for (int64_t j = threadIdx.x; j < M; j += blockDim.x) counts[j] = 0;
             __syncthreads();
@@ -941,14 +977,10 @@ int karma_contigs_create(karma_ctx* ctx, const uint8_t* seq, const int64_t* offs
         return rc;
     }
     KARMA_LAUNCH(ctx, "word_count", word_count_kernel, ceil_div(n + 1, 256), 256, 0, c->off, n, wc.ptr);
-    size_t tmp_bytes = 0;
-    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, wc.ptr, c->woff.ptr, (int)(n + 1), ctx->stream));
-    DevArray<uint8_t> tmp;
-    if ((rc = tmp.alloc(ctx, tmp_bytes))) {
+    if ((rc = scan_excl_i64(ctx, wc.ptr, c->woff.ptr, n + 1))) {  // one look-back launch (sort.hip)
         delete c;
         return rc;
     }
-    KARMA_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.ptr, tmp_bytes, wc.ptr, c->woff.ptr, (int)(n + 1), ctx->stream));
     KARMA_HIP(hipMemcpyAsync(&c->words, c->woff.ptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
     if ((rc = c->packed.alloc(ctx, c->words + kPadWords)) || (rc = c->mask.alloc(ctx, c->words + kPadWords))) {
@@ -1063,33 +1095,9 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
     }
     KARMA_CHECK((int64_t)ninst <= exc_cap, KARMA_ERR_STATE, "exception k-mer buffer overflow (%llu > %lld)", ninst,
                 (long long)exc_cap);
-    if (ninst) {
-        // sort + unique the exception keys (low volume; hipCUB)
-        DevArray<uint64_t> sorted, uniq;
-        DevArray<int64_t> nsel;
-        if ((rc = sorted.alloc(ctx, ninst)) || (rc = uniq.alloc(ctx, ninst)) || (rc = nsel.alloc(ctx, 1))) {
-            delete p;
-            return rc;
-        }
-        size_t tb1 = 0, tb2 = 0;
-        KARMA_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb1, exc_buf.ptr, sorted.ptr, (int)ninst, 0, 64, ctx->stream));
-        KARMA_HIP(hipcub::DeviceSelect::Unique(nullptr, tb2, sorted.ptr, uniq.ptr, nsel.ptr, (int)ninst, ctx->stream));
-        DevArray<uint8_t> tmp;
-        if ((rc = tmp.alloc(ctx, std::max(tb1, tb2)))) {
-            delete p;
-            return rc;
-        }
-        KARMA_HIP(hipcub::DeviceRadixSort::SortKeys(tmp.ptr, tb1, exc_buf.ptr, sorted.ptr, (int)ninst, 0, 64, ctx->stream));
-        KARMA_HIP(hipcub::DeviceSelect::Unique(tmp.ptr, tb2, sorted.ptr, uniq.ptr, nsel.ptr, (int)ninst, ctx->stream));
-        int64_t nu = 0;
-        KARMA_HIP(hipMemcpyAsync(&nu, nsel.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipStreamSynchronize(ctx->stream));
-        if ((rc = p->exc_keys.alloc(ctx, nu))) {
-            delete p;
-            return rc;
-        }
-        KARMA_HIP(hipMemcpyAsync(p->exc_keys.ptr, uniq.ptr, nu * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        p->n_exc = nu;
+    if (ninst && (rc = sort_unique_keys(ctx, exc_buf.ptr, (int64_t)ninst, p->exc_keys, &p->n_exc))) {
+        delete p;
+        return rc;
     }
     *out = p;
     return KARMA_OK;
@@ -1157,24 +1165,7 @@ int karma_kmer_exceptions_set(karma_kmer_plan* p, const uint64_t* src, int64_t n
         p->n_exc = 0;
         return KARMA_OK;
     }
-    DevArray<uint64_t> sorted, uniq;
-    DevArray<int64_t> nsel;
-    int rc;
-    if ((rc = sorted.alloc(ctx, n)) || (rc = uniq.alloc(ctx, n)) || (rc = nsel.alloc(ctx, 1))) return rc;
-    size_t tb1 = 0, tb2 = 0;
-    KARMA_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb1, src, sorted.ptr, (int)n, 0, 64, ctx->stream));
-    KARMA_HIP(hipcub::DeviceSelect::Unique(nullptr, tb2, sorted.ptr, uniq.ptr, nsel.ptr, (int)n, ctx->stream));
-    DevArray<uint8_t> tmp;
-    if ((rc = tmp.alloc(ctx, std::max(tb1, tb2)))) return rc;
-    KARMA_HIP(hipcub::DeviceRadixSort::SortKeys(tmp.ptr, tb1, src, sorted.ptr, (int)n, 0, 64, ctx->stream));
-    KARMA_HIP(hipcub::DeviceSelect::Unique(tmp.ptr, tb2, sorted.ptr, uniq.ptr, nsel.ptr, (int)n, ctx->stream));
-    int64_t nu = 0;
-    KARMA_HIP(hipMemcpyAsync(&nu, nsel.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    if ((rc = p->exc_keys.alloc(ctx, nu))) return rc;
-    KARMA_HIP(hipMemcpyAsync(p->exc_keys.ptr, uniq.ptr, nu * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    p->n_exc = nu;
-    return KARMA_OK;
+    return sort_unique_keys(ctx, src, n, p->exc_keys, &p->n_exc);
 }
 
 int karma_kmer_plan_finalize_async(karma_kmer_plan* p) {
@@ -1201,6 +1192,48 @@ int karma_kmer_plan_finalize_async(karma_kmer_plan* p) {
     p->fin_pending = true;
     return KARMA_OK;
 }
+
+}  // extern "C"
+
+static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out, int64_t ld, int out_is_device,
+                        const int64_t* m_dev);
+
+namespace karma {
+// The column table without M's readback (karma_step's deferred steps): M is
+// written to m_out on the device (the caller's word) for the profile kernels;
+// the host learns it later.
+int kmer_finalize_device(karma_kmer_plan* p, int64_t* m_out) {
+    karma_ctx* ctx = p->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    int kmin, kmax;
+    uint32_t S;
+    bool with_len;
+    KARMA_TRY(kmer_shape(p->kmode, &kmin, &kmax, &S, &with_len));
+    int rc;
+    if ((rc = p->col_of_ord.alloc(ctx, S)) || (rc = p->col_of_exc.alloc(ctx, p->n_exc ? p->n_exc : 1)) ||
+        (rc = p->col_keys.alloc(ctx, S + p->n_exc)))
+        return rc;
+    const size_t lds = (p->nwords + 1) * 4;
+    KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->presence.ptr, (int)p->nwords, S,
+                 p->kmode == KARMA_KMER_5P6, p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode, with_len, p->exc_keys.ptr,
+                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, m_out);
+    return KARMA_OK;
+}
+
+int kmer_profile_device_m(karma_kmer_plan* p, double* out_dev, const int64_t* m_dev) {
+    return profile_rows(p, 0, p->store->n, out_dev, 0, 1, m_dev);
+}
+
+// the column keys of a plan finalized on the device, once M is known
+int kmer_set_m(karma_kmer_plan* p, int64_t M) {
+    KARMA_CHECK(M >= 0 && M <= kmer_m_cap(p), KARMA_ERR_STATE, "column count %lld outside [0, %lld]", (long long)M,
+                (long long)kmer_m_cap(p));
+    p->M = M;
+    return KARMA_OK;
+}
+}  // namespace karma
+
+extern "C" {
 
 int karma_kmer_plan_finalize_wait(karma_kmer_plan* p, int64_t* M) {
     KARMA_CHECK(p && M, KARMA_ERR_ARG, "null argument");
@@ -1243,15 +1276,20 @@ int karma_kmer_row_totals(karma_kmer_plan* p, int64_t* dst) {
 // Rows [lo, hi) of the profile: the per-contig arrays are passed shifted by lo
 // (packed words and raw bytes are addressed through them), so row r of `out`
 // is contig lo + r.
-static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out, int64_t ld, int out_is_device) {
-    KARMA_CHECK(p && p->M >= 0, KARMA_ERR_STATE, "karma_kmer_profile before finalize");
+// m_dev: M is read by the kernels from the column table's count on the device
+// (karma_step's path: no host wait for it); the launch is sized for
+// kmer_m_cap(p) >= M and rows are written dense (ld = M).
+static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out, int64_t ld, int out_is_device,
+                        const int64_t* m_dev) {
+    KARMA_CHECK(p && (p->M >= 0 || m_dev), KARMA_ERR_STATE, "karma_kmer_profile before finalize");
     karma_ctx* ctx = p->ctx;
     karma_contigs* c = p->store;
     KARMA_TRY(ctx_begin(ctx));
-    KARMA_CHECK(ld >= p->M, KARMA_ERR_ARG, "ld (%lld) < M (%lld)", (long long)ld, (long long)p->M);
+    KARMA_CHECK(m_dev || ld >= p->M, KARMA_ERR_ARG, "ld (%lld) < M (%lld)", (long long)ld, (long long)p->M);
+    KARMA_CHECK(!m_dev || out_is_device, KARMA_ERR_ARG, "device M needs a device output");
     KARMA_CHECK(0 <= lo && lo <= hi && hi <= c->n, KARMA_ERR_ARG, "rows [%lld, %lld) outside [0, %lld)",
                 (long long)lo, (long long)hi, (long long)c->n);
-    const int64_t n = hi - lo, M = p->M;
+    const int64_t n = hi - lo, M = m_dev ? kmer_m_cap(p) : p->M;
     if (n == 0) return KARMA_OK;
     int64_t* const row_tot = p->row_tot.ptr + lo;
     const uint8_t* const has_exc = c->has_exc.ptr + lo;
@@ -1293,7 +1331,7 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16>), g_, kPBlock, lds, c->packed.ptr,      \
                      c->mask.ptr, c->has_exc.ptr, woff, off, c->raw, keylen, n, k, with_len,                     \
                      p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err,       \
-                     (int)p->S, row_tot, lo);                                                                    \
+                     (int)p->S, row_tot, lo, m_dev);                                                             \
     } while (0)
         if (p56) {
             if (c16) KARMA_WAVE_LAUNCH(true, true);
@@ -1313,7 +1351,7 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
     KARMA_LAUNCH(ctx, "kmer_profile", (profile_kernel<P56, LDS>), grid, kPBlock, lds, c->packed.ptr, c->mask.ptr, \
                  has_exc, woff, off, c->raw, keylen, n, k, with_len, p->col_of_ord.ptr,                          \
                  p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, scratch.ptr, err, (int)p->S,      \
-                 row_tot)
+                 row_tot, m_dev)
         if (p->kmode == KARMA_KMER_5P6) {
             if (lds_ok) KARMA_PROFILE_LAUNCH(true, true);
             else KARMA_PROFILE_LAUNCH(true, false);
@@ -1332,12 +1370,12 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
 
 int karma_kmer_profile(karma_kmer_plan* p, double* out, int64_t ld, int out_is_device) {
     KARMA_CHECK(p && p->store, KARMA_ERR_STATE, "karma_kmer_profile: null plan");
-    return profile_rows(p, 0, p->store->n, out, ld, out_is_device);
+    return profile_rows(p, 0, p->store->n, out, ld, out_is_device, nullptr);
 }
 
 int karma_kmer_profile_rows(karma_kmer_plan* p, int64_t row_lo, int64_t row_hi, double* out, int64_t ld,
                             int out_is_device) {
-    return profile_rows(p, row_lo, row_hi, out, ld, out_is_device);
+    return profile_rows(p, row_lo, row_hi, out, ld, out_is_device, nullptr);
 }
 
 int karma_kmer_profile_side(karma_kmer_plan* p, double* out_dev, int64_t ld, void* side) {

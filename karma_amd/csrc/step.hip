@@ -1,0 +1,950 @@
+// step.hip — one rank's step of the sharded build as one native call
+// (the work is read_graph.py:19-50 + kmer.py:199-264).
+//
+// A step is: the records job (classify .. final kernel) on the main stream;
+// the presence pass, the column set's exchange (several ranks) and the column
+// table on the side stream beside it; the dense profile on the side stream
+// beside the graph's tail; the owners' split, the key/count all-to-all-v, the
+// owner's merge, the edge stage around the totals all-gather on the main
+// stream.  karma_amd/distributed.py drove this sequence from Python (35 HIP
+// calls and two host waits per step, ~40 us of Python between them); here it
+// is one C ABI call, and a step that needs no host decision waits for nothing.
+//
+// Two paths:
+//   synchronous  every case (several ranks over RCCL, keep = outputs read
+//                back, the per-kernel timing pass): the host waits where a
+//                size must reach it -- the column count M, the records job's
+//                control block, the all-to-all's counts.
+//   deferred     (KARMA_STEP_DEFER; one process: one GPU, or one rank's share
+//                of an emulated W-rank job) nothing waits: the profile reads M
+//                from the column table on the device (launched for the
+//                plan's capacity kmer_m_cap), the records job keeps its
+//                control block on the device, the tail kernels take their
+//                sizes from device memory, and a one-block status kernel
+//                copies every word the host would have checked (order and
+//                range errors, relabel vote, pair capacity, big reads, bucket
+//                overflow, merge order, zero totals) into a ring in mapped host
+//                memory.  The host reads entry i at most two steps later (or
+//                at karma_step_sync); a step whose words call for the general
+//                path is run again synchronously (the same work the
+//                synchronous path would have done), an error is returned.
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#include "karma_internal.h"
+
+using namespace karma;
+
+namespace {
+
+constexpr int kRing = 64;  // status entries in the mapped slot (64 B each)
+constexpr int kLag = 2;    // deferred steps the host may run ahead of the device
+
+// One deferred step's status, written by step_status_kernel (seq last).
+struct StepStatus {
+    uint64_t seq;
+    int64_t slow;   // bits: 1 relabel, 2 pair capacity, 4 big reads, 8 bucket overflow
+    int64_t err;    // bits: 1 unsorted records, 2 contig range, 4 partition check, 8 zero total, 16 merge order
+    int64_t U;      // pairs of the local list
+    int64_t E;      // edges
+    int64_t M;      // columns
+    int64_t pad[2];
+};
+static_assert(sizeof(StepStatus) == 64, "status entry");
+
+constexpr int kET = 1024;  // edge-stage tile (elements per block round)
+constexpr int kMaxRuns = 64;
+
+// ---- edge stage on device-sized lists ----------------------------------------
+// The tile loops take the list length from device memory, so the host
+// launches them without knowing it: a fixed grid strides over the tiles.
+__device__ __forceinline__ bool is_head(const uint64_t* __restrict__ k, int64_t i, uint64_t key) {
+    return i == 0 || k[i - 1] != key;
+}
+__device__ __forceinline__ int64_t run_sum(const uint64_t* __restrict__ k, const int64_t* __restrict__ c, int64_t n,
+                                           int64_t i, uint64_t key) {
+    int64_t s = c[i];
+    for (int64_t j = i + 1; j < n && k[j] == key; ++j) s += c[j];
+    return s;
+}
+
+// Tile counts of edges (non-zero off-diagonal keys) and the totals: the
+// diagonal group of contig a writes |readset(a)|, every other entry is zeroed
+// (contigs between keys by the key after the gap, those before the first and
+// after the last key by the grid).  st[0..2] cleared for the write kernel.
+__global__ void __launch_bounds__(kET) step_edge_count_kernel(const uint64_t* __restrict__ keys,
+                                                              const int64_t* __restrict__ counts,
+                                                              const int64_t* __restrict__ n_dev, int64_t n_tot,
+                                                              int64_t* __restrict__ totals,
+                                                              int64_t* __restrict__ tile_cnt,
+                                                              int64_t* __restrict__ st) {
+    const int64_t n = *n_dev;
+    if (blockIdx.x == 0 && threadIdx.x < 3) st[threadIdx.x] = 0;
+    const int64_t stride = (int64_t)gridDim.x * kET, gid = (int64_t)blockIdx.x * kET + threadIdx.x;
+    const int64_t a_first = n ? (int64_t)(keys[0] >> 32) : n_tot;
+    const int64_t a_last = n ? (int64_t)(keys[n - 1] >> 32) : n_tot;
+    for (int64_t c = gid; c < min(a_first, n_tot); c += stride) totals[c] = 0;
+    for (int64_t c = a_last + 1 + gid; c < n_tot; c += stride) totals[c] = 0;
+    const int64_t tiles = (n + kET - 1) / kET;
+    for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const int64_t i = t * kET + threadIdx.x;
+        bool f = false;
+        if (i < n) {
+            const uint64_t k = keys[i];
+            const uint32_t a = (uint32_t)(k >> 32), b = (uint32_t)k;
+            if (i > 0) {
+                const uint32_t pa = (uint32_t)(keys[i - 1] >> 32);
+                const uint32_t lim = (int64_t)a < n_tot ? a : (uint32_t)n_tot;
+                for (uint32_t c = pa + 1; c < lim; ++c) totals[c] = 0;
+                if ((int64_t)a < n_tot && pa != a && a != b) totals[a] = 0;
+            } else if ((int64_t)a < n_tot && a != b) {
+                totals[a] = 0;
+            }
+            if (is_head(keys, i, k) && (int64_t)b < n_tot) {  // b >= n_tot: reported by the write kernel
+                const int64_t s = run_sum(keys, counts, n, i, k);
+                if (a == b) totals[a] = s;
+                else f = s != 0;
+            }
+        }
+        const int cnt = __syncthreads_count(f);
+        if (threadIdx.x == 0) tile_cnt[t] = cnt;
+    }
+}
+
+// Each tile's edges at the sum of the earlier tiles' counts plus their rank in
+// the tile (ballots, then the waves before); w = (s/ta + s/tb)/2 in IEEE
+// binary64 without contraction (read_graph.py:39-42).  st[0] zero-total flag,
+// st[1] a key past the contig range (no edge), st[2] the edge count (all
+// cleared by the count kernel, earlier on the stream).
+__global__ void __launch_bounds__(kET) step_edge_write_kernel(
+    const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, const int64_t* __restrict__ n_dev,
+    const int64_t* __restrict__ totals, const int64_t* __restrict__ tile_cnt, uint32_t* __restrict__ ea,
+    uint32_t* __restrict__ eb, int64_t* __restrict__ es, double* __restrict__ ew, int64_t* __restrict__ st,
+    int64_t n_tot) {
+    __shared__ int64_t wsum[kET / 64];
+    __shared__ int64_t base_s;
+    const int64_t n = *n_dev;
+    const int64_t tiles = (n + kET - 1) / kET;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (blockIdx.x == 0 && tiles == 0 && threadIdx.x == 0) st[2] = 0;
+    for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        int64_t b = 0;
+        for (int64_t j = threadIdx.x; j < t; j += kET) b += tile_cnt[j];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) b += __shfl_xor(b, d, 64);
+        if (lane == 0) wsum[wave] = b;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t s = 0;
+            for (int w = 0; w < kET / 64; ++w) s += wsum[w];
+            base_s = s;
+        }
+        const int64_t i = t * kET + threadIdx.x;
+        uint64_t k = 0;
+        int64_t c = 0;
+        bool f = false;
+        if (i < n) {
+            k = keys[i];
+            const uint32_t a = (uint32_t)(k >> 32), bb = (uint32_t)k;
+            if ((int64_t)bb >= n_tot) {
+                st[1] = 1;
+            } else if (a != bb && is_head(keys, i, k)) {
+                c = run_sum(keys, counts, n, i, k);
+                f = c != 0;
+            }
+        }
+        const uint64_t m = __ballot(f);
+        __syncthreads();  // base_s is set, wsum free
+        if (lane == 0) wsum[wave] = __popcll(m);
+        __syncthreads();
+        int64_t before = 0, total = 0;
+        for (int w = 0; w < kET / 64; ++w) {
+            if (w < wave) before += wsum[w];
+            total += wsum[w];
+        }
+        const int64_t base = base_s;
+        if (t == tiles - 1 && threadIdx.x == 0) st[2] = base + total;
+        if (f) {
+            const int64_t o = base + before + __popcll(m & ((1ull << lane) - 1ull));
+            const uint32_t a = (uint32_t)(k >> 32), bb = (uint32_t)k;
+            const int64_t ta = totals[a], tb = totals[bb];
+            ea[o] = a;
+            eb[o] = bb;
+            es[o] = c;
+            if (ta == 0 || tb == 0) {
+                st[0] = 1;
+                ew[o] = 0.0;
+            } else {
+                const double x = __ddiv_rn((double)c, (double)ta);
+                const double y = __ddiv_rn((double)c, (double)tb);
+                ew[o] = __dadd_rn(x, y) * 0.5;
+            }
+        }
+        __syncthreads();  // wsum / base_s reused by the next tile
+    }
+}
+
+// ---- owner merge of W sorted runs, sizes on the device ---------------------------
+// The runs are the owners' slices of one rank's list (an emulated exchange:
+// this rank's own W slices stand in for the W received ones), their offsets
+// computed in every block from the final kernel's bucket offsets (dst) and
+// in-bucket split counts (split_loc), as SetsJob::finish does on the host.
+// One kernel: each tile (kMT elements of one run) finds its window in every
+// other run with 16-lane groups probing 16 keys per round (a run of 200k keys:
+// 5 dependent loads), stages the windows in LDS, and places every element at
+// its rank in its own run plus its rank in each other run (stable: equal keys
+// of different runs end up adjacent, in run order).
+constexpr int kMT = 1024;       // tile elements
+constexpr int kMLds = 6144;     // staged window keys
+constexpr int kMG = 16;         // lanes per bound search
+struct RunSrc {
+    int nr, B, bw;
+    int64_t b[kMaxRuns + 1];     // owner bounds (contig ids)
+};
+
+__device__ __forceinline__ int64_t count_below(const uint64_t* __restrict__ a, int64_t lo, int64_t hi, uint64_t k,
+                                               bool le) {
+    int64_t n = hi - lo, base = lo;
+    while (n > 0) {
+        const int64_t half = n >> 1;
+        const uint64_t m = a[base + half];
+        const bool before = le ? m <= k : m < k;
+        base = before ? base + half + 1 : base;
+        n = before ? n - half - 1 : half;
+    }
+    return base;
+}
+
+__global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restrict__ keys,
+                                                         const int64_t* __restrict__ counts,
+                                                         const int64_t* __restrict__ dst,
+                                                         const int64_t* __restrict__ split_loc, RunSrc rs,
+                                                         uint64_t* __restrict__ ko, int64_t* __restrict__ co,
+                                                         int64_t* __restrict__ bad) {
+    __shared__ int64_t ro[kMaxRuns + 1], rt[kMaxRuns + 1];
+    __shared__ int64_t wlo[kMaxRuns], whi[kMaxRuns];
+    __shared__ int wbase[kMaxRuns];
+    __shared__ uint64_t wkeys[kMLds];
+    const int nr = rs.nr;
+    const int64_t U = dst[rs.B];
+    if (threadIdx.x <= (unsigned)nr) {
+        const int64_t bd = rs.b[threadIdx.x];
+        const int64_t b = bd >> rs.bw;
+        ro[threadIdx.x] = bd <= 0 ? 0 : (b < rs.B ? dst[b] + split_loc[threadIdx.x] : U);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+        for (int r = 0; r < nr; ++r) {
+            rt[r] = t;
+            t += (ro[r + 1] - ro[r] + kMT - 1) / kMT;
+        }
+        rt[nr] = t;
+    }
+    __syncthreads();
+    const int64_t tiles = rt[nr];
+    const int lane = threadIdx.x & 63, g = lane & (kMG - 1), grp = threadIdx.x / kMG;
+    const unsigned long long gmask = ((1ull << kMG) - 1ull) << (lane & ~(kMG - 1));
+    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        int r = 0;
+        while (r + 1 < nr && rt[r + 1] <= tile) ++r;
+        const int64_t t0 = ro[r] + (tile - rt[r]) * kMT, t1 = min(ro[r + 1], t0 + kMT);
+        // window bounds: search q covers run q >> 1, (q & 1) ? last key : first key
+        for (int q0 = 0; q0 < 2 * nr; q0 += 256 / kMG) {
+            const int q = q0 + grp;
+            const int sr = q >> 1;
+            bool search = q < 2 * nr && sr != r;
+            int64_t lo = search ? ro[sr] : 0, hi = search ? ro[sr + 1] : 0;
+            const uint64_t k = search ? keys[(q & 1) ? t1 - 1 : t0] : 0;
+            const bool le = sr < r;
+            for (;;) {  // every group of the wave runs the same rounds (ballots are wave-wide)
+                const bool more = hi - lo > kMG;
+                if (!__ballot(more)) break;
+                const int64_t step = (hi - lo + kMG - 1) / kMG;
+                const int64_t p = min(hi - 1, lo + (int64_t)(g + 1) * step - 1);
+                const bool before = more && (le ? keys[p] <= k : keys[p] < k);
+                const int c = __popcll(__ballot(before) & gmask);
+                if (more) {
+                    const int64_t nlo = c ? min(hi, lo + (int64_t)c * step) : lo;
+                    const int64_t nhi = c < kMG ? min(hi, lo + (int64_t)(c + 1) * step - 1) : hi;
+                    lo = nlo;
+                    hi = nhi;
+                }
+            }
+            const int64_t p = lo + g;
+            const bool before = p < hi && (le ? keys[p] <= k : keys[p] < k);
+            const int64_t ans = lo + __popcll(__ballot(before) & gmask);
+            if (search && g == 0) {
+                if (q & 1) whi[sr] = ans;
+                else wlo[sr] = ans;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int used = 0;
+            for (int sr = 0; sr < nr; ++sr) {
+                if (sr == r) continue;
+                if (whi[sr] < wlo[sr]) whi[sr] = wlo[sr];
+                const int64_t len = whi[sr] - wlo[sr];
+                if (used + len <= kMLds) {
+                    wbase[sr] = used;
+                    used += (int)len;
+                } else {
+                    wbase[sr] = -1;
+                }
+            }
+        }
+        __syncthreads();
+        for (int sr = 0; sr < nr; ++sr) {
+            if (sr == r || wbase[sr] < 0) continue;
+            const int64_t lo = wlo[sr];
+            const int len = (int)(whi[sr] - lo);
+            for (int i = threadIdx.x; i < len; i += blockDim.x) wkeys[wbase[sr] + i] = keys[lo + i];
+        }
+        __syncthreads();
+        for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+            const uint64_t k = keys[i];
+            if (i > ro[r] && keys[i - 1] > k) *bad = 1;
+            int64_t pos = i - ro[r];
+            for (int sr = 0; sr < nr; ++sr) {
+                if (sr == r) continue;
+                const int64_t lo = wlo[sr], hi = whi[sr];
+                int64_t cnt;
+                if (wbase[sr] >= 0) {
+                    const uint64_t* w = wkeys + wbase[sr] - lo;
+                    cnt = count_below(w, lo, hi, k, sr < r);
+                } else {
+                    cnt = count_below(keys, lo, hi, k, sr < r);
+                }
+                pos += cnt - ro[sr];
+            }
+            ko[pos] = k;
+            co[pos] = counts[i];
+        }
+        __syncthreads();  // the windows are rebuilt for the next tile
+    }
+}
+
+// Every word a host would have checked after a deferred step, into the ring
+// entry (seq written last, released to the host).
+__global__ void step_status_kernel(const int* __restrict__ flags, const unsigned* __restrict__ counters,
+                                   const uint8_t* __restrict__ ovf, int B, const int64_t* __restrict__ dst,
+                                   int64_t* __restrict__ merge_bad, const int64_t* __restrict__ est,
+                                   const int64_t* __restrict__ m_dev, StepStatus* __restrict__ out, uint64_t seq) {
+    __shared__ int any_ovf;
+    if (threadIdx.x == 0) any_ovf = 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < B; b += blockDim.x)
+        if (ovf[b]) any_ovf = 1;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    int64_t slow = 0, err = 0;
+    if (counters[3]) slow |= 1;
+    if (flags[2]) slow |= 2;
+    if (counters[0]) slow |= 4;
+    if (any_ovf) slow |= 8;
+    if (flags[0]) err |= 1;
+    if (flags[1]) err |= 2;
+    if (flags[3]) err |= 4;
+    if (est[0]) err |= 8;
+    if (est[1]) err |= 2;  // a key past the contig range
+    if (merge_bad) {
+        if (*merge_bad) err |= 16;
+        *merge_bad = 0;  // cleared for the next step's merge (stream order)
+    }
+    out->slow = slow;
+    out->err = err;
+    out->U = dst[B];
+    out->E = est[2];
+    out->M = *m_dev;
+    __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace
+
+struct karma_step {
+    karma_ctx* ctx = nullptr;
+    karma_comm* comm = nullptr;   // main-stream communicator (NULL: one process)
+    karma_comm* scomm = nullptr;  // side-stream communicator (column set exchange)
+    int kmode = 0, world = 1, rank = 0, nranks = 1, emulate = 0;
+    int64_t n_glob = 0, c_lo = 0, n_loc = 0;
+    std::vector<int64_t> bounds;  // owner bounds: nranks + 1 contig ids
+    bool exchange = false;        // a split / merge happens (world > 1 or emulation)
+    hipStream_t main_s = nullptr, side_s = nullptr;
+    hipEvent_t ev = nullptr;      // side -> main join
+    // the profile (persistent; rows of n_loc x M, dense)
+    DevArray<double> prof;
+    // outputs of the last synchronous step
+    karma_kmer_plan* plan = nullptr;
+    karma_pairs* local = nullptr;
+    karma_pairs* merged = nullptr;
+    karma_edges* edges = nullptr;
+    int64_t M = -1, E = -1, pairs_local = -1, entries = -1;
+    // deferred steps
+    struct Pending {
+        uint64_t seq;
+        karma_contigs* store;
+        const uint32_t* rec;
+        int64_t A;
+    };
+    std::deque<Pending> pending;
+    uint64_t seq = 0;
+    StepStatus* ring_h = nullptr;  // mapped host memory (kMapStep)
+    StepStatus* ring_d = nullptr;
+    int sticky_sync = 0;           // deferred steps to run synchronously after a slow one
+    // deferred steps' device buffers (kept across steps: identical shapes reuse them)
+    DevArray<int64_t> m_ring;      // per ring entry: the step's column count, written by its column table
+    hipEvent_t ev_cols = nullptr;  // side stream, after a deferred step's column table
+    uint64_t prof_seq = 0;         // the deferred step whose profile `prof` holds (0: a synchronous one)
+    int64_t prof_M = -1;           // M of the profile in `prof` (-1: not known yet)
+    DevArray<uint64_t> mk;
+    DevArray<int64_t> mc, mbad, tot, tile_cnt, est;
+    DevArray<uint32_t> ea, eb;
+    DevArray<int64_t> es;
+    DevArray<double> ew;
+    // status words of synchronous steps whose edge count was not read
+    // (count = false): copied out in stream order, checked when their event
+    // has passed (or at karma_step_sync)
+    int64_t* graves_h = nullptr;  // pinned, kRing x 4 words
+    hipEvent_t grave_ev[kRing] = {};
+    std::deque<int> graves;
+    int grave_next = 0;
+    // counters
+    int64_t n_sync = 0, n_deferred = 0, n_redone = 0;
+};
+
+namespace {
+
+// The profile buffer grows only with both streams idle: the side stream may
+// still be writing the old one, and the allocator would hand it to a
+// main-stream allocation (it was allocated there) at once.
+int ensure_prof(karma_step* s, size_t n) {
+    if (s->prof.n >= n) return KARMA_OK;
+    KARMA_HIP(hipStreamSynchronize(s->side_s));
+    KARMA_HIP(hipStreamSynchronize(s->main_s));
+    return s->prof.alloc(s->ctx, n);
+}
+template <typename T>
+int ensure_arr(karma_ctx* ctx, DevArray<T>& a, size_t n) {
+    return a.n >= n ? KARMA_OK : a.alloc(ctx, n);
+}
+
+// The status words of a grave whose copy has landed: errors are returned.
+int check_grave(karma_step* s, int slot) {
+    const int64_t* w = s->graves_h + 4 * slot;
+    KARMA_CHECK(!w[2], KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
+    KARMA_CHECK(!(int)w[0], KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
+    return KARMA_OK;
+}
+
+int bury(karma_step* s, bool wait) {
+    while (!s->graves.empty()) {
+        const int slot = s->graves.front();
+        if (wait) {
+            KARMA_HIP(hipEventSynchronize(s->grave_ev[slot]));
+        } else if (hipEventQuery(s->grave_ev[slot]) != hipSuccess) {
+            break;
+        }
+        s->graves.pop_front();
+        KARMA_TRY(check_grave(s, slot));
+    }
+    return KARMA_OK;
+}
+
+int drop_outputs(karma_step* s) {
+    if (s->edges && s->E < 0) {
+        if (const int64_t* st = edges_take_pending(s->edges)) {
+            if ((int)s->graves.size() >= kRing) KARMA_TRY(bury(s, true));
+            const int slot = s->grave_next;
+            s->grave_next = (slot + 1) % kRing;
+            if (!s->grave_ev[slot]) KARMA_HIP(hipEventCreateWithFlags(&s->grave_ev[slot], hipEventDisableTiming));
+            KARMA_HIP(hipMemcpyAsync(s->graves_h + 4 * slot, st, 24, hipMemcpyDeviceToHost, s->main_s));
+            KARMA_HIP(hipEventRecord(s->grave_ev[slot], s->main_s));
+            s->graves.push_back(slot);
+        }
+    }
+    if (s->edges) karma_edges_destroy(s->edges);
+    if (s->merged) karma_pairs_destroy(s->merged);
+    if (s->local) karma_pairs_destroy(s->local);
+    if (s->plan) karma_kmer_plan_destroy(s->plan);
+    s->edges = nullptr;
+    s->merged = s->local = nullptr;
+    s->plan = nullptr;
+    s->M = s->E = s->pairs_local = s->entries = -1;
+    return bury(s, false);
+}
+
+// The column set's exchange (kmer.py:146-179 is a global sorted union): OR of
+// every rank's presence bitmap, union of every rank's exception keys.  On the
+// side communicator, issued in the same order on every rank.
+int exchange_columns(karma_step* s, karma_kmer_plan* plan, karma_comm* c) {
+    karma_ctx* ctx = s->ctx;
+    const int W = s->world;
+    int64_t nw = 0;
+    KARMA_TRY(karma_kmer_presence_words(plan, &nw));
+    DevArray<uint32_t> words, all;
+    KARMA_TRY(words.alloc(ctx, nw));
+    KARMA_TRY(all.alloc(ctx, nw * W));
+    KARMA_TRY(karma_kmer_presence_get(plan, words.ptr));
+    KARMA_TRY(karma_comm_allgather(c, words.ptr, all.ptr, nw * 4));
+    KARMA_TRY(karma_kmer_presence_merge(plan, all.ptr, W));
+    // exception keys: sizes, then one padded all-gather
+    int64_t ne = 0;
+    KARMA_TRY(karma_kmer_exceptions_count(plan, &ne));
+    std::vector<int64_t> sizes(W, 0);
+    sizes[s->rank] = ne;
+    KARMA_TRY(karma_comm_allreduce_host(c, sizes.data(), W, KARMA_DT_I64, KARMA_OP_SUM));
+    int64_t mx = 1, tot = 0;
+    for (int64_t x : sizes) {
+        mx = std::max(mx, x);
+        tot += x;
+    }
+    if (tot == 0) return karma_kmer_exceptions_set(plan, nullptr, 0);
+    DevArray<uint64_t> send, gath, keys;
+    KARMA_TRY(send.alloc(ctx, mx));
+    KARMA_TRY(gath.alloc(ctx, mx * W));
+    KARMA_TRY(keys.alloc(ctx, tot));
+    if (ne) KARMA_TRY(karma_kmer_exceptions_get(plan, send.ptr));
+    KARMA_TRY(karma_comm_allgather(c, send.ptr, gath.ptr, mx * 8));
+    int64_t off = 0;
+    for (int r = 0; r < W; ++r) {
+        if (sizes[r])
+            KARMA_HIP(hipMemcpyAsync(keys.ptr + off, gath.ptr + r * mx, sizes[r] * 8, hipMemcpyDeviceToDevice,
+                                     ctx->stream));
+        off += sizes[r];
+    }
+    return karma_kmer_exceptions_set(plan, keys.ptr, tot);  // sorts and dedups (stream-ordered)
+}
+
+// The owners' readset totals, gathered from every owner's slice (in place for
+// equal shards; otherwise a padded all-gather and copies back).
+int allgather_slices(karma_step* s, int64_t* buf) {
+    karma_ctx* ctx = s->ctx;
+    const int W = s->world;
+    const std::vector<int64_t>& b = s->bounds;
+    int64_t mx = 0;
+    bool equal = b[0] == 0;
+    for (int r = 0; r < W; ++r) {
+        mx = std::max(mx, b[r + 1] - b[r]);
+        equal = equal && (b[r + 1] - b[r]) == (b[1] - b[0]);
+    }
+    if (equal && mx > 0) return karma_comm_allgather(s->comm, buf + s->rank * mx, buf, mx * 8);
+    mx = std::max<int64_t>(mx, 1);
+    DevArray<int64_t> send, all;
+    KARMA_TRY(send.alloc(ctx, mx));
+    KARMA_TRY(all.alloc(ctx, mx * W));
+    const int64_t mine = b[s->rank + 1] - b[s->rank];
+    if (mine)
+        KARMA_HIP(hipMemcpyAsync(send.ptr, buf + b[s->rank], mine * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    KARMA_TRY(karma_comm_allgather(s->comm, send.ptr, all.ptr, mx * 8));
+    for (int r = 0; r < W; ++r) {
+        const int64_t n = b[r + 1] - b[r];
+        if (r != s->rank && n)
+            KARMA_HIP(hipMemcpyAsync(buf + b[r], all.ptr + r * mx, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    return KARMA_OK;
+}
+
+// ---- the synchronous step ------------------------------------------------------
+int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A, bool keep, bool sequential,
+             bool count) {
+    karma_ctx* ctx = s->ctx;
+    KARMA_TRY(drop_outputs(s));
+    ++s->n_sync;
+    if (s->exchange) KARMA_TRY(karma_graph_split_hint(ctx, s->bounds.data(), s->nranks));
+    int64_t M = 0;
+    if (!sequential) {
+        // the graph's kernels first on the main stream; the presence pass, the
+        // column set's exchange and the column table beside them on the side
+        // stream; the profile behind the graph's kernels on the side stream
+        karma_graph_job* job = nullptr;
+        KARMA_TRY(karma_graph_records_begin(ctx, rec, A, s->n_glob, KARMA_REC_SORTED, 1, &job));
+        int rc = KARMA_OK;
+        ctx->stream = s->side_s;
+        rc = karma_kmer_plan_create(ctx, store, s->kmode, &s->plan);
+        if (!rc && s->world > 1) rc = exchange_columns(s, s->plan, s->scomm ? s->scomm : s->comm);
+        if (!rc) rc = karma_kmer_plan_finalize_async(s->plan);
+        ctx->stream = s->main_s;
+        if (!rc) rc = karma_kmer_plan_finalize_wait(s->plan, &M);
+        if (!rc) rc = ensure_prof(s, (size_t)std::max<int64_t>(1, s->n_loc * M));
+        if (!rc && s->n_loc * M) rc = karma_kmer_profile_side(s->plan, s->prof.ptr, M, s->side_s);
+        const int rc2 = karma_graph_records_end(job, &s->local);  // consumes the job on every path
+        KARMA_TRY(rc);
+        KARMA_TRY(rc2);
+    } else {
+        // everything on the main stream (every kernel alone on the chip)
+        KARMA_TRY(karma_kmer_plan_create(ctx, store, s->kmode, &s->plan));
+        if (s->world > 1) KARMA_TRY(exchange_columns(s, s->plan, s->comm));
+        KARMA_TRY(karma_kmer_plan_finalize(s->plan, &M));
+        KARMA_TRY(ensure_prof(s, (size_t)std::max<int64_t>(1, s->n_loc * M)));
+        if (s->n_loc * M) KARMA_TRY(karma_kmer_profile(s->plan, s->prof.ptr, M, 1));
+        KARMA_TRY(karma_graph_records(ctx, rec, A, s->n_glob, KARMA_REC_SORTED, 1, &s->local));
+    }
+    s->M = M;
+    s->prof_M = M;
+    s->prof_seq = 0;
+    if (keep) {
+        KARMA_TRY(karma_pairs_count(s->local, &s->pairs_local));
+        std::vector<int64_t> c(std::max<int64_t>(1, s->pairs_local));
+        KARMA_TRY(karma_pairs_get(s->local, nullptr, c.data(), nullptr, 0));
+        int64_t t = 0;
+        for (int64_t i = 0; i < s->pairs_local; ++i) t += c[i];
+        s->entries = t;
+    }
+    int64_t E = -1;
+    if (s->exchange) {
+        std::vector<int64_t> starts(s->nranks + 1);
+        KARMA_TRY(karma_pairs_split(s->local, s->bounds.data(), s->nranks, starts.data()));
+        const uint64_t* k = nullptr;
+        const int64_t* c = nullptr;
+        KARMA_TRY(karma_pairs_device(s->local, &k, &c));
+        if (s->world > 1) {
+            // each owner's slice of the keys and of the counts, one grouped all-to-all-v
+            const int W = s->world;
+            std::vector<int64_t> sc(W), rcv(W), so(W + 1, 0), ro(W + 1, 0);
+            for (int r = 0; r < W; ++r) sc[r] = starts[r + 1] - starts[r];
+            KARMA_TRY(karma_comm_exchange_counts(s->comm, sc.data(), rcv.data()));
+            for (int r = 0; r < W; ++r) {
+                so[r + 1] = so[r] + 8 * sc[r];
+                ro[r + 1] = ro[r] + 8 * rcv[r];
+            }
+            const int64_t nr = ro[W] / 8;
+            DevArray<uint64_t> rk;
+            DevArray<int64_t> rc;
+            KARMA_TRY(rk.alloc(ctx, nr));
+            KARMA_TRY(rc.alloc(ctx, nr));
+            KARMA_TRY(karma_comm_alltoallv_kv(s->comm, k, c, so.data(), rk.ptr, rc.ptr, ro.data()));
+            std::vector<int64_t> run(W + 1, 0);
+            for (int r = 0; r < W; ++r) run[r + 1] = run[r] + rcv[r];
+            KARMA_TRY(karma_pairs_merge_runs(ctx, rk.ptr, rc.ptr, run.data(), W, 1, &s->merged));
+            // rk / rc return to the main stream's cache: the merge (stream-ordered) has read them
+        } else {  // emulation: this rank's own W slices stand in for the W received ones
+            KARMA_TRY(karma_pairs_merge_runs(ctx, k, c, starts.data(), s->nranks, 1, &s->merged));
+        }
+        int64_t* totals = nullptr;
+        KARMA_TRY(karma_edges_begin(ctx, s->merged, KARMA_MODE_READS, s->n_glob, &s->edges, &totals));
+        if (s->world > 1) KARMA_TRY(allgather_slices(s, totals));
+        KARMA_TRY(karma_edges_end(s->edges, count ? &E : nullptr));
+    } else {
+        KARMA_TRY(karma_edges_from_pairs(ctx, s->local, KARMA_MODE_READS, nullptr, s->n_glob, &s->edges, &E));
+    }
+    s->E = E;
+    if (!sequential) KARMA_TRY(karma_ctx_join(ctx, s->side_s));
+    return KARMA_OK;
+}
+
+// ---- the deferred step -----------------------------------------------------------
+int check_entry(karma_step* s, const karma_step::Pending& p, bool* slow) {
+    const StepStatus& st = const_cast<const StepStatus&>(s->ring_h[p.seq % kRing]);
+    *slow = st.slow != 0;
+    if (p.seq == s->prof_seq && !*slow) s->prof_M = st.M;
+    if (st.err) {
+        KARMA_CHECK(!(st.err & 1), KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
+        KARMA_CHECK(!(st.err & 2), KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)",
+                    (long long)s->n_glob);
+        KARMA_CHECK(!(st.err & 16), KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
+        KARMA_CHECK(!(st.err & 8), KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
+        KARMA_CHECK(false, KARMA_ERR_STATE, "code partition: block counts disagree with the classify histogram");
+    }
+    return KARMA_OK;
+}
+
+bool entry_done(const karma_step* s, uint64_t seq) {
+    return __atomic_load_n(&s->ring_h[seq % kRing].seq, __ATOMIC_ACQUIRE) == seq;
+}
+
+// Checks deferred steps: every finished one (wait = false), or all of them
+// after waiting (wait = true), or down to kLag - 1 outstanding (lag = true).
+// A step whose words call for the general path runs again synchronously.
+int drain(karma_step* s, bool wait, bool lag) {
+    while (!s->pending.empty()) {
+        karma_step::Pending p = s->pending.front();
+        const bool must = wait || (lag && (int)s->pending.size() >= kLag);
+        if (!entry_done(s, p.seq)) {
+            if (!must) break;
+            // the main stream reaches the status kernel within a step's time
+            for (int spin = 0; !entry_done(s, p.seq); ++spin) {
+                if (spin > 64) std::this_thread::yield();
+                if (spin % 4096 == 4095 && hipStreamQuery(s->main_s) == hipSuccess && !entry_done(s, p.seq)) {
+                    set_error("karma_step: a deferred step's status never arrived");
+                    return KARMA_ERR_STATE;
+                }
+            }
+        }
+        s->pending.pop_front();
+        bool slow = false;
+        KARMA_TRY(check_entry(s, p, &slow));
+        if (slow) {
+            // the general path (relabelled contigs, more pair room, big reads,
+            // an overflowed bucket): the step's work again, synchronously
+            ++s->n_redone;
+            s->sticky_sync = 8;
+            KARMA_TRY(run_sync(s, p.store, p.rec, p.A, false, false, true));
+        }
+    }
+    return KARMA_OK;
+}
+
+int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A) {
+    karma_ctx* ctx = s->ctx;
+    KARMA_TRY(drop_outputs(s));  // a deferred step has no outputs to read
+    ++s->n_deferred;
+    const uint64_t seq = ++s->seq;
+    s->prof_seq = seq;
+    s->prof_M = -1;
+    if (s->exchange) KARMA_TRY(karma_graph_split_hint(ctx, s->bounds.data(), s->nranks));
+    // records job (main stream) up to its final kernel; no readback
+    SetsJob* job = nullptr;
+    SetsDeferred v;
+    KARMA_TRY(sets_begin_deferred(ctx, reinterpret_cast<const uint2*>(rec), A, s->n_glob, &job, &v));
+    std::unique_ptr<SetsJob, void (*)(SetsJob*)> jg(job, sets_release);
+    // side stream: presence, column table (M stays on the device), then the
+    // profile behind the graph's final kernel
+    ctx->stream = s->side_s;
+    karma_kmer_plan* plan = nullptr;
+    int rc = karma_kmer_plan_create(ctx, store, s->kmode, &plan);
+    int64_t* const m_dev = s->m_ring.ptr + seq % kRing;  // read by the profile (side) and the status kernel (main)
+    if (!rc) rc = kmer_finalize_device(plan, m_dev);
+    if (!rc) {
+        ++t_hip_calls;
+        rc = hipEventRecord(s->ev_cols, s->side_s) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
+    }
+    if (!rc) rc = ensure_prof(s, (size_t)std::max<int64_t>(1, s->n_loc * kmer_m_cap(plan)));
+    if (!rc && ctx->mark_set) {
+        if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
+        rc = hipStreamWaitEvent(s->side_s, ctx->mark_ev, 0) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
+    }
+    if (!rc && s->n_loc) rc = kmer_profile_device_m(plan, s->prof.ptr, m_dev);
+    if (plan) karma_kmer_plan_destroy(plan);  // its buffers return to the side stream's cache
+    ctx->stream = s->main_s;
+    KARMA_TRY(rc);
+    // main stream: the tail, sized on the device
+    const uint64_t* lk = v.keys;
+    const int64_t* lc = v.counts;
+    const int64_t* n_dev = v.dst + v.B;
+    int64_t* mbad = nullptr;
+    const int cu = ctx->cu_count;
+    if (s->exchange) {
+        KARMA_TRY(ensure_arr(ctx, s->mk, v.cap));
+        KARMA_TRY(ensure_arr(ctx, s->mc, v.cap));
+        if (!s->mbad.ptr) {  // the merge sets it, the status kernel reads and clears it
+            KARMA_TRY(s->mbad.alloc(ctx, 1));
+            KARMA_HIP(hipMemsetAsync(s->mbad.ptr, 0, 8, ctx->stream));
+        }
+        RunSrc rs{};
+        rs.nr = s->nranks;
+        rs.B = v.B;
+        rs.bw = v.bw;
+        for (int r = 0; r <= s->nranks; ++r) rs.b[r] = s->bounds[r];
+        KARMA_CHECK((int)v.split_b.size() == s->nranks + 1, KARMA_ERR_STATE, "karma_step: the split hint was lost");
+        const int64_t tiles_cap = (v.cap + kMT - 1) / kMT + s->nranks;
+        KARMA_LAUNCH(ctx, "merge_rank", step_merge_kernel, (int)std::min<int64_t>(tiles_cap, 2 * cu), 256, 0, v.keys,
+                     v.counts, v.dst, v.split_loc, rs, s->mk.ptr, s->mc.ptr, s->mbad.ptr);
+        lk = s->mk.ptr;
+        lc = s->mc.ptr;
+        mbad = s->mbad.ptr;
+    }
+    KARMA_TRY(ensure_arr(ctx, s->tot, s->n_glob));
+    KARMA_TRY(ensure_arr(ctx, s->tile_cnt, (v.cap + kET - 1) / kET + 1));
+    KARMA_TRY(ensure_arr(ctx, s->est, 3));
+    KARMA_TRY(ensure_arr(ctx, s->ea, v.cap));
+    KARMA_TRY(ensure_arr(ctx, s->eb, v.cap));
+    KARMA_TRY(ensure_arr(ctx, s->es, v.cap));
+    KARMA_TRY(ensure_arr(ctx, s->ew, v.cap));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((v.cap + kET - 1) / kET, cu));
+    KARMA_LAUNCH(ctx, "edge_count", step_edge_count_kernel, grid, kET, 0, lk, lc, n_dev, s->n_glob, s->tot.ptr,
+                 s->tile_cnt.ptr, s->est.ptr);
+    KARMA_LAUNCH(ctx, "edge_weights", step_edge_write_kernel, grid, kET, 0, lk, lc, n_dev, s->tot.ptr,
+                 s->tile_cnt.ptr, s->ea.ptr, s->eb.ptr, s->es.ptr, s->ew.ptr, s->est.ptr, s->n_glob);
+    KARMA_HIP(hipStreamWaitEvent(s->main_s, s->ev_cols, 0));  // M: written beside classify, long done
+    KARMA_LAUNCH(ctx, "step_status", step_status_kernel, 1, 256, 0, v.flags, v.counters, v.ovf, v.B, v.dst, mbad,
+                 s->est.ptr, m_dev, s->ring_d + seq % kRing, seq);
+    s->pending.push_back({seq, store, rec, A});
+    return KARMA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, int kmode, int64_t n_glob,
+                      const int64_t* bounds, int nranks, int rank, karma_step** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && bounds && nranks >= 1 && nranks <= kMaxRuns && rank >= 0 && rank < nranks && n_glob >= 1,
+                KARMA_ERR_ARG, "karma_step_create: bad arguments (nranks %d, rank %d)", nranks, rank);
+    int world = 1, crank = 0;
+    if (comm) KARMA_TRY(karma_comm_info(comm, &world, &crank));
+    KARMA_CHECK(world == 1 || (world == nranks && crank == rank), KARMA_ERR_ARG,
+                "karma_step_create: communicator of %d ranks (rank %d) for %d owners (rank %d)", world, crank,
+                nranks, rank);
+    KARMA_CHECK(bounds[0] == 0 && bounds[nranks] == n_glob, KARMA_ERR_ARG, "owner bounds must span [0, n_glob)");
+    for (int r = 0; r < nranks; ++r)
+        KARMA_CHECK(bounds[r] <= bounds[r + 1], KARMA_ERR_ARG, "owner bounds must not decrease");
+    std::unique_ptr<karma_step> s(new karma_step());
+    s->ctx = ctx;
+    s->comm = world > 1 ? comm : nullptr;
+    s->scomm = world > 1 ? side_comm : nullptr;
+    s->kmode = kmode;
+    s->world = world;
+    s->rank = rank;
+    s->nranks = nranks;
+    s->emulate = world == 1 && nranks > 1 ? nranks : 0;
+    s->n_glob = n_glob;
+    s->bounds.assign(bounds, bounds + nranks + 1);
+    s->c_lo = bounds[rank];
+    s->n_loc = bounds[rank + 1] - bounds[rank];
+    s->exchange = nranks > 1;
+    int lo = 0, hi = 0;
+    KARMA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    // the main stream (the graph and the exchange) at high priority: its
+    // blocks dispatch first when CUs free up beside the side-stream profile
+    KARMA_HIP(hipStreamCreateWithPriority(&s->main_s, hipStreamNonBlocking, hi));
+    KARMA_HIP(hipStreamCreateWithPriority(&s->side_s, hipStreamNonBlocking, 0));
+    void *hm = nullptr, *dm = nullptr;
+    KARMA_TRY(ctx_mapped(ctx, kMapStep, kRing * sizeof(StepStatus), &hm, &dm));
+    KARMA_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->graves_h), kRing * 4 * 8, hipHostMallocDefault));
+    KARMA_HIP(hipEventCreateWithFlags(&s->ev_cols, hipEventDisableTiming));
+    {
+        hipStream_t prev = ctx->stream;
+        ctx->stream = s->main_s;
+        const int rc = s->m_ring.alloc(ctx, kRing);
+        ctx->stream = prev;
+        KARMA_TRY(rc);
+    }
+    s->ring_h = static_cast<StepStatus*>(hm);
+    s->ring_d = static_cast<StepStatus*>(dm);
+    std::memset(hm, 0, kRing * sizeof(StepStatus));
+    *out = s.release();
+    return KARMA_OK;
+}
+
+int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records, int64_t n_records, int flags,
+                   int64_t* info) {
+    KARMA_CHECK(s && store && (records || n_records == 0) && n_records >= 0, KARMA_ERR_ARG,
+                "karma_step_run: bad arguments");
+    KARMA_CHECK((flags & ~(KARMA_STEP_KEEP | KARMA_STEP_SEQUENTIAL | KARMA_STEP_DEFER)) == 0, KARMA_ERR_ARG,
+                "karma_step_run: unknown flags %d", flags);
+    karma_ctx* ctx = s->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    int64_t n_store = 0;
+    KARMA_TRY(karma_contigs_info(store, &n_store, nullptr, nullptr, nullptr));
+    KARMA_CHECK(n_store == s->n_loc, KARMA_ERR_ARG, "karma_step_run: the store holds %lld contigs, the shard %lld",
+                (long long)n_store, (long long)s->n_loc);
+    hipStream_t prev = ctx->stream;
+    ctx->stream = s->main_s;
+    const bool keep = flags & KARMA_STEP_KEEP, seq = flags & KARMA_STEP_SEQUENTIAL;
+    // deferred: one process (no collective needs a host count), nothing read back
+    const bool defer = (flags & KARMA_STEP_DEFER) && !keep && !seq && s->world == 1 && s->n_glob <= sets_max_contigs();
+    int rc = KARMA_OK;
+    if (defer && s->sticky_sync > 0) {
+        --s->sticky_sync;
+        rc = drain(s, false, true);
+        if (!rc) rc = run_sync(s, store, records, n_records, false, false, false);
+    } else if (defer) {
+        rc = drain(s, false, true);
+        if (!rc) rc = run_deferred(s, store, records, n_records);
+    } else {
+        rc = drain(s, true, false);  // earlier deferred steps complete and checked first
+        if (!rc) rc = run_sync(s, store, records, n_records, keep, seq, !(flags & KARMA_STEP_DEFER));
+    }
+    ctx->stream = prev;
+    if (rc) return rc;
+    if (info) {
+        info[0] = s->M;
+        info[1] = s->E;
+        info[2] = s->pairs_local;
+        info[3] = s->entries;
+    }
+    return KARMA_OK;
+}
+
+int karma_step_sync(karma_step* s) {
+    KARMA_CHECK(s, KARMA_ERR_ARG, "null step");
+    karma_ctx* ctx = s->ctx;
+    KARMA_TRY(ctx_begin(ctx));
+    hipStream_t prev = ctx->stream;
+    ctx->stream = s->main_s;
+    int rc = drain(s, true, false);
+    ctx->stream = prev;
+    KARMA_TRY(rc);
+    KARMA_HIP(hipStreamSynchronize(s->side_s));
+    KARMA_HIP(hipStreamSynchronize(s->main_s));
+    KARMA_TRY(bury(s, true));
+    if (s->edges && s->E < 0) KARMA_TRY(karma_edges_count(s->edges, &s->E));
+    return KARMA_OK;
+}
+
+int karma_step_info(karma_step* s, int64_t* info, int n) {
+    KARMA_CHECK(s && info && n >= 0, KARMA_ERR_ARG, "karma_step_info: bad arguments");
+    const int64_t v[] = {s->M, s->E, s->pairs_local, s->entries, s->n_sync, s->n_deferred, s->n_redone,
+                         (int64_t)s->pending.size()};
+    for (int i = 0; i < n && i < (int)(sizeof v / sizeof v[0]); ++i) info[i] = v[i];
+    return KARMA_OK;
+}
+
+// The profile of the newest step (a deferred one's once karma_step_sync has read its column count).
+int karma_step_profile(karma_step* s, double** dev, int64_t* rows, int64_t* M) {
+    KARMA_CHECK(s && dev && s->prof_M >= 0, KARMA_ERR_STATE, "karma_step_profile: no finished step");
+    *dev = s->prof.ptr;
+    if (rows) *rows = s->n_loc;
+    if (M) *M = s->prof_M;
+    return KARMA_OK;
+}
+
+int karma_step_columns(karma_step* s, uint64_t* keys_host) {
+    KARMA_CHECK(s && s->plan, KARMA_ERR_STATE, "karma_step_columns: no kept step");
+    KARMA_TRY(ctx_begin(s->ctx));
+    hipStream_t prev = s->ctx->stream;
+    s->ctx->stream = s->main_s;
+    const int rc = karma_kmer_columns(s->plan, keys_host);
+    s->ctx->stream = prev;
+    return rc;
+}
+
+int karma_step_edges(karma_step* s, karma_edges** e) {
+    KARMA_CHECK(s && e && s->edges, KARMA_ERR_STATE, "karma_step_edges: no kept step");
+    *e = s->edges;
+    return KARMA_OK;
+}
+
+int karma_step_destroy(karma_step* s) {
+    if (!s) return KARMA_OK;
+    hipSetDevice(s->ctx->device);
+    if (s->main_s) hipStreamSynchronize(s->main_s);
+    if (s->side_s) hipStreamSynchronize(s->side_s);
+    s->pending.clear();
+    s->E = 0;  // outputs dropped unread
+    drop_outputs(s);
+    bury(s, true);
+    for (auto& ev : s->grave_ev)
+        if (ev) hipEventDestroy(ev);
+    if (s->graves_h) hipHostFree(s->graves_h);
+    // the step's buffers return to the context's cache under streams about to
+    // be destroyed: release them first, then hand cached blocks to the context
+    s->prof.release();
+    s->m_ring.release();
+    if (s->ev_cols) hipEventDestroy(s->ev_cols);
+    s->mk.release();
+    s->mc.release();
+    s->mbad.release();
+    s->tot.release();
+    s->tile_cnt.release();
+    s->est.release();
+    s->ea.release();
+    s->eb.release();
+    s->es.release();
+    s->ew.release();
+    karma_ctx* ctx = s->ctx;
+    hipStream_t prev = ctx->stream;
+    if (prev == s->main_s || prev == s->side_s) ctx->stream = ctx->own_stream;
+    if (s->side_s) karma_stream_destroy(ctx, s->side_s);
+    if (s->main_s) karma_stream_destroy(ctx, s->main_s);
+    delete s;
+    return KARMA_OK;
+}
+
+}  // extern "C"

@@ -32,9 +32,11 @@ import os
 
 import numpy as np
 
+import ctypes
+
 from . import _lib
-from ._lib import DevBuf, Stream
-from .comm import SoloComm
+from ._lib import DevBuf, Stream, call, ptr
+from .comm import RcclComm, SoloComm
 
 
 class HipOps:
@@ -217,6 +219,81 @@ class HipOps:
         self.stream.close()
 
 
+class NativeStep:
+    """One step as one C ABI call (karma_step, csrc/step.hip): the sequence
+    ShardedBuild._run drives from Python, natively, with the library's RCCL
+    communicators (main and side) or none.  A step whose outputs are not read
+    (count=False) in one process returns without waiting for anything."""
+
+    def __init__(self, ctx, comm, kmode, n_glob, bounds, rank, n_loc):
+        self.ctx, self.n_glob = ctx, n_glob
+        b = np.ascontiguousarray(bounds, np.int64)
+        assert int(b[rank + 1] - b[rank]) == n_loc, "the owner bounds disagree with this rank's contig shard"
+        multi = comm.world > 1
+        h = ctypes.c_void_p()
+        call("karma_step_create", ctx.h, comm.h if multi else None, comm.side.h if multi else None, int(kmode),
+             int(n_glob), ptr(b), len(b) - 1, int(rank), ctypes.byref(h))
+        self.h = h
+        self._info = np.zeros(4, np.int64)
+
+    def run(self, store, records, n_records, keep=False, sequential=False, count=True):
+        flags = (_lib.KARMA_STEP_KEEP if keep else 0) | (_lib.KARMA_STEP_SEQUENTIAL if sequential else 0) | \
+            (_lib.KARMA_STEP_DEFER if not count and not keep else 0)
+        info = self._info
+        call("karma_step_run", self.h, store.h, ctypes.c_void_p(records), int(n_records), flags, ptr(info))
+        M, E = int(info[0]), int(info[1])
+        stats = {"M": M if M >= 0 else None, "E_local": E if E >= 0 else None}
+        if keep:
+            from .engine import EdgeArrays
+
+            stats["pairs_local"], stats["entries"] = int(info[2]), int(info[3])
+            dev, rows = ctypes.c_void_p(), ctypes.c_int64()
+            call("karma_step_profile", self.h, ctypes.byref(dev), ctypes.byref(rows), None)
+            stats["profile"] = DevBuf(self.ctx, (rows.value, M), np.float64, _ptr=dev.value or 0, _owner=self)
+            keys = np.zeros(max(M, 1), np.uint64)
+            call("karma_step_columns", self.h, ptr(keys))
+            stats["columns"] = keys[:M]
+            eh = ctypes.c_void_p()
+            call("karma_step_edges", self.h, ctypes.byref(eh))
+            a, b = np.zeros(max(E, 1), np.uint32), np.zeros(max(E, 1), np.uint32)
+            s, w = np.zeros(max(E, 1), np.int64), np.zeros(max(E, 1), np.float64)
+            call("karma_edges_get", eh, ptr(a), ptr(b), ptr(s), ptr(w), None, 0)
+            tot = np.zeros(max(self.n_glob, 1), np.int64)
+            call("karma_edges_totals", eh, ptr(tot), 0)
+            stats["edges"] = EdgeArrays(a[:E], b[:E], s[:E], w[:E], np.zeros(E, np.uint64), tot[:self.n_glob])
+        return stats
+
+    def sync(self):
+        call("karma_step_sync", self.h)
+
+    def profile(self):
+        """The newest step's profile (device, rows x M) after sync(): deferred steps included."""
+        dev, rows, M = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int64()
+        call("karma_step_profile", self.h, ctypes.byref(dev), ctypes.byref(rows), ctypes.byref(M))
+        return DevBuf(self.ctx, (rows.value, M.value), np.float64, _ptr=dev.value or 0, _owner=self)
+
+    def info(self):
+        """[M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending]."""
+        v = np.zeros(8, np.int64)
+        call("karma_step_info", self.h, ptr(v), 8)
+        return v
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.load().karma_step_destroy(self.h)
+            self.h = None
+
+
+def native_step_on(comm, ops, overlap):
+    """The native step runs the production path (the library's own kernels and
+    RCCL communicators); the Python driver stays for an injected compute backend
+    (tests/test_distributed_cpu.py), the host-staged rehearsal transport
+    (HostComm) and the opt-in concurrent graph build."""
+    if ops is not None or overlap or os.environ.get("KARMA_NATIVE_STEP", "1") == "0":
+        return False
+    return isinstance(comm, (SoloComm, RcclComm))
+
+
 class ShardedBuild:
     """k-mer profile + shared-read graph over contig/fragment shards."""
 
@@ -226,7 +303,11 @@ class ShardedBuild:
         # --emulate-ranks W): the exchange's local work runs -- split at the W
         # owners' bounds, merge of W sorted slices, totals -- its collectives do not
         self.emulate = emulate_ranks if comm.world == 1 and emulate_ranks > 1 else 0
-        self.ops = ops if ops is not None else HipOps(ctx)
+        if overlap is None:
+            overlap = ops is None and os.environ.get("KARMA_OVERLAP", "0") == "1"
+        self.native = None
+        native = native_step_on(comm, ops, overlap)
+        self.ops = ops if ops is not None else (None if native else HipOps(ctx))
         self._prof = None
         # The local graph build (records -> pair list) shares nothing with the
         # k-mer profile: with overlap it runs from a worker thread on a second
@@ -234,8 +315,6 @@ class ShardedBuild:
         # stays on this thread, in the same order on every rank.
         # Off by default: sharing the chip stretches both kernels, which blurs
         # per-kernel measurement for ~2.5 % of step time.
-        if overlap is None:
-            overlap = ops is None and os.environ.get("KARMA_OVERLAP", "0") == "1"
         self.gctx = self.gops = self._pool = None
         if overlap:
             from concurrent.futures import ThreadPoolExecutor
@@ -258,11 +337,25 @@ class ShardedBuild:
         if comm.world > 1:
             self.split_bounds = bounds
         elif self.emulate:
-            self.split_bounds = np.linspace(0, n_glob, self.emulate + 1).astype(np.int64)
+            # the W owners' contig ranges, rank 0's first (bench.py shard())
+            self.split_bounds = np.array([n_glob * r // self.emulate for r in range(self.emulate + 1)], np.int64)
+        if native:
+            own = self.split_bounds if self.split_bounds is not None else np.array([0, n_glob], np.int64)
+            self.native = NativeStep(ctx, comm, kmode, n_glob, own, comm.rank if comm.world > 1 else 0, n_loc)
+        self._ctx = ctx
 
     def contexts(self):
         """The karma contexts this build launches on (per-kernel timing)."""
+        if self.native is not None:
+            return [self._ctx]
         return [c for c in (self.ops.ctx if hasattr(self.ops, "ctx") else None, self.gctx) if c is not None]
+
+    def sync(self):
+        """Wait for every step enqueued so far (and check deferred ones)."""
+        if self.native is not None:
+            self.native.sync()
+        for c in self.contexts():
+            c.sync()
 
     def run(self, store, records, n_records, keep=False, sequential=False, count=True):
         """One step.  sequential=True keeps the profile on the main stream (no
@@ -271,6 +364,8 @@ class ShardedBuild:
         of identical steps; with an exchange only): the owner's edge count is
         not read back, so the step ends without waiting for its last kernels,
         and stats["E_local"] is None."""
+        if self.native is not None:
+            return self.native.run(store, records, n_records, keep=keep, sequential=sequential, count=count)
         ops = self.ops
         # Default order (one stream pair): k-mer columns, then the graph's
         # kernels alone on the chip (classify .. final), then the profile on
@@ -407,6 +502,9 @@ class ShardedBuild:
 
     def close(self):
         self._prof = None
+        if self.native is not None:
+            self.native.close()
+            self.native = None
         if hasattr(self.ops, "shutdown"):
             self.ops.shutdown()
         if self.gops is not None:

@@ -26,3 +26,24 @@ def test_comm_sources_use_the_guarded_group():
     src = open(os.path.join(CSRC, "comm.hip")).read()
     assert "ncclGroupStart" not in src and "ncclGroupEnd" not in src
     assert src.count("NcclGroup g;") == 3  # count exchange, alltoallv, alltoallv_kv
+
+
+def test_fake_rccl_double_builds_and_exports_the_bound_entry_points():
+    """tools/fake_rccl/librccl.so.1 (the multi-rank test double, GPU tests only)
+    provides every RCCL symbol libkarma_hip.so imports, under RCCL's soname."""
+    import ctypes
+    import subprocess
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(repo, "karma_amd", "csrc"), "fake_rccl"], check=True)
+    fake = os.path.join(repo, "tools", "fake_rccl", "librccl.so.1")
+    lib = ctypes.CDLL(fake)
+    assert lib.fake_rccl_marker() == 0x7ACE
+    need = subprocess.run(["nm", "-D", "--undefined-only", os.path.join(repo, "karma_amd", "libkarma_hip.so")],
+                          capture_output=True, text=True, check=True).stdout
+    imported = sorted({ln.split()[-1] for ln in need.splitlines() if " nccl" in ln or ln.split()[-1].startswith("nccl")})
+    assert len(imported) >= 10
+    for name in imported:
+        assert hasattr(lib, name), name
+    soname = subprocess.run(["readelf", "-d", fake], capture_output=True, text=True, check=True).stdout
+    assert "librccl.so.1" in soname

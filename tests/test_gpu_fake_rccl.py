@@ -1,0 +1,100 @@
+"""The library's RCCL communicator at world size > 1 on a one-GPU box.
+
+RCCL refuses several ranks on one device, so these tests start a child process
+(tests/fake_rccl_ranks.py) whose ranks are threads sharing cuda:0 and whose
+librccl.so.1 is tools/fake_rccl/ (a host-staged test double of the RCCL entry
+points, ahead of ROCm's in LD_LIBRARY_PATH; libkarma_hip.so itself is the
+shipped build, unchanged).  What runs is the product's multi-GPU code --
+karma_amd/comm.py RcclComm and csrc/comm.hip, the side-stream communicator,
+the sharded driver -- so the only piece left unverified before a real
+multi-GPU run is RCCL's own transport.  The child refuses to run (exit 3) if
+the fake is not the librccl it loaded."""
+import json
+import os
+import subprocess
+import sys
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+
+import digests as D
+from karma_amd import engine
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAKE_DIR = os.path.join(REPO, "tools", "fake_rccl")
+
+
+def run_child(*args, timeout=240):
+    assert os.path.exists(os.path.join(FAKE_DIR, "librccl.so.1")), \
+        "tools/fake_rccl/librccl.so.1 not built (make -C karma_amd/csrc fake_rccl)"
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = FAKE_DIR + (":" + env["LD_LIBRARY_PATH"] if env.get("LD_LIBRARY_PATH") else "")
+    r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "tests", "fake_rccl_ranks.py"), *args],
+                       capture_output=True, text=True, timeout=timeout, cwd=REPO, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, f"rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
+    out = json.loads(lines[-1])
+    assert out["fake_rccl_loaded"], "the child did not load tools/fake_rccl/librccl.so.1"
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_rccl_comm_collectives_unequal_sizes(world):
+    """Every RcclComm call with unequal per-rank sizes: host scalars, the fixed
+    all-gather, the padded variable all-gather on the side communicator (rank 0
+    empty), unequal and equal (in place) totals slices, the count exchange and
+    the grouped key/count all-to-all-v (some slices empty)."""
+    out = run_child("--case", "collectives", "--world", str(world))
+    assert out["errors"] == []
+
+
+def test_rccl_sharded_build_three_unequal_ranks_match_oracle(tmp_path):
+    """The sharded build through RcclComm at world 3 with unequal contig shards
+    and N-injected contigs (exception keys on every rank), two stream steps then
+    a kept one: the union must equal the single-process oracle bit for bit."""
+    sizes, frags, seed = [700, 831, 962], 150_000, 29
+    run_child("--case", "oracle", "--world", "3", "--sizes", ",".join(map(str, sizes)), "--frags", str(frags),
+              "--seed", str(seed), "--out", str(tmp_path))
+    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(3)]
+    n_glob = sum(sizes)
+    seqs, recs = OrderedDict(), []
+    genes = engine.synth_genes(seed, n_glob)
+    lo = 0
+    for r in range(3):
+        blob, offs, _ = engine.synth_contigs(seed, sizes[r], 30, 900, 300, first=lo)
+        for i in range(sizes[r]):
+            seqs[f">ctg{lo + i}"] = bytes(blob[offs[i]:offs[i + 1]]).decode()
+        lo += sizes[r]
+        recs.append(engine.synth_records(seed, n_glob, frags * r // 3, frags * (r + 1) // 3, True, genes=genes))
+    prof, cols, _ = oracle.calc_kmer_profile(seqs, "5p6")
+    for p in parts:
+        assert engine.decode_keys(p["cols"], -1) == cols
+    got = np.concatenate([p["profile"] for p in parts])
+    assert np.array_equal(got.view(np.uint64), prof.view(np.uint64))
+    rec = np.concatenate(recs).astype(np.int64)
+    st = np.flatnonzero(np.r_[True, rec[1:, 0] != rec[:-1, 0]])
+    o = oracle.graph_groups(np.r_[st, len(rec)], rec[:, 1], None, None, n_glob, dedup=True)
+    a = np.concatenate([p["a"] for p in parts])
+    b = np.concatenate([p["b"] for p in parts])
+    w = np.concatenate([p["w"] for p in parts])
+    assert np.array_equal(a, o["a"]) and np.array_equal(b, o["b"])
+    assert np.array_equal(w.view(np.uint64), o["weight"].view(np.uint64))
+    for p in parts:
+        assert np.array_equal(p["tot"], o["totals"])
+
+
+def test_rccl_config4_strong_8_ranks_digests():
+    """BASELINE configs[3] through the library's RCCL communicator: config 3
+    split over 8 ranks (bench.py's strong workload), the union of the ranks'
+    outputs against digests.json config3 (the oracle's digests, which the
+    reference's own config-3 outputs also match)."""
+    g = D.load()["config3"]
+    out = run_child("--case", "config4", "--world", "8", timeout=600)
+    assert out["M"] == [g["M"]] and out["columns"] == [g["columns"]]
+    assert out["profile_rows"] == g["profile_rows"]
+    assert out["edges"] == g["edges"]
+    assert out["totals_equal"] and out["owners_ok"]

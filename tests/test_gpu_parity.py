@@ -339,7 +339,9 @@ def test_profile_presence_two_phase(kmer, n_rate):
 
 
 @pytest.mark.parametrize("seed,n_runs,n", [(61, 8, 2_000_000), (62, 3, 5000), (63, 1, 17), (64, 5, 0),
-                                           (65, 2, 1)])
+                                           (65, 2, 1),
+                                           # past 64 runs: ranking merges of 64-run groups, level by level
+                                           (66, 100, 300_000), (67, 300, 40_000), (68, 65, 65)])
 def test_merge_runs_and_split(seed, n_runs, n):
     # the exchange owner's merge of sorted per-sender slices
     # (karma_pairs_merge_runs: merge tree + sum of equal keys) equals numpy and

@@ -1,0 +1,186 @@
+"""The native step (karma_step, csrc/step.hip) against the oracle.
+
+karma_amd/distributed.py ShardedBuild drives the library's karma_step for the
+production path (one GPU, an emulated rank, RCCL ranks).  Its deferred steps
+(outputs not read: count=False) wait for nothing: M, the records job's control
+block and the tail's sizes stay on the device, a status kernel reports the
+checks through mapped memory, and a step whose checks call for the general
+path (relabelled contigs, bucket overflow, reads of > 8 records) runs again
+synchronously.  Here: deferred steps, then sync, then the profile of the
+newest deferred step and a kept step -- all bit-exact against the oracle --
+and the slow paths and errors seen through the deferred checks."""
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+
+from karma_amd import _lib, engine
+from karma_amd.comm import SoloComm
+from karma_amd.distributed import ShardedBuild
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+SEED = 41
+
+
+def contigs(n, c_lo=0, n_rate=300):
+    blob, offs, key_len = engine.synth_contigs(SEED, n, 30, 900, n_rate, first=c_lo)
+    return blob, offs, key_len
+
+
+def oracle_graph(rec, n):
+    rs = np.asarray(rec, np.int64)
+    st = np.flatnonzero(np.r_[True, rs[1:, 0] != rs[:-1, 0]]) if len(rs) else np.zeros(0, np.int64)
+    return oracle.graph_groups(np.r_[st, len(rs)], rs[:, 1] if len(rs) else np.zeros(0), None, None, n, dedup=True)
+
+
+def oracle_profile(blob, offs, c_lo, n):
+    seqs = OrderedDict((f">ctg{c_lo + i}", bytes(blob[offs[i]:offs[i + 1]]).decode()) for i in range(n))
+    prof, cols, _ = oracle.calc_kmer_profile(seqs, "5p6")
+    return prof, cols
+
+
+class Run:
+    def __init__(self, n_glob, rec, emulate=1):
+        self.ctx = _lib.Context(0)
+        self.n_glob = n_glob
+        n_loc = n_glob // emulate if emulate > 1 else n_glob
+        self.n_loc = n_loc
+        self.blob, self.offs, kl = contigs(n_loc)
+        self.build = ShardedBuild(self.ctx, SoloComm(), -1, n_glob, 0, n_loc, emulate_ranks=emulate)
+        assert self.build.native is not None, "the native step drives the production path"
+        self.store = engine.ContigStore(self.ctx, self.blob, self.offs, kl)
+        self.rec = np.ascontiguousarray(rec)
+        self.dev = _lib.DevBuf.from_numpy(self.ctx, self.rec.view(np.int64).reshape(-1))
+
+    def step(self, **kw):
+        return self.build.run(self.store, self.dev.ptr, len(self.rec), **kw)
+
+    def close(self):
+        self.build.close()
+        self.store.close()
+        self.dev.close()
+        self.ctx.close()
+
+
+def check_edges(e, o):
+    assert np.array_equal(e.a, o["a"]) and np.array_equal(e.b, o["b"])
+    assert np.array_equal(e.shared, o["shared"])
+    assert np.array_equal(e.weight.view(np.uint64), o["weight"].view(np.uint64))
+    assert np.array_equal(e.totals, o["totals"])
+
+
+@pytest.mark.parametrize("emulate", [1, 3])
+def test_deferred_steps_then_kept_step_match_oracle(emulate):
+    n = 3000 if emulate == 1 else 3001  # 3001 / 3: owner bounds that do not divide evenly
+    rec = engine.synth_records(SEED, n, 0, 300_000, True)
+    r = Run(n, rec, emulate)
+    try:
+        calls0 = _lib.api_calls()
+        for _ in range(4):
+            res = r.step(count=False)
+            assert res["E_local"] is None
+        r.build.sync()
+        info = r.build.native.info()
+        assert info[5] == 4 and info[6] == 0, info  # 4 deferred steps, none run again
+        # the newest deferred step's profile (M read by the kernels on the device)
+        prof_o, cols_o = oracle_profile(r.blob, r.offs, 0, r.n_loc)
+        got = r.build.native.profile().numpy()
+        assert got.shape == prof_o.shape
+        assert np.array_equal(got.view(np.uint64), prof_o.view(np.uint64))
+        # a deferred step makes at most ~40 HIP calls, never a host wait
+        assert (_lib.api_calls() - calls0) / 4 < 60
+        res = r.step(keep=True)
+        assert engine.decode_keys(res["columns"], -1) == cols_o
+        assert np.array_equal(res["profile"].numpy().view(np.uint64), prof_o.view(np.uint64))
+        check_edges(res["edges"], oracle_graph(rec, n))
+        assert res["E_local"] == len(res["edges"].a)
+    finally:
+        r.close()
+
+
+def test_deferred_steps_slow_path_runs_again():
+    """Shuffled contig ids (most reads leave the compact path: the relabel vote)
+    plus reads of > 8 records: the deferred step's status calls for the general
+    path and the step runs again synchronously; the next deferred steps run
+    synchronously for a while; results stay exact."""
+    n = 4000
+    rec = np.ascontiguousarray(engine.synth_records(SEED, n, 0, 200_000, True))
+    perm = np.random.default_rng(3).permutation(n).astype(np.uint32)
+    rec[:, 1] = perm[rec[:, 1]]
+    rng = np.random.default_rng(4)
+    r0 = int(rec[-1, 0]) + 1
+    big = np.array([(r0 + i, int(c)) for i in range(200) for c in rng.integers(0, n, 12)], np.uint32)
+    rec = np.concatenate([rec, big])
+    r = Run(n, rec)
+    try:
+        for _ in range(3):
+            r.step(count=False)
+        r.build.sync()
+        info = r.build.native.info()
+        assert info[6] >= 1, info  # run again on the general path
+        res = r.step(keep=True)
+        check_edges(res["edges"], oracle_graph(rec, n))
+    finally:
+        r.close()
+
+
+def test_deferred_step_bucket_overflow_runs_again():
+    rng = np.random.default_rng(1)
+    R = 60_000
+    reads = np.repeat(np.arange(R, dtype=np.uint32), 8)
+    cs = rng.integers(0, 1000, R * 8).astype(np.uint32)
+    rec = np.stack([reads, cs], 1)
+    r = Run(1000, rec)
+    try:
+        r.step(count=False)
+        r.build.sync()
+        assert r.build.native.info()[6] == 1
+        res = r.step(keep=True)
+        check_edges(res["edges"], oracle_graph(rec, 1000))
+    finally:
+        r.close()
+
+
+def test_deferred_step_unsorted_records_error_reported():
+    rec = engine.synth_records(SEED, 2000, 0, 50_000, True)
+    shuf = rec[np.random.default_rng(0).permutation(len(rec))]
+    r = Run(2000, shuf)
+    try:
+        r.step(count=False)  # returns at once; the error arrives with the deferred check
+        with pytest.raises(_lib.KarmaError) as ei:
+            r.build.sync()
+        assert ei.value.code == _lib.KARMA_ERR_UNSORTED
+    finally:
+        r.close()
+
+
+def test_native_step_equals_python_driver():
+    """The native step and the Python driver (HipOps, kept for the host-staged
+    rehearsal transport) give the same bytes, one GPU and an emulated rank."""
+    from karma_amd.distributed import HipOps
+
+    n = 2500
+    rec = engine.synth_records(SEED + 1, n, 0, 150_000, True)
+    for emulate in (1, 4):
+        outs = []
+        for python in (False, True):
+            ctx = _lib.Context(0)
+            n_loc = n // emulate
+            blob, offs, kl = contigs(n_loc)
+            b = ShardedBuild(ctx, SoloComm(), -1, n, 0, n_loc, ops=HipOps(ctx) if python else None,
+                             emulate_ranks=emulate)
+            assert (b.native is None) == python
+            st = engine.ContigStore(ctx, blob, offs, kl)
+            d = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))
+            res = b.run(st, d.ptr, len(rec), keep=True)
+            e = res["edges"]
+            outs.append([res["profile"].numpy(), np.asarray(res["columns"]), e.a, e.b, e.shared, e.weight, e.totals,
+                         np.array([res["M"], res["E_local"], res["entries"], res["pairs_local"]])])
+            b.close()
+            st.close()
+            d.close()
+            ctx.close()
+        for x, y in zip(*outs):
+            assert x.shape == y.shape and np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
