@@ -162,8 +162,8 @@ class Leg:
             for c in self.ctxs:
                 c.timing(True)
                 c.timing_reset()
-            for _ in range(steps):
-                self.step(sequential=True)
+            for _ in range(steps):  # the same kernels as the timed steps (deferred where they are)
+                self.step(sequential=True, count=False)
             self.sync_all()
             for c in self.ctxs:
                 for name, (ms, nl) in c.timing_read().items():
@@ -347,6 +347,7 @@ def main():
                 "traffic": traffic, "bytes_per_launch": b,
                 "intermediate_bytes_per_launch": intermediate_bytes.get(dom, 0),
                 "avg_launch_ms": round(ms / nl, 4), "launches": nl}
+    write_ceiling = profile_write_ceiling(ctx, leg, n_loc, M, kern, args.steps)
     step_bytes = leg.packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
     host_us, api_calls = leg.host_us_per_step, leg.api_calls_per_step
     si = leg.step_info
@@ -412,6 +413,7 @@ def main():
             "parity": parity["parity"] if parity else None,
             "parity_detail": parity,
             "roofline": roof,
+            "profile_write_ceiling": write_ceiling,
             "step": {"hbm_bytes_per_gpu": step_bytes, "achieved_GBs": round(step_bytes / step_s / 1e9, 1),
                      "frac": round(step_bytes / step_s / 1e9 / PEAK_HBM_GBS, 4),
                      "formula": "sum ceil(L/4) + 8*N*M + 8*A + 16*E + 8*N (SURVEY.md 8(d))"},
@@ -430,6 +432,33 @@ def main():
         print(json.dumps(line), flush=True)
     comm.close()
     ctx.close()
+
+
+def profile_write_ceiling(ctx, leg, n_loc, M, kern, steps):
+    """The profile's write rate against this device's own ceiling for the same
+    buffer, measured in this process: hipMemsetAsync of the N x M x 8 bytes
+    (karma_memset_timed, HIP events).  The profile is write-bound (its counting
+    hides under the row writes), so memset is the bar."""
+    import ctypes
+
+    from karma_amd import _lib
+
+    nbytes = 8 * n_loc * M
+    if not nbytes or "kmer_profile" not in kern:
+        return None
+    buf = _lib.DevBuf(ctx, (nbytes,), np.uint8)
+    ms = ctypes.c_double(0)
+    try:
+        _lib.call("karma_memset_timed", ctx.h, ctypes.c_void_p(buf.ptr), nbytes, 10, ctypes.byref(ms))
+    finally:
+        buf.close()
+    prof_ms = kern["kmer_profile"][0] / kern["kmer_profile"][1]
+    ceil = nbytes / (ms.value / 1e3) / 1e9
+    rate = nbytes / (prof_ms / 1e3) / 1e9
+    return {"bytes": nbytes, "memset_ms": round(ms.value, 4), "write_ceiling_GBs": round(ceil, 1),
+            "profile_ms": round(prof_ms, 4), "profile_write_GBs": round(rate, 1),
+            "profile_vs_ceiling": round(rate / ceil, 3),
+            "note": "profile time from the sequential per-kernel pass; memset of the same bytes, same process"}
 
 
 def reference_measured(config):

@@ -95,6 +95,9 @@ int karma_memcpy(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int k
  * must stay valid until the stream reaches the copy). */
 int karma_memcpy_async(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
 int karma_memset_async(karma_ctx* ctx, void* dst, int value, size_t bytes);
+/* Average ms of `reps` hipMemsetAsync of `bytes` at dst (HIP events on the
+ * context's stream): the device's write ceiling for a buffer of that size. */
+int karma_memset_timed(karma_ctx* ctx, void* dst, size_t bytes, int reps, double* ms);
 /* Streams owned by the library (a side stream for the profile, a high-priority
  * main stream); priority: 0 normal, < 0 higher (hipStreamCreateWithPriority). */
 int karma_stream_create(karma_ctx* ctx, int priority, void** stream);
@@ -322,8 +325,9 @@ int karma_edges_totals(karma_edges* e, int64_t* totals, int is_device);
  * host-staged rehearsal transport).
  * comm: the main-stream communicator (NULL or world 1: one process);
  * side_comm: the column-set exchange's communicator (KARMA_COMM_SIDE; NULL: comm).
- * bounds[nranks + 1]: owner contig ranges; this rank's store holds
- * [bounds[rank], bounds[rank + 1]).  One process with nranks > 1 emulates
+ * bounds[nranks + 1]: owner contig ranges tiling [0, n_glob); this rank's store
+ * holds [bounds[rank], bounds[rank + 1]) (nranks = 1: any shard of the n_glob
+ * contig ids, no exchange).  One process with nranks > 1 emulates
  * rank `rank` of an nranks-rank job (the exchange's local work, no collectives).
  * The step owns two streams; inputs stay on the device (records: n x {u32 read,
  * u32 contig}, grouped by read). */
@@ -331,7 +335,7 @@ typedef struct karma_step karma_step;
 #define KARMA_STEP_KEEP 1       /* outputs kept for karma_step_profile / _columns / _edges */
 #define KARMA_STEP_SEQUENTIAL 2 /* every kernel on the main stream (per-kernel timing) */
 #define KARMA_STEP_DEFER 4      /* outputs not read: one process returns without waiting for anything (the
-                                 * step's checks arrive through mapped memory and are read <= 2 steps later;
+                                 * step's checks arrive through mapped memory and are read <= 3 steps later;
                                  * a step needing the general path runs again synchronously); with several
                                  * ranks the edge count is not read back.  Inputs must stay valid until the
                                  * next non-deferred step or karma_step_sync. */

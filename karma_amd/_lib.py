@@ -64,6 +64,7 @@ _SIGS = {
     "karma_memcpy": [_c_p, _c_p, _c_p, ctypes.c_size_t, _i32],
     "karma_memcpy_async": [_c_p, _c_p, _c_p, ctypes.c_size_t, _i32],
     "karma_memset_async": [_c_p, _c_p, _i32, ctypes.c_size_t],
+    "karma_memset_timed": [_c_p, _c_p, ctypes.c_size_t, _i32, ctypes.POINTER(ctypes.c_double)],
     "karma_stream_create": [_c_p, _i32, _PP],
     "karma_stream_destroy": [_c_p, _c_p],
     "karma_stream_sync": [_c_p, _c_p],

@@ -137,7 +137,7 @@ static constexpr int64_t kMapCap[kMapSlots] = {
     16 * 1024 + 256,   // split: nranks <= 1023
     256,               // merge status
     256,               // edge status
-    4096,              // step status
+    8192,              // step status (64 entries of 64 B) and column counts (64 x 8 B)
     8 * 1024,          // side communicator scalars
 };
 
@@ -360,6 +360,28 @@ int karma_memcpy_async(karma_ctx* ctx, void* dst, const void* src, size_t bytes,
     if (!bytes) return KARMA_OK;
     hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     KARMA_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->stream));
+    return KARMA_OK;
+}
+
+// The write ceiling of this device for a buffer of `bytes`: hipMemsetAsync
+// timed with events on the context's stream (bench.py reports the profile's
+// write rate against it, measured in the same process).
+int karma_memset_timed(karma_ctx* ctx, void* dst, size_t bytes, int reps, double* ms) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(dst && ms && reps >= 1, KARMA_ERR_ARG, "karma_memset_timed: bad arguments");
+    hipEvent_t a, b;
+    KARMA_HIP(hipEventCreate(&a));
+    KARMA_HIP(hipEventCreate(&b));
+    KARMA_HIP(hipMemsetAsync(dst, 0, bytes, ctx->stream));  // warm
+    KARMA_HIP(hipEventRecord(a, ctx->stream));
+    for (int r = 0; r < reps; ++r) KARMA_HIP(hipMemsetAsync(dst, r & 1, bytes, ctx->stream));
+    KARMA_HIP(hipEventRecord(b, ctx->stream));
+    KARMA_HIP(hipEventSynchronize(b));
+    float t = 0.f;
+    KARMA_HIP(hipEventElapsedTime(&t, a, b));
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    *ms = t / reps;
     return KARMA_OK;
 }
 

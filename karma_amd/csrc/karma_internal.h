@@ -210,7 +210,7 @@ int reduce_sorted(karma_ctx* ctx, const uint64_t* keys, const uint32_t* perm, co
 
 // k-mer plan internals for karma_step (kmer.hip)
 int64_t kmer_m_cap(const karma_kmer_plan* p);
-int kmer_finalize_device(karma_kmer_plan* p, int64_t* m_out);
+int kmer_finalize_device(karma_kmer_plan* p, int64_t* m_out, int64_t* m_host);
 int kmer_profile_device_m(karma_kmer_plan* p, double* out_dev, const int64_t* m_dev);
 int kmer_set_m(karma_kmer_plan* p, int64_t M);
 // graph.hip: a pending edge stage's status words (see karma_edges_end), handed over

@@ -424,7 +424,8 @@ __global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* __re
                                                             const uint64_t* __restrict__ exc, int64_t X,
                                                             int32_t* __restrict__ col_of_ord,
                                                             int32_t* __restrict__ col_of_exc,
-                                                            uint64_t* __restrict__ col_keys, int64_t* __restrict__ M_out) {
+                                                            uint64_t* __restrict__ col_keys, int64_t* __restrict__ M_out,
+                                                            int64_t* __restrict__ M_host) {
     extern __shared__ __attribute__((aligned(16))) uint32_t prefix[];  // nwords + 1
     // exclusive popcount prefix over the bitmap (nwords <= 2048)
     __shared__ uint32_t chunk_sum[kColBlock];
@@ -488,7 +489,11 @@ __global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* __re
         col_of_exc[x] = (int32_t)col;
         col_keys[col] = key;
     }
-    if (threadIdx.x == 0) *M_out = (int64_t)n_present + X;
+    if (threadIdx.x == 0) {
+        *M_out = (int64_t)n_present + X;
+        // karma_step: also into mapped host memory, read there once the step is done
+        if (M_host) __hip_atomic_store(M_host, (int64_t)n_present + X, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // -------------------------------------------------------------- profile ------
@@ -1184,7 +1189,7 @@ int karma_kmer_plan_finalize_async(karma_kmer_plan* p) {
     const size_t lds = (p->nwords + 1) * 4;
     KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->presence.ptr, (int)p->nwords, S,
                  p->kmode == KARMA_KMER_5P6, p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode, with_len, p->exc_keys.ptr,
-                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, p->m_dev.ptr);
+                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, p->m_dev.ptr, (int64_t*)nullptr);
     if (!ctx->fin_pinned) KARMA_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->fin_pinned), 64, hipHostMallocDefault));
     KARMA_HIP(hipMemcpyAsync(ctx->fin_pinned, p->m_dev.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
     if (!p->fin_ev) KARMA_HIP(hipEventCreateWithFlags(&p->fin_ev, hipEventDisableTiming));
@@ -1202,7 +1207,7 @@ namespace karma {
 // The column table without M's readback (karma_step's deferred steps): M is
 // written to m_out on the device (the caller's word) for the profile kernels;
 // the host learns it later.
-int kmer_finalize_device(karma_kmer_plan* p, int64_t* m_out) {
+int kmer_finalize_device(karma_kmer_plan* p, int64_t* m_out, int64_t* m_host) {
     karma_ctx* ctx = p->ctx;
     KARMA_TRY(ctx_begin(ctx));
     int kmin, kmax;
@@ -1216,7 +1221,7 @@ int kmer_finalize_device(karma_kmer_plan* p, int64_t* m_out) {
     const size_t lds = (p->nwords + 1) * 4;
     KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->presence.ptr, (int)p->nwords, S,
                  p->kmode == KARMA_KMER_5P6, p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode, with_len, p->exc_keys.ptr,
-                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, m_out);
+                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, m_out, m_host);
     return KARMA_OK;
 }
 

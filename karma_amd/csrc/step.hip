@@ -29,6 +29,7 @@
 //                path is run again synchronously (the same work the
 //                synchronous path would have done), an error is returned.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -42,7 +43,7 @@ using namespace karma;
 namespace {
 
 constexpr int kRing = 64;  // status entries in the mapped slot (64 B each)
-constexpr int kLag = 2;    // deferred steps the host may run ahead of the device
+constexpr int kLag = 3;    // deferred steps the host may have in flight (two main streams alternate)
 
 // One deferred step's status, written by step_status_kernel (seq last).
 struct StepStatus {
@@ -51,8 +52,7 @@ struct StepStatus {
     int64_t err;    // bits: 1 unsorted records, 2 contig range, 4 partition check, 8 zero total, 16 merge order
     int64_t U;      // pairs of the local list
     int64_t E;      // edges
-    int64_t M;      // columns
-    int64_t pad[2];
+    int64_t pad[3];
 };
 static_assert(sizeof(StepStatus) == 64, "status entry");
 
@@ -198,8 +198,10 @@ __global__ void __launch_bounds__(kET) step_edge_write_kernel(
 // 5 dependent loads), stages the windows in LDS, and places every element at
 // its rank in its own run plus its rank in each other run (stable: equal keys
 // of different runs end up adjacent, in run order).
-constexpr int kMT = 1024;       // tile elements
-constexpr int kMLds = 6144;     // staged window keys
+constexpr int64_t kAltMaxRecords = int64_t(1) << 27;  // batches below this alternate main streams
+constexpr int kMT = 512;        // tile elements (1024: 7 windows of ~1024 keys overflowed the stage)
+constexpr int kMLds = 8192;     // staged window keys
+constexpr int kMFast = 8;       // up to this many runs: every element's searches run in lockstep
 constexpr int kMG = 16;         // lanes per bound search
 struct RunSrc {
     int nr, B, bw;
@@ -228,6 +230,7 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
     __shared__ int64_t ro[kMaxRuns + 1], rt[kMaxRuns + 1];
     __shared__ int64_t wlo[kMaxRuns], whi[kMaxRuns];
     __shared__ int wbase[kMaxRuns];
+    __shared__ int all_fit;
     __shared__ uint64_t wkeys[kMLds];
     const int nr = rs.nr;
     const int64_t U = dst[rs.B];
@@ -257,10 +260,17 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
         for (int q0 = 0; q0 < 2 * nr; q0 += 256 / kMG) {
             const int q = q0 + grp;
             const int sr = q >> 1;
-            bool search = q < 2 * nr && sr != r;
+            const bool search = q < 2 * nr && sr != r;
             int64_t lo = search ? ro[sr] : 0, hi = search ? ro[sr + 1] : 0;
             const uint64_t k = search ? keys[(q & 1) ? t1 - 1 : t0] : 0;
             const bool le = sr < r;
+            // a run wholly before or after the key needs no search (the
+            // emulated exchange's runs are disjoint owner slices)
+            if (hi > lo) {
+                const uint64_t f = keys[lo], l = keys[hi - 1];
+                if (le ? l <= k : l < k) lo = hi;
+                else if (le ? f > k : f >= k) hi = lo;
+            }
             for (;;) {  // every group of the wave runs the same rounds (ballots are wave-wide)
                 const bool more = hi - lo > kMG;
                 if (!__ballot(more)) break;
@@ -285,7 +295,7 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
         }
         __syncthreads();
         if (threadIdx.x == 0) {
-            int used = 0;
+            int used = 0, fit = 1;
             for (int sr = 0; sr < nr; ++sr) {
                 if (sr == r) continue;
                 if (whi[sr] < wlo[sr]) whi[sr] = wlo[sr];
@@ -295,8 +305,10 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
                     used += (int)len;
                 } else {
                     wbase[sr] = -1;
+                    fit = 0;
                 }
             }
+            all_fit = fit && nr <= kMFast;
         }
         __syncthreads();
         for (int sr = 0; sr < nr; ++sr) {
@@ -306,6 +318,49 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
             for (int i = threadIdx.x; i < len; i += blockDim.x) wkeys[wbase[sr] + i] = keys[lo + i];
         }
         __syncthreads();
+        if (all_fit) {
+            // every window staged, <= kMFast runs: the element's binary
+            // searches of all runs advance together (independent LDS loads in
+            // flight instead of one dependent chain per run)
+            int b[kMFast], n[kMFast], maxn = 0;
+            int64_t adj = 0;
+#pragma unroll
+            for (int sr = 0; sr < kMFast; ++sr) {
+                const bool on = sr < nr && sr != r;
+                b[sr] = on ? wbase[sr] : 0;
+                n[sr] = on ? (int)(whi[sr] - wlo[sr]) : 0;
+                maxn = max(maxn, n[sr]);
+                if (on) adj += wlo[sr] - wbase[sr] - ro[sr];
+            }
+            const int nit = 32 - __clz(maxn);  // halving steps until every window is empty
+            for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+                const uint64_t k = keys[i];
+                if (i > ro[r] && keys[i - 1] > k) *bad = 1;
+                int bb[kMFast], nn[kMFast];
+#pragma unroll
+                for (int sr = 0; sr < kMFast; ++sr) {
+                    bb[sr] = b[sr];
+                    nn[sr] = n[sr];
+                }
+                for (int it = 0; it < nit; ++it) {
+#pragma unroll
+                    for (int sr = 0; sr < kMFast; ++sr) {
+                        const int half = nn[sr] >> 1;
+                        const uint64_t m = wkeys[min(bb[sr] + half, kMLds - 1)];
+                        const bool before = nn[sr] > 0 && (sr < r ? m <= k : m < k);
+                        bb[sr] = before ? bb[sr] + half + 1 : bb[sr];
+                        nn[sr] = before ? nn[sr] - half - 1 : half;
+                    }
+                }
+                int64_t pos = i - ro[r] + adj;
+#pragma unroll
+                for (int sr = 0; sr < kMFast; ++sr) pos += bb[sr];
+                ko[pos] = k;
+                co[pos] = counts[i];
+            }
+            __syncthreads();  // the windows are rebuilt for the next tile
+            continue;
+        }
         for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
             const uint64_t k = keys[i];
             if (i > ro[r] && keys[i - 1] > k) *bad = 1;
@@ -334,7 +389,7 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
 __global__ void step_status_kernel(const int* __restrict__ flags, const unsigned* __restrict__ counters,
                                    const uint8_t* __restrict__ ovf, int B, const int64_t* __restrict__ dst,
                                    int64_t* __restrict__ merge_bad, const int64_t* __restrict__ est,
-                                   const int64_t* __restrict__ m_dev, StepStatus* __restrict__ out, uint64_t seq) {
+                                   StepStatus* __restrict__ out, uint64_t seq) {
     __shared__ int any_ovf;
     if (threadIdx.x == 0) any_ovf = 0;
     __syncthreads();
@@ -360,7 +415,6 @@ __global__ void step_status_kernel(const int* __restrict__ flags, const unsigned
     out->err = err;
     out->U = dst[B];
     out->E = est[2];
-    out->M = *m_dev;
     __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -375,6 +429,11 @@ struct karma_step {
     std::vector<int64_t> bounds;  // owner bounds: nranks + 1 contig ids
     bool exchange = false;        // a split / merge happens (world > 1 or emulation)
     hipStream_t main_s = nullptr, side_s = nullptr;
+    // deferred steps alternate between main_s and alt_s: nothing ties step
+    // i + 1's records job to step i's tail, so the next batch's classify runs
+    // beside this batch's merge and edge stage (a stream of batches)
+    hipStream_t alt_s = nullptr;
+    int streams = 0;              // KARMA_STEP_STREAMS: 1 / 2 main streams (0: by the batch's size)
     hipEvent_t ev = nullptr;      // side -> main join
     // the profile (persistent; rows of n_loc x M, dense)
     DevArray<double> prof;
@@ -393,19 +452,38 @@ struct karma_step {
     };
     std::deque<Pending> pending;
     uint64_t seq = 0;
-    StepStatus* ring_h = nullptr;  // mapped host memory (kMapStep)
+    StepStatus* ring_h = nullptr;  // mapped host memory (kMapStep): per step its status words ...
     StepStatus* ring_d = nullptr;
+    int64_t* mring_h = nullptr;    // ... and its column count, written by its column table
+    int64_t* mring_d = nullptr;
     int sticky_sync = 0;           // deferred steps to run synchronously after a slow one
-    // deferred steps' device buffers (kept across steps: identical shapes reuse them)
+    // deferred steps' device buffers, one set per main stream (kept across
+    // steps: identical shapes reuse them)
     DevArray<int64_t> m_ring;      // per ring entry: the step's column count, written by its column table
-    hipEvent_t ev_cols = nullptr;  // side stream, after a deferred step's column table
-    uint64_t prof_seq = 0;         // the deferred step whose profile `prof` holds (0: a synchronous one)
+    struct Tail {
+        DevArray<double> prof;         // the step's profile
+        DevArray<uint64_t> mk;
+        DevArray<int64_t> mc, mbad, tot, tile_cnt, est;
+        DevArray<uint32_t> ea, eb;
+        DevArray<int64_t> es;
+        DevArray<double> ew;
+        void release() {
+            prof.release();
+            mk.release();
+            mc.release();
+            mbad.release();
+            tot.release();
+            tile_cnt.release();
+            est.release();
+            ea.release();
+            eb.release();
+            es.release();
+            ew.release();
+        }
+    } tail[2];
+    uint64_t prof_seq = 0;         // the deferred step whose profile is the newest (0: a synchronous one)
+    int prof_par = 0;              // its buffer: tail[prof_par].prof
     int64_t prof_M = -1;           // M of the profile in `prof` (-1: not known yet)
-    DevArray<uint64_t> mk;
-    DevArray<int64_t> mc, mbad, tot, tile_cnt, est;
-    DevArray<uint32_t> ea, eb;
-    DevArray<int64_t> es;
-    DevArray<double> ew;
     // status words of synchronous steps whose edge count was not read
     // (count = false): copied out in stream order, checked when their event
     // has passed (or at karma_step_sync)
@@ -422,11 +500,12 @@ namespace {
 // The profile buffer grows only with both streams idle: the side stream may
 // still be writing the old one, and the allocator would hand it to a
 // main-stream allocation (it was allocated there) at once.
-int ensure_prof(karma_step* s, size_t n) {
-    if (s->prof.n >= n) return KARMA_OK;
+int ensure_prof(karma_step* s, DevArray<double>& prof, size_t n) {
+    if (prof.n >= n) return KARMA_OK;
     KARMA_HIP(hipStreamSynchronize(s->side_s));
     KARMA_HIP(hipStreamSynchronize(s->main_s));
-    return s->prof.alloc(s->ctx, n);
+    KARMA_HIP(hipStreamSynchronize(s->alt_s));
+    return prof.alloc(s->ctx, n);
 }
 template <typename T>
 int ensure_arr(karma_ctx* ctx, DevArray<T>& a, size_t n) {
@@ -570,7 +649,7 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
         if (!rc) rc = karma_kmer_plan_finalize_async(s->plan);
         ctx->stream = s->main_s;
         if (!rc) rc = karma_kmer_plan_finalize_wait(s->plan, &M);
-        if (!rc) rc = ensure_prof(s, (size_t)std::max<int64_t>(1, s->n_loc * M));
+        if (!rc) rc = ensure_prof(s, s->prof, (size_t)std::max<int64_t>(1, s->n_loc * M));
         if (!rc && s->n_loc * M) rc = karma_kmer_profile_side(s->plan, s->prof.ptr, M, s->side_s);
         const int rc2 = karma_graph_records_end(job, &s->local);  // consumes the job on every path
         KARMA_TRY(rc);
@@ -580,7 +659,7 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
         KARMA_TRY(karma_kmer_plan_create(ctx, store, s->kmode, &s->plan));
         if (s->world > 1) KARMA_TRY(exchange_columns(s, s->plan, s->comm));
         KARMA_TRY(karma_kmer_plan_finalize(s->plan, &M));
-        KARMA_TRY(ensure_prof(s, (size_t)std::max<int64_t>(1, s->n_loc * M)));
+        KARMA_TRY(ensure_prof(s, s->prof, (size_t)std::max<int64_t>(1, s->n_loc * M)));
         if (s->n_loc * M) KARMA_TRY(karma_kmer_profile(s->plan, s->prof.ptr, M, 1));
         KARMA_TRY(karma_graph_records(ctx, rec, A, s->n_glob, KARMA_REC_SORTED, 1, &s->local));
     }
@@ -641,7 +720,7 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
 int check_entry(karma_step* s, const karma_step::Pending& p, bool* slow) {
     const StepStatus& st = const_cast<const StepStatus&>(s->ring_h[p.seq % kRing]);
     *slow = st.slow != 0;
-    if (p.seq == s->prof_seq && !*slow) s->prof_M = st.M;
+
     if (st.err) {
         KARMA_CHECK(!(st.err & 1), KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
         KARMA_CHECK(!(st.err & 2), KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)",
@@ -669,7 +748,8 @@ int drain(karma_step* s, bool wait, bool lag) {
             // the main stream reaches the status kernel within a step's time
             for (int spin = 0; !entry_done(s, p.seq); ++spin) {
                 if (spin > 64) std::this_thread::yield();
-                if (spin % 4096 == 4095 && hipStreamQuery(s->main_s) == hipSuccess && !entry_done(s, p.seq)) {
+                if (spin % 4096 == 4095 && hipStreamQuery(s->main_s) == hipSuccess &&
+                    hipStreamQuery(s->alt_s) == hipSuccess && !entry_done(s, p.seq)) {
                     set_error("karma_step: a deferred step's status never arrived");
                     return KARMA_ERR_STATE;
                 }
@@ -689,12 +769,23 @@ int drain(karma_step* s, bool wait, bool lag) {
     return KARMA_OK;
 }
 
-int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A) {
+int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A, bool sequential) {
     karma_ctx* ctx = s->ctx;
     KARMA_TRY(drop_outputs(s));  // a deferred step has no outputs to read
     ++s->n_deferred;
     const uint64_t seq = ++s->seq;
+    // Two batches in flight pay off only while one batch leaves the chip idle
+    // between its short kernels: at config 3's size (308M records) two records
+    // jobs side by side took 1.89 ms per batch against 1.23 ms one after the
+    // other (they evict each other's partition runs from the caches); the
+    // 8-rank strong preview (38.6M records) went 0.237 -> 0.199 ms.
+    const bool two = s->streams ? s->streams == 2 : A < kAltMaxRecords;
+    const int par = sequential || !two ? 0 : (int)(seq & 1);
+    hipStream_t const ms = par ? s->alt_s : s->main_s;
+    karma_step::Tail& tl = s->tail[par];
+    ctx->stream = ms;
     s->prof_seq = seq;
+    s->prof_par = par;
     s->prof_M = -1;
     if (s->exchange) KARMA_TRY(karma_graph_split_hint(ctx, s->bounds.data(), s->nranks));
     // records job (main stream) up to its final kernel; no readback
@@ -703,24 +794,24 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     KARMA_TRY(sets_begin_deferred(ctx, reinterpret_cast<const uint2*>(rec), A, s->n_glob, &job, &v));
     std::unique_ptr<SetsJob, void (*)(SetsJob*)> jg(job, sets_release);
     // side stream: presence, column table (M stays on the device), then the
-    // profile behind the graph's final kernel
-    ctx->stream = s->side_s;
+    // profile behind the graph's final kernel (sequential: all on the main
+    // stream, every kernel alone on the chip -- the per-kernel timing pass)
+    hipStream_t const side = sequential ? ms : s->side_s;
+    ctx->stream = side;
     karma_kmer_plan* plan = nullptr;
     int rc = karma_kmer_plan_create(ctx, store, s->kmode, &plan);
-    int64_t* const m_dev = s->m_ring.ptr + seq % kRing;  // read by the profile (side) and the status kernel (main)
-    if (!rc) rc = kmer_finalize_device(plan, m_dev);
-    if (!rc) {
-        ++t_hip_calls;
-        rc = hipEventRecord(s->ev_cols, s->side_s) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
-    }
-    if (!rc) rc = ensure_prof(s, (size_t)std::max<int64_t>(1, s->n_loc * kmer_m_cap(plan)));
-    if (!rc && ctx->mark_set) {
+    // M: into the device ring (the profile reads it) and the mapped ring (the
+    // host reads it once the step is done); nothing on the main streams waits for it
+    int64_t* const m_dev = s->m_ring.ptr + seq % kRing;
+    if (!rc) rc = kmer_finalize_device(plan, m_dev, s->mring_d + seq % kRing);
+    if (!rc) rc = ensure_prof(s, tl.prof, (size_t)std::max<int64_t>(1, s->n_loc * kmer_m_cap(plan)));
+    if (!rc && ctx->mark_set && !sequential) {
         if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
         rc = hipStreamWaitEvent(s->side_s, ctx->mark_ev, 0) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
     }
-    if (!rc && s->n_loc) rc = kmer_profile_device_m(plan, s->prof.ptr, m_dev);
+    if (!rc && s->n_loc) rc = kmer_profile_device_m(plan, tl.prof.ptr, m_dev);
     if (plan) karma_kmer_plan_destroy(plan);  // its buffers return to the side stream's cache
-    ctx->stream = s->main_s;
+    ctx->stream = ms;
     KARMA_TRY(rc);
     // main stream: the tail, sized on the device
     const uint64_t* lk = v.keys;
@@ -729,11 +820,11 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     int64_t* mbad = nullptr;
     const int cu = ctx->cu_count;
     if (s->exchange) {
-        KARMA_TRY(ensure_arr(ctx, s->mk, v.cap));
-        KARMA_TRY(ensure_arr(ctx, s->mc, v.cap));
-        if (!s->mbad.ptr) {  // the merge sets it, the status kernel reads and clears it
-            KARMA_TRY(s->mbad.alloc(ctx, 1));
-            KARMA_HIP(hipMemsetAsync(s->mbad.ptr, 0, 8, ctx->stream));
+        KARMA_TRY(ensure_arr(ctx, tl.mk, v.cap));
+        KARMA_TRY(ensure_arr(ctx, tl.mc, v.cap));
+        if (!tl.mbad.ptr) {  // the merge sets it, the status kernel reads and clears it
+            KARMA_TRY(tl.mbad.alloc(ctx, 1));
+            KARMA_HIP(hipMemsetAsync(tl.mbad.ptr, 0, 8, ctx->stream));
         }
         RunSrc rs{};
         rs.nr = s->nranks;
@@ -743,26 +834,25 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         KARMA_CHECK((int)v.split_b.size() == s->nranks + 1, KARMA_ERR_STATE, "karma_step: the split hint was lost");
         const int64_t tiles_cap = (v.cap + kMT - 1) / kMT + s->nranks;
         KARMA_LAUNCH(ctx, "merge_rank", step_merge_kernel, (int)std::min<int64_t>(tiles_cap, 2 * cu), 256, 0, v.keys,
-                     v.counts, v.dst, v.split_loc, rs, s->mk.ptr, s->mc.ptr, s->mbad.ptr);
-        lk = s->mk.ptr;
-        lc = s->mc.ptr;
-        mbad = s->mbad.ptr;
+                     v.counts, v.dst, v.split_loc, rs, tl.mk.ptr, tl.mc.ptr, tl.mbad.ptr);
+        lk = tl.mk.ptr;
+        lc = tl.mc.ptr;
+        mbad = tl.mbad.ptr;
     }
-    KARMA_TRY(ensure_arr(ctx, s->tot, s->n_glob));
-    KARMA_TRY(ensure_arr(ctx, s->tile_cnt, (v.cap + kET - 1) / kET + 1));
-    KARMA_TRY(ensure_arr(ctx, s->est, 3));
-    KARMA_TRY(ensure_arr(ctx, s->ea, v.cap));
-    KARMA_TRY(ensure_arr(ctx, s->eb, v.cap));
-    KARMA_TRY(ensure_arr(ctx, s->es, v.cap));
-    KARMA_TRY(ensure_arr(ctx, s->ew, v.cap));
+    KARMA_TRY(ensure_arr(ctx, tl.tot, s->n_glob));
+    KARMA_TRY(ensure_arr(ctx, tl.tile_cnt, (v.cap + kET - 1) / kET + 1));
+    KARMA_TRY(ensure_arr(ctx, tl.est, 3));
+    KARMA_TRY(ensure_arr(ctx, tl.ea, v.cap));
+    KARMA_TRY(ensure_arr(ctx, tl.eb, v.cap));
+    KARMA_TRY(ensure_arr(ctx, tl.es, v.cap));
+    KARMA_TRY(ensure_arr(ctx, tl.ew, v.cap));
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((v.cap + kET - 1) / kET, cu));
-    KARMA_LAUNCH(ctx, "edge_count", step_edge_count_kernel, grid, kET, 0, lk, lc, n_dev, s->n_glob, s->tot.ptr,
-                 s->tile_cnt.ptr, s->est.ptr);
-    KARMA_LAUNCH(ctx, "edge_weights", step_edge_write_kernel, grid, kET, 0, lk, lc, n_dev, s->tot.ptr,
-                 s->tile_cnt.ptr, s->ea.ptr, s->eb.ptr, s->es.ptr, s->ew.ptr, s->est.ptr, s->n_glob);
-    KARMA_HIP(hipStreamWaitEvent(s->main_s, s->ev_cols, 0));  // M: written beside classify, long done
+    KARMA_LAUNCH(ctx, "edge_count", step_edge_count_kernel, grid, kET, 0, lk, lc, n_dev, s->n_glob, tl.tot.ptr,
+                 tl.tile_cnt.ptr, tl.est.ptr);
+    KARMA_LAUNCH(ctx, "edge_weights", step_edge_write_kernel, grid, kET, 0, lk, lc, n_dev, tl.tot.ptr,
+                 tl.tile_cnt.ptr, tl.ea.ptr, tl.eb.ptr, tl.es.ptr, tl.ew.ptr, tl.est.ptr, s->n_glob);
     KARMA_LAUNCH(ctx, "step_status", step_status_kernel, 1, 256, 0, v.flags, v.counters, v.ovf, v.B, v.dst, mbad,
-                 s->est.ptr, m_dev, s->ring_d + seq % kRing, seq);
+                 tl.est.ptr, s->ring_d + seq % kRing, seq);
     s->pending.push_back({seq, store, rec, A});
     return KARMA_OK;
 }
@@ -781,7 +871,11 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     KARMA_CHECK(world == 1 || (world == nranks && crank == rank), KARMA_ERR_ARG,
                 "karma_step_create: communicator of %d ranks (rank %d) for %d owners (rank %d)", world, crank,
                 nranks, rank);
-    KARMA_CHECK(bounds[0] == 0 && bounds[nranks] == n_glob, KARMA_ERR_ARG, "owner bounds must span [0, n_glob)");
+    // several owners: their bounds tile [0, n_glob); one: [bounds[0], bounds[1]) is
+    // this process's contig rows (a shard of n_glob ids, no exchange)
+    KARMA_CHECK(nranks == 1 || (bounds[0] == 0 && bounds[nranks] == n_glob), KARMA_ERR_ARG,
+                "owner bounds must span [0, n_glob)");
+    KARMA_CHECK(bounds[0] >= 0 && bounds[nranks] <= n_glob, KARMA_ERR_ARG, "owner bounds outside [0, n_glob)");
     for (int r = 0; r < nranks; ++r)
         KARMA_CHECK(bounds[r] <= bounds[r + 1], KARMA_ERR_ARG, "owner bounds must not decrease");
     std::unique_ptr<karma_step> s(new karma_step());
@@ -793,6 +887,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     s->rank = rank;
     s->nranks = nranks;
     s->emulate = world == 1 && nranks > 1 ? nranks : 0;
+    if (const char* e = getenv("KARMA_STEP_STREAMS")) s->streams = atoi(e) == 1 ? 1 : atoi(e) == 2 ? 2 : 0;
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
@@ -803,11 +898,13 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     // the main stream (the graph and the exchange) at high priority: its
     // blocks dispatch first when CUs free up beside the side-stream profile
     KARMA_HIP(hipStreamCreateWithPriority(&s->main_s, hipStreamNonBlocking, hi));
+    KARMA_HIP(hipStreamCreateWithPriority(&s->alt_s, hipStreamNonBlocking, hi));
     KARMA_HIP(hipStreamCreateWithPriority(&s->side_s, hipStreamNonBlocking, 0));
     void *hm = nullptr, *dm = nullptr;
-    KARMA_TRY(ctx_mapped(ctx, kMapStep, kRing * sizeof(StepStatus), &hm, &dm));
+    KARMA_TRY(ctx_mapped(ctx, kMapStep, kRing * sizeof(StepStatus) + kRing * 8, &hm, &dm));
+    s->mring_h = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(hm) + kRing * sizeof(StepStatus));
+    s->mring_d = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(dm) + kRing * sizeof(StepStatus));
     KARMA_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->graves_h), kRing * 4 * 8, hipHostMallocDefault));
-    KARMA_HIP(hipEventCreateWithFlags(&s->ev_cols, hipEventDisableTiming));
     {
         hipStream_t prev = ctx->stream;
         ctx->stream = s->main_s;
@@ -817,7 +914,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     }
     s->ring_h = static_cast<StepStatus*>(hm);
     s->ring_d = static_cast<StepStatus*>(dm);
-    std::memset(hm, 0, kRing * sizeof(StepStatus));
+    std::memset(hm, 0, kRing * sizeof(StepStatus) + kRing * 8);
     *out = s.release();
     return KARMA_OK;
 }
@@ -838,15 +935,15 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
     ctx->stream = s->main_s;
     const bool keep = flags & KARMA_STEP_KEEP, seq = flags & KARMA_STEP_SEQUENTIAL;
     // deferred: one process (no collective needs a host count), nothing read back
-    const bool defer = (flags & KARMA_STEP_DEFER) && !keep && !seq && s->world == 1 && s->n_glob <= sets_max_contigs();
+    const bool defer = (flags & KARMA_STEP_DEFER) && !keep && s->world == 1 && s->n_glob <= sets_max_contigs();
     int rc = KARMA_OK;
     if (defer && s->sticky_sync > 0) {
         --s->sticky_sync;
         rc = drain(s, false, true);
-        if (!rc) rc = run_sync(s, store, records, n_records, false, false, false);
+        if (!rc) rc = run_sync(s, store, records, n_records, false, seq, false);
     } else if (defer) {
         rc = drain(s, false, true);
-        if (!rc) rc = run_deferred(s, store, records, n_records);
+        if (!rc) rc = run_deferred(s, store, records, n_records, seq);
     } else {
         rc = drain(s, true, false);  // earlier deferred steps complete and checked first
         if (!rc) rc = run_sync(s, store, records, n_records, keep, seq, !(flags & KARMA_STEP_DEFER));
@@ -872,8 +969,11 @@ int karma_step_sync(karma_step* s) {
     ctx->stream = prev;
     KARMA_TRY(rc);
     KARMA_HIP(hipStreamSynchronize(s->side_s));
+    KARMA_HIP(hipStreamSynchronize(s->alt_s));
     KARMA_HIP(hipStreamSynchronize(s->main_s));
     KARMA_TRY(bury(s, true));
+    if (s->prof_seq)  // every stream is idle: the newest deferred step's column count has landed
+        s->prof_M = __atomic_load_n(&s->mring_h[s->prof_seq % kRing], __ATOMIC_ACQUIRE);
     if (s->edges && s->E < 0) KARMA_TRY(karma_edges_count(s->edges, &s->E));
     return KARMA_OK;
 }
@@ -889,7 +989,8 @@ int karma_step_info(karma_step* s, int64_t* info, int n) {
 // The profile of the newest step (a deferred one's once karma_step_sync has read its column count).
 int karma_step_profile(karma_step* s, double** dev, int64_t* rows, int64_t* M) {
     KARMA_CHECK(s && dev && s->prof_M >= 0, KARMA_ERR_STATE, "karma_step_profile: no finished step");
-    *dev = s->prof.ptr;
+    // a deferred step's profile is in its main stream's buffer
+    *dev = s->prof_seq ? s->tail[s->prof_par].prof.ptr : s->prof.ptr;
     if (rows) *rows = s->n_loc;
     if (M) *M = s->prof_M;
     return KARMA_OK;
@@ -915,6 +1016,7 @@ int karma_step_destroy(karma_step* s) {
     if (!s) return KARMA_OK;
     hipSetDevice(s->ctx->device);
     if (s->main_s) hipStreamSynchronize(s->main_s);
+    if (s->alt_s) hipStreamSynchronize(s->alt_s);
     if (s->side_s) hipStreamSynchronize(s->side_s);
     s->pending.clear();
     s->E = 0;  // outputs dropped unread
@@ -927,21 +1029,12 @@ int karma_step_destroy(karma_step* s) {
     // be destroyed: release them first, then hand cached blocks to the context
     s->prof.release();
     s->m_ring.release();
-    if (s->ev_cols) hipEventDestroy(s->ev_cols);
-    s->mk.release();
-    s->mc.release();
-    s->mbad.release();
-    s->tot.release();
-    s->tile_cnt.release();
-    s->est.release();
-    s->ea.release();
-    s->eb.release();
-    s->es.release();
-    s->ew.release();
+    for (auto& tl : s->tail) tl.release();
     karma_ctx* ctx = s->ctx;
     hipStream_t prev = ctx->stream;
-    if (prev == s->main_s || prev == s->side_s) ctx->stream = ctx->own_stream;
+    if (prev == s->main_s || prev == s->side_s || prev == s->alt_s) ctx->stream = ctx->own_stream;
     if (s->side_s) karma_stream_destroy(ctx, s->side_s);
+    if (s->alt_s) karma_stream_destroy(ctx, s->alt_s);
     if (s->main_s) karma_stream_destroy(ctx, s->main_s);
     delete s;
     return KARMA_OK;

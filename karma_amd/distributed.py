@@ -340,7 +340,7 @@ class ShardedBuild:
             # the W owners' contig ranges, rank 0's first (bench.py shard())
             self.split_bounds = np.array([n_glob * r // self.emulate for r in range(self.emulate + 1)], np.int64)
         if native:
-            own = self.split_bounds if self.split_bounds is not None else np.array([0, n_glob], np.int64)
+            own = self.split_bounds if self.split_bounds is not None else np.array([c_lo, c_lo + n_loc], np.int64)
             self.native = NativeStep(ctx, comm, kmode, n_glob, own, comm.rank if comm.world > 1 else 0, n_loc)
         self._ctx = ctx
 

@@ -401,7 +401,11 @@ def test_merge_runs_and_split(seed, n_runs, n):
         _lib.call("karma_dev_alloc", ctx.h, kcb.nbytes, ctypes.byref(dev))
         try:
             _lib.call("karma_memcpy", ctx.h, dev, _lib.ptr(kcb), kcb.nbytes, 0)
-            for use in ("get", "edges", "edges_deferred"):
+            if n_runs > 64:  # past 64 runs the level-by-level merge checks at once
+                with pytest.raises(_lib.KarmaError) as ei:
+                    engine.Pairs.merge_runs_kc(ctx, dev.value, lens.tolist())
+                assert ei.value.code == _lib.KARMA_ERR_UNSORTED
+            for use in (("get", "edges", "edges_deferred") if n_runs <= 64 else ()):
                 p = engine.Pairs.merge_runs_kc(ctx, dev.value, lens.tolist())
                 with pytest.raises(_lib.KarmaError) as ei:
                     if use == "get":

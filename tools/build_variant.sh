@@ -16,7 +16,7 @@ HASH=$(cat $(ls $SRC/*.hip $SRC/*.h $SRC/*.cpp $REPO/include/karma.h | sort) | s
 # the variant's -D flags are recorded in karma_build_info() (bench.py refuses
 # a variant unless KARMA_ALLOW_VARIANT=1)
 /opt/rocm/bin/hipcc $FLAGS $EXTRA -DKARMA_BUILD_DEFINES="\"$EXTRA\"" -DKARMA_SRC_HASH="\"$HASH\"" -c $SRC/core.hip -o $B/core.o &
-for f in kmer graph graph_sets eq consumers comm; do
+for f in kmer graph graph_sets eq consumers comm step sort; do
   /opt/rocm/bin/hipcc $FLAGS $EXTRA -c $SRC/$f.hip -o $B/$f.o &
 done
 wait
