@@ -94,6 +94,10 @@ int karma_memcpy(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int k
 /* The same, ordered on the context's stream and not waited for (host memory
  * must stay valid until the stream reaches the copy). */
 int karma_memcpy_async(karma_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
+/* Pinned host memory for results (device -> host copies into it run at the
+ * full PCIe rate): blocks are cached by size class after karma_host_free. */
+int karma_host_alloc(size_t bytes, void** out);
+int karma_host_free(void* p);
 int karma_memset_async(karma_ctx* ctx, void* dst, int value, size_t bytes);
 /* Average ms of `reps` hipMemsetAsync of `bytes` at dst (HIP events on the
  * context's stream): the device's write ceiling for a buffer of that size. */
@@ -347,7 +351,8 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records_
                    int64_t* info);
 /* Waits for every enqueued step and checks the deferred ones. */
 int karma_step_sync(karma_step* s);
-/* [M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending] (first n). */
+/* [M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending, host ns inside
+ * karma_step_run, of which ns waiting for a deferred step's status] (first n). */
 int karma_step_info(karma_step* s, int64_t* info, int n);
 /* Outputs (valid until the next run).  _profile: the newest step's profile
  * (device, rows x M dense f64; a deferred step's once karma_step_sync has read

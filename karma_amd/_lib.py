@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -64,6 +65,8 @@ _SIGS = {
     "karma_memcpy": [_c_p, _c_p, _c_p, ctypes.c_size_t, _i32],
     "karma_memcpy_async": [_c_p, _c_p, _c_p, ctypes.c_size_t, _i32],
     "karma_memset_async": [_c_p, _c_p, _i32, ctypes.c_size_t],
+    "karma_host_alloc": [ctypes.c_size_t, _PP],
+    "karma_host_free": [_c_p],
     "karma_memset_timed": [_c_p, _c_p, ctypes.c_size_t, _i32, ctypes.POINTER(ctypes.c_double)],
     "karma_stream_create": [_c_p, _i32, _PP],
     "karma_stream_destroy": [_c_p, _c_p],
@@ -412,6 +415,26 @@ class DevBuf:
             self.close()
         except Exception:
             pass
+
+
+def pinned_empty(n, dtype):
+    """An uninitialised numpy array of n items in pinned host memory
+    (karma_host_alloc): device -> host copies into it run at the full PCIe
+    rate.  The block returns to the library's cache when the last array or
+    view over it is collected."""
+    dtype = np.dtype(dtype)
+    nbytes = max(int(n), 1) * dtype.itemsize
+    p = ctypes.c_void_p()
+    call("karma_host_alloc", nbytes, ctypes.byref(p))
+    buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+    weakref.finalize(buf, _host_free, p.value)
+    return np.frombuffer(buf, dtype=dtype, count=int(n))
+
+
+def _host_free(addr):
+    lib = _LIB
+    if lib is not None:
+        lib.karma_host_free(ctypes.c_void_p(addr))
 
 
 def api_calls():

@@ -5,15 +5,16 @@
 // distinct pair, with the pair's first emission index (the intermediate
 // graph's edge order, read_graph.py:120).  No library sort or reduce.
 //
-// Data are small next to the records path (config 3: 519k classes, 977k
-// members, 617k pairs), so the design is about launch count and balance:
-//   1. eq_count    one thread per class (a block per class above kSmallM
-//                  members): totals (u64 atomics), the class's pair count,
-//                  and per contig a the number of pairs whose lower id is a;
-//   2. two exclusive scans (single-launch look-back, sort.hip): class pair
-//      offsets (first-emission indices) and contig segment offsets;
-//   3. eq_scatter  the same walk writes every pair into the segment of its
-//                  lower contig: a counting sort by a, no comparisons;
+// Data are small next to the records path (config 3: 519k classes of at most 4
+// members, 977k members, 617k pairs), so the design is about launch count,
+// balance and hiding the host->device copies of the inputs:
+//   1. one look-back scan of the classes' pair counts (m (m - 1) / 2, fused
+//      into the scan's loads): class pair offsets = first-emission indices;
+//   2. eq_rank     one thread per class (a block per class above kSmallM
+//                  members): every pair's key, class, and rank among the pairs
+//                  of its lower contig a (one returning atomic on a's count);
+//   3. a scan of the per-contig counts (segment offsets) and eq_place: every
+//      pair to segment start + rank -- a counting sort by a, no comparisons;
 //   4. seg_reduce  a block takes a run of whole segments (<= kSegCap entries,
 //                  snapped to segment starts), ranks every entry inside its
 //                  segment by (b, position) in LDS, and sums equal (a, b) keys
@@ -21,9 +22,12 @@
 //                  than kSegCap (one contig with > kSeg pairs as lower id) is
 //                  sorted in global memory by a block-wide merge sort instead;
 //   5. seg_compact every block places its distinct keys after the ones of the
-//                  blocks before it (a scan of the per-block counts).
-// One host synchronisation reads the pair total (to size the scratch) and one
-// the distinct-key total at the end.
+//                  blocks before it (a scan of the per-block counts);
+//   eq_totals      per-contig totals, one thread per member, u64 atomics, on
+//                  the fork stream beside 2-5.
+// Host inputs go up on the fork stream in the order the kernels need them;
+// one readback sizes the scratch (the pair total, while the members and counts
+// are still being copied) and one reads the distinct-key total at the end.
 #include <memory>
 
 #include "karma_internal.h"
@@ -60,107 +64,104 @@ struct EqIn {
     uint32_t N;
 };
 
-// ---- 1. totals, pair counts, segment sizes ----------------------------------------
-__global__ void __launch_bounds__(kEqT) eq_count_kernel(EqIn in, unsigned long long* __restrict__ totals,
-                                                        int64_t* __restrict__ pc, uint32_t* __restrict__ segcnt,
-                                                        uint32_t* __restrict__ big, unsigned* __restrict__ n_big,
-                                                        int* __restrict__ bad) {
+// ---- 1. each pair's rank inside its lower contig's segment ------------------------
+// Pair t of class c (t = poff[c] + its combinations index) gets its key, its
+// class and its rank among the pairs whose lower contig is a (a returning
+// atomic on segcnt[a]; every pair's three words are written, a pair with a
+// member >= N as a sentinel the placement skips, the call then fails).
+struct Pairs3 {
+    uint64_t* key;
+    uint32_t* rank;
+    uint32_t* cls;
+};
+
+__device__ __forceinline__ void rank_pair(uint32_t xi, uint32_t xj, uint32_t N, uint32_t c, int64_t t,
+                                          uint32_t* __restrict__ segcnt, Pairs3 P3, int* __restrict__ bad) {
+    const uint32_t a = min(xi, xj), b = max(xi, xj);
+    if (b >= N) {
+        *bad = 1;
+        P3.rank[t] = ~0u;
+        return;
+    }
+    P3.key[t] = ((uint64_t)a << 32) | b;
+    P3.rank[t] = atomicAdd(&segcnt[a], 1u);
+    P3.cls[t] = c;
+}
+
+__global__ void __launch_bounds__(kEqT) eq_rank_kernel(EqIn in, const int64_t* __restrict__ poff,
+                                                       uint32_t* __restrict__ segcnt, Pairs3 P3,
+                                                       uint32_t* __restrict__ big, unsigned* __restrict__ n_big,
+                                                       int* __restrict__ bad) {
     for (int64_t c = (int64_t)blockIdx.x * kEqT + threadIdx.x; c < in.C; c += (int64_t)gridDim.x * kEqT) {
         const int64_t s = in.off[c], e = in.off[c + 1], m = e - s;
-        const bool sk = in.skip[c] != 0;
-        pc[c] = sk ? 0 : m * (m - 1) / 2;
+        if (m < 2 || (in.skip && in.skip[c])) continue;
         if (m > kSmallM) {
             big[atomicAdd(n_big, 1u)] = (uint32_t)c;
             continue;
         }
-        const unsigned long long k = (unsigned long long)in.cnt[c];
-        for (int64_t t = s; t < e; ++t) {
-            const uint32_t x = in.mem[t];
-            if (x >= in.N) *bad = 1;
-            else atomicAdd(&totals[x], k);  // two's complement: exact for negative counts too
-        }
-        if (sk) continue;
+        int64_t t = poff[c];
         for (int64_t i = s; i + 1 < e; ++i) {
             const uint32_t xi = in.mem[i];
-            for (int64_t j = i + 1; j < e; ++j) {
-                const uint32_t xj = in.mem[j];
-                if (max(xi, xj) < in.N) atomicAdd(&segcnt[min(xi, xj)], 1u);
-            }
+            for (int64_t j = i + 1; j < e; ++j, ++t) rank_pair(xi, in.mem[j], in.N, (uint32_t)c, t, segcnt, P3, bad);
         }
     }
 }
 
-__global__ void __launch_bounds__(kEqT) eq_count_big_kernel(EqIn in, unsigned long long* __restrict__ totals,
-                                                            uint32_t* __restrict__ segcnt,
-                                                            const uint32_t* __restrict__ big,
-                                                            const unsigned* __restrict__ n_big, int* __restrict__ bad) {
+__global__ void __launch_bounds__(kEqT) eq_rank_big_kernel(EqIn in, const int64_t* __restrict__ poff,
+                                                           uint32_t* __restrict__ segcnt, Pairs3 P3,
+                                                           const uint32_t* __restrict__ big,
+                                                           const unsigned* __restrict__ n_big, int* __restrict__ bad) {
     const unsigned nb = *n_big;
     for (unsigned q = blockIdx.x; q < nb; q += gridDim.x) {
-        const int64_t c = big[q], s = in.off[c], m = in.off[c + 1] - s;
-        const unsigned long long k = (unsigned long long)in.cnt[c];
-        for (int64_t t = threadIdx.x; t < m; t += kEqT) {
-            const uint32_t x = in.mem[s + t];
-            if (x >= in.N) *bad = 1;
-            else atomicAdd(&totals[x], k);
-        }
-        if (in.skip[c]) continue;
-        const int64_t P = m * (m - 1) / 2;
+        const int64_t c = big[q], s = in.off[c], m = in.off[c + 1] - s, P = m * (m - 1) / 2;
         for (int64_t t = threadIdx.x; t < P; t += kEqT) {
             int64_t i, j;
             pair_ij(t, m, &i, &j);
-            const uint32_t xi = in.mem[s + i], xj = in.mem[s + j];
-            if (max(xi, xj) < in.N) atomicAdd(&segcnt[min(xi, xj)], 1u);
+            rank_pair(in.mem[s + i], in.mem[s + j], in.N, (uint32_t)c, poff[c] + t, segcnt, P3, bad);
         }
     }
 }
 
-// ---- 3. counting sort of the pairs by lower contig --------------------------------
+// ---- per-contig totals (read_graph.py:86-92), beside the pair pipeline -----------
+// One thread per member, its class by binary search over the class offsets.
+__global__ void __launch_bounds__(kEqT) eq_totals_kernel(EqIn in, int64_t n_mem,
+                                                         unsigned long long* __restrict__ totals,
+                                                         int* __restrict__ bad) {
+    for (int64_t j = (int64_t)blockIdx.x * kEqT + threadIdx.x; j < n_mem; j += (int64_t)gridDim.x * kEqT) {
+        int64_t lo = 0, hi = in.C;  // the last class with off[c] <= j
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (in.off[mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t x = in.mem[j];
+        if (x >= in.N) *bad = 1;
+        else atomicAdd(&totals[x], (unsigned long long)in.cnt[lo]);  // two's complement: exact for negative counts
+    }
+}
+
+// ---- 2. every pair into its segment (a counting sort by a) -----------------------
 struct Entries {
     uint64_t* key;    // a << 32 | b, a <= b
     int64_t* cnt;
     uint64_t* first;  // global emission index (class pair offset + combinations index)
 };
+struct Placed {       // a pair in its segment: key, emission index, class
+    uint64_t* key;
+    uint32_t* ref;
+    uint32_t* cls;
+};
 
-__device__ __forceinline__ void put_pair(uint32_t xi, uint32_t xj, int64_t k, uint64_t first,
-                                         const int64_t* __restrict__ segoff, uint32_t* __restrict__ cursor,
-                                         Entries E) {
-    const uint32_t a = min(xi, xj), b = max(xi, xj);
-    const int64_t slot = segoff[a] + (int64_t)(atomicSub(&cursor[a], 1u) - 1u);
-    E.key[slot] = ((uint64_t)a << 32) | b;
-    E.cnt[slot] = k;
-    E.first[slot] = first;
-}
-
-__global__ void __launch_bounds__(kEqT) eq_scatter_kernel(EqIn in, const int64_t* __restrict__ poff,
-                                                          const int64_t* __restrict__ segoff,
-                                                          uint32_t* __restrict__ cursor, Entries E) {
-    for (int64_t c = (int64_t)blockIdx.x * kEqT + threadIdx.x; c < in.C; c += (int64_t)gridDim.x * kEqT) {
-        const int64_t s = in.off[c], e = in.off[c + 1], m = e - s;
-        if (m > kSmallM || in.skip[c] || m < 2) continue;
-        const int64_t k = in.cnt[c];
-        uint64_t f = (uint64_t)poff[c];
-        for (int64_t i = s; i + 1 < e; ++i) {
-            const uint32_t xi = in.mem[i];
-            for (int64_t j = i + 1; j < e; ++j, ++f) put_pair(xi, in.mem[j], k, f, segoff, cursor, E);
-        }
-    }
-}
-
-__global__ void __launch_bounds__(kEqT) eq_scatter_big_kernel(EqIn in, const int64_t* __restrict__ poff,
-                                                              const int64_t* __restrict__ segoff,
-                                                              uint32_t* __restrict__ cursor, Entries E,
-                                                              const uint32_t* __restrict__ big,
-                                                              const unsigned* __restrict__ n_big) {
-    const unsigned nb = *n_big;
-    for (unsigned q = blockIdx.x; q < nb; q += gridDim.x) {
-        const int64_t c = big[q], s = in.off[c], m = in.off[c + 1] - s;
-        if (in.skip[c]) continue;
-        const int64_t k = in.cnt[c], P = m * (m - 1) / 2;
-        for (int64_t t = threadIdx.x; t < P; t += kEqT) {
-            int64_t i, j;
-            pair_ij(t, m, &i, &j);
-            put_pair(in.mem[s + i], in.mem[s + j], k, (uint64_t)(poff[c] + t), segoff, cursor, E);
-        }
+__global__ void __launch_bounds__(kEqT) eq_place_kernel(int64_t P, Pairs3 P3, const int64_t* __restrict__ segoff,
+                                                        Placed E) {
+    for (int64_t t = (int64_t)blockIdx.x * kEqT + threadIdx.x; t < P; t += (int64_t)gridDim.x * kEqT) {
+        const uint32_t r = P3.rank[t];
+        if (r == ~0u) continue;
+        const uint64_t k = P3.key[t];
+        const int64_t slot = segoff[k >> 32] + r;
+        E.key[slot] = k;
+        E.ref[slot] = (uint32_t)t;
+        E.cls[slot] = P3.cls[t];
     }
 }
 
@@ -206,8 +207,8 @@ __device__ __forceinline__ int64_t run_start(const int64_t* __restrict__ segoff,
 // key(p) / the original entry index idx(p).  Writes them to the staging
 // arrays at [r0, r0 + u) and returns u (every thread).
 template <typename KeyAt, typename IdxAt>
-__device__ int64_t reduce_sorted_run(int64_t r0, int64_t n, KeyAt key_at, IdxAt idx_at, Entries in, Entries st,
-                                     int64_t* lds_w) {
+__device__ int64_t reduce_sorted_run(int64_t r0, int64_t n, KeyAt key_at, IdxAt idx_at, Placed in,
+                                     const int64_t* __restrict__ cnt, Entries st, int64_t* lds_w) {
     int64_t u_total = 0, base_u = 0;
     for (int64_t c0 = 0; c0 < n; c0 += kRT) {
         const int64_t p = c0 + threadIdx.x;
@@ -220,8 +221,8 @@ __device__ int64_t reduce_sorted_run(int64_t r0, int64_t n, KeyAt key_at, IdxAt 
             uint64_t f = ~0ull;
             for (int64_t q = p; q < n && key_at(q) == k; ++q) {
                 const int64_t e = idx_at(q);
-                sum += in.cnt[e];
-                f = min(f, in.first[e]);
+                sum += cnt[in.cls[e]];
+                f = min(f, (uint64_t)in.ref[e]);
             }
             st.key[r0 + pos] = k;
             st.cnt[r0 + pos] = sum;
@@ -234,7 +235,8 @@ __device__ int64_t reduce_sorted_run(int64_t r0, int64_t n, KeyAt key_at, IdxAt 
 }
 
 __global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restrict__ segoff, int64_t N, int64_t P,
-                                                         Entries in, Entries st, uint64_t* __restrict__ gk0,
+                                                         Placed in, const int64_t* __restrict__ cnt, Entries st,
+                                                         uint64_t* __restrict__ gk0,
                                                          uint64_t* __restrict__ gk1, uint32_t* __restrict__ gi0,
                                                          uint32_t* __restrict__ gi1,
                                                          int64_t* __restrict__ run_u) {
@@ -275,7 +277,7 @@ __global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restri
         }
         __syncthreads();
         u = reduce_sorted_run(
-            r0, n, [&](int64_t p) { return okey[p]; }, [&](int64_t p) { return r0 + (int64_t)oidx[p]; }, in, st,
+            r0, n, [&](int64_t p) { return okey[p]; }, [&](int64_t p) { return r0 + (int64_t)oidx[p]; }, in, cnt, st,
             lds_w);
     } else {
         // a run with a segment of > kSeg entries: bottom-up merge sort of
@@ -322,7 +324,8 @@ __global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restri
             ib = ti;
         }
         u = reduce_sorted_run(
-            r0, n, [&](int64_t p) { return ka[p]; }, [&](int64_t p) { return r0 + (int64_t)ia[p]; }, in, st, lds_w);
+            r0, n, [&](int64_t p) { return ka[p]; }, [&](int64_t p) { return r0 + (int64_t)ia[p]; }, in, cnt, st,
+            lds_w);
     }
     if (threadIdx.x == 0) run_u[r] = u;
 }
@@ -346,20 +349,6 @@ int grid_of(int64_t n, int block) {
 
 }  // namespace
 
-namespace karma {
-
-// out[i] = in[0] + ... + in[i - 1] for i < n: the single-launch look-back
-// scans of sort.hip
-int scan_excl_device(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n, DevArray<int64_t>&) {
-    return scan_excl_i64(ctx, in, out, n);
-}
-int scan_excl_device(karma_ctx* ctx, const uint32_t* in, int64_t* out, int64_t n, DevArray<int64_t>&) {
-    return scan_excl_u32(ctx, in, out, n);
-}
-
-
-}  // namespace karma
-
 using namespace karma;
 
 extern "C" {
@@ -369,29 +358,18 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(out && cls_off && C >= 0 && N >= 0 && N < (int64_t(1) << 32), KARMA_ERR_ARG,
                 "karma_graph_eq: bad arguments");
+    hipStream_t const ms = ctx->stream;
+    int64_t* hp = nullptr;  // pinned: [0] pairs, [1] distinct keys, [2] bad member flag
+    KARMA_TRY(ctx_pinned(ctx, 32, reinterpret_cast<void**>(&hp)));
     int64_t n_mem = 0;
     if (is_device) {
-        KARMA_HIP(hipMemcpyAsync(&n_mem, cls_off + C, 8, hipMemcpyDeviceToHost, ctx->stream));
-        KARMA_HIP(hipStreamSynchronize(ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(hp, cls_off + C, 8, hipMemcpyDeviceToHost, ms));
+        KARMA_HIP(hipStreamSynchronize(ms));
+        n_mem = hp[0];
     } else {
         n_mem = cls_off[C];
     }
     KARMA_CHECK(n_mem >= 0, KARMA_ERR_ARG, "karma_graph_eq: negative member count");
-    DevArray<int64_t> d_off, d_cnt;
-    DevArray<uint32_t> d_mem;
-    DevArray<uint8_t> d_skip;
-    KARMA_TRY(d_off.alloc(ctx, C + 1));
-    KARMA_TRY(d_cnt.alloc(ctx, C));
-    KARMA_TRY(d_mem.alloc(ctx, n_mem));
-    KARMA_TRY(d_skip.alloc(ctx, C));
-    const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    KARMA_HIP(hipMemcpyAsync(d_off.ptr, cls_off, (C + 1) * 8, kind, ctx->stream));
-    if (C) KARMA_HIP(hipMemcpyAsync(d_cnt.ptr, counts, C * 8, kind, ctx->stream));
-    if (n_mem) KARMA_HIP(hipMemcpyAsync(d_mem.ptr, members, n_mem * 4, kind, ctx->stream));
-    if (C) {
-        if (pair_skip) KARMA_HIP(hipMemcpyAsync(d_skip.ptr, pair_skip, C, kind, ctx->stream));
-        else KARMA_HIP(hipMemsetAsync(d_skip.ptr, 0, C, ctx->stream));
-    }
     auto* p = new karma_pairs();
     p->ctx = ctx;
     p->n_contigs = N;
@@ -399,82 +377,129 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
     KARMA_TRY(p->totals.alloc(ctx, N));
     p->has_totals = true;
     p->has_first = true;
-
-    // one zeroed block: segcnt (N + 1) | counters (n_big, bad)
-    const int64_t seg_words = (N + 2) / 2;  // u32 x (N + 1), in 8-byte words
-    DevArray<int64_t> zero;
+    // one zeroed block: segcnt (N + 1 u32) | counters (n_big, bad)
+    const int64_t seg_words = (N + 2) / 2;
+    DevArray<int64_t> zero, poff, segoff;
+    DevArray<uint32_t> big;
     KARMA_TRY(zero.alloc(ctx, seg_words + 1 + 4));
-    KARMA_HIP(hipMemsetAsync(zero.ptr, 0, (seg_words + 1 + 4) * 8, ctx->stream));
-    if (N) KARMA_HIP(hipMemsetAsync(p->totals.ptr, 0, N * 8, ctx->stream));
+    KARMA_TRY(poff.alloc(ctx, C + 1));
+    KARMA_TRY(segoff.alloc(ctx, N + 1));
+    KARMA_TRY(big.alloc(ctx, std::max<int64_t>(C, 1)));
     uint32_t* segcnt = reinterpret_cast<uint32_t*>(zero.ptr);
     int64_t* ctr = zero.ptr + seg_words + 1;
     unsigned* n_big = reinterpret_cast<unsigned*>(ctr);
     int* bad = reinterpret_cast<int*>(ctr + 1);
-    DevArray<int64_t> pc, poff, segoff, sums;
-    DevArray<uint32_t> big;
-    KARMA_TRY(pc.alloc(ctx, C + 1));
-    KARMA_TRY(poff.alloc(ctx, C + 1));
-    KARMA_TRY(segoff.alloc(ctx, N + 1));
-    KARMA_TRY(big.alloc(ctx, C));
-    KARMA_HIP(hipMemsetAsync(pc.ptr + C, 0, 8, ctx->stream));
-    const EqIn in{d_off.ptr, d_mem.ptr, d_cnt.ptr, d_skip.ptr, C, (uint32_t)N};
-    const int cg = grid_of(C, kEqT), bg = std::max(1, ctx->cu_count);
-    if (C) {
-        KARMA_LAUNCH(ctx, "eq_count", eq_count_kernel, cg, kEqT, 0, in, (unsigned long long*)p->totals.ptr, pc.ptr,
-                     segcnt, big.ptr, n_big, bad);
-        KARMA_LAUNCH(ctx, "eq_count", eq_count_big_kernel, bg, kEqT, 0, in, (unsigned long long*)p->totals.ptr, segcnt,
-                     big.ptr, n_big, bad);
+    // Host inputs go up on the fork stream in the order the kernels need them
+    // (class offsets, members, counts) while the main stream computes with
+    // what has arrived; the totals run on the fork stream beside the pair
+    // pipeline.  Every buffer is the main stream's (allocator), so the fork
+    // stream first waits for the main stream's earlier work.
+    DevArray<int64_t> d_off, d_cnt;
+    DevArray<uint32_t> d_mem;
+    DevArray<uint8_t> d_skip;
+    const int64_t* off = cls_off;
+    const uint32_t* mem = members;
+    const int64_t* cnt = counts;
+    const uint8_t* skip = pair_skip;
+    hipStream_t xs = ms;
+    hipEvent_t* ev = ctx->xfer_ev;
+    if (!is_device) {
+        KARMA_TRY(ctx_fork(ctx));
+        for (int i = 0; i < 4; ++i)
+            if (!ev[i]) KARMA_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+        xs = ctx->fork_stream;
+        KARMA_TRY(d_off.alloc(ctx, C + 1));
+        KARMA_TRY(d_cnt.alloc(ctx, std::max<int64_t>(C, 1)));
+        KARMA_TRY(d_mem.alloc(ctx, std::max<int64_t>(n_mem, 1)));
+        if (pair_skip) KARMA_TRY(d_skip.alloc(ctx, std::max<int64_t>(C, 1)));
+        KARMA_HIP(hipEventRecord(ev[0], ms));
+        KARMA_HIP(hipStreamWaitEvent(xs, ev[0], 0));
+        KARMA_HIP(hipMemsetAsync(zero.ptr, 0, (seg_words + 1 + 4) * 8, xs));
+        KARMA_HIP(hipMemcpyAsync(d_off.ptr, cls_off, (C + 1) * 8, hipMemcpyHostToDevice, xs));
+        if (pair_skip && C) KARMA_HIP(hipMemcpyAsync(d_skip.ptr, pair_skip, C, hipMemcpyHostToDevice, xs));
+        KARMA_HIP(hipEventRecord(ev[1], xs));
+        off = d_off.ptr;
+        skip = pair_skip ? d_skip.ptr : nullptr;
+        mem = d_mem.ptr;
+        cnt = d_cnt.ptr;
+        KARMA_HIP(hipStreamWaitEvent(ms, ev[1], 0));
+    } else {
+        KARMA_HIP(hipMemsetAsync(zero.ptr, 0, (seg_words + 1 + 4) * 8, ms));
     }
-    KARMA_TRY(scan_excl_device(ctx, pc.ptr, poff.ptr, C + 1, sums));
-    KARMA_TRY(scan_excl_device(ctx, segcnt, segoff.ptr, N + 1, sums));
-    // the pair total sizes the scratch: one readback (with the member check)
-    int64_t* hp = nullptr;
-    KARMA_TRY(ctx_pinned(ctx, 16, reinterpret_cast<void**>(&hp)));
-    KARMA_HIP(hipMemcpyAsync(hp, poff.ptr + C, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipMemcpyAsync(hp + 1, bad, 4, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    // pair offsets of the classes (first-emission indices), one launch
+    KARMA_TRY(scan_excl_pairs(ctx, off, skip, C, poff.ptr));
+    KARMA_HIP(hipMemcpyAsync(hp, poff.ptr + C, 8, hipMemcpyDeviceToHost, ms));
+    if (!is_device) {
+        if (n_mem) KARMA_HIP(hipMemcpyAsync(d_mem.ptr, members, n_mem * 4, hipMemcpyHostToDevice, xs));
+        KARMA_HIP(hipEventRecord(ev[2], xs));
+        if (C) KARMA_HIP(hipMemcpyAsync(d_cnt.ptr, counts, C * 8, hipMemcpyHostToDevice, xs));
+        KARMA_HIP(hipEventRecord(ev[3], xs));
+    }
+    const EqIn in{off, mem, cnt, skip, C, (uint32_t)N};
+    const int bg = std::max(1, ctx->cu_count);
+    // totals (fork stream for host inputs: beside the pair pipeline)
+    {
+        ctx->stream = xs;
+        if (N) KARMA_HIP(hipMemsetAsync(p->totals.ptr, 0, N * 8, xs));
+        if (n_mem)
+            KARMA_LAUNCH(ctx, "eq_totals", eq_totals_kernel, grid_of(n_mem, kEqT), kEqT, 0, in, n_mem,
+                         (unsigned long long*)p->totals.ptr, bad);
+        ctx->stream = ms;
+        if (!is_device) KARMA_HIP(hipEventRecord(ev[0], xs));  // totals done (ev[0] reused)
+    }
+    // the pair total sizes the scratch: the one readback before the end
+    KARMA_HIP(hipStreamSynchronize(ms));
     const int64_t P = hp[0];
-    KARMA_CHECK(!(int)hp[1], KARMA_ERR_ARG, "eq class member index >= n_contigs");
-    KARMA_CHECK(P < (int64_t(1) << 32), KARMA_ERR_ARG, "karma_graph_eq: %lld pairs exceed 2^32", (long long)P);
-    KARMA_TRY(p->keys.alloc(ctx, P));
-    KARMA_TRY(p->counts.alloc(ctx, P));
-    KARMA_TRY(p->first.alloc(ctx, P));
-    if (P == 0) {
-        p->n = 0;
-        *out = guard.release();
-        return KARMA_OK;
+    KARMA_CHECK(P >= 0 && P < (int64_t(1) << 32), KARMA_ERR_ARG, "karma_graph_eq: %lld pairs exceed 2^32",
+                (long long)P);
+    KARMA_TRY(p->keys.alloc(ctx, std::max<int64_t>(P, 1)));
+    KARMA_TRY(p->counts.alloc(ctx, std::max<int64_t>(P, 1)));
+    KARMA_TRY(p->first.alloc(ctx, std::max<int64_t>(P, 1)));
+    const int cg = grid_of(C, kEqT);
+    DevArray<uint64_t> pk, ek, sk, sf, gk0, gk1;
+    DevArray<uint32_t> pr, pcl, er, ecl, gi0, gi1;
+    DevArray<int64_t> sc, run_u, run_base;
+    const int64_t n_runs = ceil_div(std::max<int64_t>(P, 1), kSeg);
+    if (!is_device) KARMA_HIP(hipStreamWaitEvent(ms, ev[2], 0));  // members
+    if (P) {
+        KARMA_TRY(pk.alloc(ctx, P));
+        KARMA_TRY(pr.alloc(ctx, P));
+        KARMA_TRY(pcl.alloc(ctx, P));
+        KARMA_TRY(ek.alloc(ctx, P));
+        KARMA_TRY(er.alloc(ctx, P));
+        KARMA_TRY(ecl.alloc(ctx, P));
+        KARMA_TRY(sk.alloc(ctx, P));
+        KARMA_TRY(sc.alloc(ctx, P));
+        KARMA_TRY(sf.alloc(ctx, P));
+        KARMA_TRY(gk0.alloc(ctx, P));
+        KARMA_TRY(gk1.alloc(ctx, P));
+        KARMA_TRY(gi0.alloc(ctx, P));
+        KARMA_TRY(gi1.alloc(ctx, P));
+        KARMA_TRY(run_u.alloc(ctx, n_runs + 1));
+        KARMA_TRY(run_base.alloc(ctx, n_runs + 1));
+        const Pairs3 P3{pk.ptr, pr.ptr, pcl.ptr};
+        KARMA_LAUNCH(ctx, "eq_rank", eq_rank_kernel, cg, kEqT, 0, in, poff.ptr, segcnt, P3, big.ptr, n_big, bad);
+        KARMA_LAUNCH(ctx, "eq_rank", eq_rank_big_kernel, bg, kEqT, 0, in, poff.ptr, segcnt, P3, big.ptr, n_big, bad);
+        KARMA_TRY(scan_excl_u32(ctx, segcnt, segoff.ptr, N + 1));
+        const Placed E{ek.ptr, er.ptr, ecl.ptr};
+        KARMA_LAUNCH(ctx, "eq_place", eq_place_kernel, grid_of(P, kEqT), kEqT, 0, P, P3, segoff.ptr, E);
+        if (!is_device) KARMA_HIP(hipStreamWaitEvent(ms, ev[3], 0));  // counts
+        // runs of whole segments; a run over kSegCap (one long segment) sorts in global scratch
+        const Entries S{sk.ptr, sc.ptr, sf.ptr}, O{p->keys.ptr, p->counts.ptr, p->first.ptr};
+        KARMA_HIP(hipMemsetAsync(run_u.ptr + n_runs, 0, 8, ms));
+        KARMA_LAUNCH(ctx, "seg_reduce", seg_reduce_kernel, n_runs, kRT, 0, segoff.ptr, N, P, E, cnt, S, gk0.ptr,
+                     gk1.ptr, gi0.ptr, gi1.ptr, run_u.ptr);
+        KARMA_TRY(scan_excl_i64(ctx, run_u.ptr, run_base.ptr, n_runs + 1));
+        KARMA_LAUNCH(ctx, "seg_compact", seg_compact_kernel, n_runs, kRT, 0, segoff.ptr, N, P, run_base.ptr, S, O);
+        KARMA_HIP(hipMemcpyAsync(hp + 1, run_base.ptr + n_runs, 8, hipMemcpyDeviceToHost, ms));
+    } else {
+        hp[1] = 0;
     }
-    DevArray<uint64_t> ek, ef, sk, sf, gk0, gk1;
-    DevArray<int64_t> ec, sc, run_u;
-    DevArray<uint32_t> gi0, gi1;
-    KARMA_TRY(ek.alloc(ctx, P));
-    KARMA_TRY(ec.alloc(ctx, P));
-    KARMA_TRY(ef.alloc(ctx, P));
-    KARMA_TRY(sk.alloc(ctx, P));
-    KARMA_TRY(sc.alloc(ctx, P));
-    KARMA_TRY(sf.alloc(ctx, P));
-    const Entries E{ek.ptr, ec.ptr, ef.ptr}, S{sk.ptr, sc.ptr, sf.ptr}, O{p->keys.ptr, p->counts.ptr, p->first.ptr};
-    KARMA_LAUNCH(ctx, "eq_scatter", eq_scatter_kernel, cg, kEqT, 0, in, poff.ptr, segoff.ptr, segcnt, E);
-    KARMA_LAUNCH(ctx, "eq_scatter", eq_scatter_big_kernel, bg, kEqT, 0, in, poff.ptr, segoff.ptr, segcnt, E, big.ptr,
-                 n_big);
-    // runs of whole segments; a run over kSegCap (one long segment) sorts in
-    // global scratch, which is only allocated when the host-side bound allows it
-    const int64_t n_runs = ceil_div(P, kSeg);
-    DevArray<int64_t> run_base;
-    KARMA_TRY(run_u.alloc(ctx, n_runs + 1));
-    KARMA_TRY(run_base.alloc(ctx, n_runs + 1));
-    KARMA_HIP(hipMemsetAsync(run_u.ptr + n_runs, 0, 8, ctx->stream));
-    KARMA_TRY(gk0.alloc(ctx, P));
-    KARMA_TRY(gk1.alloc(ctx, P));
-    KARMA_TRY(gi0.alloc(ctx, P));
-    KARMA_TRY(gi1.alloc(ctx, P));
-    KARMA_LAUNCH(ctx, "seg_reduce", seg_reduce_kernel, n_runs, kRT, 0, segoff.ptr, N, P, E, S, gk0.ptr, gk1.ptr,
-                 gi0.ptr, gi1.ptr, run_u.ptr);
-    KARMA_TRY(scan_excl_device(ctx, run_u.ptr, run_base.ptr, n_runs + 1, sums));
-    KARMA_LAUNCH(ctx, "seg_compact", seg_compact_kernel, n_runs, kRT, 0, segoff.ptr, N, P, run_base.ptr, S, O);
-    KARMA_HIP(hipMemcpyAsync(hp, run_base.ptr + n_runs, 8, hipMemcpyDeviceToHost, ctx->stream));
-    KARMA_HIP(hipStreamSynchronize(ctx->stream));
-    p->n = hp[0];
+    if (!is_device) KARMA_HIP(hipStreamWaitEvent(ms, ev[0], 0));  // totals
+    KARMA_HIP(hipMemcpyAsync(hp + 2, bad, 4, hipMemcpyDeviceToHost, ms));
+    KARMA_HIP(hipStreamSynchronize(ms));
+    KARMA_CHECK(!(int)hp[2], KARMA_ERR_ARG, "eq class member index >= n_contigs");
+    p->n = hp[1];
     *out = guard.release();
     return KARMA_OK;
 }

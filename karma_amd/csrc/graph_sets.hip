@@ -2000,16 +2000,6 @@ bool fork_on() {
     }();
     return on;
 }
-int ctx_fork(karma_ctx* ctx) {
-    if (!ctx->fork_stream) {
-        int lo = 0, hi = 0;
-        KARMA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        KARMA_HIP(hipStreamCreateWithPriority(&ctx->fork_stream, hipStreamNonBlocking, hi));
-        KARMA_HIP(hipEventCreateWithFlags(&ctx->fork_a, hipEventDisableTiming));
-        KARMA_HIP(hipEventCreateWithFlags(&ctx->fork_b, hipEventDisableTiming));
-    }
-    return KARMA_OK;
-}
 // Records per classify chunk (one wave each, 4 waves per SIMD resident).  A
 // launch of few chunks per wave slot ends in a partial round: 38.6M records
 // (config 3 over 8 ranks) are 4,711 chunks of 8192 on 4,096 slots.  Half-size

@@ -107,6 +107,7 @@ struct karma_ctx {
     // after classify and joined before the final kernel (SetsJob::launch)
     hipStream_t fork_stream = nullptr;
     hipEvent_t fork_a = nullptr, fork_b = nullptr;
+    hipEvent_t xfer_ev[4] = {};  // the eq path's staged host->device copies on fork_stream
 };
 
 namespace karma {
@@ -118,6 +119,7 @@ int ctx_begin(karma_ctx* ctx);  // hipSetDevice
 // block size and dynamic LDS (at least 1, at most `work` blocks).
 int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int64_t work);
 // Pinned host scratch of >= bytes (valid until the next call on this ctx).
+int ctx_fork(karma_ctx* ctx);  // creates ctx->fork_stream and its two events on first use
 int ctx_pinned(karma_ctx* ctx, size_t bytes, void** out);
 // Mapped coherent pinned host memory that kernels read and write directly.
 // One region per context, allocated once and freed only with the context, cut
@@ -201,6 +203,8 @@ int sort_reduce_pairs(karma_ctx* ctx, const uint64_t* keys_in, const int64_t* co
 // may be NULL; the group count lands in *n_out_dev on the device).
 int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);
 int scan_excl_u32(karma_ctx* ctx, const uint32_t* in, int64_t* out, int64_t n);
+// out[c] = sum over classes before c of m (m - 1) / 2 (0 where skip[c]), c <= C
+int scan_excl_pairs(karma_ctx* ctx, const int64_t* off, const uint8_t* skip, int64_t C, int64_t* out);
 int radix_sort_u64(karma_ctx* ctx, const uint64_t* kin, const uint32_t* vin, int64_t n, int key_bits,
                    uint64_t* kout, uint32_t* vout);
 int radix_sort_u32(karma_ctx* ctx, const uint32_t* kin, const uint32_t* vin, int64_t n, int key_bits,

@@ -745,6 +745,18 @@ template <bool P56, bool C16>
 #ifndef KARMA_PROF_WAVES
 #define KARMA_PROF_WAVES 6
 #endif
+// Row writers per block at a time (0: every wave writes when its row is
+// counted).  The chip writes fastest with few waves writing at once
+// (tools/micro/write_bw7: a linear stream from 4 waves per CU runs at the
+// memset rate, 6.5 TB/s; from 8 or 16 waves per CU at 5.0-6.0).
+// KARMA_PROF_TOKEN 1: the token passes once the row's stores are issued;
+// 2: once they have completed.
+#ifndef KARMA_PROF_WRITERS
+#define KARMA_PROF_WRITERS 0
+#endif
+#ifndef KARMA_PROF_TOKEN
+#define KARMA_PROF_TOKEN 1
+#endif
 __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(KARMA_PROF_WAVES, KARMA_PROF_WAVES)))
 profile_wave_kernel(
     const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
@@ -754,6 +766,7 @@ profile_wave_kernel(
     double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
     int64_t exc0, const int64_t* __restrict__ m_dev) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ int writers;  // waves of the block writing a row now (KARMA_PROF_WRITERS)
     // wave index in an SGPR: contig offsets and lengths load with scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
@@ -784,6 +797,7 @@ profile_wave_kernel(
         for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
     }
     for (int j = lane; j < h_words; j += 64) counts[j] = 0;  // write_row_wave clears it after each row
+    if (threadIdx.x == 0) writers = 0;
     __syncthreads();
     const int kmin = P56 ? 5 : k;
     // software pipeline over this wave's contigs: the next contig's offsets
@@ -852,7 +866,21 @@ profile_wave_kernel(
         // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
         my = wave_total(my);
         if (lane == 0) row_tot[c] = (int64_t)my;
+        if (KARMA_PROF_WRITERS > 0) {
+            if (lane == 0) {
+                while (atomicAdd(&writers, 1) >= KARMA_PROF_WRITERS) {
+                    atomicSub(&writers, 1);
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
         write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
+        if (KARMA_PROF_WRITERS > 0) {
+            if (KARMA_PROF_TOKEN == 2) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) atomicSub(&writers, 1);
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         cur = nxt;

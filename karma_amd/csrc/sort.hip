@@ -58,8 +58,25 @@ __device__ __forceinline__ int64_t block_excl(int64_t v, int64_t* lds_w, int64_t
     return before + inc - v;
 }
 
+// inputs of the scan: an array, or the pair count of each eq class
 template <typename T>
-__global__ void __launch_bounds__(kST) scan_lb_kernel(const T* __restrict__ in, int64_t n, int64_t* __restrict__ out,
+struct ArrayIn {
+    const T* __restrict__ p;
+    __device__ int64_t operator()(int64_t i) const { return (int64_t)p[i]; }
+};
+struct PairCountIn {  // m (m - 1) / 2 for class i of m members, 0 when skipped (and for i = C)
+    const int64_t* __restrict__ off;
+    const uint8_t* __restrict__ skip;
+    int64_t C;
+    __device__ int64_t operator()(int64_t i) const {
+        if (i >= C) return 0;
+        const int64_t m = off[i + 1] - off[i];
+        return (skip && skip[i]) ? 0 : m * (m - 1) / 2;
+    }
+};
+
+template <typename In>
+__global__ void __launch_bounds__(kST) scan_lb_kernel(In in, int64_t n, int64_t* __restrict__ out,
                                                       uint64_t* __restrict__ st, unsigned* __restrict__ ticket) {
     __shared__ int64_t lds_w[kST / 64];
     __shared__ int64_t tile_s, excl_s;
@@ -73,7 +90,7 @@ __global__ void __launch_bounds__(kST) scan_lb_kernel(const T* __restrict__ in, 
 #pragma unroll
     for (int i = 0; i < kSPer; ++i) {
         const int64_t p = t0 + (int64_t)threadIdx.x * kSPer + i;
-        v[i] = p < n ? (int64_t)in[p] : 0;
+        v[i] = p < n ? in(p) : 0;
         s += v[i];
     }
     int64_t total;
@@ -284,26 +301,29 @@ __global__ void __launch_bounds__(kGT) heads_write_kernel(const uint64_t* __rest
 
 namespace karma {
 
-int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
+template <typename In>
+static int scan_excl(karma_ctx* ctx, In in, int64_t* out, int64_t n) {
     if (n <= 0) return KARMA_OK;
     const int64_t tiles = ceil_div(n, kSTile);
     DevArray<uint64_t> st;
     KARMA_TRY(st.alloc(ctx, tiles + 1));
     KARMA_HIP(hipMemsetAsync(st.ptr, 0, (tiles + 1) * 8, ctx->stream));
-    KARMA_LAUNCH(ctx, "scan", scan_lb_kernel<int64_t>, tiles, kST, 0, in, n, out, st.ptr,
+    KARMA_LAUNCH(ctx, "scan", scan_lb_kernel<In>, tiles, kST, 0, in, n, out, st.ptr,
                  reinterpret_cast<unsigned*>(st.ptr + tiles));
     return KARMA_OK;
 }
 
+int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
+    return scan_excl(ctx, ArrayIn<int64_t>{in}, out, n);
+}
+
 int scan_excl_u32(karma_ctx* ctx, const uint32_t* in, int64_t* out, int64_t n) {
-    if (n <= 0) return KARMA_OK;
-    const int64_t tiles = ceil_div(n, kSTile);
-    DevArray<uint64_t> st;
-    KARMA_TRY(st.alloc(ctx, tiles + 1));
-    KARMA_HIP(hipMemsetAsync(st.ptr, 0, (tiles + 1) * 8, ctx->stream));
-    KARMA_LAUNCH(ctx, "scan", scan_lb_kernel<uint32_t>, tiles, kST, 0, in, n, out, st.ptr,
-                 reinterpret_cast<unsigned*>(st.ptr + tiles));
-    return KARMA_OK;
+    return scan_excl(ctx, ArrayIn<uint32_t>{in}, out, n);
+}
+
+// out[c] = pairs of the eq classes before c (c <= C; out[C] = all pairs)
+int scan_excl_pairs(karma_ctx* ctx, const int64_t* off, const uint8_t* skip, int64_t C, int64_t* out) {
+    return scan_excl(ctx, PairCountIn{off, skip, C}, out, C + 1);
 }
 
 template <typename K>

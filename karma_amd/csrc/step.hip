@@ -29,6 +29,7 @@
 //                path is run again synchronously (the same work the
 //                synchronous path would have done), an error is returned.
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -199,7 +200,7 @@ __global__ void __launch_bounds__(kET) step_edge_write_kernel(
 // its rank in its own run plus its rank in each other run (stable: equal keys
 // of different runs end up adjacent, in run order).
 constexpr int64_t kAltMaxRecords = int64_t(1) << 27;  // batches below this alternate main streams
-constexpr int kMT = 512;        // tile elements (1024: 7 windows of ~1024 keys overflowed the stage)
+constexpr int kMT = 1024;       // tile elements (one round of tiles at the 8-rank preview's ~300k keys)
 constexpr int kMLds = 8192;     // staged window keys
 constexpr int kMFast = 8;       // up to this many runs: every element's searches run in lockstep
 constexpr int kMG = 16;         // lanes per bound search
@@ -493,6 +494,10 @@ struct karma_step {
     int grave_next = 0;
     // counters
     int64_t n_sync = 0, n_deferred = 0, n_redone = 0;
+    // host time inside karma_step_run, and the part spent waiting for the
+    // device (a deferred step's status kLag steps back, synchronous readbacks
+    // excluded)
+    int64_t run_ns = 0, wait_ns = 0;
 };
 
 namespace {
@@ -746,6 +751,7 @@ int drain(karma_step* s, bool wait, bool lag) {
         if (!entry_done(s, p.seq)) {
             if (!must) break;
             // the main stream reaches the status kernel within a step's time
+            const auto w0 = std::chrono::steady_clock::now();
             for (int spin = 0; !entry_done(s, p.seq); ++spin) {
                 if (spin > 64) std::this_thread::yield();
                 if (spin % 4096 == 4095 && hipStreamQuery(s->main_s) == hipSuccess &&
@@ -754,6 +760,8 @@ int drain(karma_step* s, bool wait, bool lag) {
                     return KARMA_ERR_STATE;
                 }
             }
+            s->wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0)
+                              .count();
         }
         s->pending.pop_front();
         bool slow = false;
@@ -931,6 +939,7 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
     KARMA_TRY(karma_contigs_info(store, &n_store, nullptr, nullptr, nullptr));
     KARMA_CHECK(n_store == s->n_loc, KARMA_ERR_ARG, "karma_step_run: the store holds %lld contigs, the shard %lld",
                 (long long)n_store, (long long)s->n_loc);
+    const auto t0 = std::chrono::steady_clock::now();
     hipStream_t prev = ctx->stream;
     ctx->stream = s->main_s;
     const bool keep = flags & KARMA_STEP_KEEP, seq = flags & KARMA_STEP_SEQUENTIAL;
@@ -949,6 +958,7 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
         if (!rc) rc = run_sync(s, store, records, n_records, keep, seq, !(flags & KARMA_STEP_DEFER));
     }
     ctx->stream = prev;
+    s->run_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     if (rc) return rc;
     if (info) {
         info[0] = s->M;
@@ -980,8 +990,9 @@ int karma_step_sync(karma_step* s) {
 
 int karma_step_info(karma_step* s, int64_t* info, int n) {
     KARMA_CHECK(s && info && n >= 0, KARMA_ERR_ARG, "karma_step_info: bad arguments");
-    const int64_t v[] = {s->M, s->E, s->pairs_local, s->entries, s->n_sync, s->n_deferred, s->n_redone,
-                         (int64_t)s->pending.size()};
+    const int64_t v[] = {s->M,          s->E,        s->pairs_local, s->entries,
+                         s->n_sync,     s->n_deferred, s->n_redone,  (int64_t)s->pending.size(),
+                         s->run_ns,     s->wait_ns};
     for (int i = 0; i < n && i < (int)(sizeof v / sizeof v[0]); ++i) info[i] = v[i];
     return KARMA_OK;
 }

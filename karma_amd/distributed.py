@@ -273,9 +273,10 @@ class NativeStep:
         return DevBuf(self.ctx, (rows.value, M.value), np.float64, _ptr=dev.value or 0, _owner=self)
 
     def info(self):
-        """[M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending]."""
-        v = np.zeros(8, np.int64)
-        call("karma_step_info", self.h, ptr(v), 8)
+        """[M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending,
+        host ns inside karma_step_run, of which ns waiting for deferred statuses]."""
+        v = np.zeros(10, np.int64)
+        call("karma_step_info", self.h, ptr(v), 10)
         return v
 
     def close(self):

@@ -8,6 +8,7 @@ Two references are used:
 Everything here is bit-exact: integer counts, and f64 values that are one IEEE
 division (profile) or two divisions, one add and one halving (weights).
 """
+import ctypes
 import hashlib
 from collections import OrderedDict
 
@@ -305,6 +306,69 @@ def test_eq_vs_oracle_seeded():
     for k in ("a", "b", "shared", "first", "totals"):
         assert np.array_equal(getattr(e, k), o[k]), k
     assert np.array_equal(e.weight.view(np.uint64), o["weight"].view(np.uint64))
+
+
+def test_eq_big_classes_device_inputs_and_errors():
+    """Classes past the per-thread size (a block each in eq_rank), duplicate
+    members, size-token-"1" classes of several members, the skip array absent,
+    and the inputs already on the device (karma_graph_eq is_device = 1):
+    bit-exact against the oracle; a member id >= n_contigs fails the call on
+    both paths, in a pair or alone in its class."""
+    rng = np.random.default_rng(77)
+    n = 1500
+    sizes = list(rng.integers(1, 5, 3000)) + [33, 40, 100, 600, 2]
+    classes = []
+    for m in sizes:
+        mem = rng.integers(0, n, int(m)) if m < 100 else np.r_[rng.integers(0, n, int(m) - 3), [5, 5, 5]]
+        classes.append(np.asarray(mem, np.uint32))
+    off = np.r_[0, np.cumsum([len(c) for c in classes])].astype(np.int64)
+    mem = np.concatenate(classes).astype(np.uint32)
+    cnt = rng.integers(1, 50, len(classes)).astype(np.int64)
+    skip = (rng.random(len(classes)) < 0.05).astype(np.uint8)
+    skip[-3] = 1  # a 100-member class with size token "1"
+    for sk in (skip, None):
+        e = engine.graph_from_eq(off, mem, cnt, sk if sk is not None else np.zeros(0, np.uint8), n) \
+            if sk is not None else None
+        o = oracle.graph_groups(off, mem, cnt, sk, n, dedup=False)
+        if e is None:  # no skip array: through the C ABI with NULL
+            ctx = _lib.default_context()
+            h = ctypes.c_void_p()
+            _lib.call("karma_graph_eq", ctx.h, _lib.ptr(off), _lib.ptr(mem), _lib.ptr(cnt), None, len(classes), n, 0,
+                      ctypes.byref(h))
+            p = engine.Pairs(ctx, h)
+            ed = p.edges(_lib.KARMA_MODE_EQ, n)
+            e = ed.get()
+            ed.close()
+            p.close()
+        for k in ("a", "b", "shared", "first", "totals"):
+            assert np.array_equal(getattr(e, k), o[k]), k
+        assert np.array_equal(e.weight.view(np.uint64), o["weight"].view(np.uint64))
+    # the same from device arrays
+    ctx = _lib.default_context()
+    bufs = [_lib.DevBuf.from_numpy(ctx, x) for x in (off, mem, cnt, skip)]
+    try:
+        h = ctypes.c_void_p()
+        _lib.call("karma_graph_eq", ctx.h, *(ctypes.c_void_p(b.ptr) for b in bufs), len(classes), n, 1,
+                  ctypes.byref(h))
+        p = engine.Pairs(ctx, h)
+        ed = p.edges(_lib.KARMA_MODE_EQ, n)
+        e = ed.get()
+        ed.close()
+        p.close()
+        o = oracle.graph_groups(off, mem, cnt, skip, n, dedup=False)
+        for k in ("a", "b", "shared", "first", "totals"):
+            assert np.array_equal(getattr(e, k), o[k]), k
+    finally:
+        for b in bufs:
+            b.close()
+    for bad_at in (int(off[10]), int(off[-1]) - 1):  # inside a pair / the last class
+        m2 = mem.copy()
+        m2[bad_at] = n + 3
+        with pytest.raises(_lib.KarmaError):
+            engine.graph_from_eq(off, m2, cnt, skip, n)
+    one = np.array([0, 1], np.int64)
+    with pytest.raises(_lib.KarmaError):  # a lone member out of range
+        engine.graph_from_eq(one, np.array([n], np.uint32), np.array([3], np.int64), np.zeros(1, np.uint8), n)
 
 
 def test_eq_path_equals_readset_path():

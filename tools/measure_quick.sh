@@ -11,7 +11,7 @@ run() {
   timeout -k 10 240 python bench.py --cpu-baseline off --no-e2e --steps ${STEPS:-20} "$@" > $OUT/$n.json 2> $OUT/$n.err
   local rc=$?
   [ $rc -ne 0 ] && { echo "$n failed rc=$rc"; tail -5 $OUT/$n.err; exit $rc; }
-  python -c "import json; d=json.load(open('$OUT/$n.json')); k=d['kernels_ms_per_step']; print('$n', d['ms_per_step'], 'ms/step', 'parity', d.get('parity'), 'host_us', d.get('host_us_per_step'), 'calls', d.get('api_calls_per_step'), {x: k[x] for x in k if k[x] > 0.012})"
+  python -c "import json; d=json.load(open('$OUT/$n.json')); k=d['kernels_ms_per_step']; print('$n', d['ms_per_step'], 'ms/step', 'parity', d.get('parity'), 'host_us', d.get('host_us_per_step'), 'calls', d.get('api_calls_per_step'), 'wait_us', (d.get('step_driver') or {}).get('host_wait_us_per_step'), {x: k[x] for x in k if k[x] > 0.012})"
 }
 for leg in ${LEGS:-config3 strong_emu2 strong_emu4 strong_emu8 weak_emu8}; do
   case $leg in
