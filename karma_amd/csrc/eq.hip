@@ -21,8 +21,8 @@
 //                  (counts: i64 adds in key order; first: min).  A run longer
 //                  than kSegCap (one contig with > kSeg pairs as lower id) is
 //                  sorted in global memory by a block-wide merge sort instead;
-//   5. seg_compact every block places its distinct keys after the ones of the
-//                  blocks before it (a scan of the per-block counts);
+//                  the run's distinct keys go to their final place after the
+//                  runs before it (decoupled look-back, runs in ticket order);
 //   eq_totals      per-contig totals, one thread per member, u64 atomics, on
 //                  the fork stream beside 2-5.
 // Host inputs go up on the fork stream in the order the kernels need them;
@@ -35,6 +35,8 @@
 using karma::ceil_div;
 
 namespace {
+
+#include "graph_device.h"
 
 constexpr int kEqT = 256;      // threads of the per-class kernels
 constexpr int64_t kSmallM = 32;  // classes above this size: a block each
@@ -73,10 +75,15 @@ struct Pairs3 {
     uint64_t* key;
     uint32_t* rank;
     uint32_t* cls;
+    int64_t cap;  // entries allocated
 };
 
 __device__ __forceinline__ void rank_pair(uint32_t xi, uint32_t xj, uint32_t N, uint32_t c, int64_t t,
                                           uint32_t* __restrict__ segcnt, Pairs3 P3, int* __restrict__ bad) {
+    if (t >= P3.cap) {  // more pairs than the speculative capacity: the call runs again, sized
+        bad[1] = 1;
+        return;
+    }
     const uint32_t a = min(xi, xj), b = max(xi, xj);
     if (b >= N) {
         *bad = 1;
@@ -152,8 +159,9 @@ struct Placed {       // a pair in its segment: key, emission index, class
     uint32_t* cls;
 };
 
-__global__ void __launch_bounds__(kEqT) eq_place_kernel(int64_t P, Pairs3 P3, const int64_t* __restrict__ segoff,
-                                                        Placed E) {
+__global__ void __launch_bounds__(kEqT) eq_place_kernel(const int64_t* __restrict__ P_dev, Pairs3 P3,
+                                                        const int64_t* __restrict__ segoff, Placed E) {
+    const int64_t P = min(*P_dev, P3.cap);
     for (int64_t t = (int64_t)blockIdx.x * kEqT + threadIdx.x; t < P; t += (int64_t)gridDim.x * kEqT) {
         const uint32_t r = P3.rank[t];
         if (r == ~0u) continue;
@@ -189,18 +197,33 @@ __device__ int64_t block_scan_excl(int64_t v, int64_t* lds_w, int64_t* total) {
 }
 
 // ---- 4. sort + reduce of whole segments, one block per run -------------------------
-// Block r takes the entries [lo(r), lo(r + 1)), lo(r) = the first segment start
-// at or after r * kSeg (segments never straddle two blocks).
-__device__ __forceinline__ int64_t run_start(const int64_t* __restrict__ segoff, int64_t N, int64_t P, int64_t r) {
+// Run r takes the entries [lo(r), lo(r + 1)), lo(r) = the first segment start
+// at or after r * kSeg (segments never straddle two runs).  One 32-lane group
+// per bound probes 32 segment offsets per round (200k contigs: 4 dependent
+// loads instead of 18).
+__device__ __forceinline__ int64_t run_start_g(const int64_t* __restrict__ segoff, int64_t N, int64_t P, int64_t r,
+                                               int g) {
     const int64_t target = r * kSeg;
-    if (target >= P) return P;
+    const bool done = target >= P;
     int64_t lo = 0, hi = N;  // first a with segoff[a] >= target (segoff[N] = P >= target)
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (segoff[mid] >= target) hi = mid;
-        else lo = mid + 1;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long gm = 0xFFFFFFFFull << (lane & 32);
+    for (;;) {
+        const bool more = !done && hi - lo > 32;
+        if (!(__ballot(more) & gm)) break;
+        const int64_t step = (hi - lo + 31) / 32;
+        const int64_t p = min(hi, lo + (int64_t)(g + 1) * step) - 1;
+        const bool below = more && segoff[p] < target;
+        const int c = __popcll(__ballot(below) & gm);
+        if (more) {
+            lo = min(hi, lo + (int64_t)c * step);
+            hi = c < 32 ? min(hi, lo + step) : hi;
+        }
     }
-    return segoff[lo];
+    const int64_t p = lo + g;
+    const bool below = !done && p < hi && segoff[p] < target;
+    const int64_t a = lo + __popcll(__ballot(below) & gm);
+    return done ? P : segoff[a];
 }
 
 // Distinct keys of a sorted run, summed: position p of the run holds
@@ -234,19 +257,35 @@ __device__ int64_t reduce_sorted_run(int64_t r0, int64_t n, KeyAt key_at, IdxAt 
     return u_total;
 }
 
-__global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restrict__ segoff, int64_t N, int64_t P,
-                                                         Placed in, const int64_t* __restrict__ cnt, Entries st,
-                                                         uint64_t* __restrict__ gk0,
+// Runs are taken in ticket order; each run's distinct keys go straight to
+// their final place, after the runs before it (decoupled look-back), so no
+// scan or compaction launch follows.  The last run writes the total.
+__global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restrict__ segoff, int64_t N,
+                                                         int64_t n_runs, Placed in, const int64_t* __restrict__ cnt,
+                                                         Entries st, uint64_t* __restrict__ gk0,
                                                          uint64_t* __restrict__ gk1, uint32_t* __restrict__ gi0,
-                                                         uint32_t* __restrict__ gi1,
-                                                         int64_t* __restrict__ run_u) {
+                                                         uint32_t* __restrict__ gi1, uint64_t* __restrict__ lb,
+                                                         unsigned* __restrict__ ticket, Entries out,
+                                                         int64_t* __restrict__ n_out) {
     __shared__ uint64_t skey[kSegCap];
     __shared__ uint32_t sidx[kSegCap];
     __shared__ uint64_t okey[kSegCap];
     __shared__ uint32_t oidx[kSegCap];
     __shared__ int64_t lds_w[kRT / 64];
-    const int64_t r = blockIdx.x;
-    const int64_t r0 = run_start(segoff, N, P, r), r1 = run_start(segoff, N, P, r + 1);
+    __shared__ int64_t r_s, r0_s, r1_s, base_s;
+    if (threadIdx.x == 0) r_s = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t r = r_s;
+    // the placed pairs (segoff[N]): fewer than P when a member id is out of
+    // range (those pairs are not placed; the call then fails)
+    const int64_t P = segoff[N];
+    if (threadIdx.x < 64) {
+        const int64_t b = run_start_g(segoff, N, P, r + (threadIdx.x >> 5), threadIdx.x & 31);
+        if (threadIdx.x == 0) r0_s = b;
+        if (threadIdx.x == 32) r1_s = b;
+    }
+    __syncthreads();
+    const int64_t r0 = r0_s, r1 = r1_s;
     const int64_t n = r1 - r0;
     int64_t u = 0;
     if (n <= kSegCap) {
@@ -327,15 +366,14 @@ __global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restri
             r0, n, [&](int64_t p) { return ka[p]; }, [&](int64_t p) { return r0 + (int64_t)ia[p]; }, in, cnt, st,
             lds_w);
     }
-    if (threadIdx.x == 0) run_u[r] = u;
-}
-
-// ---- 5. distinct keys to their final positions ---------------------------------------
-__global__ void __launch_bounds__(kRT) seg_compact_kernel(const int64_t* __restrict__ segoff, int64_t N, int64_t P,
-                                                          const int64_t* __restrict__ run_base, Entries st,
-                                                          Entries out) {
-    const int64_t r = blockIdx.x;
-    const int64_t r0 = run_start(segoff, N, P, r), base = run_base[r], u = run_base[r + 1] - base;
+    // 5. the run's distinct keys after those of the runs before it
+    if (threadIdx.x < 64) {
+        const int64_t o = lookback_offset(lb, (int)r, u, (int)threadIdx.x);
+        if (threadIdx.x == 0) base_s = o;
+    }
+    __syncthreads();  // base known; the staged keys visible to the whole block
+    const int64_t base = base_s;
+    if (r == n_runs - 1 && threadIdx.x == 0) *n_out = base + u;
     for (int64_t p = threadIdx.x; p < u; p += kRT) {
         out.key[base + p] = st.key[r0 + p];
         out.cnt[base + p] = st.cnt[r0 + p];
@@ -351,15 +389,17 @@ int grid_of(int64_t n, int block) {
 
 using namespace karma;
 
-extern "C" {
+namespace {
 
-int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
-                   const uint8_t* pair_skip, int64_t C, int64_t N, int is_device, karma_pairs** out) {
-    KARMA_TRY(ctx_begin(ctx));
-    KARMA_CHECK(out && cls_off && C >= 0 && N >= 0 && N < (int64_t(1) << 32), KARMA_ERR_ARG,
-                "karma_graph_eq: bad arguments");
+// One pass of karma_graph_eq.  cap > 0: the pair scratch is sized speculatively
+// (the context's previous pair total) and nothing waits for the pair total;
+// *P_out > cap then means the pass must run again with cap = *P_out.  cap = 0:
+// one readback of the pair total sizes the scratch.
+int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
+                 const uint8_t* pair_skip, int64_t C, int64_t N, int is_device, int64_t cap, int64_t* P_out,
+                 karma_pairs** out) {
     hipStream_t const ms = ctx->stream;
-    int64_t* hp = nullptr;  // pinned: [0] pairs, [1] distinct keys, [2] bad member flag
+    int64_t* hp = nullptr;  // pinned: [0] pairs, [1] distinct keys, [2] bad member flag, [3] over capacity
     KARMA_TRY(ctx_pinned(ctx, 32, reinterpret_cast<void**>(&hp)));
     int64_t n_mem = 0;
     if (is_device) {
@@ -432,12 +472,57 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
     if (!is_device) {
         if (n_mem) KARMA_HIP(hipMemcpyAsync(d_mem.ptr, members, n_mem * 4, hipMemcpyHostToDevice, xs));
         KARMA_HIP(hipEventRecord(ev[2], xs));
-        if (C) KARMA_HIP(hipMemcpyAsync(d_cnt.ptr, counts, C * 8, hipMemcpyHostToDevice, xs));
-        KARMA_HIP(hipEventRecord(ev[3], xs));
     }
     const EqIn in{off, mem, cnt, skip, C, (uint32_t)N};
     const int bg = std::max(1, ctx->cu_count);
-    // totals (fork stream for host inputs: beside the pair pipeline)
+    // the pair total sizes the scratch: the one readback before the end
+    // (none when the previous call's total is taken as the capacity)
+    const bool spec = cap > 0;
+    if (!spec) {
+        KARMA_HIP(hipStreamSynchronize(ms));
+        cap = hp[0];
+        KARMA_CHECK(cap >= 0 && cap < (int64_t(1) << 32), KARMA_ERR_ARG, "karma_graph_eq: %lld pairs exceed 2^32",
+                    (long long)cap);
+    }
+    const int64_t P = cap;  // scratch entries
+    KARMA_TRY(p->keys.alloc(ctx, std::max<int64_t>(P, 1)));
+    KARMA_TRY(p->counts.alloc(ctx, std::max<int64_t>(P, 1)));
+    KARMA_TRY(p->first.alloc(ctx, std::max<int64_t>(P, 1)));
+    const int cg = grid_of(C, kEqT);
+    DevArray<uint64_t> pk, ek, sk, sf, gk0, gk1;
+    DevArray<uint32_t> pr, pcl, er, ecl, gi0, gi1;
+    DevArray<int64_t> sc;
+    DevArray<uint64_t> lb;  // n_runs look-back words | ticket | distinct-key total
+    const int64_t n_runs = ceil_div(std::max<int64_t>(P, 1), kSeg);
+    Placed E{nullptr, nullptr, nullptr};
+    if (!is_device) KARMA_HIP(hipStreamWaitEvent(ms, ev[2], 0));  // members
+    if (P) {
+        KARMA_TRY(pk.alloc(ctx, P));
+        KARMA_TRY(pr.alloc(ctx, P));
+        KARMA_TRY(pcl.alloc(ctx, P));
+        KARMA_TRY(ek.alloc(ctx, P));
+        KARMA_TRY(er.alloc(ctx, P));
+        KARMA_TRY(ecl.alloc(ctx, P));
+        E = Placed{ek.ptr, er.ptr, ecl.ptr};
+        KARMA_TRY(sk.alloc(ctx, P));
+        KARMA_TRY(sc.alloc(ctx, P));
+        KARMA_TRY(sf.alloc(ctx, P));
+        KARMA_TRY(gk0.alloc(ctx, P));
+        KARMA_TRY(gk1.alloc(ctx, P));
+        KARMA_TRY(gi0.alloc(ctx, P));
+        KARMA_TRY(gi1.alloc(ctx, P));
+        KARMA_TRY(lb.alloc(ctx, n_runs + 2));
+        const Pairs3 P3{pk.ptr, pr.ptr, pcl.ptr, P};
+        KARMA_LAUNCH(ctx, "eq_rank", eq_rank_kernel, cg, kEqT, 0, in, poff.ptr, segcnt, P3, big.ptr, n_big, bad);
+        KARMA_LAUNCH(ctx, "eq_rank", eq_rank_big_kernel, bg, kEqT, 0, in, poff.ptr, segcnt, P3, big.ptr, n_big, bad);
+        KARMA_TRY(scan_excl_u32(ctx, segcnt, segoff.ptr, N + 1));
+        KARMA_LAUNCH(ctx, "eq_place", eq_place_kernel, grid_of(P, kEqT), kEqT, 0, poff.ptr + C, P3, segoff.ptr, E);
+    }
+    // the counts go up while the pair kernels run; then the totals beside them
+    if (!is_device) {
+        if (C) KARMA_HIP(hipMemcpyAsync(d_cnt.ptr, counts, C * 8, hipMemcpyHostToDevice, xs));
+        KARMA_HIP(hipEventRecord(ev[3], xs));
+    }
     {
         ctx->stream = xs;
         if (N) KARMA_HIP(hipMemsetAsync(p->totals.ptr, 0, N * 8, xs));
@@ -447,60 +532,49 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
         ctx->stream = ms;
         if (!is_device) KARMA_HIP(hipEventRecord(ev[0], xs));  // totals done (ev[0] reused)
     }
-    // the pair total sizes the scratch: the one readback before the end
-    KARMA_HIP(hipStreamSynchronize(ms));
-    const int64_t P = hp[0];
-    KARMA_CHECK(P >= 0 && P < (int64_t(1) << 32), KARMA_ERR_ARG, "karma_graph_eq: %lld pairs exceed 2^32",
-                (long long)P);
-    KARMA_TRY(p->keys.alloc(ctx, std::max<int64_t>(P, 1)));
-    KARMA_TRY(p->counts.alloc(ctx, std::max<int64_t>(P, 1)));
-    KARMA_TRY(p->first.alloc(ctx, std::max<int64_t>(P, 1)));
-    const int cg = grid_of(C, kEqT);
-    DevArray<uint64_t> pk, ek, sk, sf, gk0, gk1;
-    DevArray<uint32_t> pr, pcl, er, ecl, gi0, gi1;
-    DevArray<int64_t> sc, run_u, run_base;
-    const int64_t n_runs = ceil_div(std::max<int64_t>(P, 1), kSeg);
-    if (!is_device) KARMA_HIP(hipStreamWaitEvent(ms, ev[2], 0));  // members
     if (P) {
-        KARMA_TRY(pk.alloc(ctx, P));
-        KARMA_TRY(pr.alloc(ctx, P));
-        KARMA_TRY(pcl.alloc(ctx, P));
-        KARMA_TRY(ek.alloc(ctx, P));
-        KARMA_TRY(er.alloc(ctx, P));
-        KARMA_TRY(ecl.alloc(ctx, P));
-        KARMA_TRY(sk.alloc(ctx, P));
-        KARMA_TRY(sc.alloc(ctx, P));
-        KARMA_TRY(sf.alloc(ctx, P));
-        KARMA_TRY(gk0.alloc(ctx, P));
-        KARMA_TRY(gk1.alloc(ctx, P));
-        KARMA_TRY(gi0.alloc(ctx, P));
-        KARMA_TRY(gi1.alloc(ctx, P));
-        KARMA_TRY(run_u.alloc(ctx, n_runs + 1));
-        KARMA_TRY(run_base.alloc(ctx, n_runs + 1));
-        const Pairs3 P3{pk.ptr, pr.ptr, pcl.ptr};
-        KARMA_LAUNCH(ctx, "eq_rank", eq_rank_kernel, cg, kEqT, 0, in, poff.ptr, segcnt, P3, big.ptr, n_big, bad);
-        KARMA_LAUNCH(ctx, "eq_rank", eq_rank_big_kernel, bg, kEqT, 0, in, poff.ptr, segcnt, P3, big.ptr, n_big, bad);
-        KARMA_TRY(scan_excl_u32(ctx, segcnt, segoff.ptr, N + 1));
-        const Placed E{ek.ptr, er.ptr, ecl.ptr};
-        KARMA_LAUNCH(ctx, "eq_place", eq_place_kernel, grid_of(P, kEqT), kEqT, 0, P, P3, segoff.ptr, E);
         if (!is_device) KARMA_HIP(hipStreamWaitEvent(ms, ev[3], 0));  // counts
         // runs of whole segments; a run over kSegCap (one long segment) sorts in global scratch
         const Entries S{sk.ptr, sc.ptr, sf.ptr}, O{p->keys.ptr, p->counts.ptr, p->first.ptr};
-        KARMA_HIP(hipMemsetAsync(run_u.ptr + n_runs, 0, 8, ms));
-        KARMA_LAUNCH(ctx, "seg_reduce", seg_reduce_kernel, n_runs, kRT, 0, segoff.ptr, N, P, E, cnt, S, gk0.ptr,
-                     gk1.ptr, gi0.ptr, gi1.ptr, run_u.ptr);
-        KARMA_TRY(scan_excl_i64(ctx, run_u.ptr, run_base.ptr, n_runs + 1));
-        KARMA_LAUNCH(ctx, "seg_compact", seg_compact_kernel, n_runs, kRT, 0, segoff.ptr, N, P, run_base.ptr, S, O);
-        KARMA_HIP(hipMemcpyAsync(hp + 1, run_base.ptr + n_runs, 8, hipMemcpyDeviceToHost, ms));
+        KARMA_HIP(hipMemsetAsync(lb.ptr, 0, (n_runs + 2) * 8, ms));
+        int64_t* n_out = reinterpret_cast<int64_t*>(lb.ptr + n_runs + 1);
+        KARMA_LAUNCH(ctx, "seg_reduce", seg_reduce_kernel, n_runs, kRT, 0, segoff.ptr, N, n_runs, E, cnt, S, gk0.ptr,
+                     gk1.ptr, gi0.ptr, gi1.ptr, lb.ptr, reinterpret_cast<unsigned*>(lb.ptr + n_runs), O, n_out);
+        KARMA_HIP(hipMemcpyAsync(hp + 1, n_out, 8, hipMemcpyDeviceToHost, ms));
     } else {
         hp[1] = 0;
     }
     if (!is_device) KARMA_HIP(hipStreamWaitEvent(ms, ev[0], 0));  // totals
     KARMA_HIP(hipMemcpyAsync(hp + 2, bad, 4, hipMemcpyDeviceToHost, ms));
+    KARMA_HIP(hipMemcpyAsync(hp + 3, bad + 1, 4, hipMemcpyDeviceToHost, ms));
     KARMA_HIP(hipStreamSynchronize(ms));
+    *P_out = hp[0];
+    KARMA_CHECK(hp[0] >= 0 && hp[0] < (int64_t(1) << 32), KARMA_ERR_ARG, "karma_graph_eq: %lld pairs exceed 2^32",
+                (long long)hp[0]);
     KARMA_CHECK(!(int)hp[2], KARMA_ERR_ARG, "eq class member index >= n_contigs");
+    if (spec && hp[0] > cap) return KARMA_OK;  // *out untouched: run again, sized
     p->n = hp[1];
     *out = guard.release();
+    return KARMA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
+                   const uint8_t* pair_skip, int64_t C, int64_t N, int is_device, karma_pairs** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && cls_off && C >= 0 && N >= 0 && N < (int64_t(1) << 32), KARMA_ERR_ARG,
+                "karma_graph_eq: bad arguments");
+    // the previous call's pair total as the scratch capacity: a stream of
+    // similar calls never waits for the pair total
+    const int64_t cap = ctx->eq_pair_cap;
+    int64_t P = 0;
+    *out = nullptr;
+    KARMA_TRY(graph_eq_run(ctx, cls_off, members, counts, pair_skip, C, N, is_device, cap, &P, out));
+    if (!*out) KARMA_TRY(graph_eq_run(ctx, cls_off, members, counts, pair_skip, C, N, is_device, 0, &P, out));
+    ctx->eq_pair_cap = std::max(cap, P);
     return KARMA_OK;
 }
 

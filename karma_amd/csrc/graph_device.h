@@ -50,7 +50,7 @@ __device__ __forceinline__ void sort_dedup(ReadSet& s) {
 // global memory, one thread per read.
 // contig ids relabelled by map (a bijection of [0, N); the identity below)
 template <typename Map, typename Emit>
-__device__ void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_t i, Map map, Emit emit) {
+__device__ inline void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_t i, Map map, Emit emit) {
     const uint32_t rid = rec[i].x;
     int64_t end = i;
     while (end < A && rec[end].x == rid) ++end;
@@ -70,7 +70,7 @@ __device__ void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_
 }
 
 template <typename Emit>
-__device__ void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_t i, Emit emit) {
+__device__ inline void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_t i, Emit emit) {
     read_pairs_slow(rec, A, i, [](uint32_t c) { return c; }, emit);
 }
 
@@ -95,7 +95,7 @@ __device__ __forceinline__ void wave_lds_order() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ void lds_bitonic(uint32_t* keys, uint32_t* vals, int n) {
+__device__ inline void lds_bitonic(uint32_t* keys, uint32_t* vals, int n) {
     auto step = [&](int size, int stride) {
         for (int t = threadIdx.x; t < n / 2; t += blockDim.x) {
             const int i = 2 * t - (t & (stride - 1));
@@ -124,4 +124,45 @@ __device__ void lds_bitonic(uint32_t* keys, uint32_t* vals, int n) {
         if (size >= 128) __syncthreads();  // the next size starts with a cross-wave stride
     }
     __syncthreads();
+}
+
+// ---- decoupled look-back offsets ------------------------------------------------
+// Lists written back to back in one array (the final kernel's buckets, the eq
+// path's segment runs): block b's offset is the sum of the lists of blocks < b,
+// found by a decoupled look-back (one wave): the block publishes its own size
+// at once (kLbAgg), reads its predecessors' words
+// 64 at a time from the nearest down, and stops at the first that carries an
+// inclusive prefix (kLbPre); block 0 (and the virtual block -1) carry one.
+// Predecessors were dispatched first and publish before they wait, so every
+// wave's spin ends.
+constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 2ull << 62, kLbVal = kLbAgg - 1;
+
+__device__ inline int64_t lookback_offset(uint64_t* lb, int b, int64_t total, int lane) {
+    if (b == 0) {
+        if (lane == 0) __hip_atomic_store(&lb[0], kLbPre | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(&lb[b], kLbAgg | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t excl = 0;
+    for (int top = b - 1;; top -= 64) {
+        const int idx = top - lane;  // lane 0: the nearest predecessor
+        uint64_t v;
+        unsigned long long pre, none;
+        for (;;) {
+            v = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
+            pre = __ballot((v & ~kLbVal) == kLbPre);
+            none = __ballot((v & ~kLbVal) == 0);
+            const unsigned long long need = pre ? (pre & (~pre + 1)) * 2 - 1 : ~0ull;  // lanes up to the first prefix
+            if (!(none & need)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const int first = pre ? __ffsll((long long)pre) - 1 : 64;
+        int64_t x = lane <= first ? (int64_t)(v & kLbVal) : 0;
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        excl += x;
+        if (pre) break;
+    }
+    if (lane == 0)
+        __hip_atomic_store(&lb[b], kLbPre | (uint64_t)(excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
 }

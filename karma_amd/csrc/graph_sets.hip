@@ -438,7 +438,6 @@ classify2_kernel(ClassArgs P) {
             for (int i = 0; i < 8; ++i) {
                 if (i > 0) {
                     const uint64_t cap = Si & ~started;  // the first start: the head ends here
-                    hd.fm3 = in_mask(cap) ? st.fm3 : hd.fm3;
                     hd.win = in_mask(cap) ? st.win : hd.win;
                     hlen = in_mask(cap) ? (uint32_t)i : hlen;
                     started |= Si;
@@ -461,7 +460,9 @@ classify2_kernel(ClassArgs P) {
                     emit(e, ok, code, ubase + spos, 0ull);
                 }
             }
-            hd.fm3 = in_mask(started) ? hd.fm3 : st.fm3;  // no read starts here: the whole lane is a head
+            // the head began at record 0 (its first contig is ctg[0]); no read
+            // starts here: the whole lane is a head
+            hd.fm3 = ctg[0] - 3u;
             hd.win = in_mask(started) ? hd.win : st.win;
             // the incoming tail (the previous lane's last read), merged with this
             // lane's head when the read continues (else with itself: the same code)
@@ -1390,45 +1391,6 @@ struct SplitArgs {
     int64_t* out;  // per bound: keys of its bucket below it
 };
 
-// The buckets' lists back to back in one array: block b's offset is the sum
-// of the lists of blocks < b, found by a decoupled look-back (one wave): the
-// block publishes its own size at once (kLbAgg), reads its predecessors' words
-// 64 at a time from the nearest down, and stops at the first that carries an
-// inclusive prefix (kLbPre); block 0 (and the virtual block -1) carry one.
-// Predecessors were dispatched first and publish before they wait, so every
-// wave's spin ends.
-constexpr uint64_t kLbAgg = 1ull << 62, kLbPre = 2ull << 62, kLbVal = kLbAgg - 1;
-
-__device__ int64_t lookback_offset(uint64_t* lb, int b, int64_t total, int lane) {
-    if (b == 0) {
-        if (lane == 0) __hip_atomic_store(&lb[0], kLbPre | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return 0;
-    }
-    if (lane == 0) __hip_atomic_store(&lb[b], kLbAgg | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int64_t excl = 0;
-    for (int top = b - 1;; top -= 64) {
-        const int idx = top - lane;  // lane 0: the nearest predecessor
-        uint64_t v;
-        unsigned long long pre, none;
-        for (;;) {
-            v = idx >= 0 ? __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
-            pre = __ballot((v & ~kLbVal) == kLbPre);
-            none = __ballot((v & ~kLbVal) == 0);
-            const unsigned long long need = pre ? (pre & (~pre + 1)) * 2 - 1 : ~0ull;  // lanes up to the first prefix
-            if (!(none & need)) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        const int first = pre ? __ffsll((long long)pre) - 1 : 64;
-        int64_t x = lane <= first ? (int64_t)(v & kLbVal) : 0;
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-        excl += x;
-        if (pre) break;
-    }
-    if (lane == 0)
-        __hip_atomic_store(&lb[b], kLbPre | (uint64_t)(excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
-}
-
 template <int HF>
 __global__ void __launch_bounds__(kFT) final_kernel(
     int n_pg, int n_cg, int bw, int bbits, int dbits, int bwc, const uint32_t* __restrict__ part_band,
@@ -2012,7 +1974,7 @@ bool fork_on() {
 int64_t chunk_records(const karma_ctx* ctx, int64_t A) {
     if (const char* e = std::getenv("KARMA_CHUNK")) {
         const int64_t c = std::atoll(e);
-        if (c == kCChunk || c == kCChunk / 2) return c;
+        if (c == kCChunk || c == kCChunk / 2 || c == kCChunk / 4) return c;
     }
     const int64_t slots = (int64_t)ctx->cu_count * 16;
     return ceil_div(A, kCChunk) < 4 * slots ? kCChunk / 2 : kCChunk;

@@ -108,6 +108,7 @@ struct karma_ctx {
     hipStream_t fork_stream = nullptr;
     hipEvent_t fork_a = nullptr, fork_b = nullptr;
     hipEvent_t xfer_ev[4] = {};  // the eq path's staged host->device copies on fork_stream
+    int64_t eq_pair_cap = 0;     // the eq path's previous pair total (its speculative scratch size)
 };
 
 namespace karma {

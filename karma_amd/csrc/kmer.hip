@@ -57,7 +57,7 @@ struct karma_kmer_plan {
     DevArray<int32_t> col_of_ord;
     DevArray<int32_t> col_of_exc;
     DevArray<uint64_t> col_keys;
-    DevArray<int64_t> row_tot;
+    int64_t* row_tot = nullptr;  // per row: k-mer occurrences (inside `presence`'s allocation)
     DevArray<int> err;  // zero-length-key guard flag of the profile kernels (the host checks first)
     DevArray<int64_t> m_dev;
     hipEvent_t fin_ev = nullptr;  // after the column table and M's readback
@@ -745,18 +745,6 @@ template <bool P56, bool C16>
 #ifndef KARMA_PROF_WAVES
 #define KARMA_PROF_WAVES 6
 #endif
-// Row writers per block at a time (0: every wave writes when its row is
-// counted).  The chip writes fastest with few waves writing at once
-// (tools/micro/write_bw7: a linear stream from 4 waves per CU runs at the
-// memset rate, 6.5 TB/s; from 8 or 16 waves per CU at 5.0-6.0).
-// KARMA_PROF_TOKEN 1: the token passes once the row's stores are issued;
-// 2: once they have completed.
-#ifndef KARMA_PROF_WRITERS
-#define KARMA_PROF_WRITERS 0
-#endif
-#ifndef KARMA_PROF_TOKEN
-#define KARMA_PROF_TOKEN 1
-#endif
 __global__ void __launch_bounds__(kPBlock) __attribute__((amdgpu_waves_per_eu(KARMA_PROF_WAVES, KARMA_PROF_WAVES)))
 profile_wave_kernel(
     const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
@@ -766,7 +754,6 @@ profile_wave_kernel(
     double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
     int64_t exc0, const int64_t* __restrict__ m_dev) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ int writers;  // waves of the block writing a row now (KARMA_PROF_WRITERS)
     // wave index in an SGPR: contig offsets and lengths load with scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
@@ -797,7 +784,6 @@ profile_wave_kernel(
         for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
     }
     for (int j = lane; j < h_words; j += 64) counts[j] = 0;  // write_row_wave clears it after each row
-    if (threadIdx.x == 0) writers = 0;
     __syncthreads();
     const int kmin = P56 ? 5 : k;
     // software pipeline over this wave's contigs: the next contig's offsets
@@ -866,21 +852,7 @@ profile_wave_kernel(
         // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
         my = wave_total(my);
         if (lane == 0) row_tot[c] = (int64_t)my;
-        if (KARMA_PROF_WRITERS > 0) {
-            if (lane == 0) {
-                while (atomicAdd(&writers, 1) >= KARMA_PROF_WRITERS) {
-                    atomicSub(&writers, 1);
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
         write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
-        if (KARMA_PROF_WRITERS > 0) {
-            if (KARMA_PROF_TOKEN == 2) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) atomicSub(&writers, 1);
-        }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         cur = nxt;
@@ -1080,15 +1052,20 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
     int rc;
     const int64_t exc_cap = c->exc_bases * (kmode == KARMA_KMER_5P6 ? 11 : kmax) + 1;
     DevArray<uint64_t> exc_buf;
-    DevArray<unsigned long long> exc_cnt;
-    if ((rc = p->presence.alloc(ctx, p->nwords)) || (rc = p->row_tot.alloc(ctx, c->n ? c->n : 1)) ||
-        (rc = p->err.alloc(ctx, 1)) || (rc = exc_buf.alloc(ctx, exc_cap)) || (rc = exc_cnt.alloc(ctx, 1))) {
+    // one zeroed allocation (one memset): the presence bitmap, the exception
+    // k-mer counter, the row totals (8-byte aligned behind the bitmap)
+    const int64_t pw = (p->nwords + 1) & ~int64_t(1);
+    const int64_t nrow = c->n ? c->n : 1;
+    if ((rc = p->presence.alloc(ctx, pw + 2 + 2 * nrow)) || (rc = p->err.alloc(ctx, 1)) ||
+        (rc = exc_buf.alloc(ctx, exc_cap))) {
         delete p;
         return rc;
     }
-    KARMA_HIP(hipMemsetAsync(p->presence.ptr, 0, p->nwords * 4, ctx->stream));
-    KARMA_HIP(hipMemsetAsync(p->row_tot.ptr, 0, (c->n ? c->n : 1) * 8, ctx->stream));
-    KARMA_HIP(hipMemsetAsync(exc_cnt.ptr, 0, 8, ctx->stream));
+    KARMA_HIP(hipMemsetAsync(p->presence.ptr, 0, (pw + 2 + 2 * nrow) * 4, ctx->stream));
+    struct {
+        unsigned long long* ptr;
+    } exc_cnt{reinterpret_cast<unsigned long long*>(p->presence.ptr + pw)};
+    p->row_tot = reinterpret_cast<int64_t*>(p->presence.ptr + pw + 2);
     DevArray<int> full;
     if ((rc = full.alloc(ctx, 1))) {
         delete p;
@@ -1300,7 +1277,7 @@ int karma_kmer_row_totals(karma_kmer_plan* p, int64_t* dst) {
     KARMA_TRY(ctx_begin(p->ctx));
     if (p->store->n) {
         KARMA_CHECK(dst, KARMA_ERR_ARG, "null dst");
-        KARMA_HIP(hipMemcpyAsync(dst, p->row_tot.ptr, p->store->n * 8, hipMemcpyDeviceToHost, p->ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(dst, p->row_tot, p->store->n * 8, hipMemcpyDeviceToHost, p->ctx->stream));
         KARMA_HIP(hipStreamSynchronize(p->ctx->stream));
     }
     return KARMA_OK;
@@ -1324,7 +1301,7 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
                 (long long)lo, (long long)hi, (long long)c->n);
     const int64_t n = hi - lo, M = m_dev ? kmer_m_cap(p) : p->M;
     if (n == 0) return KARMA_OK;
-    int64_t* const row_tot = p->row_tot.ptr + lo;
+    int64_t* const row_tot = p->row_tot + lo;
     const uint8_t* const has_exc = c->has_exc.ptr + lo;
     const int64_t* const woff = c->woff.ptr + lo;
     const int64_t* const off = c->off + lo;

@@ -334,9 +334,24 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
                 if (on) adj += wlo[sr] - wbase[sr] - ro[sr];
             }
             const int nit = 32 - __clz(maxn);  // halving steps until every window is empty
-            for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
-                const uint64_t k = keys[i];
-                if (i > ro[r] && keys[i - 1] > k) *bad = 1;
+            // the tile's loads first (kMT / 256 elements per thread, all in flight)
+            constexpr int kPer = kMT / 256;
+            uint64_t kv[kPer], kp[kPer];
+            int64_t cv[kPer];
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int64_t i = t0 + threadIdx.x + (int64_t)u * 256;
+                const bool ok = i < t1;
+                kv[u] = ok ? keys[i] : 0;
+                kp[u] = ok && i > ro[r] ? keys[i - 1] : 0;
+                cv[u] = ok ? counts[i] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int64_t i = t0 + threadIdx.x + (int64_t)u * 256;
+                if (i >= t1) break;
+                const uint64_t k = kv[u];
+                if (kp[u] > k) *bad = 1;
                 int bb[kMFast], nn[kMFast];
 #pragma unroll
                 for (int sr = 0; sr < kMFast; ++sr) {
@@ -357,7 +372,7 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
 #pragma unroll
                 for (int sr = 0; sr < kMFast; ++sr) pos += bb[sr];
                 ko[pos] = k;
-                co[pos] = counts[i];
+                co[pos] = cv[u];
             }
             __syncthreads();  // the windows are rebuilt for the next tile
             continue;

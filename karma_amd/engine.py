@@ -529,13 +529,19 @@ class Edges:
         """The edges in host arrays (pinned host memory: the copies run at the
         full PCIe rate; the blocks return to the library's cache with the arrays)."""
         E = self.E
-        a = _lib.pinned_empty(max(E, 1), np.uint32)
-        b = _lib.pinned_empty(max(E, 1), np.uint32)
-        s = _lib.pinned_empty(max(E, 1), np.int64)
-        w = _lib.pinned_empty(max(E, 1), np.float64)
-        f = _lib.pinned_empty(max(E, 1), np.uint64)
+        e1, n1 = max(E, 1), max(self.n_contigs, 1)
+        # one pinned block: s, w, f, totals (8-byte items) then a, b (4-byte)
+        blk = _lib.pinned_empty(8 * (3 * e1 + n1) + 4 * (2 * e1 + 1), np.uint8)
+        o = [0]
+
+        def take(n, dt):
+            dt = np.dtype(dt)
+            v = blk[o[0]:o[0] + n * dt.itemsize].view(dt)
+            o[0] += n * dt.itemsize
+            return v
+        s, w, f, t = take(e1, np.int64), take(e1, np.float64), take(e1, np.uint64), take(n1, np.int64)
+        a, b = take(e1, np.uint32), take(e1, np.uint32)
         call("karma_edges_get", self.h, ptr(a), ptr(b), ptr(s), ptr(w), ptr(f), 0)
-        t = _lib.pinned_empty(max(self.n_contigs, 1), np.int64)
         call("karma_edges_totals", self.h, ptr(t), 0)
         return EdgeArrays(a[:E], b[:E], s[:E], w[:E], f[:E], t[: self.n_contigs])
 

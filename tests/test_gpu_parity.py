@@ -361,14 +361,41 @@ def test_eq_big_classes_device_inputs_and_errors():
     finally:
         for b in bufs:
             b.close()
+    # out-of-range members: the argument error, and no kernel touches memory
+    # out of bounds on the way (the context stays usable)
     for bad_at in (int(off[10]), int(off[-1]) - 1):  # inside a pair / the last class
         m2 = mem.copy()
         m2[bad_at] = n + 3
-        with pytest.raises(_lib.KarmaError):
+        with pytest.raises(_lib.KarmaError) as ei:
             engine.graph_from_eq(off, m2, cnt, skip, n)
+        assert ei.value.code == _lib.KARMA_ERR_ARG, str(ei.value)
     one = np.array([0, 1], np.int64)
-    with pytest.raises(_lib.KarmaError):  # a lone member out of range
+    with pytest.raises(_lib.KarmaError) as ei:  # a lone member out of range
         engine.graph_from_eq(one, np.array([n], np.uint32), np.array([3], np.int64), np.zeros(1, np.uint8), n)
+    assert ei.value.code == _lib.KARMA_ERR_ARG, str(ei.value)
+    e = engine.graph_from_eq(off, mem, cnt, skip, n)  # the context still works
+    assert len(e.a) > 0
+
+
+def test_eq_speculative_capacity_grows_and_shrinks():
+    """karma_graph_eq sizes its pair scratch from the context's previous pair
+    total (no readback): a call with more pairs than that runs again, sized;
+    one with fewer uses the larger scratch.  Both bit-exact."""
+    ctx = _lib.Context(0)
+    try:
+        for seed, n, nf in ((5, 300, 3000), (6, 3000, 200_000), (7, 200, 1000), (8, 4000, 300_000)):
+            classes = synth.eq_classes(seed, n, nf, True)
+            off = np.r_[0, np.cumsum([len(c) for c, _ in classes])].astype(np.int64)
+            mem = np.array([x for c, _ in classes for x in c], np.uint32)
+            cnt = np.array([k for _, k in classes], np.int64)
+            skip = np.array([1 if len(c) == 1 else 0 for c, _ in classes], np.uint8)
+            e = engine.graph_from_eq(off, mem, cnt, skip, n, ctx=ctx)
+            o = oracle.graph_groups(off, mem, cnt, skip, n, dedup=False)
+            for k in ("a", "b", "shared", "first", "totals"):
+                assert np.array_equal(getattr(e, k), o[k]), (seed, k)
+            assert np.array_equal(e.weight.view(np.uint64), o["weight"].view(np.uint64))
+    finally:
+        ctx.close()
 
 
 def test_eq_path_equals_readset_path():
@@ -568,7 +595,7 @@ def test_graph_records_split_call():
         _lib.load().karma_dev_free(ctx.h, dev)
 
 
-@pytest.mark.parametrize("chunk", ["4096", "8192"])
+@pytest.mark.parametrize("chunk", ["2048", "4096", "8192"])
 def test_records_both_chunk_sizes(chunk, monkeypatch):
     """Classify's chunk size follows the launch size (graph_sets.hip
     chunk_records): inputs below ~134M records take 4096-record chunks, config
