@@ -265,6 +265,14 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
+// KARMA_CLS_SORT (A/B build): classify stages its codes
+// in a wave-private LDS buffer of this many codes and writes each buffer
+// counting-sorted by code bucket (runs of one bucket back to back), as a
+// classify that feeds a reducer directly would; the partition still consumes
+// the chunk's codes (order inside a chunk is free), so results are unchanged.
+#ifndef KARMA_CLS_SORT
+#define KARMA_CLS_SORT 0
+#endif
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
@@ -303,6 +311,40 @@ classify2_kernel(ClassArgs P) {
     // the chunk's codes per code bucket, added to its partition block's row at the end
     __shared__ uint32_t whist[kCW / 64][HIST ? kMaxBc : 1];
     uint32_t* wh = whist[wave];
+    constexpr int kStage = KARMA_CLS_SORT > 0 ? KARMA_CLS_SORT : 1;
+    __shared__ uint32_t cstage[kCW / 64][kStage];
+    __shared__ uint32_t chist[kCW / 64][KARMA_CLS_SORT > 0 ? kMaxBc : 1];
+    uint32_t* stg = cstage[wave];
+    uint32_t* shh = chist[wave];
+    uint32_t ncs = 0, nc_out = 0;  // codes staged; codes written (the chunk region's fill)
+    // the staged codes to the chunk region, counting-sorted by code bucket
+    auto flush_stage = [&]() {
+        if (KARMA_CLS_SORT <= 0 || ncs == 0) return;
+        for (int b = lane; b < P.Bc; b += 64) shh[b] = 0;
+        wave_sync();
+        for (uint32_t j = lane; j < ncs; j += 64) atomicAdd(&shh[(stg[j] & 0xFFFFFFu) >> P.bwc], 1u);
+        wave_sync();
+        // exclusive scan of the bucket counts (lane l: buckets 2l, 2l + 1)
+        const uint32_t c0 = 2 * lane < P.Bc ? shh[2 * lane] : 0u, c1 = 2 * lane + 1 < P.Bc ? shh[2 * lane + 1] : 0u;
+        uint32_t x = c0 + c1;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        const uint32_t ex = x - c0 - c1;
+        wave_sync();
+        if (2 * lane < P.Bc) shh[2 * lane] = ex;
+        if (2 * lane + 1 < P.Bc) shh[2 * lane + 1] = ex + c0;
+        wave_sync();
+        for (uint32_t j = lane; j < ncs; j += 64) {
+            const uint32_t code = stg[j];
+            const uint32_t pos = atomicAdd(&shh[(code & 0xFFFFFFu) >> P.bwc], 1u);
+            out[nc_out + pos] = code;
+        }
+        nc_out += ncs;
+        ncs = 0;
+        wave_sync();
+    };
     constexpr bool hist_on = HIST;
     if (hist_on) {
         for (int b = lane; b < P.Bc; b += 64) wh[b] = 0;
@@ -355,6 +397,8 @@ classify2_kernel(ClassArgs P) {
     };
     auto step = [&](auto full_tag, u32x4 (&buf)[kCPer], u32x4 (&nxt)[kCPer], int64_t t0) {
         constexpr bool FULL = decltype(full_tag)::value;
+        // a step emits <= kCIter codes, the chunk tail one more
+        if (KARMA_CLS_SORT > 0 && ncs + kCIter + 1 > (uint32_t)kStage) flush_stage();
         uint32_t rid[8], ctg[8];
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
 #pragma unroll
@@ -403,9 +447,15 @@ classify2_kernel(ClassArgs P) {
             auto emit = [&](uint64_t e, uint64_t ok, uint32_t code, uint32_t pos, uint64_t big) {
                 if (!RARE) {
                     const uint64_t b = e & ok & ~big;
-                    // lanes without a code store past the region (bit 31): dropped
-                    const uint32_t boff = ((nc + (uint32_t)rank_below(b)) * 4u) | (in_mask(b) ? 0u : 0x80000000u);
-                    __builtin_amdgcn_raw_buffer_store_b32(code, out_rsrc, (int)boff, 0, KARMA_CODE_AUX);
+                    if (KARMA_CLS_SORT > 0) {
+                        if (in_mask(b)) stg[ncs + (uint32_t)rank_below(b)] = code;
+                        ncs += __popcll(b);
+                    } else {
+                        // lanes without a code store past the region (bit 31): dropped
+                        const uint32_t boff =
+                            ((nc + (uint32_t)rank_below(b)) * 4u) | (in_mask(b) ? 0u : 0x80000000u);
+                        __builtin_amdgcn_raw_buffer_store_b32(code, out_rsrc, (int)boff, 0, KARMA_CODE_AUX);
+                    }
                     if (hist_on && in_mask(b)) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
                     nc += __popcll(b);
                     rare |= e & (big | ~ok);
@@ -550,12 +600,18 @@ classify2_kernel(ClassArgs P) {
         if (lane == 0) {
             if (big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + ct_pos;
             else if (ok) {
-                out[nc] = code;
+                if (KARMA_CLS_SORT > 0) stg[ncs] = code;
+                else out[nc] = code;
                 if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
             } else out[P.chunk - 1 - ng] = ct_pos;
         }
+        if (KARMA_CLS_SORT > 0 && !big && ok) ++ncs;
         nc += ok ? 1u : 0u;
         ng += !big && !ok ? 1u : 0u;
+    }
+    if (KARMA_CLS_SORT > 0) {
+        wave_sync();
+        flush_stage();
     }
     if (lane == 0) {
         P.n_codes[chunk] = nc;
@@ -578,9 +634,17 @@ classify2_kernel(ClassArgs P) {
 
 // ---- general reads -----------------------------------------------------------------
 constexpr int kGW = 256;  // general-kernel threads (4 waves, one chunk each)
+// the general kernel's grid: a wave per chunk up to 4 blocks per CU
+int general_grid(const karma_ctx* ctx, int64_t n_chunks) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_chunks, kGW / 64), (int64_t)ctx->cu_count * 4));
+}
 
-// One wave per chunk: every pair (p <= q) of each general read's distinct
-// contigs, as (a << 32 | b), appended to the chunk's pair list.
+// A wave per chunk, grid-stride (the grid is sized to the chip, not to the
+// chunk count: on assembled transcriptomes almost every chunk has no general
+// read, and dispatching one wave per chunk cost 17-23 us at the 8-rank strong
+// preview while the code partition waited for CU slots): every pair (p <= q)
+// of each general read's distinct contigs, as (a << 32 | b), appended to the
+// chunk's pair list.
 __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ rec, int64_t A, uint32_t N,
                                                        const uint32_t* __restrict__ codes,
                                                        const uint32_t* __restrict__ n_gen, int64_t n_chunks,
@@ -591,10 +655,11 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
                                                        const uint32_t* __restrict__ remap,
                                                        const unsigned* __restrict__ relabel, int64_t chunk_len) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t chunk = (int64_t)blockIdx.x * (kGW / 64) + wave;
-    if (chunk >= n_chunks) return;
     // a relabelled rerun follows (relabel_probe_kernel): no pairs now
-    const uint32_t ng = relabel && *relabel ? 0u : n_gen[chunk];
+    const bool skip = relabel && *relabel;
+    for (int64_t chunk = (int64_t)blockIdx.x * (kGW / 64) + wave; chunk < n_chunks;
+         chunk += (int64_t)gridDim.x * (kGW / 64)) {
+    const uint32_t ng = skip ? 0u : n_gen[chunk];
     uint32_t np = 0;
     uint64_t* out = pairs + chunk * pcap;
     const int64_t c_lo = chunk * chunk_len;
@@ -640,18 +705,22 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
         if (np) atomicAdd(blk_items + chunk / lists_per_block, (unsigned long long)np);
         if (full) flags[2] = 1;  // the host reruns with room for every pair
     }
+    }
 }
 
 // ---- partition: chunk lists -> bucket-major padded runs ---------------------------
 constexpr int kPT = 512;                 // partition threads (several blocks per CU overlap their phases)
 constexpr int kMaxListsPerBlock = 128;   // chunk lists per partition block, at most (a power of 2)
 
+#ifndef KARMA_CODE_FILL
+#define KARMA_CODE_FILL 8192  // codes per partition flush (A/B builds: shorter runs for the reduce)
+#endif
 // compact-read codes: u32 (m0 | M << 24) -> u16 (m0_local << 3 | M) per code bucket
 template <int NB>
 struct CodeStreamT {
     using S = uint32_t;
     using D = uint16_t;
-    static constexpr int kCap = 8192;   // codes per flush (32 KB of LDS)
+    static constexpr int kCap = KARMA_CODE_FILL;  // codes per flush (8192: 32 KB of LDS)
     static constexpr int kPad = 8;      // 16 B of u16
     static constexpr int kMaxNb = NB;
     static constexpr D kPadV = 0xFFFF;  // codes are < 2^15
@@ -1786,7 +1855,7 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
                         nullptr,   0,         0,       nullptr, 0, nullptr, kCChunk};
             KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false>), ceil_div(n_chunks, kCW / 64), kCW, 0, C);
         }
-        KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
+        KARMA_LAUNCH(ctx, "graph_general", general_kernel, general_grid(ctx, n_chunks), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags,
                      (const uint32_t*)nullptr, (const unsigned*)nullptr, kCChunk);
         KARMA_LAUNCH(ctx, "widen_counts", widen_counts_kernel, grid_n(n_chunks + 1), 256, 0, n_pl.ptr, n_chunks,
@@ -2199,7 +2268,7 @@ int SetsJob::launch() {
         ctx->stream = ctx->fork_stream;
     }
     int rc_pair = [&]() -> int {
-        KARMA_LAUNCH(ctx, "graph_general", general_kernel, ceil_div(n_chunks, kGW / 64), kGW, 0, rec, A, (uint32_t)N,
+        KARMA_LAUNCH(ctx, "graph_general", general_kernel, general_grid(ctx, n_chunks), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items + n_pblk, lpb, flags,
                      relabeled ? (const uint32_t*)remap_map.ptr : nullptr, (const unsigned*)(counters + 3), chunk);
         if (wide_p)
