@@ -318,6 +318,9 @@ int karma_edges_destroy(karma_edges* e);
 int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* shared, double* weight, uint64_t* first,
                     int is_device);
 int karma_edges_totals(karma_edges* e, int64_t* totals, int is_device);
+/* karma_edges_get and karma_edges_totals with one synchronisation. */
+int karma_edges_get_all(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, double* w, uint64_t* first,
+                        int64_t* totals, int is_device);
 
 /* ---- one rank's step of the sharded build ---------------
  * The whole hot path of one batch on this rank as one call: the records job

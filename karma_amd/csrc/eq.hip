@@ -41,7 +41,7 @@ namespace {
 constexpr int kEqT = 256;      // threads of the per-class kernels
 constexpr int64_t kSmallM = 32;  // classes above this size: a block each
 constexpr int kRT = 512;         // seg_reduce threads
-constexpr int kSeg = 2048;       // target entries per seg_reduce block
+constexpr int kSeg = 1024;       // target entries per seg_reduce block (48 KB of LDS: 3 blocks per CU, one round)
 constexpr int kSegCap = 2 * kSeg;  // LDS capacity of one block's run (runs snap to segment starts)
 
 // pair t (combinations order) of a class of m members -> (i, j), i < j:
@@ -226,12 +226,12 @@ __device__ __forceinline__ int64_t run_start_g(const int64_t* __restrict__ segof
     return done ? P : segoff[a];
 }
 
-// Distinct keys of a sorted run, summed: position p of the run holds
-// key(p) / the original entry index idx(p).  Writes them to the staging
-// arrays at [r0, r0 + u) and returns u (every thread).
-template <typename KeyAt, typename IdxAt>
-__device__ int64_t reduce_sorted_run(int64_t r0, int64_t n, KeyAt key_at, IdxAt idx_at, Placed in,
-                                     const int64_t* __restrict__ cnt, Entries st, int64_t* lds_w) {
+// Distinct keys of a sorted run, summed: position p of the run holds key(p),
+// its class count cnt_at(p) and emission index ref_at(p).  Writes them to the
+// staging arrays at [r0, r0 + u) and returns u (every thread).
+template <typename KeyAt, typename CntAt, typename RefAt>
+__device__ int64_t reduce_sorted_run(int64_t r0, int64_t n, KeyAt key_at, CntAt cnt_at, RefAt ref_at, Entries st,
+                                     int64_t* lds_w) {
     int64_t u_total = 0, base_u = 0;
     for (int64_t c0 = 0; c0 < n; c0 += kRT) {
         const int64_t p = c0 + threadIdx.x;
@@ -243,9 +243,8 @@ __device__ int64_t reduce_sorted_run(int64_t r0, int64_t n, KeyAt key_at, IdxAt 
             int64_t sum = 0;
             uint64_t f = ~0ull;
             for (int64_t q = p; q < n && key_at(q) == k; ++q) {
-                const int64_t e = idx_at(q);
-                sum += cnt[in.cls[e]];
-                f = min(f, (uint64_t)in.ref[e]);
+                sum += cnt_at(q);
+                f = min(f, (uint64_t)ref_at(q));
             }
             st.key[r0 + pos] = k;
             st.cnt[r0 + pos] = sum;
@@ -315,9 +314,19 @@ __global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restri
             oidx[rank] = (uint32_t)p;
         }
         __syncthreads();
+        // each entry's class count and emission index into LDS in sorted order
+        // (independent gathers, all in flight; the group sums then read LDS)
+        int64_t* scnt = reinterpret_cast<int64_t*>(skey);
+        uint32_t* sref = sidx;
+        for (int64_t p = threadIdx.x; p < n; p += kRT) {
+            const int64_t e = r0 + (int64_t)oidx[p];
+            scnt[p] = cnt[in.cls[e]];
+            sref[p] = in.ref[e];
+        }
+        __syncthreads();
         u = reduce_sorted_run(
-            r0, n, [&](int64_t p) { return okey[p]; }, [&](int64_t p) { return r0 + (int64_t)oidx[p]; }, in, cnt, st,
-            lds_w);
+            r0, n, [&](int64_t p) { return okey[p]; }, [&](int64_t p) { return scnt[p]; },
+            [&](int64_t p) { return sref[p]; }, st, lds_w);
     } else {
         // a run with a segment of > kSeg entries: bottom-up merge sort of
         // (key, index) in global scratch (stable merge ranks), then the same reduce
@@ -363,8 +372,8 @@ __global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restri
             ib = ti;
         }
         u = reduce_sorted_run(
-            r0, n, [&](int64_t p) { return ka[p]; }, [&](int64_t p) { return r0 + (int64_t)ia[p]; }, in, cnt, st,
-            lds_w);
+            r0, n, [&](int64_t p) { return ka[p]; }, [&](int64_t p) { return cnt[in.cls[r0 + (int64_t)ia[p]]]; },
+            [&](int64_t p) { return in.ref[r0 + (int64_t)ia[p]]; }, st, lds_w);
     }
     // 5. the run's distinct keys after those of the runs before it
     if (threadIdx.x < 64) {

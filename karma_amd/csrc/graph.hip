@@ -1149,6 +1149,26 @@ int karma_edges_get(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, double
     return KARMA_OK;
 }
 
+// karma_edges_get and karma_edges_totals in one synchronisation
+int karma_edges_get_all(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, double* w, uint64_t* first,
+                        int64_t* totals, int is_device) {
+    KARMA_CHECK(e && (totals || !e->n_contigs), KARMA_ERR_ARG, "bad arguments");
+    KARMA_TRY(ctx_begin(e->ctx));
+    KARMA_TRY(edges_resolve(e));
+    const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    hipStream_t st = e->ctx->stream;
+    if (e->n_contigs) KARMA_HIP(hipMemcpyAsync(totals, e->totals.ptr, e->n_contigs * 8, kind, st));
+    if (e->E) {
+        if (a) KARMA_HIP(hipMemcpyAsync(a, e->a.ptr, e->E * 4, kind, st));
+        if (b) KARMA_HIP(hipMemcpyAsync(b, e->b.ptr, e->E * 4, kind, st));
+        if (s) KARMA_HIP(hipMemcpyAsync(s, e->s.ptr, e->E * 8, kind, st));
+        if (w) KARMA_HIP(hipMemcpyAsync(w, e->w.ptr, e->E * 8, kind, st));
+        if (first && e->has_first) KARMA_HIP(hipMemcpyAsync(first, e->first.ptr, e->E * 8, kind, st));
+    }
+    KARMA_HIP(hipStreamSynchronize(st));
+    return KARMA_OK;
+}
+
 int karma_edges_totals(karma_edges* e, int64_t* totals, int is_device) {
     KARMA_CHECK(e && (totals || !e->n_contigs), KARMA_ERR_ARG, "bad arguments");
     KARMA_TRY(ctx_begin(e->ctx));

@@ -273,6 +273,12 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 #ifndef KARMA_CLS_SORT
 #define KARMA_CLS_SORT 0
 #endif
+// KARMA_CLS_STAGE (A/B build): the same LDS staging without the sort -- each
+// stage written out as one contiguous, coalesced copy (are the scattered
+// per-emit buffer stores what keeps classify off the read rate?)
+#ifndef KARMA_CLS_STAGE
+#define KARMA_CLS_STAGE 0
+#endif
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
@@ -311,7 +317,8 @@ classify2_kernel(ClassArgs P) {
     // the chunk's codes per code bucket, added to its partition block's row at the end
     __shared__ uint32_t whist[kCW / 64][HIST ? kMaxBc : 1];
     uint32_t* wh = whist[wave];
-    constexpr int kStage = KARMA_CLS_SORT > 0 ? KARMA_CLS_SORT : 1;
+    constexpr int kStage = KARMA_CLS_SORT > 0 ? KARMA_CLS_SORT : (KARMA_CLS_STAGE > 0 ? KARMA_CLS_STAGE : 1);
+    constexpr bool kStaged = KARMA_CLS_SORT > 0 || KARMA_CLS_STAGE > 0;
     __shared__ uint32_t cstage[kCW / 64][kStage];
     __shared__ uint32_t chist[kCW / 64][KARMA_CLS_SORT > 0 ? kMaxBc : 1];
     uint32_t* stg = cstage[wave];
@@ -319,7 +326,15 @@ classify2_kernel(ClassArgs P) {
     uint32_t ncs = 0, nc_out = 0;  // codes staged; codes written (the chunk region's fill)
     // the staged codes to the chunk region, counting-sorted by code bucket
     auto flush_stage = [&]() {
-        if (KARMA_CLS_SORT <= 0 || ncs == 0) return;
+        if (!kStaged || ncs == 0) return;
+        if (KARMA_CLS_STAGE > 0) {  // a contiguous copy, 64 codes per store instruction
+            wave_sync();
+            for (uint32_t j = lane; j < ncs; j += 64) out[nc_out + j] = stg[j];
+            nc_out += ncs;
+            ncs = 0;
+            wave_sync();
+            return;
+        }
         for (int b = lane; b < P.Bc; b += 64) shh[b] = 0;
         wave_sync();
         for (uint32_t j = lane; j < ncs; j += 64) atomicAdd(&shh[(stg[j] & 0xFFFFFFu) >> P.bwc], 1u);
@@ -398,7 +413,7 @@ classify2_kernel(ClassArgs P) {
     auto step = [&](auto full_tag, u32x4 (&buf)[kCPer], u32x4 (&nxt)[kCPer], int64_t t0) {
         constexpr bool FULL = decltype(full_tag)::value;
         // a step emits <= kCIter codes, the chunk tail one more
-        if (KARMA_CLS_SORT > 0 && ncs + kCIter + 1 > (uint32_t)kStage) flush_stage();
+        if (kStaged && ncs + kCIter + 1 > (uint32_t)kStage) flush_stage();
         uint32_t rid[8], ctg[8];
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
 #pragma unroll
@@ -447,7 +462,7 @@ classify2_kernel(ClassArgs P) {
             auto emit = [&](uint64_t e, uint64_t ok, uint32_t code, uint32_t pos, uint64_t big) {
                 if (!RARE) {
                     const uint64_t b = e & ok & ~big;
-                    if (KARMA_CLS_SORT > 0) {
+                    if (kStaged) {
                         if (in_mask(b)) stg[ncs + (uint32_t)rank_below(b)] = code;
                         ncs += __popcll(b);
                     } else {
@@ -600,16 +615,16 @@ classify2_kernel(ClassArgs P) {
         if (lane == 0) {
             if (big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + ct_pos;
             else if (ok) {
-                if (KARMA_CLS_SORT > 0) stg[ncs] = code;
+                if (kStaged) stg[ncs] = code;
                 else out[nc] = code;
                 if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
             } else out[P.chunk - 1 - ng] = ct_pos;
         }
-        if (KARMA_CLS_SORT > 0 && !big && ok) ++ncs;
+        if (kStaged && !big && ok) ++ncs;
         nc += ok ? 1u : 0u;
         ng += !big && !ok ? 1u : 0u;
     }
-    if (KARMA_CLS_SORT > 0) {
+    if (kStaged) {
         wave_sync();
         flush_stage();
     }

@@ -541,8 +541,7 @@ class Edges:
             return v
         s, w, f, t = take(e1, np.int64), take(e1, np.float64), take(e1, np.uint64), take(n1, np.int64)
         a, b = take(e1, np.uint32), take(e1, np.uint32)
-        call("karma_edges_get", self.h, ptr(a), ptr(b), ptr(s), ptr(w), ptr(f), 0)
-        call("karma_edges_totals", self.h, ptr(t), 0)
+        call("karma_edges_get_all", self.h, ptr(a), ptr(b), ptr(s), ptr(w), ptr(f), ptr(t), 0)
         return EdgeArrays(a[:E], b[:E], s[:E], w[:E], f[:E], t[: self.n_contigs])
 
     def close(self):
