@@ -46,7 +46,7 @@ namespace {
 constexpr int kRing = 64;  // status entries in the mapped slot (64 B each)
 constexpr int kLag = 3;    // deferred steps the host may have in flight (two main streams alternate)
 
-// One deferred step's status, written by the edge write kernel's last block (seq last).
+// One deferred step's status, written by step_status_kernel (seq last).
 struct StepStatus {
     uint64_t seq;
     int64_t slow;   // bits: 1 relabel, 2 pair capacity, 4 big reads, 8 bucket overflow
@@ -121,59 +121,13 @@ __global__ void __launch_bounds__(kET) step_edge_count_kernel(const uint64_t* __
 // binary64 without contraction (read_graph.py:39-42).  st[0] zero-total flag,
 // st[1] a key past the contig range (no edge), st[2] the edge count (all
 // cleared by the count kernel, earlier on the stream).
-// Every word a host would have checked after a deferred step, into its ring
-// entry (seq written last, released to the host): written by the edge write
-// kernel's last block, so no launch of its own.
-struct StatusIn {
-    const int* flags;
-    const unsigned* counters;
-    const uint8_t* ovf;
-    int B;
-    const int64_t* dst;
-    int64_t* merge_bad;   // null: no merge
-    StepStatus* out;
-    uint64_t seq;
-    unsigned* done;       // blocks of the write kernel finished (reset by the last)
-};
-
-__device__ void write_status(const StatusIn& s, const int64_t* est) {
-    __shared__ int any_ovf;
-    if (threadIdx.x == 0) any_ovf = 0;
-    __syncthreads();
-    for (int b = threadIdx.x; b < s.B; b += blockDim.x)
-        if (s.ovf[b]) any_ovf = 1;
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    int64_t slow = 0, err = 0;
-    if (s.counters[3]) slow |= 1;
-    if (s.flags[2]) slow |= 2;
-    if (s.counters[0]) slow |= 4;
-    if (any_ovf) slow |= 8;
-    if (s.flags[0]) err |= 1;
-    if (s.flags[1]) err |= 2;
-    if (s.flags[3]) err |= 4;
-    if (est[0]) err |= 8;
-    if (est[1]) err |= 2;  // a key past the contig range
-    if (s.merge_bad) {
-        if (*s.merge_bad) err |= 16;
-        *s.merge_bad = 0;  // cleared for the next step's merge (stream order)
-    }
-    s.out->slow = slow;
-    s.out->err = err;
-    s.out->U = s.dst[s.B];
-    s.out->E = est[2];
-    *s.done = 0;
-    __hip_atomic_store(&s.out->seq, s.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __global__ void __launch_bounds__(kET) step_edge_write_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ counts, const int64_t* __restrict__ n_dev,
     const int64_t* __restrict__ totals, const int64_t* __restrict__ tile_cnt, uint32_t* __restrict__ ea,
     uint32_t* __restrict__ eb, int64_t* __restrict__ es, double* __restrict__ ew, int64_t* __restrict__ st,
-    int64_t n_tot, StatusIn sin) {
+    int64_t n_tot) {
     __shared__ int64_t wsum[kET / 64];
     __shared__ int64_t base_s;
-    __shared__ bool last;
     const int64_t n = *n_dev;
     const int64_t tiles = (n + kET - 1) / kET;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -232,16 +186,6 @@ __global__ void __launch_bounds__(kET) step_edge_write_kernel(
             }
         }
         __syncthreads();  // wsum / base_s reused by the next tile
-    }
-    // the last block to finish writes the step's status (every block's edge
-    // and flag writes are visible to it: fence, then the count)
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(sin.done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (last) {
-        __threadfence();
-        write_status(sin, st);
     }
 }
 
@@ -454,6 +398,40 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
         }
         __syncthreads();  // the windows are rebuilt for the next tile
     }
+}
+
+// Every word a host would have checked after a deferred step, into the ring
+// entry (seq written last, released to the host).
+__global__ void step_status_kernel(const int* __restrict__ flags, const unsigned* __restrict__ counters,
+                                   const uint8_t* __restrict__ ovf, int B, const int64_t* __restrict__ dst,
+                                   int64_t* __restrict__ merge_bad, const int64_t* __restrict__ est,
+                                   StepStatus* __restrict__ out, uint64_t seq) {
+    __shared__ int any_ovf;
+    if (threadIdx.x == 0) any_ovf = 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < B; b += blockDim.x)
+        if (ovf[b]) any_ovf = 1;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    int64_t slow = 0, err = 0;
+    if (counters[3]) slow |= 1;
+    if (flags[2]) slow |= 2;
+    if (counters[0]) slow |= 4;
+    if (any_ovf) slow |= 8;
+    if (flags[0]) err |= 1;
+    if (flags[1]) err |= 2;
+    if (flags[3]) err |= 4;
+    if (est[0]) err |= 8;
+    if (est[1]) err |= 2;  // a key past the contig range
+    if (merge_bad) {
+        if (*merge_bad) err |= 16;
+        *merge_bad = 0;  // cleared for the next step's merge (stream order)
+    }
+    out->slow = slow;
+    out->err = err;
+    out->U = dst[B];
+    out->E = est[2];
+    __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -886,10 +864,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     }
     KARMA_TRY(ensure_arr(ctx, tl.tot, s->n_glob));
     KARMA_TRY(ensure_arr(ctx, tl.tile_cnt, (v.cap + kET - 1) / kET + 1));
-    if (!tl.est.ptr) {  // [0..2] the edge stage's flags and count, [3] the write kernel's finished blocks
-        KARMA_TRY(tl.est.alloc(ctx, 4));
-        KARMA_HIP(hipMemsetAsync(tl.est.ptr, 0, 32, ctx->stream));
-    }
+    KARMA_TRY(ensure_arr(ctx, tl.est, 3));
     KARMA_TRY(ensure_arr(ctx, tl.ea, v.cap));
     KARMA_TRY(ensure_arr(ctx, tl.eb, v.cap));
     KARMA_TRY(ensure_arr(ctx, tl.es, v.cap));
@@ -897,10 +872,10 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((v.cap + kET - 1) / kET, cu));
     KARMA_LAUNCH(ctx, "edge_count", step_edge_count_kernel, grid, kET, 0, lk, lc, n_dev, s->n_glob, tl.tot.ptr,
                  tl.tile_cnt.ptr, tl.est.ptr);
-    const StatusIn sin{v.flags, v.counters, v.ovf, v.B, v.dst, mbad, s->ring_d + seq % kRing, seq,
-                       reinterpret_cast<unsigned*>(tl.est.ptr + 3)};
     KARMA_LAUNCH(ctx, "edge_weights", step_edge_write_kernel, grid, kET, 0, lk, lc, n_dev, tl.tot.ptr,
-                 tl.tile_cnt.ptr, tl.ea.ptr, tl.eb.ptr, tl.es.ptr, tl.ew.ptr, tl.est.ptr, s->n_glob, sin);
+                 tl.tile_cnt.ptr, tl.ea.ptr, tl.eb.ptr, tl.es.ptr, tl.ew.ptr, tl.est.ptr, s->n_glob);
+    KARMA_LAUNCH(ctx, "step_status", step_status_kernel, 1, 256, 0, v.flags, v.counters, v.ovf, v.B, v.dst, mbad,
+                 tl.est.ptr, s->ring_d + seq % kRing, seq);
     s->pending.push_back({seq, store, rec, A});
     return KARMA_OK;
 }
