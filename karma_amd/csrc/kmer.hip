@@ -859,6 +859,177 @@ profile_wave_kernel(
     }
 }
 
+// ---- counting waves and writing waves (A/B build: KARMA_PROF_SPLIT writers) ----
+// The chip writes rows fastest from few waves per CU (tools/micro/write_bw7:
+// 6.5 TB/s from 4 streaming waves per CU, 5.2 TB/s from the 24 row-writing
+// waves the profile runs).  Here a 16-wave block splits into counting waves
+// (two LDS histograms each, ping-pong) and KARMA_PROF_SPLIT writing waves that
+// take full histograms from an LDS queue, write the row and clear it.  Every
+// wait has a partner that always progresses (writers leave only when every
+// counter has finished and no histogram is full), so the waits end.
+#ifndef KARMA_PROF_SPLIT
+#define KARMA_PROF_SPLIT 0
+#endif
+constexpr int kSplitW = KARMA_PROF_SPLIT > 0 ? KARMA_PROF_SPLIT : 1;
+constexpr int kSplitNC = 16 - kSplitW;
+
+template <bool P56, bool C16>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
+profile_split_kernel(
+    const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
+    const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
+    const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
+    const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
+    double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
+    int64_t exc0, const int64_t* __restrict__ m_dev) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    __shared__ int bstate[2 * kSplitNC];  // 0 free (its counter's), 1 full, 2 being written
+    __shared__ int64_t brow[2 * kSplitNC];
+    __shared__ int bklen[2 * kSplitNC];
+    __shared__ int ndone;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
+    const int t_pad = (int)((tab_entries(P56, S) + 7) & ~7);
+    const int h_words = (int)hist_words(M, C16);
+    if (m_dev) {
+        M = *m_dev;
+        ld = M;
+    }
+    uint32_t* cbase = lds + t_pad / 2;
+    const int per_c = 2 * h_words + kProfWin;
+    if (P56) {
+        for (int o = threadIdx.x; o < 1088; o += blockDim.x) {
+            uint32_t ord;
+            if (o < 1024) {
+                ord = 5u * o;
+            } else {
+                const uint32_t h3 = o - 1024, c6 = h3 << 6 | rev3(h3);
+                ord = (c6 >> 2) * 5u + 1u + (c6 & 3u);
+            }
+            tab[o] = (uint16_t)col_of_ord[ord];
+        }
+    } else {
+        for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
+    }
+    if (wave < kSplitNC)
+        for (int j = lane; j < 2 * h_words; j += 64) cbase[wave * per_c + j] = 0;
+    if (threadIdx.x < 2 * kSplitNC) bstate[threadIdx.x] = 0;
+    if (threadIdx.x == 0) ndone = 0;
+    __syncthreads();
+    if (wave < kSplitNC) {
+        const int kmin = P56 ? 5 : k;
+        uint32_t* win = cbase + wave * per_c + 2 * h_words;
+        uint16_t* mbuf = reinterpret_cast<uint16_t*>(win + 80);
+        struct Meta {
+            int64_t s = 0, L = 0, w0 = 0;
+            int32_t klen = 0;
+            bool exc = false;
+        };
+        auto meta = [&](int64_t cc, Meta& m) {
+            if (cc < n) {
+                m.s = off[cc];
+                m.L = off[cc + 1] - m.s;
+                m.w0 = woff[cc];
+                m.klen = keylen[cc];
+                const int64_t ce = exc0 + cc;
+                const uint32_t hw = reinterpret_cast<const uint32_t*>(has_exc)[ce >> 2];
+                m.exc = ((hw >> (8 * (ce & 3))) & 0xFFu) != 0;
+            }
+        };
+        const int64_t stride = (int64_t)gridDim.x * kSplitNC;
+        int64_t c = (int64_t)blockIdx.x * kSplitNC + wave;
+        Meta cur, nxt;
+        Stage st0;
+        meta(c, cur);
+        if (c < n) st0.load(packed, mask, cur.exc, cur.w0, lane);
+        int b = 0;
+        for (; c < n; c += stride) {
+            meta(c + stride, nxt);
+            const int slot = 2 * wave + b;
+            while (__hip_atomic_load(&bstate[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+                __builtin_amdgcn_s_sleep(1);
+            uint32_t* counts = cbase + wave * per_c + b * h_words;
+            const int64_t L = cur.L;
+            unsigned my = 0;
+            if (!cur.exc) {
+                count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
+            } else {
+                const uint8_t* craw = raw + cur.s;
+                auto add = [&](uint32_t cl) {
+                    hist_add<C16>(counts, cl);
+                    ++my;
+                };
+                for_each_window(packed, mask, true, cur.w0, L - kmin + 1, win, mbuf, lane,
+                                [&](int64_t i, const Window& v) {
+                    if (P56) {
+                        if (v.clean(5)) add(tab[v.code(5)]);
+                        else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 5, true))]);
+                        if (i + 6 <= L) {
+                            if (v.clean(6)) {
+                                const uint32_t c6 = v.code(6);
+                                if (pal6_code(c6)) add(tab[1024u + (c6 >> 6)]);
+                            } else if (pal_bytes(craw + i, 6)) {
+                                add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 6, true))]);
+                            }
+                        }
+                    } else {
+                        if (v.clean(k)) add(tab[v.code(k)]);
+                        else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
+                    }
+                }, &st0);
+            }
+            if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
+            my = wave_total(my);
+            if (lane == 0) {
+                row_tot[c] = (int64_t)my;
+                brow[slot] = c;
+                bklen[slot] = cur.klen;
+                __hip_atomic_store(&bstate[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            __builtin_amdgcn_wave_barrier();
+            b ^= 1;
+            cur = nxt;
+        }
+        if (lane == 0) __hip_atomic_fetch_add(&ndone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        const int wi = wave - kSplitNC;
+        double* lut = reinterpret_cast<double*>(cbase + kSplitNC * per_c + wi * kProfWin);
+        for (;;) {
+            int st = lane < 2 * kSplitNC
+                         ? __hip_atomic_load(&bstate[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
+                         : 0;
+            unsigned long long full = __ballot(st == 1);
+            if (!full) {
+                if (__hip_atomic_load(&ndone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == kSplitNC) {
+                    st = lane < 2 * kSplitNC
+                             ? __hip_atomic_load(&bstate[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
+                             : 0;
+                    if (!__ballot(st == 1)) break;
+                    continue;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            // writers start their search at different slots
+            const int sh = (2 * wi) & 63;
+            const unsigned long long rot = sh ? ((full >> sh) | (full << (64 - sh))) : full;
+            const int pick = (__ffsll((long long)rot) - 1 + sh) & 63;
+            int got = 0;
+            if (lane == 0) got = atomicCAS(&bstate[pick], 1, 2) == 1;
+            got = __shfl(got, 0, 64);
+            if (!got) continue;
+            const int64_t row = brow[pick];
+            const int klen = bklen[pick];
+            uint32_t* counts = cbase + (pick >> 1) * per_c + (pick & 1) * h_words;
+            write_row_wave<C16>(out + row * ld, counts, M, klen, err, lut, lane);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) __hip_atomic_store(&bstate[pick], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
 // ---- block-per-contig profile (large M) --------------------------------------
 // One block per contig: histogram in LDS or, past the LDS budget, in a global
 // scratch row.
@@ -1343,7 +1514,16 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
                      p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err,       \
                      (int)p->S, row_tot, lo, m_dev);                                                             \
     } while (0)
-        if (p56) {
+        if (KARMA_PROF_SPLIT > 0 && p56 && c16) {
+            const size_t lds_s = (size_t)((tab_entries(true, p->S) + 7) & ~7) * 2 +
+                                 (size_t)kSplitNC * (2 * hist_words(M, true) + kProfWin) * 4 +
+                                 (size_t)kSplitW * kProfWin * 4;
+            const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_split_kernel<true, true>), 1024,
+                                         lds_s, ceil_div(n, kSplitNC));
+            KARMA_LAUNCH(ctx, "kmer_profile", (profile_split_kernel<true, true>), g_, 1024, lds_s, c->packed.ptr,
+                         c->mask.ptr, c->has_exc.ptr, woff, off, c->raw, keylen, n, k, with_len, p->col_of_ord.ptr,
+                         p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err, (int)p->S, row_tot, lo, m_dev);
+        } else if (p56) {
             if (c16) KARMA_WAVE_LAUNCH(true, true);
             else KARMA_WAVE_LAUNCH(true, false);
         } else {

@@ -450,7 +450,9 @@ struct karma_step {
     // beside this batch's merge and edge stage (a stream of batches)
     hipStream_t alt_s = nullptr;
     int streams = 0;              // KARMA_STEP_STREAMS: 1 / 2 main streams (0: by the batch's size)
-    hipEvent_t ev = nullptr;      // side -> main join
+    hipEvent_t ev = nullptr;      // side -> main join: the last deferred step's profile (one main stream)
+    bool ev_set = false;
+    bool join = false;            // KARMA_STEP_JOIN=1: join (A/B; measured slower, see run_deferred)
     // the profile (persistent; rows of n_loc x M, dense)
     DevArray<double> prof;
     // outputs of the last synchronous step
@@ -805,6 +807,15 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     const bool two = s->streams ? s->streams == 2 : A < kAltMaxRecords;
     const int par = sequential || !two ? 0 : (int)(seq & 1);
     hipStream_t const ms = par ? s->alt_s : s->main_s;
+    // One main stream (large batches): the records job does not wait for the
+    // previous batch's profile.  With KARMA_STEP_JOIN=1 it does (classify then
+    // never shares HBM with a profile): config 3 1.29-1.31 against 1.16-1.21 ms
+    // per step without the join (profiles/r04/ab_join/).
+    if (!two && !sequential && s->ev_set && s->join) {
+        if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
+        KARMA_HIP(hipStreamWaitEvent(ms, s->ev, 0));
+        s->ev_set = false;
+    }
     karma_step::Tail& tl = s->tail[par];
     ctx->stream = ms;
     s->prof_seq = seq;
@@ -833,6 +844,12 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         rc = hipStreamWaitEvent(s->side_s, ctx->mark_ev, 0) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
     }
     if (!rc && s->n_loc) rc = kmer_profile_device_m(plan, tl.prof.ptr, m_dev);
+    if (!rc && !two && !sequential && s->join) {
+        if (!s->ev && hipEventCreateWithFlags(&s->ev, hipEventDisableTiming) != hipSuccess) rc = KARMA_ERR_HIP;
+        if (counted_call("hipEventRecord")) ++t_hip_calls;
+        if (!rc) rc = hipEventRecord(s->ev, side) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
+        s->ev_set = !rc;
+    }
     if (plan) karma_kmer_plan_destroy(plan);  // its buffers return to the side stream's cache
     ctx->stream = ms;
     KARMA_TRY(rc);
@@ -911,6 +928,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     s->nranks = nranks;
     s->emulate = world == 1 && nranks > 1 ? nranks : 0;
     if (const char* e = getenv("KARMA_STEP_STREAMS")) s->streams = atoi(e) == 1 ? 1 : atoi(e) == 2 ? 2 : 0;
+    if (const char* e = getenv("KARMA_STEP_JOIN")) s->join = atoi(e) != 0;  // A/B only
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
