@@ -182,6 +182,7 @@ class Leg:
         comm.barrier()
         self.sync_all()
         calls0 = _lib.api_calls()
+        info0 = self.build.native.info() if self.build.native is not None else None
         host = 0.0
         t0 = time.perf_counter()
         # a stream of batches: the outputs of every step but the last are not
@@ -202,6 +203,10 @@ class Leg:
         self.host_us_per_step = host / steps * 1e6
         self.api_calls_per_step = (_lib.api_calls() - calls0) / steps
         self.step_info = self.build.native.info().tolist() if self.build.native is not None else None
+        # of the host time inside the step calls: waiting for the device (a
+        # deferred step's status kLag steps back) vs enqueueing the step
+        self.host_wait_us_per_step = ((self.step_info[9] - int(info0[9])) / steps / 1e3
+                                      if info0 is not None else None)
         dom_live = None
         if dom:
             for c in self.ctxs:
@@ -347,13 +352,27 @@ def main():
                 "traffic": traffic, "bytes_per_launch": b,
                 "intermediate_bytes_per_launch": intermediate_bytes.get(dom, 0),
                 "avg_launch_ms": round(ms / nl, 4), "launches": nl}
+        solo = kern.get(dom)
+        if solo and solo[1]:
+            # the same kernel alone on the chip (the sequential pass): in the
+            # timed stream a deferred batch's classify shares HBM with the
+            # previous batch's profile, which lengthens its live launches
+            solo_s = solo[0] / solo[1] / 1e3
+            roof["solo_launch_ms"] = round(solo[0] / solo[1], 4)
+            roof["solo_achieved"] = round(b / solo_s / 1e9, 1)
+            roof["solo_frac"] = round(b / solo_s / 1e9 / PEAK_HBM_GBS, 4)
+            roof["note"] = ("achieved/frac: live launches of the timed stream (deferred batches overlap: this kernel "
+                            "shares HBM with the previous batch's profile); solo_*: the sequential pass, alone on "
+                            "the chip")
     write_ceiling = profile_write_ceiling(ctx, leg, n_loc, M, kern, args.steps)
     step_bytes = leg.packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
     host_us, api_calls = leg.host_us_per_step, leg.api_calls_per_step
     si = leg.step_info
     step_driver = ({"native": True, "deferred_steps": si[5], "synchronous_steps": si[4], "rerun_steps": si[6],
+                    "host_wait_us_per_step": round(leg.host_wait_us_per_step, 1),
                     "note": "karma_step (csrc/step.hip): one C ABI call per step; host_us_per_step is the time "
-                            "inside those calls, api_calls_per_step the HIP/RCCL calls they made"}
+                            "inside those calls (host_wait_us_per_step of it waiting for the device: the status "
+                            "of the step kLag = 3 back), api_calls_per_step the HIP/RCCL calls they made"}
                    if si else {"native": False})
     step_s = dt / args.steps
     parity = None

@@ -122,12 +122,14 @@ int resident_grid(karma_ctx* ctx, const void* kernel, int block, size_t lds, int
 // the context's second stream (a records job's general branch, the eq path's
 // staged copies), created on first use at the highest priority
 int ctx_fork(karma_ctx* ctx) {
-    if (!ctx->fork_stream) {
+    if (!ctx->fork_a) {
+        KARMA_HIP(hipEventCreateWithFlags(&ctx->fork_a, hipEventDisableTiming));
+        KARMA_HIP(hipEventCreateWithFlags(&ctx->fork_b, hipEventDisableTiming));
+    }
+    if (!ctx->fork_stream && !ctx->fork_use) {
         int lo = 0, hi = 0;
         KARMA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
         KARMA_HIP(hipStreamCreateWithPriority(&ctx->fork_stream, hipStreamNonBlocking, hi));
-        KARMA_HIP(hipEventCreateWithFlags(&ctx->fork_a, hipEventDisableTiming));
-        KARMA_HIP(hipEventCreateWithFlags(&ctx->fork_b, hipEventDisableTiming));
     }
     return KARMA_OK;
 }

@@ -456,7 +456,7 @@ int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members
         KARMA_TRY(ctx_fork(ctx));
         for (int i = 0; i < 4; ++i)
             if (!ev[i]) KARMA_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
-        xs = ctx->fork_stream;
+        xs = ctx->fork_use ? ctx->fork_use : ctx->fork_stream;
         KARMA_TRY(d_off.alloc(ctx, C + 1));
         KARMA_TRY(d_cnt.alloc(ctx, std::max<int64_t>(C, 1)));
         KARMA_TRY(d_mem.alloc(ctx, std::max<int64_t>(n_mem, 1)));

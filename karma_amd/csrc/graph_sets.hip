@@ -2275,12 +2275,14 @@ int SetsJob::launch() {
     hipStream_t const main_stream = ctx->stream;
     // (not while every launch is timed: the per-kernel pass wants each kernel
     // alone on the chip)
-    const bool fork = fork_on() && !(ctx->timing && ctx->timing_only.empty());
+    const bool fork = fork_on() && !ctx->no_fork && !(ctx->timing && ctx->timing_only.empty());
+    hipStream_t fork_s = nullptr;  // set by ctx_fork: ctx->fork_use or ctx->fork_stream
     if (fork) {
         KARMA_TRY(ctx_fork(ctx));
+        fork_s = ctx->fork_use ? ctx->fork_use : ctx->fork_stream;
         KARMA_HIP(hipEventRecord(ctx->fork_a, main_stream));
-        KARMA_HIP(hipStreamWaitEvent(ctx->fork_stream, ctx->fork_a, 0));
-        ctx->stream = ctx->fork_stream;
+        KARMA_HIP(hipStreamWaitEvent(fork_s, ctx->fork_a, 0));
+        ctx->stream = fork_s;
     }
     int rc_pair = [&]() -> int {
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, general_grid(ctx, n_chunks), kGW, 0, rec, A, (uint32_t)N,
@@ -2294,7 +2296,7 @@ int SetsJob::launch() {
                          n_pl.ptr, n_chunks, lpb, g, pent.ptr, pdir);
         KARMA_LAUNCH(ctx, "graph_pair_reduce", pair_reduce_kernel, nsl, kRT, 0, pent.ptr, pdir, n_pg, g.bw, g.bbits,
                      g.dbits, B, part_b.ptr, part_k.ptr, part_c.ptr, part_n.ptr, ovf);
-        if (fork) KARMA_HIP(hipEventRecord(ctx->fork_b, ctx->fork_stream));
+        if (fork) KARMA_HIP(hipEventRecord(ctx->fork_b, fork_s));
         return KARMA_OK;
     }();
     ctx->stream = main_stream;

@@ -108,6 +108,12 @@ struct karma_ctx {
     hipStream_t fork_stream = nullptr;
     hipEvent_t fork_a = nullptr, fork_b = nullptr;
     hipEvent_t xfer_ev[4] = {};  // the eq path's staged host->device copies on fork_stream
+    bool no_fork = false;        // the next records job keeps its general branch on its own stream
+    // an idle stream of the caller's to fork onto instead of fork_stream (a
+    // step's spare main stream): every stream the process creates takes one of
+    // its 4 hardware queues in turn, and a 6th stream shares the 2nd's -- a
+    // records job's main stream (config 3: 1.52 against 1.2 ms per step)
+    hipStream_t fork_use = nullptr;
     int64_t eq_pair_cap = 0;     // the eq path's previous pair total (its speculative scratch size)
 };
 

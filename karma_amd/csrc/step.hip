@@ -449,6 +449,13 @@ struct karma_step {
     // i + 1's records job to step i's tail, so the next batch's classify runs
     // beside this batch's merge and edge stage (a stream of batches)
     hipStream_t alt_s = nullptr;
+    // with two main streams, the odd batches' presence, column table and
+    // profile go to side_alt_s (one side stream made every batch's column
+    // table wait for the previous batch's profile); the general-read branch
+    // then stays on the main stream, so no two busy streams share one of the
+    // process's 4 hardware queues
+    hipStream_t side_alt_s = nullptr;
+    int sides = 2;                // KARMA_STEP_SIDES=1: one side stream (A/B)
     int streams = 0;              // KARMA_STEP_STREAMS: 1 / 2 main streams (0: by the batch's size)
     hipEvent_t ev = nullptr;      // side -> main join: the last deferred step's profile (one main stream)
     bool ev_set = false;
@@ -525,6 +532,7 @@ namespace {
 int ensure_prof(karma_step* s, DevArray<double>& prof, size_t n) {
     if (prof.n >= n) return KARMA_OK;
     KARMA_HIP(hipStreamSynchronize(s->side_s));
+    KARMA_HIP(hipStreamSynchronize(s->side_alt_s));
     KARMA_HIP(hipStreamSynchronize(s->main_s));
     KARMA_HIP(hipStreamSynchronize(s->alt_s));
     return prof.alloc(s->ctx, n);
@@ -663,7 +671,10 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
         // column set's exchange and the column table beside them on the side
         // stream; the profile behind the graph's kernels on the side stream
         karma_graph_job* job = nullptr;
-        KARMA_TRY(karma_graph_records_begin(ctx, rec, A, s->n_glob, KARMA_REC_SORTED, 1, &job));
+        ctx->fork_use = s->alt_s;  // the general-read branch on the spare main stream (see karma_ctx::fork_use)
+        const int brc = karma_graph_records_begin(ctx, rec, A, s->n_glob, KARMA_REC_SORTED, 1, &job);
+        ctx->fork_use = nullptr;
+        KARMA_TRY(brc);
         int rc = KARMA_OK;
         ctx->stream = s->side_s;
         rc = karma_kmer_plan_create(ctx, store, s->kmode, &s->plan);
@@ -825,12 +836,19 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // records job (main stream) up to its final kernel; no readback
     SetsJob* job = nullptr;
     SetsDeferred v;
-    KARMA_TRY(sets_begin_deferred(ctx, reinterpret_cast<const uint2*>(rec), A, s->n_glob, &job, &v));
+    // the general-read branch: on the idle spare main stream with one main
+    // stream; kept on the main stream with two (see side_alt_s)
+    ctx->no_fork = two && s->sides == 2;
+    ctx->fork_use = two ? nullptr : s->alt_s;
+    const int jrc = sets_begin_deferred(ctx, reinterpret_cast<const uint2*>(rec), A, s->n_glob, &job, &v);
+    ctx->no_fork = false;
+    ctx->fork_use = nullptr;
+    KARMA_TRY(jrc);
     std::unique_ptr<SetsJob, void (*)(SetsJob*)> jg(job, sets_release);
     // side stream: presence, column table (M stays on the device), then the
     // profile behind the graph's final kernel (sequential: all on the main
     // stream, every kernel alone on the chip -- the per-kernel timing pass)
-    hipStream_t const side = sequential ? ms : s->side_s;
+    hipStream_t const side = sequential ? ms : (par && s->sides == 2 ? s->side_alt_s : s->side_s);
     ctx->stream = side;
     karma_kmer_plan* plan = nullptr;
     int rc = karma_kmer_plan_create(ctx, store, s->kmode, &plan);
@@ -841,7 +859,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     if (!rc) rc = ensure_prof(s, tl.prof, (size_t)std::max<int64_t>(1, s->n_loc * kmer_m_cap(plan)));
     if (!rc && ctx->mark_set && !sequential) {
         if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
-        rc = hipStreamWaitEvent(s->side_s, ctx->mark_ev, 0) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
+        rc = hipStreamWaitEvent(side, ctx->mark_ev, 0) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
     }
     if (!rc && s->n_loc) rc = kmer_profile_device_m(plan, tl.prof.ptr, m_dev);
     if (!rc && !two && !sequential && s->join) {
@@ -929,6 +947,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     s->emulate = world == 1 && nranks > 1 ? nranks : 0;
     if (const char* e = getenv("KARMA_STEP_STREAMS")) s->streams = atoi(e) == 1 ? 1 : atoi(e) == 2 ? 2 : 0;
     if (const char* e = getenv("KARMA_STEP_JOIN")) s->join = atoi(e) != 0;  // A/B only
+    if (const char* e = getenv("KARMA_STEP_SIDES")) s->sides = atoi(e) == 1 ? 1 : 2;
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
@@ -941,6 +960,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     KARMA_HIP(hipStreamCreateWithPriority(&s->main_s, hipStreamNonBlocking, hi));
     KARMA_HIP(hipStreamCreateWithPriority(&s->alt_s, hipStreamNonBlocking, hi));
     KARMA_HIP(hipStreamCreateWithPriority(&s->side_s, hipStreamNonBlocking, 0));
+    KARMA_HIP(hipStreamCreateWithPriority(&s->side_alt_s, hipStreamNonBlocking, 0));
     void *hm = nullptr, *dm = nullptr;
     KARMA_TRY(ctx_mapped(ctx, kMapStep, kRing * sizeof(StepStatus) + kRing * 8, &hm, &dm));
     s->mring_h = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(hm) + kRing * sizeof(StepStatus));
@@ -1012,6 +1032,7 @@ int karma_step_sync(karma_step* s) {
     ctx->stream = prev;
     KARMA_TRY(rc);
     KARMA_HIP(hipStreamSynchronize(s->side_s));
+    KARMA_HIP(hipStreamSynchronize(s->side_alt_s));
     KARMA_HIP(hipStreamSynchronize(s->alt_s));
     KARMA_HIP(hipStreamSynchronize(s->main_s));
     KARMA_TRY(bury(s, true));
@@ -1062,6 +1083,7 @@ int karma_step_destroy(karma_step* s) {
     if (s->main_s) hipStreamSynchronize(s->main_s);
     if (s->alt_s) hipStreamSynchronize(s->alt_s);
     if (s->side_s) hipStreamSynchronize(s->side_s);
+    if (s->side_alt_s) hipStreamSynchronize(s->side_alt_s);
     s->pending.clear();
     s->E = 0;  // outputs dropped unread
     drop_outputs(s);
@@ -1076,7 +1098,9 @@ int karma_step_destroy(karma_step* s) {
     for (auto& tl : s->tail) tl.release();
     karma_ctx* ctx = s->ctx;
     hipStream_t prev = ctx->stream;
-    if (prev == s->main_s || prev == s->side_s || prev == s->alt_s) ctx->stream = ctx->own_stream;
+    if (prev == s->main_s || prev == s->side_s || prev == s->alt_s || prev == s->side_alt_s)
+        ctx->stream = ctx->own_stream;
+    if (s->side_alt_s) karma_stream_destroy(ctx, s->side_alt_s);
     if (s->side_s) karma_stream_destroy(ctx, s->side_s);
     if (s->alt_s) karma_stream_destroy(ctx, s->alt_s);
     if (s->main_s) karma_stream_destroy(ctx, s->main_s);
