@@ -49,7 +49,8 @@ constexpr int kLag = 3;    // deferred steps the host may have in flight (two ma
 // One deferred step's status, written by step_status_kernel (seq last).
 struct StepStatus {
     uint64_t seq;
-    int64_t slow;   // bits: 1 relabel, 2 pair capacity, 4 big reads, 8 bucket overflow
+    int64_t slow;   // bits: 1 relabel, 2 pair capacity, 4 big reads, 8 bucket overflow, 16 exchange slots,
+                    // 32 another rank's step needs the general path
     int64_t err;    // bits: 1 unsorted records, 2 contig range, 4 partition check, 8 zero total, 16 merge order
     int64_t U;      // pairs of the local list
     int64_t E;      // edges
@@ -207,6 +208,8 @@ constexpr int kMG = 16;         // lanes per bound search
 struct RunSrc {
     int nr, B, bw;
     int64_t b[kMaxRuns + 1];     // owner bounds (contig ids)
+    int64_t slot = 0;            // > 0: runs are all-to-all slots of this many words (length first)
+    int64_t* n_out = nullptr;    // the merged length (device), or null
 };
 
 __device__ __forceinline__ int64_t count_below(const uint64_t* __restrict__ a, int64_t lo, int64_t hi, uint64_t k,
@@ -228,24 +231,43 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
                                                          const int64_t* __restrict__ split_loc, RunSrc rs,
                                                          uint64_t* __restrict__ ko, int64_t* __restrict__ co,
                                                          int64_t* __restrict__ bad) {
-    __shared__ int64_t ro[kMaxRuns + 1], rt[kMaxRuns + 1];
+    __shared__ int64_t ro[kMaxRuns + 1], re[kMaxRuns + 1], rt[kMaxRuns + 1];
     __shared__ int64_t wlo[kMaxRuns], whi[kMaxRuns];
     __shared__ int wbase[kMaxRuns];
     __shared__ int all_fit;
     __shared__ uint64_t wkeys[kMLds];
     const int nr = rs.nr;
-    const int64_t U = dst[rs.B];
-    if (threadIdx.x <= (unsigned)nr) {
+    const int64_t U = rs.slot > 0 ? 0 : dst[rs.B];
+    if (rs.slot == 0 && threadIdx.x <= (unsigned)nr) {
         const int64_t bd = rs.b[threadIdx.x];
         const int64_t b = bd >> rs.bw;
         ro[threadIdx.x] = bd <= 0 ? 0 : (b < rs.B ? dst[b] + split_loc[threadIdx.x] : U);
     }
     __syncthreads();
+    // run r = [ro[r], re[r]): consecutive slices of one list, or (rs.slot > 0)
+    // the padded slots of an all-to-all, the length in the slot's first word
+    if (threadIdx.x < (unsigned)nr) {
+        const int r = threadIdx.x;
+        if (rs.slot > 0) {
+            const uint64_t h = keys[(int64_t)r * rs.slot];
+            if (h >> 63) atomicOr(reinterpret_cast<unsigned long long*>(bad), 2ull);  // a slice outgrew its slot: run again
+            ro[r] = (int64_t)r * rs.slot + 1;
+            re[r] = ro[r] + (int64_t)min<uint64_t>(h & ~(1ull << 63), (uint64_t)(rs.slot - 1));
+        } else {
+            re[r] = ro[r + 1];
+        }
+    }
+    __syncthreads();
+    if (rs.n_out && blockIdx.x == 0 && threadIdx.x == 0) {
+        int64_t tot = 0;
+        for (int r = 0; r < nr; ++r) tot += re[r] - ro[r];
+        *rs.n_out = tot;  // the merged list's length, for the edge stage
+    }
     if (threadIdx.x == 0) {
         int64_t t = 0;
         for (int r = 0; r < nr; ++r) {
             rt[r] = t;
-            t += (ro[r + 1] - ro[r] + kMT - 1) / kMT;
+            t += (re[r] - ro[r] + kMT - 1) / kMT;
         }
         rt[nr] = t;
     }
@@ -256,13 +278,13 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
     for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         int r = 0;
         while (r + 1 < nr && rt[r + 1] <= tile) ++r;
-        const int64_t t0 = ro[r] + (tile - rt[r]) * kMT, t1 = min(ro[r + 1], t0 + kMT);
+        const int64_t t0 = ro[r] + (tile - rt[r]) * kMT, t1 = min(re[r], t0 + kMT);
         // window bounds: search q covers run q >> 1, (q & 1) ? last key : first key
         for (int q0 = 0; q0 < 2 * nr; q0 += 256 / kMG) {
             const int q = q0 + grp;
             const int sr = q >> 1;
             const bool search = q < 2 * nr && sr != r;
-            int64_t lo = search ? ro[sr] : 0, hi = search ? ro[sr + 1] : 0;
+            int64_t lo = search ? ro[sr] : 0, hi = search ? re[sr] : 0;
             const uint64_t k = search ? keys[(q & 1) ? t1 - 1 : t0] : 0;
             const bool le = sr < r;
             // a run wholly before or after the key needs no search (the
@@ -351,7 +373,7 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
                 const int64_t i = t0 + threadIdx.x + (int64_t)u * 256;
                 if (i >= t1) break;
                 const uint64_t k = kv[u];
-                if (kp[u] > k) *bad = 1;
+                if (kp[u] > k) atomicOr(reinterpret_cast<unsigned long long*>(bad), 1ull);
                 int bb[kMFast], nn[kMFast];
 #pragma unroll
                 for (int sr = 0; sr < kMFast; ++sr) {
@@ -379,7 +401,7 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
         }
         for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
             const uint64_t k = keys[i];
-            if (i > ro[r] && keys[i - 1] > k) *bad = 1;
+            if (i > ro[r] && keys[i - 1] > k) atomicOr(reinterpret_cast<unsigned long long*>(bad), 1ull);
             int64_t pos = i - ro[r];
             for (int sr = 0; sr < nr; ++sr) {
                 if (sr == r) continue;
@@ -400,12 +422,54 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
     }
 }
 
+// ---- the exchange's send slots, sized on the device ----------------------------
+// Owner r's slice of this rank's list (offsets from the final kernel's bucket
+// offsets and split counts, as in step_merge_kernel) into slot r of a padded
+// all-to-all: word 0 the length, bit 63 set in every slot when any slice
+// outgrew its slot (so every receiver sees the same flag and every rank runs
+// the step again), then up to slot - 1 keys (counts in the same layout).
+__global__ void __launch_bounds__(256) step_pack_kernel(const uint64_t* __restrict__ keys,
+                                                        const int64_t* __restrict__ counts,
+                                                        const int64_t* __restrict__ dst,
+                                                        const int64_t* __restrict__ split_loc, RunSrc rs, int64_t slot,
+                                                        uint64_t* __restrict__ sk, int64_t* __restrict__ sc) {
+    __shared__ int64_t ro[kMaxRuns + 1];
+    __shared__ int over;
+    const int nr = rs.nr;
+    const int64_t U = dst[rs.B];
+    if (threadIdx.x <= (unsigned)nr) {
+        const int64_t bd = rs.b[threadIdx.x];
+        const int64_t b = bd >> rs.bw;
+        ro[threadIdx.x] = bd <= 0 ? 0 : (b < rs.B ? dst[b] + split_loc[threadIdx.x] : U);
+    }
+    if (threadIdx.x == 0) over = 0;
+    __syncthreads();
+    if (threadIdx.x < (unsigned)nr && ro[threadIdx.x + 1] - ro[threadIdx.x] > slot - 1) over = 1;
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < (unsigned)nr) {
+        const int r = threadIdx.x;
+        sk[(int64_t)r * slot] = (uint64_t)(ro[r + 1] - ro[r]) | ((uint64_t)over << 63);
+    }
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < U; i += (int64_t)gridDim.x * 256) {
+        int r = 0;
+        while (r + 1 < nr && ro[r + 1] <= i) ++r;
+        const int64_t j = i - ro[r];
+        if (j < slot - 1) {
+            sk[(int64_t)r * slot + 1 + j] = keys[i];
+            sc[(int64_t)r * slot + 1 + j] = counts[i];
+        }
+    }
+}
+
 // Every word a host would have checked after a deferred step, into the ring
 // entry (seq written last, released to the host).
+// gslow (several processes): the entry is completed by step_publish_kernel
+// once every rank's slow words are summed into gslow (every rank then runs the
+// same steps again, so the collectives stay matched).
 __global__ void step_status_kernel(const int* __restrict__ flags, const unsigned* __restrict__ counters,
                                    const uint8_t* __restrict__ ovf, int B, const int64_t* __restrict__ dst,
                                    int64_t* __restrict__ merge_bad, const int64_t* __restrict__ est,
-                                   StepStatus* __restrict__ out, uint64_t seq) {
+                                   StepStatus* __restrict__ out, uint64_t seq, int64_t* __restrict__ gslow) {
     __shared__ int any_ovf;
     if (threadIdx.x == 0) any_ovf = 0;
     __syncthreads();
@@ -424,13 +488,23 @@ __global__ void step_status_kernel(const int* __restrict__ flags, const unsigned
     if (est[0]) err |= 8;
     if (est[1]) err |= 2;  // a key past the contig range
     if (merge_bad) {
-        if (*merge_bad) err |= 16;
+        if (*merge_bad & 1) err |= 16;
+        if (*merge_bad & 2) slow |= 16;  // the exchange's slots were too small
         *merge_bad = 0;  // cleared for the next step's merge (stream order)
     }
     out->slow = slow;
     out->err = err;
     out->U = dst[B];
     out->E = est[2];
+    if (gslow) {
+        *gslow = slow != 0;
+        return;
+    }
+    __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void step_publish_kernel(const int64_t* __restrict__ gslow, StepStatus* __restrict__ out, uint64_t seq) {
+    if (*gslow) out->slow |= 32;  // some rank needs the general path: all run the step again
     __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -487,13 +561,18 @@ struct karma_step {
     DevArray<int64_t> m_ring;      // per ring entry: the step's column count, written by its column table
     struct Tail {
         DevArray<double> prof;         // the step's profile
-        DevArray<uint64_t> mk;
-        DevArray<int64_t> mc, mbad, tot, tile_cnt, est;
+        DevArray<uint64_t> mk, sk, rk;  // merged keys; the exchange's send and receive slots
+        DevArray<int64_t> mc, mbad, tot, tile_cnt, est, sc, rc, nm;
         DevArray<uint32_t> ea, eb;
         DevArray<int64_t> es;
         DevArray<double> ew;
         void release() {
             prof.release();
+            sk.release();
+            rk.release();
+            sc.release();
+            rc.release();
+            nm.release();
             mk.release();
             mc.release();
             mbad.release();
@@ -522,6 +601,12 @@ struct karma_step {
     // device (a deferred step's status kLag steps back, synchronous readbacks
     // excluded)
     int64_t run_ns = 0, wait_ns = 0;
+    // several processes: deferred steps once every rank's store is known to
+    // be ACGT-only (no exception k-mers to exchange) and the exchange's slot
+    // size is known from a synchronous step (the largest slice + 25 %)
+    karma_contigs* acgt_store = nullptr;
+    int64_t kc = 0;
+    bool defer_ranks = true;      // KARMA_STEP_DEFER_RANKS=0: synchronous steps with several processes
 };
 
 namespace {
@@ -629,6 +714,20 @@ int exchange_columns(karma_step* s, karma_kmer_plan* plan, karma_comm* c) {
     return karma_kmer_exceptions_set(plan, keys.ptr, tot);  // sorts and dedups (stream-ordered)
 }
 
+// The presence bitmaps alone (a deferred step: every rank's store is ACGT-only,
+// so there are no exception keys to exchange).
+int exchange_presence(karma_step* s, karma_kmer_plan* plan, karma_comm* c) {
+    karma_ctx* ctx = s->ctx;
+    int64_t nw = 0;
+    KARMA_TRY(karma_kmer_presence_words(plan, &nw));
+    DevArray<uint32_t> words, all;
+    KARMA_TRY(words.alloc(ctx, nw));
+    KARMA_TRY(all.alloc(ctx, nw * s->world));
+    KARMA_TRY(karma_kmer_presence_get(plan, words.ptr));
+    KARMA_TRY(karma_comm_allgather(c, words.ptr, all.ptr, nw * 4));
+    return karma_kmer_presence_merge(plan, all.ptr, s->world);  // stream-ordered: words / all back to the cache
+}
+
 // The owners' readset totals, gathered from every owner's slice (in place for
 // equal shards; otherwise a padded all-gather and copies back).
 int allgather_slices(karma_step* s, int64_t* buf) {
@@ -678,6 +777,13 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
         int rc = KARMA_OK;
         ctx->stream = s->side_s;
         rc = karma_kmer_plan_create(ctx, store, s->kmode, &s->plan);
+        if (!rc && s->world > 1 && s->acgt_store != store) {
+            // may later steps skip the exception keys' exchange?  (every rank agrees)
+            int64_t exc = 0;
+            rc = karma_contigs_info(store, nullptr, nullptr, &exc, nullptr);
+            if (!rc) rc = karma_comm_allreduce_host(s->scomm ? s->scomm : s->comm, &exc, 1, KARMA_DT_I64, KARMA_OP_SUM);
+            if (!rc) s->acgt_store = exc == 0 ? store : nullptr;
+        }
         if (!rc && s->world > 1) rc = exchange_columns(s, s->plan, s->scomm ? s->scomm : s->comm);
         if (!rc) rc = karma_kmer_plan_finalize_async(s->plan);
         ctx->stream = s->main_s;
@@ -720,6 +826,12 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
             std::vector<int64_t> sc(W), rcv(W), so(W + 1, 0), ro(W + 1, 0);
             for (int r = 0; r < W; ++r) sc[r] = starts[r + 1] - starts[r];
             KARMA_TRY(karma_comm_exchange_counts(s->comm, sc.data(), rcv.data()));
+            {   // the deferred steps' slot size: the largest slice of any rank, + 25 %
+                int64_t mx = 0;
+                for (int r = 0; r < W; ++r) mx = std::max(mx, sc[r]);
+                KARMA_TRY(karma_comm_allreduce_host(s->comm, &mx, 1, KARMA_DT_I64, KARMA_OP_MAX));
+                s->kc = std::max(s->kc, mx + mx / 4 + 1024);
+            }
             for (int r = 0; r < W; ++r) {
                 so[r + 1] = so[r] + 8 * sc[r];
                 ro[r + 1] = ro[r] + 8 * rcv[r];
@@ -753,13 +865,16 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
 int check_entry(karma_step* s, const karma_step::Pending& p, bool* slow) {
     const StepStatus& st = const_cast<const StepStatus&>(s->ring_h[p.seq % kRing]);
     *slow = st.slow != 0;
-
-    if (st.err) {
-        KARMA_CHECK(!(st.err & 1), KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
-        KARMA_CHECK(!(st.err & 2), KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)",
+    // a step that runs again: its pair list may be incomplete (an overflowed
+    // bucket or exchange slot), so the merge-order and zero-total words are
+    // artifacts of the truncation; the re-run checks them on complete lists
+    const int64_t err = *slow ? st.err & ~int64_t(8 | 16) : st.err;
+    if (err) {
+        KARMA_CHECK(!(err & 1), KARMA_ERR_UNSORTED, "records are not grouped by read (read ids decrease)");
+        KARMA_CHECK(!(err & 2), KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)",
                     (long long)s->n_glob);
-        KARMA_CHECK(!(st.err & 16), KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
-        KARMA_CHECK(!(st.err & 8), KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
+        KARMA_CHECK(!(err & 16), KARMA_ERR_UNSORTED, "karma_pairs_merge_runs: a run is not sorted by key");
+        KARMA_CHECK(!(err & 8), KARMA_ERR_ZERO_DIV, "division by zero: a shared count over a zero total");
         KARMA_CHECK(false, KARMA_ERR_STATE, "code partition: block counts disagree with the classify histogram");
     }
     return KARMA_OK;
@@ -776,6 +891,9 @@ int drain(karma_step* s, bool wait, bool lag) {
     while (!s->pending.empty()) {
         karma_step::Pending p = s->pending.front();
         const bool must = wait || (lag && (int)s->pending.size() >= kLag);
+        // several processes: a step's entry is read at the same point of the
+        // step sequence on every rank (a rerun issues collectives)
+        if (s->world > 1 && !must) break;
         if (!entry_done(s, p.seq)) {
             if (!must) break;
             // the main stream reaches the status kernel within a step's time
@@ -815,7 +933,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // jobs side by side took 1.89 ms per batch against 1.23 ms one after the
     // other (they evict each other's partition runs from the caches); the
     // 8-rank strong preview (38.6M records) went 0.237 -> 0.199 ms.
-    const bool two = s->streams ? s->streams == 2 : A < kAltMaxRecords;
+    const bool two = s->world == 1 && (s->streams ? s->streams == 2 : A < kAltMaxRecords);
     const int par = sequential || !two ? 0 : (int)(seq & 1);
     hipStream_t const ms = par ? s->alt_s : s->main_s;
     // One main stream (large batches): the records job does not wait for the
@@ -852,6 +970,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     ctx->stream = side;
     karma_kmer_plan* plan = nullptr;
     int rc = karma_kmer_plan_create(ctx, store, s->kmode, &plan);
+    if (!rc && s->world > 1) rc = exchange_presence(s, plan, s->scomm ? s->scomm : s->comm);
     // M: into the device ring (the profile reads it) and the mapped ring (the
     // host reads it once the step is done); nothing on the main streams waits for it
     int64_t* const m_dev = s->m_ring.ptr + seq % kRing;
@@ -877,9 +996,8 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     const int64_t* n_dev = v.dst + v.B;
     int64_t* mbad = nullptr;
     const int cu = ctx->cu_count;
+    int64_t cap = v.cap;  // entries of the list the edge stage reads, at most
     if (s->exchange) {
-        KARMA_TRY(ensure_arr(ctx, tl.mk, v.cap));
-        KARMA_TRY(ensure_arr(ctx, tl.mc, v.cap));
         if (!tl.mbad.ptr) {  // the merge sets it, the status kernel reads and clears it
             KARMA_TRY(tl.mbad.alloc(ctx, 1));
             KARMA_HIP(hipMemsetAsync(tl.mbad.ptr, 0, 8, ctx->stream));
@@ -890,27 +1008,66 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         rs.bw = v.bw;
         for (int r = 0; r <= s->nranks; ++r) rs.b[r] = s->bounds[r];
         KARMA_CHECK((int)v.split_b.size() == s->nranks + 1, KARMA_ERR_STATE, "karma_step: the split hint was lost");
-        const int64_t tiles_cap = (v.cap + kMT - 1) / kMT + s->nranks;
-        KARMA_LAUNCH(ctx, "merge_rank", step_merge_kernel, (int)std::min<int64_t>(tiles_cap, 2 * cu), 256, 0, v.keys,
-                     v.counts, v.dst, v.split_loc, rs, tl.mk.ptr, tl.mc.ptr, tl.mbad.ptr);
+        const uint64_t* mkeys = v.keys;
+        const int64_t* mcounts = v.counts;
+        if (s->world > 1) {
+            // each owner's slice into a fixed slot of a padded all-to-all (its
+            // length on the device), so nothing waits for the slice sizes
+            const int W = s->world;
+            const int64_t slot = s->kc + 1;
+            KARMA_TRY(ensure_arr(ctx, tl.sk, W * slot));
+            KARMA_TRY(ensure_arr(ctx, tl.sc, W * slot));
+            KARMA_TRY(ensure_arr(ctx, tl.rk, W * slot));
+            KARMA_TRY(ensure_arr(ctx, tl.rc, W * slot));
+            KARMA_TRY(ensure_arr(ctx, tl.nm, 2));
+            KARMA_LAUNCH(ctx, "exchange_pack", step_pack_kernel,
+                         (int)std::max<int64_t>(1, std::min<int64_t>((v.cap + 255) / 256, 4 * cu)), 256, 0, v.keys,
+                         v.counts, v.dst, v.split_loc, rs, slot, tl.sk.ptr, tl.sc.ptr);
+            std::vector<int64_t> off(W + 1);
+            for (int r = 0; r <= W; ++r) off[r] = (int64_t)r * slot * 8;
+            KARMA_TRY(karma_comm_alltoallv_kv(s->comm, tl.sk.ptr, tl.sc.ptr, off.data(), tl.rk.ptr, tl.rc.ptr,
+                                              off.data()));
+            rs.slot = slot;
+            rs.n_out = tl.nm.ptr;
+            mkeys = tl.rk.ptr;
+            mcounts = tl.rc.ptr;
+            cap = W * (slot - 1);
+            n_dev = tl.nm.ptr;
+        }
+        KARMA_TRY(ensure_arr(ctx, tl.mk, cap));
+        KARMA_TRY(ensure_arr(ctx, tl.mc, cap));
+        const int64_t tiles_cap = (cap + kMT - 1) / kMT + s->nranks;
+        KARMA_LAUNCH(ctx, "merge_rank", step_merge_kernel, (int)std::min<int64_t>(tiles_cap, 2 * cu), 256, 0, mkeys,
+                     mcounts, v.dst, v.split_loc, rs, tl.mk.ptr, tl.mc.ptr, tl.mbad.ptr);
         lk = tl.mk.ptr;
         lc = tl.mc.ptr;
         mbad = tl.mbad.ptr;
     }
     KARMA_TRY(ensure_arr(ctx, tl.tot, s->n_glob));
-    KARMA_TRY(ensure_arr(ctx, tl.tile_cnt, (v.cap + kET - 1) / kET + 1));
+    KARMA_TRY(ensure_arr(ctx, tl.tile_cnt, (cap + kET - 1) / kET + 1));
     KARMA_TRY(ensure_arr(ctx, tl.est, 3));
-    KARMA_TRY(ensure_arr(ctx, tl.ea, v.cap));
-    KARMA_TRY(ensure_arr(ctx, tl.eb, v.cap));
-    KARMA_TRY(ensure_arr(ctx, tl.es, v.cap));
-    KARMA_TRY(ensure_arr(ctx, tl.ew, v.cap));
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((v.cap + kET - 1) / kET, cu));
+    KARMA_TRY(ensure_arr(ctx, tl.ea, cap));
+    KARMA_TRY(ensure_arr(ctx, tl.eb, cap));
+    KARMA_TRY(ensure_arr(ctx, tl.es, cap));
+    KARMA_TRY(ensure_arr(ctx, tl.ew, cap));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((cap + kET - 1) / kET, cu));
     KARMA_LAUNCH(ctx, "edge_count", step_edge_count_kernel, grid, kET, 0, lk, lc, n_dev, s->n_glob, tl.tot.ptr,
                  tl.tile_cnt.ptr, tl.est.ptr);
+    // the owners' readset totals from every owner (fixed sizes: no host wait)
+    if (s->world > 1) KARMA_TRY(allgather_slices(s, tl.tot.ptr));
     KARMA_LAUNCH(ctx, "edge_weights", step_edge_write_kernel, grid, kET, 0, lk, lc, n_dev, tl.tot.ptr,
                  tl.tile_cnt.ptr, tl.ea.ptr, tl.eb.ptr, tl.es.ptr, tl.ew.ptr, tl.est.ptr, s->n_glob);
+    int64_t* gslow = nullptr;
+    if (s->world > 1) {
+        KARMA_TRY(ensure_arr(ctx, tl.nm, 2));
+        gslow = tl.nm.ptr + 1;
+    }
     KARMA_LAUNCH(ctx, "step_status", step_status_kernel, 1, 256, 0, v.flags, v.counters, v.ovf, v.B, v.dst, mbad,
-                 tl.est.ptr, s->ring_d + seq % kRing, seq);
+                 tl.est.ptr, s->ring_d + seq % kRing, seq, gslow);
+    if (gslow) {  // every rank's slow flag, summed: all ranks run the same steps again
+        KARMA_TRY(karma_comm_allreduce(s->comm, gslow, 1, KARMA_DT_I64, KARMA_OP_SUM));
+        KARMA_LAUNCH(ctx, "step_status", step_publish_kernel, 1, 64, 0, gslow, s->ring_d + seq % kRing, seq);
+    }
     s->pending.push_back({seq, store, rec, A});
     return KARMA_OK;
 }
@@ -948,6 +1105,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     if (const char* e = getenv("KARMA_STEP_STREAMS")) s->streams = atoi(e) == 1 ? 1 : atoi(e) == 2 ? 2 : 0;
     if (const char* e = getenv("KARMA_STEP_JOIN")) s->join = atoi(e) != 0;  // A/B only
     if (const char* e = getenv("KARMA_STEP_SIDES")) s->sides = atoi(e) == 1 ? 1 : 2;
+    if (const char* e = getenv("KARMA_STEP_DEFER_RANKS")) s->defer_ranks = atoi(e) != 0;
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
@@ -997,7 +1155,10 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
     ctx->stream = s->main_s;
     const bool keep = flags & KARMA_STEP_KEEP, seq = flags & KARMA_STEP_SEQUENTIAL;
     // deferred: one process (no collective needs a host count), nothing read back
-    const bool defer = (flags & KARMA_STEP_DEFER) && !keep && s->world == 1 && s->n_glob <= sets_max_contigs();
+    // several processes: once a synchronous step has sized the exchange's
+    // slots and every rank's store is known to be ACGT-only
+    const bool ranks_ok = s->world == 1 || (s->defer_ranks && s->kc > 0 && s->acgt_store == store);
+    const bool defer = (flags & KARMA_STEP_DEFER) && !keep && ranks_ok && s->n_glob <= sets_max_contigs();
     int rc = KARMA_OK;
     if (defer && s->sticky_sync > 0) {
         --s->sticky_sync;

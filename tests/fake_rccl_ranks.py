@@ -15,6 +15,11 @@ Cases (--case):
   collectives  every RcclComm call with unequal sizes, checked against numpy
   oracle       the sharded build over unequal contig shards; outputs to npz
                (the parent compares them with the single-process oracle)
+  defer        deferred steps over RCCL (several processes): a first synchronous
+               step on 1 % of the records sizes the exchange's slots, so
+               the deferred full steps overflow them and run again; then a
+               second build whose deferred steps fit; infos, newest profiles
+               and kept results to npz
   config4      BASELINE configs[3]: config 3 over W ranks (bench.py's exact
                strong workload); the union of outputs hashed with
                tests/digests.py (the parent compares with digests.json config3)
@@ -143,6 +148,48 @@ def oracle_rank(group, rank, sizes, frags, seed):
         ctx.close()
 
 
+def defer_rank(group, rank, sizes, frags, seed):
+    world = group.world
+    n_glob, c_lo, n_loc = sum(sizes), sum(sizes[:rank]), sizes[rank]
+    ctx = _lib.Context(0)
+    comm = RcclComm(group, ctx)
+    out = {}
+    try:
+        blob, offs, key_len = engine.synth_contigs(seed, n_loc, 30, 100, 0, first=c_lo)
+        genes = engine.synth_genes(seed, n_glob)
+        rec = engine.synth_records(seed, n_glob, frags * rank // world, frags * (rank + 1) // world, True,
+                                   genes=genes)
+        # 1 % of the reads (records stay grouped by read)
+        k = int(np.searchsorted(rec[:, 0], rec[len(rec) // 100, 0]))
+        store = engine.ContigStore(ctx, blob, offs, key_len)
+        full = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))
+        small = _lib.DevBuf.from_numpy(ctx, np.ascontiguousarray(rec[:k]).view(np.int64).reshape(-1))
+        try:
+            for tag, first in (("over", (small, k)), ("fit", (full, len(rec)))):
+                build = ShardedBuild(ctx, comm, -1, n_glob, c_lo, n_loc)
+                try:
+                    assert build.native is not None
+                    build.run(store, first[0].ptr, first[1], count=False)  # synchronous: sizes the slots
+                    for _ in range(3):
+                        build.run(store, full.ptr, len(rec), count=False)
+                    build.sync()
+                    out[f"{tag}_info"] = build.native.info()
+                    out[f"{tag}_profile"] = build.native.profile().numpy()
+                    res = build.run(store, full.ptr, len(rec), keep=True)
+                    e = res["edges"]
+                    out.update({f"{tag}_a": e.a, f"{tag}_b": e.b, f"{tag}_w": e.weight, f"{tag}_tot": e.totals})
+                finally:
+                    build.close()
+            return out
+        finally:
+            store.close()
+            full.close()
+            small.close()
+    finally:
+        comm.close()
+        ctx.close()
+
+
 def config4_rank(group, rank):
     import digests as D
 
@@ -172,7 +219,7 @@ def config4_rank(group, rank):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--case", choices=("collectives", "oracle", "config4"), required=True)
+    ap.add_argument("--case", choices=("collectives", "oracle", "defer", "config4"), required=True)
     ap.add_argument("--world", type=int, default=3)
     ap.add_argument("--out", default=".")
     ap.add_argument("--sizes", default="")
@@ -187,9 +234,9 @@ def main():
     if a.case == "collectives":
         outs = run_ranks(a.world, collectives)
         summary["errors"] = check_collectives(outs)
-    elif a.case == "oracle":
+    elif a.case in ("oracle", "defer"):
         sizes = [int(x) for x in a.sizes.split(",")]
-        parts = run_ranks(a.world, oracle_rank, sizes, a.frags, a.seed)
+        parts = run_ranks(a.world, oracle_rank if a.case == "oracle" else defer_rank, sizes, a.frags, a.seed)
         for r, p in enumerate(parts):
             np.savez(os.path.join(a.out, f"rank{r}.npz"), **p)
     else:

@@ -52,6 +52,37 @@ def test_rccl_comm_collectives_unequal_sizes(world):
     assert out["errors"] == []
 
 
+def oracle_of(sizes, frags, seed, n_rate=300, len_span=900):
+    """The single-process oracle's profile, columns and graph for the union of
+    the ranks' shards (tests/fake_rccl_ranks.py builds the same inputs)."""
+    n_glob = sum(sizes)
+    seqs, recs = OrderedDict(), []
+    genes = engine.synth_genes(seed, n_glob)
+    lo = 0
+    W = len(sizes)
+    for r in range(W):
+        blob, offs, _ = engine.synth_contigs(seed, sizes[r], 30, len_span, n_rate, first=lo)
+        for i in range(sizes[r]):
+            seqs[f">ctg{lo + i}"] = bytes(blob[offs[i]:offs[i + 1]]).decode()
+        lo += sizes[r]
+        recs.append(engine.synth_records(seed, n_glob, frags * r // W, frags * (r + 1) // W, True, genes=genes))
+    prof, cols, _ = oracle.calc_kmer_profile(seqs, "5p6")
+    rec = np.concatenate(recs).astype(np.int64)
+    st = np.flatnonzero(np.r_[True, rec[1:, 0] != rec[:-1, 0]])
+    o = oracle.graph_groups(np.r_[st, len(rec)], rec[:, 1], None, None, n_glob, dedup=True)
+    return prof, cols, o
+
+
+def check_graph(parts, o, pre=""):
+    a = np.concatenate([p[pre + "a"] for p in parts])
+    b = np.concatenate([p[pre + "b"] for p in parts])
+    w = np.concatenate([p[pre + "w"] for p in parts])
+    assert np.array_equal(a, o["a"]) and np.array_equal(b, o["b"])
+    assert np.array_equal(w.view(np.uint64), o["weight"].view(np.uint64))
+    for p in parts:
+        assert np.array_equal(p[pre + "tot"], o["totals"])
+
+
 def test_rccl_sharded_build_three_unequal_ranks_match_oracle(tmp_path):
     """The sharded build through RcclComm at world 3 with unequal contig shards
     and N-injected contigs (exception keys on every rank), two stream steps then
@@ -60,31 +91,39 @@ def test_rccl_sharded_build_three_unequal_ranks_match_oracle(tmp_path):
     run_child("--case", "oracle", "--world", "3", "--sizes", ",".join(map(str, sizes)), "--frags", str(frags),
               "--seed", str(seed), "--out", str(tmp_path))
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(3)]
-    n_glob = sum(sizes)
-    seqs, recs = OrderedDict(), []
-    genes = engine.synth_genes(seed, n_glob)
-    lo = 0
-    for r in range(3):
-        blob, offs, _ = engine.synth_contigs(seed, sizes[r], 30, 900, 300, first=lo)
-        for i in range(sizes[r]):
-            seqs[f">ctg{lo + i}"] = bytes(blob[offs[i]:offs[i + 1]]).decode()
-        lo += sizes[r]
-        recs.append(engine.synth_records(seed, n_glob, frags * r // 3, frags * (r + 1) // 3, True, genes=genes))
-    prof, cols, _ = oracle.calc_kmer_profile(seqs, "5p6")
+    prof, cols, o = oracle_of(sizes, frags, seed)
     for p in parts:
         assert engine.decode_keys(p["cols"], -1) == cols
     got = np.concatenate([p["profile"] for p in parts])
     assert np.array_equal(got.view(np.uint64), prof.view(np.uint64))
-    rec = np.concatenate(recs).astype(np.int64)
-    st = np.flatnonzero(np.r_[True, rec[1:, 0] != rec[:-1, 0]])
-    o = oracle.graph_groups(np.r_[st, len(rec)], rec[:, 1], None, None, n_glob, dedup=True)
-    a = np.concatenate([p["a"] for p in parts])
-    b = np.concatenate([p["b"] for p in parts])
-    w = np.concatenate([p["w"] for p in parts])
-    assert np.array_equal(a, o["a"]) and np.array_equal(b, o["b"])
-    assert np.array_equal(w.view(np.uint64), o["weight"].view(np.uint64))
-    for p in parts:
-        assert np.array_equal(p["tot"], o["totals"])
+    check_graph(parts, o)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world):
+    """Deferred steps with several processes (csrc/step.hip run_deferred: the
+    padded fixed-slot all-to-all, the merge from slots, the totals all-gather
+    and the summed slow flag).  A first synchronous step on 1 % of the
+    reads sizes the slots, so the three deferred full steps overflow them: every
+    rank runs them again synchronously.  A second build sized on the full step
+    defers three steps that fit (no re-run).  The newest profile after sync and
+    the kept step after each must equal the oracle bit for bit (ACGT-only
+    contigs: the deferred path needs no exception keys)."""
+    sizes = [5000, 6000, 5500][:world]  # ~5000 distinct pairs per owner's slice
+    frags, seed = 200_000, 31
+    run_child("--case", "defer", "--world", str(world), "--sizes", ",".join(map(str, sizes)), "--frags",
+              str(frags), "--seed", str(seed), "--out", str(tmp_path))
+    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    prof, _, o = oracle_of(sizes, frags, seed, n_rate=0, len_span=100)
+    for tag in ("over", "fit"):
+        infos = [p[f"{tag}_info"] for p in parts]
+        # [M, E, pairs, entries, synchronous, deferred, re-run, pending, ...]
+        for i in infos:
+            assert i[5] == 3 and i[7] == 0, (tag, i.tolist())
+            assert i[6] == (3 if tag == "over" else 0), (tag, i.tolist())
+        got = np.concatenate([p[f"{tag}_profile"] for p in parts])
+        assert np.array_equal(got.view(np.uint64), prof.view(np.uint64)), tag
+        check_graph(parts, o, tag + "_")
 
 
 def test_rccl_config4_strong_8_ranks_digests():
