@@ -341,11 +341,15 @@ int karma_edges_get_all(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, do
 typedef struct karma_step karma_step;
 #define KARMA_STEP_KEEP 1       /* outputs kept for karma_step_profile / _columns / _edges */
 #define KARMA_STEP_SEQUENTIAL 2 /* every kernel on the main stream (per-kernel timing) */
-#define KARMA_STEP_DEFER 4      /* outputs not read: one process returns without waiting for anything (the
-                                 * step's checks arrive through mapped memory and are read <= 3 steps later;
-                                 * a step needing the general path runs again synchronously); with several
-                                 * ranks the edge count is not read back.  Inputs must stay valid until the
-                                 * next non-deferred step or karma_step_sync. */
+#define KARMA_STEP_DEFER 4      /* outputs not read: the step returns without waiting for anything (its
+                                 * checks arrive through mapped memory and are read <= 3 steps later; a
+                                 * step needing the general path runs again synchronously).  Several ranks:
+                                 * once a synchronous step has sized the exchange's slots and the store is
+                                 * ACGT-only on every rank (else the step runs synchronously, its edge
+                                 * count not read back); the slow verdict is summed over the ranks, so all
+                                 * of them re-run the same steps.  Every rank must pass the same flags.
+                                 * Inputs must stay valid until the next non-deferred step or
+                                 * karma_step_sync. */
 int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, int kmode, int64_t n_glob,
                       const int64_t* bounds, int nranks, int rank, karma_step** out);
 /* info (may be NULL): [0] M, [1] local edges (-1: not read), [2] local pair list

@@ -905,6 +905,13 @@ int drain(karma_step* s, bool wait, bool lag) {
                     set_error("karma_step: a deferred step's status never arrived");
                     return KARMA_ERR_STATE;
                 }
+                // a step takes milliseconds: two minutes means a peer that
+                // stopped issuing collectives; an error beats a silent hang
+                if (spin % 65536 == 65535 && std::chrono::steady_clock::now() - w0 > std::chrono::seconds(120)) {
+                    set_error("karma_step: a deferred step's status did not arrive within 120 s (%s)",
+                              s->world > 1 ? "a rank's collectives stalled?" : "device stalled?");
+                    return KARMA_ERR_STATE;
+                }
             }
             s->wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0)
                               .count();
