@@ -250,9 +250,11 @@ __global__ void __launch_bounds__(256) step_merge_kernel(const uint64_t* __restr
         const int r = threadIdx.x;
         if (rs.slot > 0) {
             const uint64_t h = keys[(int64_t)r * rs.slot];
-            if (h >> 63) atomicOr(reinterpret_cast<unsigned long long*>(bad), 2ull);  // a slice outgrew its slot: run again
+            if (h >> 62) {  // a slice outgrew its slot (bit 63) or the sender's step needs the general path (62)
+                atomicOr(reinterpret_cast<unsigned long long*>(bad), (h >> 63 ? 2ull : 0ull) | (h >> 62 & 1 ? 4ull : 0ull));
+            }
             ro[r] = (int64_t)r * rs.slot + 1;
-            re[r] = ro[r] + (int64_t)min<uint64_t>(h & ~(1ull << 63), (uint64_t)(rs.slot - 1));
+            re[r] = ro[r] + (int64_t)min<uint64_t>(h & ~(3ull << 62), (uint64_t)(rs.slot - 1));
         } else {
             re[r] = ro[r + 1];
         }
@@ -432,9 +434,12 @@ __global__ void __launch_bounds__(256) step_pack_kernel(const uint64_t* __restri
                                                         const int64_t* __restrict__ counts,
                                                         const int64_t* __restrict__ dst,
                                                         const int64_t* __restrict__ split_loc, RunSrc rs, int64_t slot,
-                                                        uint64_t* __restrict__ sk, int64_t* __restrict__ sc) {
+                                                        uint64_t* __restrict__ sk, int64_t* __restrict__ sc,
+                                                        const int* __restrict__ flags,
+                                                        const unsigned* __restrict__ counters,
+                                                        const uint8_t* __restrict__ ovf) {
     __shared__ int64_t ro[kMaxRuns + 1];
-    __shared__ int over;
+    __shared__ int over, slow;
     const int nr = rs.nr;
     const int64_t U = dst[rs.B];
     if (threadIdx.x <= (unsigned)nr) {
@@ -442,13 +447,23 @@ __global__ void __launch_bounds__(256) step_pack_kernel(const uint64_t* __restri
         const int64_t b = bd >> rs.bw;
         ro[threadIdx.x] = bd <= 0 ? 0 : (b < rs.B ? dst[b] + split_loc[threadIdx.x] : U);
     }
-    if (threadIdx.x == 0) over = 0;
+    if (threadIdx.x == 0) {
+        over = 0;
+        slow = counters[3] || flags[2] || counters[0];  // the status kernel's slow words, less the slots
+    }
     __syncthreads();
     if (threadIdx.x < (unsigned)nr && ro[threadIdx.x + 1] - ro[threadIdx.x] > slot - 1) over = 1;
+    if (blockIdx.x == 0)
+        for (int b = threadIdx.x; b < rs.B; b += blockDim.x)
+            if (ovf[b]) slow = 1;
     __syncthreads();
+    // the slot's first word: the slice length; bit 63: some slice of this
+    // sender outgrew its slot; bit 62: this sender's step needs the general
+    // path.  Every rank receives every sender's word, so every rank learns
+    // that the step runs again (no separate all-reduce of the verdict).
     if (blockIdx.x == 0 && threadIdx.x < (unsigned)nr) {
         const int r = threadIdx.x;
-        sk[(int64_t)r * slot] = (uint64_t)(ro[r + 1] - ro[r]) | ((uint64_t)over << 63);
+        sk[(int64_t)r * slot] = (uint64_t)(ro[r + 1] - ro[r]) | ((uint64_t)over << 63) | ((uint64_t)slow << 62);
     }
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < U; i += (int64_t)gridDim.x * 256) {
         int r = 0;
@@ -462,14 +477,13 @@ __global__ void __launch_bounds__(256) step_pack_kernel(const uint64_t* __restri
 }
 
 // Every word a host would have checked after a deferred step, into the ring
-// entry (seq written last, released to the host).
-// gslow (several processes): the entry is completed by step_publish_kernel
-// once every rank's slow words are summed into gslow (every rank then runs the
-// same steps again, so the collectives stay matched).
+// entry (seq written last, released to the host).  With several processes the
+// merge's word carries the other ranks' verdicts (step_pack_kernel), so every
+// rank's entry asks for the same re-runs and the collectives stay matched.
 __global__ void step_status_kernel(const int* __restrict__ flags, const unsigned* __restrict__ counters,
                                    const uint8_t* __restrict__ ovf, int B, const int64_t* __restrict__ dst,
                                    int64_t* __restrict__ merge_bad, const int64_t* __restrict__ est,
-                                   StepStatus* __restrict__ out, uint64_t seq, int64_t* __restrict__ gslow) {
+                                   StepStatus* __restrict__ out, uint64_t seq) {
     __shared__ int any_ovf;
     if (threadIdx.x == 0) any_ovf = 0;
     __syncthreads();
@@ -490,21 +504,13 @@ __global__ void step_status_kernel(const int* __restrict__ flags, const unsigned
     if (merge_bad) {
         if (*merge_bad & 1) err |= 16;
         if (*merge_bad & 2) slow |= 16;  // the exchange's slots were too small
+        if (*merge_bad & 4) slow |= 32;  // another rank's step needs the general path
         *merge_bad = 0;  // cleared for the next step's merge (stream order)
     }
     out->slow = slow;
     out->err = err;
     out->U = dst[B];
     out->E = est[2];
-    if (gslow) {
-        *gslow = slow != 0;
-        return;
-    }
-    __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__global__ void step_publish_kernel(const int64_t* __restrict__ gslow, StepStatus* __restrict__ out, uint64_t seq) {
-    if (*gslow) out->slow |= 32;  // some rank needs the general path: all run the step again
     __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -1026,10 +1032,10 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
             KARMA_TRY(ensure_arr(ctx, tl.sc, W * slot));
             KARMA_TRY(ensure_arr(ctx, tl.rk, W * slot));
             KARMA_TRY(ensure_arr(ctx, tl.rc, W * slot));
-            KARMA_TRY(ensure_arr(ctx, tl.nm, 2));
+            KARMA_TRY(ensure_arr(ctx, tl.nm, 1));
             KARMA_LAUNCH(ctx, "exchange_pack", step_pack_kernel,
                          (int)std::max<int64_t>(1, std::min<int64_t>((v.cap + 255) / 256, 4 * cu)), 256, 0, v.keys,
-                         v.counts, v.dst, v.split_loc, rs, slot, tl.sk.ptr, tl.sc.ptr);
+                         v.counts, v.dst, v.split_loc, rs, slot, tl.sk.ptr, tl.sc.ptr, v.flags, v.counters, v.ovf);
             std::vector<int64_t> off(W + 1);
             for (int r = 0; r <= W; ++r) off[r] = (int64_t)r * slot * 8;
             KARMA_TRY(karma_comm_alltoallv_kv(s->comm, tl.sk.ptr, tl.sc.ptr, off.data(), tl.rk.ptr, tl.rc.ptr,
@@ -1064,17 +1070,8 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     if (s->world > 1) KARMA_TRY(allgather_slices(s, tl.tot.ptr));
     KARMA_LAUNCH(ctx, "edge_weights", step_edge_write_kernel, grid, kET, 0, lk, lc, n_dev, tl.tot.ptr,
                  tl.tile_cnt.ptr, tl.ea.ptr, tl.eb.ptr, tl.es.ptr, tl.ew.ptr, tl.est.ptr, s->n_glob);
-    int64_t* gslow = nullptr;
-    if (s->world > 1) {
-        KARMA_TRY(ensure_arr(ctx, tl.nm, 2));
-        gslow = tl.nm.ptr + 1;
-    }
     KARMA_LAUNCH(ctx, "step_status", step_status_kernel, 1, 256, 0, v.flags, v.counters, v.ovf, v.B, v.dst, mbad,
-                 tl.est.ptr, s->ring_d + seq % kRing, seq, gslow);
-    if (gslow) {  // every rank's slow flag, summed: all ranks run the same steps again
-        KARMA_TRY(karma_comm_allreduce(s->comm, gslow, 1, KARMA_DT_I64, KARMA_OP_SUM));
-        KARMA_LAUNCH(ctx, "step_status", step_publish_kernel, 1, 64, 0, gslow, s->ring_d + seq % kRing, seq);
-    }
+                 tl.est.ptr, s->ring_d + seq % kRing, seq);
     s->pending.push_back({seq, store, rec, A});
     return KARMA_OK;
 }

@@ -18,8 +18,9 @@ Cases (--case):
   defer        deferred steps over RCCL (several processes): a first synchronous
                step on 1 % of the records sizes the exchange's slots, so
                the deferred full steps overflow them and run again; then a
-               second build whose deferred steps fit; infos, newest profiles
-               and kept results to npz
+               second build whose deferred steps fit; a third where only
+               rank 0's batches hold a read for the general path; infos,
+               newest profiles and kept results to npz
   config4      BASELINE configs[3]: config 3 over W ranks (bench.py's exact
                strong workload); the union of outputs hashed with
                tests/digests.py (the parent compares with digests.json config3)
@@ -165,17 +166,27 @@ def defer_rank(group, rank, sizes, frags, seed):
         full = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))
         small = _lib.DevBuf.from_numpy(ctx, np.ascontiguousarray(rec[:k]).view(np.int64).reshape(-1))
         try:
-            for tag, first in (("over", (small, k)), ("fit", (full, len(rec)))):
+            # rank 0 alone gets a read of 12 records (the general path): every
+            # rank must run the deferred steps again
+            rp = rec
+            if rank == 0:
+                big = np.stack([np.full(12, rec[-1, 0] + 1, np.uint32),
+                                (np.arange(12, dtype=np.uint32) * 37) % n_glob], axis=1)
+                rp = np.concatenate([rec, big])
+            out["peer_rec"] = rp
+            peer = _lib.DevBuf.from_numpy(ctx, np.ascontiguousarray(rp).view(np.int64).reshape(-1))
+            for tag, first, batch in (("over", (small, k), (full, len(rec))), ("fit", (full, len(rec)), (full, len(rec))),
+                                      ("peer", (peer, len(rp)), (peer, len(rp)))):
                 build = ShardedBuild(ctx, comm, -1, n_glob, c_lo, n_loc)
                 try:
                     assert build.native is not None
                     build.run(store, first[0].ptr, first[1], count=False)  # synchronous: sizes the slots
                     for _ in range(3):
-                        build.run(store, full.ptr, len(rec), count=False)
+                        build.run(store, batch[0].ptr, batch[1], count=False)
                     build.sync()
                     out[f"{tag}_info"] = build.native.info()
                     out[f"{tag}_profile"] = build.native.profile().numpy()
-                    res = build.run(store, full.ptr, len(rec), keep=True)
+                    res = build.run(store, batch[0].ptr, batch[1], keep=True)
                     e = res["edges"]
                     out.update({f"{tag}_a": e.a, f"{tag}_b": e.b, f"{tag}_w": e.weight, f"{tag}_tot": e.totals})
                 finally:
@@ -185,6 +196,7 @@ def defer_rank(group, rank, sizes, frags, seed):
             store.close()
             full.close()
             small.close()
+            peer.close()
     finally:
         comm.close()
         ctx.close()

@@ -106,7 +106,9 @@ def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world):
     and the summed slow flag).  A first synchronous step on 1 % of the
     reads sizes the slots, so the three deferred full steps overflow them: every
     rank runs them again synchronously.  A second build sized on the full step
-    defers three steps that fit (no re-run).  The newest profile after sync and
+    defers three steps that fit (no re-run).  In a third, only rank 0's batches
+    hold a read for the general path (12 records): its verdict reaches the
+    other ranks in the slot headers, and every rank re-runs the three steps.  The newest profile after sync and
     the kept step after each must equal the oracle bit for bit (ACGT-only
     contigs: the deferred path needs no exception keys)."""
     sizes = [5000, 6000, 5500][:world]  # ~5000 distinct pairs per owner's slice
@@ -115,15 +117,21 @@ def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world):
               str(frags), "--seed", str(seed), "--out", str(tmp_path))
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     prof, _, o = oracle_of(sizes, frags, seed, n_rate=0, len_span=100)
-    for tag in ("over", "fit"):
+    # rank 0's batches in the third build carry one more read, of 12 records
+    recs = [p["peer_rec"].astype(np.int64) for p in parts]
+    st = np.concatenate([np.flatnonzero(np.r_[True, r[1:, 0] != r[:-1, 0]]) + sum(map(len, recs[:i]))
+                         for i, r in enumerate(recs)])
+    rec = np.concatenate(recs)
+    o_peer = oracle.graph_groups(np.r_[st, len(rec)], rec[:, 1], None, None, sum(sizes), dedup=True)
+    for tag in ("over", "fit", "peer"):
         infos = [p[f"{tag}_info"] for p in parts]
         # [M, E, pairs, entries, synchronous, deferred, re-run, pending, ...]
         for i in infos:
             assert i[5] == 3 and i[7] == 0, (tag, i.tolist())
-            assert i[6] == (3 if tag == "over" else 0), (tag, i.tolist())
+            assert i[6] == (0 if tag == "fit" else 3), (tag, i.tolist())
         got = np.concatenate([p[f"{tag}_profile"] for p in parts])
         assert np.array_equal(got.view(np.uint64), prof.view(np.uint64)), tag
-        check_graph(parts, o, tag + "_")
+        check_graph(parts, o_peer if tag == "peer" else o, tag + "_")
 
 
 def test_rccl_config4_strong_8_ranks_digests():
