@@ -613,6 +613,18 @@ struct karma_step {
     karma_contigs* acgt_store = nullptr;
     int64_t kc = 0;
     bool defer_ranks = true;      // KARMA_STEP_DEFER_RANKS=0: synchronous steps with several processes
+    // several processes, two main streams: every deferred step's exchange and
+    // edge stage (all of the main communicator's operations) on one exchange
+    // stream, side_alt_s (idle then: the column exchange keeps to side_s), so
+    // batch i + 1's records job runs beside batch i's collectives.  Events
+    // hand the records job's lists to it (ev_rec), return them before the
+    // same main stream's next records job reuses them (ev_tail[par]), and
+    // order the communicator's operations across the exchange stream and the
+    // synchronous steps' main stream (ev_tail, ev_sync).
+    bool xstream = true;          // KARMA_STEP_XSTREAM=0: one main stream with several processes
+    hipEvent_t ev_rec = nullptr, ev_sync = nullptr, ev_tail[2] = {};
+    bool tail_set[2] = {}, sync_set = false;
+    int tail_last = -1;
 };
 
 namespace {
@@ -763,12 +775,30 @@ int allgather_slices(karma_step* s, int64_t* buf) {
     return KARMA_OK;
 }
 
+// stream `w` waits for everything recorded so far on stream `on` (one event
+// per purpose, created on first use)
+int stream_after(hipEvent_t* ev, hipStream_t on, hipStream_t w) {
+    if (!*ev) KARMA_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    if (counted_call("hipEventRecord")) ++t_hip_calls;
+    KARMA_HIP(hipEventRecord(*ev, on));
+    if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
+    KARMA_HIP(hipStreamWaitEvent(w, *ev, 0));
+    return KARMA_OK;
+}
+
 // ---- the synchronous step ------------------------------------------------------
 int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A, bool keep, bool sequential,
              bool count) {
     karma_ctx* ctx = s->ctx;
     KARMA_TRY(drop_outputs(s));
     ++s->n_sync;
+    if (s->tail_last >= 0) {
+        // deferred steps' exchanges may still be queued on the exchange stream
+        // (a re-run checked 3 steps back): the main stream's collectives and
+        // the records job's reuse of their lists come after them
+        if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
+        KARMA_HIP(hipStreamWaitEvent(s->main_s, s->ev_tail[s->tail_last], 0));
+    }
     if (s->exchange) KARMA_TRY(karma_graph_split_hint(ctx, s->bounds.data(), s->nranks));
     int64_t M = 0;
     if (!sequential) {
@@ -864,6 +894,7 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
     }
     s->E = E;
     if (!sequential) KARMA_TRY(karma_ctx_join(ctx, s->side_s));
+    s->sync_set = s->world > 1;  // the next exchange-stream tail waits for this step's collectives
     return KARMA_OK;
 }
 
@@ -907,7 +938,8 @@ int drain(karma_step* s, bool wait, bool lag) {
             for (int spin = 0; !entry_done(s, p.seq); ++spin) {
                 if (spin > 64) std::this_thread::yield();
                 if (spin % 4096 == 4095 && hipStreamQuery(s->main_s) == hipSuccess &&
-                    hipStreamQuery(s->alt_s) == hipSuccess && !entry_done(s, p.seq)) {
+                    hipStreamQuery(s->alt_s) == hipSuccess && hipStreamQuery(s->side_alt_s) == hipSuccess &&
+                    !entry_done(s, p.seq)) {
                     set_error("karma_step: a deferred step's status never arrived");
                     return KARMA_ERR_STATE;
                 }
@@ -946,9 +978,20 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // jobs side by side took 1.89 ms per batch against 1.23 ms one after the
     // other (they evict each other's partition runs from the caches); the
     // 8-rank strong preview (38.6M records) went 0.237 -> 0.199 ms.
-    const bool two = s->world == 1 && (s->streams ? s->streams == 2 : A < kAltMaxRecords);
+    // several processes: two main streams only with the exchange stream
+    // (the main communicator's operations then all go to side_alt_s)
+    const bool two = (s->world == 1 || (s->xstream && !sequential)) &&
+                     (s->streams ? s->streams == 2 : A < kAltMaxRecords);
+    const bool xs_on = s->world > 1 && two;
     const int par = sequential || !two ? 0 : (int)(seq & 1);
     hipStream_t const ms = par ? s->alt_s : s->main_s;
+    hipStream_t const xs = s->side_alt_s;
+    if (s->tail_set[par]) {
+        // the records job's lists (this main stream's cache) and tail[par]
+        // were last used on the exchange stream
+        if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
+        KARMA_HIP(hipStreamWaitEvent(ms, s->ev_tail[par], 0));
+    }
     // One main stream (large batches): the records job does not wait for the
     // previous batch's profile.  With KARMA_STEP_JOIN=1 it does (classify then
     // never shares HBM with a profile): config 3 1.29-1.31 against 1.16-1.21 ms
@@ -979,7 +1022,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // side stream: presence, column table (M stays on the device), then the
     // profile behind the graph's final kernel (sequential: all on the main
     // stream, every kernel alone on the chip -- the per-kernel timing pass)
-    hipStream_t const side = sequential ? ms : (par && s->sides == 2 ? s->side_alt_s : s->side_s);
+    hipStream_t const side = sequential ? ms : (par && s->sides == 2 && !xs_on ? s->side_alt_s : s->side_s);
     ctx->stream = side;
     karma_kmer_plan* plan = nullptr;
     int rc = karma_kmer_plan_create(ctx, store, s->kmode, &plan);
@@ -1003,6 +1046,14 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     if (plan) karma_kmer_plan_destroy(plan);  // its buffers return to the side stream's cache
     ctx->stream = ms;
     KARMA_TRY(rc);
+    if (xs_on) {  // the tail on the exchange stream, behind this records job (and a synchronous step's collectives)
+        KARMA_TRY(stream_after(&s->ev_rec, ms, xs));
+        if (s->sync_set) {
+            KARMA_TRY(stream_after(&s->ev_sync, s->main_s, xs));
+            s->sync_set = false;
+        }
+        ctx->stream = xs;
+    }
     // main stream: the tail, sized on the device
     const uint64_t* lk = v.keys;
     const int64_t* lc = v.counts;
@@ -1072,6 +1123,14 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
                  tl.tile_cnt.ptr, tl.ea.ptr, tl.eb.ptr, tl.es.ptr, tl.ew.ptr, tl.est.ptr, s->n_glob);
     KARMA_LAUNCH(ctx, "step_status", step_status_kernel, 1, 256, 0, v.flags, v.counters, v.ovf, v.B, v.dst, mbad,
                  tl.est.ptr, s->ring_d + seq % kRing, seq);
+    if (xs_on) {
+        if (!s->ev_tail[par]) KARMA_HIP(hipEventCreateWithFlags(&s->ev_tail[par], hipEventDisableTiming));
+        if (counted_call("hipEventRecord")) ++t_hip_calls;
+        KARMA_HIP(hipEventRecord(s->ev_tail[par], xs));
+        s->tail_set[par] = true;
+        s->tail_last = par;
+        ctx->stream = ms;
+    }
     s->pending.push_back({seq, store, rec, A});
     return KARMA_OK;
 }
@@ -1110,6 +1169,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     if (const char* e = getenv("KARMA_STEP_JOIN")) s->join = atoi(e) != 0;  // A/B only
     if (const char* e = getenv("KARMA_STEP_SIDES")) s->sides = atoi(e) == 1 ? 1 : 2;
     if (const char* e = getenv("KARMA_STEP_DEFER_RANKS")) s->defer_ranks = atoi(e) != 0;
+    if (const char* e = getenv("KARMA_STEP_XSTREAM")) s->xstream = atoi(e) != 0;
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
@@ -1254,6 +1314,8 @@ int karma_step_destroy(karma_step* s) {
     drop_outputs(s);
     bury(s, true);
     for (auto& ev : s->grave_ev)
+        if (ev) hipEventDestroy(ev);
+    for (hipEvent_t ev : {s->ev, s->ev_rec, s->ev_sync, s->ev_tail[0], s->ev_tail[1]})
         if (ev) hipEventDestroy(ev);
     if (s->graves_h) hipHostFree(s->graves_h);
     // the step's buffers return to the context's cache under streams about to
