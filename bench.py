@@ -568,8 +568,8 @@ def end_to_end_legs(args, inp, ctx, build, store):
 
     def eq_once():
         t0 = time.perf_counter()
-        e = engine.graph_from_eq(cls_off, members, counts, skip, inp["n_glob"], ctx=ctx)
-        return time.perf_counter() - t0, len(e.a)
+        a, _, _ = engine.graph_from_eq_ordered(cls_off, members, counts, skip, inp["n_glob"], ctx=ctx)
+        return time.perf_counter() - t0, len(a)
 
     eq_once()
     te = [eq_once() for _ in range(5)]
@@ -580,8 +580,9 @@ def end_to_end_legs(args, inp, ctx, build, store):
     ctx.timing(False)
     out["eq_path"] = {"ms": round(min(x[0] for x in te) * 1e3, 3), "classes": int(len(counts)),
                       "members": int(len(members)), "edges": te[0][1],
-                      "includes": "host eq arrays -> H2D -> eq_count, scans, eq_scatter, seg_reduce, seg_compact "
-                                  "(csrc/eq.hip) -> weights -> edges D2H",
+                      "includes": "host eq arrays -> H2D -> pair-count scan, eq_rank, eq_place, seg_reduce, "
+                                  "eq_totals (csrc/eq.hip) -> weights -> eq_order (the reference's insertion "
+                                  "order, as the drop-in reads it) -> (a, b, w) D2H",
                       "kernels_ms": eq_k,
                       "value": round((n + inp["f_loc"]) / min(x[0] for x in te), 1)}
     out["dropin"] = dropin_leg(inp)

@@ -321,6 +321,12 @@ int karma_edges_totals(karma_edges* e, int64_t* totals, int is_device);
 /* karma_edges_get and karma_edges_totals with one synchronisation. */
 int karma_edges_get_all(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, double* w, uint64_t* first,
                         int64_t* totals, int is_device);
+/* Eq-class edge stages (KARMA_MODE_EQ) only: a, b, w[E] in the reference's
+ * insertion order -- edges grouped by a ascending, inside a group by the pair's
+ * first emission (read_graph.py:96-131 adds (u, v) from u as pairs are first
+ * seen; cls(incoming_graph_data=) keeps that order, read_graph.py:148).  The
+ * order is computed on the device; one synchronisation. */
+int karma_edges_get_ordered(karma_edges* e, uint32_t* a, uint32_t* b, double* w, int is_device);
 
 /* ---- one rank's step of the sharded build ---------------
  * The whole hot path of one batch on this rank as one call: the records job

@@ -131,6 +131,7 @@ _SIGS = {
     "karma_edges_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _i32],
     "karma_edges_totals": [_c_p, _c_p, _i32],
     "karma_edges_get_all": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _i32],
+    "karma_edges_get_ordered": [_c_p, _c_p, _c_p, _c_p, _i32],
     "karma_api_calls": [_c_p],
     "karma_step_create": [_c_p, _c_p, _c_p, _i32, _i64, _c_p, _i32, _i32, _PP],
     "karma_step_run": [_c_p, _c_p, _c_p, _i64, _i32, _c_p],

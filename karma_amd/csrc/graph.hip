@@ -241,6 +241,66 @@ __global__ void __launch_bounds__(kET) group_sum_kernel(const uint64_t* __restri
 
 int grid1(int64_t n, int block = 256) { return (int)std::max<int64_t>(1, ceil_div(n, block)); }
 
+// ---- eq edges in the reference's insertion order -------------------------------
+// read_graph.py:96-131 adds edge (u, v) to the intermediate graph at the pair's
+// first emission, from its lower endpoint u; the copy cls(incoming_graph_data=)
+// keeps that order per node.  The edge list is sorted by (a, b); each edge's
+// place inside its run of equal a is its rank by first emission (distinct per
+// pair).  A block takes 256 consecutive edges; the runs they belong to are
+// streamed through LDS in chunks, and every thread counts the smaller first
+// emissions of its own run.  Outputs are the (a, b, w) arrays in that order.
+constexpr int kOrdT = 256, kOrdChunk = 4096;
+__global__ void __launch_bounds__(kOrdT) eq_order_kernel(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                                        const double* __restrict__ w,
+                                                        const uint64_t* __restrict__ first, int64_t E,
+                                                        uint32_t* __restrict__ oa, uint32_t* __restrict__ ob,
+                                                        double* __restrict__ ow) {
+    __shared__ uint64_t sf[kOrdChunk];
+    __shared__ int64_t span[2];
+    const int64_t t0 = (int64_t)blockIdx.x * kOrdT, i = t0 + threadIdx.x;
+    const int64_t t1 = min(E, t0 + kOrdT);
+    const bool own = i < E;
+    const uint32_t ai = own ? a[i] : 0u;
+    const uint64_t fi = own ? first[i] : 0ull;
+    // the run of a[i]: [lo, hi)
+    int64_t lo = 0, hi = 0;
+    if (own) {
+        int64_t l = 0, h = i;  // first index with a == ai
+        while (l < h) {
+            const int64_t m = (l + h) >> 1;
+            if (a[m] < ai) l = m + 1;
+            else h = m;
+        }
+        lo = l;
+        l = i + 1, h = E;  // first index with a > ai
+        while (l < h) {
+            const int64_t m = (l + h) >> 1;
+            if (a[m] <= ai) l = m + 1;
+            else h = m;
+        }
+        hi = l;
+    }
+    if (threadIdx.x == 0) span[0] = lo;                 // the block's first edge opens the span
+    if (i == t1 - 1) span[1] = hi;                      // ... its last one closes it
+    __syncthreads();
+    const int64_t s0 = span[0], s1 = span[1];
+    int64_t rank = 0;
+    for (int64_t c0 = s0; c0 < s1; c0 += kOrdChunk) {
+        const int64_t c1 = min(s1, c0 + kOrdChunk);
+        __syncthreads();
+        for (int64_t j = c0 + threadIdx.x; j < c1; j += kOrdT) sf[j - c0] = first[j];
+        __syncthreads();
+        const int64_t j0 = max(lo, c0), j1 = min(hi, c1);
+        for (int64_t j = j0; j < j1; ++j) rank += sf[j - c0] < fi ? 1 : 0;
+    }
+    if (own) {
+        const int64_t pos = lo + rank;
+        oa[pos] = ai;
+        ob[pos] = b[i];
+        ow[pos] = w[i];
+    }
+}
+
 __global__ void interleave_kernel(const uint32_t* __restrict__ rid, const uint32_t* __restrict__ cid, int64_t n,
                                   uint2* __restrict__ out) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1166,6 +1226,29 @@ int karma_edges_get_all(karma_edges* e, uint32_t* a, uint32_t* b, int64_t* s, do
         if (first && e->has_first) KARMA_HIP(hipMemcpyAsync(first, e->first.ptr, e->E * 8, kind, st));
     }
     KARMA_HIP(hipStreamSynchronize(st));
+    return KARMA_OK;
+}
+
+int karma_edges_get_ordered(karma_edges* e, uint32_t* a, uint32_t* b, double* w, int is_device) {
+    KARMA_CHECK(e && a && b && w, KARMA_ERR_ARG, "bad arguments");
+    KARMA_TRY(ctx_begin(e->ctx));
+    KARMA_TRY(edges_resolve(e));
+    KARMA_CHECK(e->has_first, KARMA_ERR_STATE, "karma_edges_get_ordered: not an equivalence-class edge stage");
+    karma_ctx* ctx = e->ctx;
+    const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (e->E) {
+        DevArray<uint32_t> oa, ob;
+        DevArray<double> ow;
+        KARMA_TRY(oa.alloc(ctx, e->E));
+        KARMA_TRY(ob.alloc(ctx, e->E));
+        KARMA_TRY(ow.alloc(ctx, e->E));
+        KARMA_LAUNCH(ctx, "eq_order", eq_order_kernel, (int)ceil_div(e->E, kOrdT), kOrdT, 0, e->a.ptr, e->b.ptr,
+                     e->w.ptr, e->first.ptr, e->E, oa.ptr, ob.ptr, ow.ptr);
+        KARMA_HIP(hipMemcpyAsync(a, oa.ptr, e->E * 4, kind, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(b, ob.ptr, e->E * 4, kind, ctx->stream));
+        KARMA_HIP(hipMemcpyAsync(w, ow.ptr, e->E * 8, kind, ctx->stream));
+        KARMA_HIP(hipStreamSynchronize(ctx->stream));  // before the scratch returns to the cache
+    }
     return KARMA_OK;
 }
 

@@ -544,6 +544,19 @@ class Edges:
         call("karma_edges_get_all", self.h, ptr(a), ptr(b), ptr(s), ptr(w), ptr(f), ptr(t), 0)
         return EdgeArrays(a[:E], b[:E], s[:E], w[:E], f[:E], t[: self.n_contigs])
 
+    def get_ordered(self):
+        """Eq edge stages: (a, b, w) in the reference's insertion order -- by a,
+        then by the pair's first emission (read_graph.py:96-131), ordered on the
+        device (karma_edges_get_ordered); one pinned block."""
+        E = self.E
+        e1 = max(E, 1)
+        blk = _lib.pinned_empty(16 * e1, np.uint8)
+        w = blk[: 8 * e1].view(np.float64)
+        a = blk[8 * e1: 12 * e1].view(np.uint32)
+        b = blk[12 * e1:].view(np.uint32)
+        call("karma_edges_get_ordered", self.h, ptr(a), ptr(b), ptr(w), 0)
+        return a[:E], b[:E], w[:E]
+
     def close(self):
         if getattr(self, "h", None):
             _lib.load().karma_edges_destroy(self.h)
@@ -575,6 +588,21 @@ def graph_from_eq(cls_off, members, counts, pair_skip, n_contigs, ctx=None) -> E
         e = p.edges(_lib.KARMA_MODE_EQ, n_contigs)
         try:
             return e.get()
+        finally:
+            e.close()
+    finally:
+        p.close()
+
+
+def graph_from_eq_ordered(cls_off, members, counts, pair_skip, n_contigs, ctx=None):
+    """Eq-class edges as the drop-in needs them: (a, b, w) in the reference's
+    insertion order (read_graph.py:96-131), ordered on the device."""
+    ctx = ctx or _lib.default_context()
+    p = Pairs.from_eq(ctx, cls_off, members, counts, pair_skip, n_contigs)
+    try:
+        e = p.edges(_lib.KARMA_MODE_EQ, n_contigs)
+        try:
+            return e.get_ordered()
         finally:
             e.close()
     finally:

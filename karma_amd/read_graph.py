@@ -271,17 +271,13 @@ class ReadGraph(nx.Graph):
         """from_equivalence_classes after the parse (read_graph.py:86-148): eq
         names, class offsets/members/counts and the size-token-"1" flags."""
         n = len(names)
-        if n == 0:
-            e = None
-        else:
-            e = _edges_or_zero_div(engine.graph_from_eq, off, members, counts, skip, n)
         ea = eb = np.zeros(0, np.uint32)
         ew = np.zeros(0, np.float64)
-        if e is not None and len(e.a):
+        if n:
             # the reference's intermediate graph (read_graph.py:96-131) gets edge
-            # (u, v) from its lower-index endpoint u, in first-insertion order
-            order = np.lexsort((e.first, e.a))
-            ea, eb, ew = e.a[order], e.b[order], e.weight[order]
+            # (u, v) from its lower-index endpoint u, in first-insertion order:
+            # that order comes from the device
+            ea, eb, ew = _edges_or_zero_div(engine.graph_from_eq_ordered, off, members, counts, skip, n)
         # read_graph.py:136-143: FASTA names missing from the eq file become
         # isolated nodes, in the order of this set difference (hash seed
         # dependent, as in the reference); eq names are distinct (:93 assert)

@@ -308,6 +308,35 @@ def test_eq_vs_oracle_seeded():
     assert np.array_equal(e.weight.view(np.uint64), o["weight"].view(np.uint64))
 
 
+@pytest.mark.parametrize("hub", [0, 9000])
+def test_eq_ordered_edges_are_the_insertion_order(hub):
+    """karma_edges_get_ordered: (a, b, w) grouped by a, inside a group by the
+    pair's first emission -- the order read_graph.py:96-131 inserts edges in
+    (the drop-in builds its graph from it).  Against the oracle's (a, first)
+    order; hub > 0 adds a contig paired with `hub` others in shuffled class
+    order (one run longer than the kernel's 4,096-entry LDS chunk)."""
+    rng = np.random.default_rng(5 + hub)
+    n = 12_000
+    classes = synth.eq_classes(33, n, 200_000, True)
+    cl = [np.asarray(c, np.uint32) for c, _ in classes]
+    cn = [k for _, k in classes]
+    if hub:
+        for v in rng.permutation(np.arange(1, hub + 1)):
+            cl.append(np.array([0, v], np.uint32))
+            cn.append(int(rng.integers(1, 9)))
+    off = np.r_[0, np.cumsum([len(c) for c in cl])].astype(np.int64)
+    mem = np.concatenate(cl).astype(np.uint32)
+    cnt = np.asarray(cn, np.int64)
+    skip = np.array([1 if len(c) == 1 else 0 for c in cl], np.uint8)
+    a, b, w = engine.graph_from_eq_ordered(off, mem, cnt, skip, n)
+    o = oracle.graph_groups(off, mem, cnt, skip, n, dedup=False)
+    order = np.lexsort((o["first"], o["a"]))
+    assert np.array_equal(a, o["a"][order]) and np.array_equal(b, o["b"][order])
+    assert np.array_equal(w.view(np.uint64), o["weight"][order].view(np.uint64))
+    if hub:
+        assert int(np.sum(a == 0)) >= hub
+
+
 def test_eq_big_classes_device_inputs_and_errors():
     """Classes past the per-thread size (a block each in eq_rank), duplicate
     members, size-token-"1" classes of several members, the skip array absent,
