@@ -565,10 +565,19 @@ def end_to_end_legs(args, inp, ctx, build, store):
     cls_off, members, counts = engine.synth_eq_classes(inp["seed"], inp["n_glob"], inp["f_lo"],
                                                        inp["f_lo"] + inp["f_loc"], inp["paired"], genes=inp["genes"])
     skip = (np.diff(cls_off) == 1).astype(np.uint8)  # eq_size token "1"
+    # the form the drop-in's C++ parser hands over (ingest.parse_eq(compact=True):
+    # sizes u8, counts u32, pinned host memory), built before the timed calls
+    cq = engine.eq_compact(cls_off, counts, skip)
+    if cq is not None:
+        c_sz, c_mem, c_cnt = (_lib.pinned_empty(len(x), x.dtype) for x in (cq[0], members, cq[1]))
+        c_sz[:], c_mem[:], c_cnt[:] = cq[0], members, cq[1]
 
     def eq_once():
         t0 = time.perf_counter()
-        a, _, _ = engine.graph_from_eq_ordered(cls_off, members, counts, skip, inp["n_glob"], ctx=ctx)
+        if cq is not None:
+            a, _, _ = engine.graph_from_eq_compact_ordered(c_sz, c_mem, c_cnt, inp["n_glob"], ctx=ctx)
+        else:
+            a, _, _ = engine.graph_from_eq_ordered(cls_off, members, counts, skip, inp["n_glob"], ctx=ctx)
         return time.perf_counter() - t0, len(a)
 
     eq_once()
@@ -580,9 +589,11 @@ def end_to_end_legs(args, inp, ctx, build, store):
     ctx.timing(False)
     out["eq_path"] = {"ms": round(min(x[0] for x in te) * 1e3, 3), "classes": int(len(counts)),
                       "members": int(len(members)), "edges": te[0][1],
-                      "includes": "host eq arrays -> H2D -> pair-count scan, eq_rank, eq_place, seg_reduce, "
-                                  "eq_totals (csrc/eq.hip) -> weights -> eq_order (the reference's insertion "
-                                  "order, as the drop-in reads it) -> (a, b, w) D2H",
+                      "includes": "host eq arrays as the C++ parser emits them (sizes u8, members u32, counts "
+                                  "u32, pinned) -> H2D -> size and pair-count scans, eq_rank, eq_place, "
+                                  "seg_reduce, eq_totals (csrc/eq.hip) -> weights -> eq_order (the reference's "
+                                  "insertion order, as the drop-in reads it) -> (a, b, w) D2H",
+                      "compact": cq is not None,
                       "kernels_ms": eq_k,
                       "value": round((n + inp["f_loc"]) / min(x[0] for x in te), 1)}
     out["dropin"] = dropin_leg(inp)

@@ -111,6 +111,7 @@ _SIGS = {
     "karma_graph_records_end": [_c_p, _PP],
     "karma_graph_split_hint": [_c_p, _c_p, _i32],
     "karma_graph_eq": [_c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i64, _i32, _PP],
+    "karma_graph_eq_compact": [_c_p, _c_p, _c_p, _c_p, _i64, _i64, _PP],
     "karma_pairs_merge": [_c_p, _c_p, _c_p, _i64, _i32, _PP],
     "karma_pairs_merge_runs": [_c_p, _c_p, _c_p, _c_p, _i32, _i32, _PP],
     "karma_pairs_merge_runs_kc": [_c_p, _c_p, _c_p, _i32, _PP],
@@ -156,6 +157,7 @@ _SIGS = {
     "karma_eq_parse": [_c_p, ctypes.c_size_t, _i32, _PP],
     "karma_eq_info": [_c_p, _I64P, _I64P, _I64P, _I64P],
     "karma_eq_get": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
+    "karma_eq_get_compact": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p],
     "karma_eq_destroy": [_c_p],
     "karma_sam_parse": [_c_p, ctypes.c_size_t, _i32, _i32, _PP],
     "karma_sam_info": [_c_p, _I64P, _I64P, _I64P, _I64P, _I64P],

@@ -390,6 +390,12 @@ __global__ void __launch_bounds__(kRT) seg_reduce_kernel(const int64_t* __restri
     }
 }
 
+// compact inputs: u32 counts widened on the device
+__global__ void widen_counts_kernel(const uint32_t* __restrict__ in, int64_t n, int64_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
 int grid_of(int64_t n, int block) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(karma::ceil_div(n, block), 1 << 20));
 }
@@ -404,14 +410,25 @@ namespace {
 // (the context's previous pair total) and nothing waits for the pair total;
 // *P_out > cap then means the pass must run again with cap = *P_out.  cap = 0:
 // one readback of the pair total sizes the scratch.
+// Compact host inputs (karma_graph_eq_compact): sizes (member count | size
+// token "1" << 7) and u32 counts; n_mem their summed sizes.
+struct EqCompact {
+    const uint8_t* sizes = nullptr;
+    const uint32_t* counts32 = nullptr;
+    int64_t n_mem = 0;
+};
+
 int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
                  const uint8_t* pair_skip, int64_t C, int64_t N, int is_device, int64_t cap, int64_t* P_out,
-                 karma_pairs** out) {
+                 karma_pairs** out, const EqCompact& cq = EqCompact{}) {
     hipStream_t const ms = ctx->stream;
     int64_t* hp = nullptr;  // pinned: [0] pairs, [1] distinct keys, [2] bad member flag, [3] over capacity
     KARMA_TRY(ctx_pinned(ctx, 32, reinterpret_cast<void**>(&hp)));
+    const bool compact = cq.sizes != nullptr;
     int64_t n_mem = 0;
-    if (is_device) {
+    if (compact) {
+        n_mem = cq.n_mem;
+    } else if (is_device) {
         KARMA_HIP(hipMemcpyAsync(hp, cls_off + C, 8, hipMemcpyDeviceToHost, ms));
         KARMA_HIP(hipStreamSynchronize(ms));
         n_mem = hp[0];
@@ -444,8 +461,8 @@ int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members
     // pipeline.  Every buffer is the main stream's (allocator), so the fork
     // stream first waits for the main stream's earlier work.
     DevArray<int64_t> d_off, d_cnt;
-    DevArray<uint32_t> d_mem;
-    DevArray<uint8_t> d_skip;
+    DevArray<uint32_t> d_mem, d_c32;
+    DevArray<uint8_t> d_skip, d_sz;
     const int64_t* off = cls_off;
     const uint32_t* mem = members;
     const int64_t* cnt = counts;
@@ -460,18 +477,28 @@ int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members
         KARMA_TRY(d_off.alloc(ctx, C + 1));
         KARMA_TRY(d_cnt.alloc(ctx, std::max<int64_t>(C, 1)));
         KARMA_TRY(d_mem.alloc(ctx, std::max<int64_t>(n_mem, 1)));
-        if (pair_skip) KARMA_TRY(d_skip.alloc(ctx, std::max<int64_t>(C, 1)));
+        if (pair_skip || compact) KARMA_TRY(d_skip.alloc(ctx, std::max<int64_t>(C, 1)));
+        if (compact) {
+            KARMA_TRY(d_sz.alloc(ctx, std::max<int64_t>(C, 1)));
+            KARMA_TRY(d_c32.alloc(ctx, std::max<int64_t>(C, 1)));
+        }
         KARMA_HIP(hipEventRecord(ev[0], ms));
         KARMA_HIP(hipStreamWaitEvent(xs, ev[0], 0));
         KARMA_HIP(hipMemsetAsync(zero.ptr, 0, (seg_words + 1 + 4) * 8, xs));
-        KARMA_HIP(hipMemcpyAsync(d_off.ptr, cls_off, (C + 1) * 8, hipMemcpyHostToDevice, xs));
-        if (pair_skip && C) KARMA_HIP(hipMemcpyAsync(d_skip.ptr, pair_skip, C, hipMemcpyHostToDevice, xs));
+        if (compact) {  // 1 byte per class instead of 9 (offset + skip)
+            if (C) KARMA_HIP(hipMemcpyAsync(d_sz.ptr, cq.sizes, C, hipMemcpyHostToDevice, xs));
+        } else {
+            KARMA_HIP(hipMemcpyAsync(d_off.ptr, cls_off, (C + 1) * 8, hipMemcpyHostToDevice, xs));
+            if (pair_skip && C) KARMA_HIP(hipMemcpyAsync(d_skip.ptr, pair_skip, C, hipMemcpyHostToDevice, xs));
+        }
         KARMA_HIP(hipEventRecord(ev[1], xs));
         off = d_off.ptr;
-        skip = pair_skip ? d_skip.ptr : nullptr;
+        skip = pair_skip || compact ? d_skip.ptr : nullptr;
         mem = d_mem.ptr;
         cnt = d_cnt.ptr;
         KARMA_HIP(hipStreamWaitEvent(ms, ev[1], 0));
+        // the class offsets and skip flags from the sizes, in one scan
+        if (compact) KARMA_TRY(scan_excl_sizes(ctx, d_sz.ptr, d_skip.ptr, C, d_off.ptr));
     } else {
         KARMA_HIP(hipMemsetAsync(zero.ptr, 0, (seg_words + 1 + 4) * 8, ms));
     }
@@ -529,7 +556,16 @@ int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members
     }
     // the counts go up while the pair kernels run; then the totals beside them
     if (!is_device) {
-        if (C) KARMA_HIP(hipMemcpyAsync(d_cnt.ptr, counts, C * 8, hipMemcpyHostToDevice, xs));
+        if (compact) {
+            if (C) {
+                KARMA_HIP(hipMemcpyAsync(d_c32.ptr, cq.counts32, C * 4, hipMemcpyHostToDevice, xs));
+                ctx->stream = xs;
+                KARMA_LAUNCH(ctx, "eq_widen", widen_counts_kernel, grid_of(C, 256), 256, 0, d_c32.ptr, C, d_cnt.ptr);
+                ctx->stream = ms;
+            }
+        } else if (C) {
+            KARMA_HIP(hipMemcpyAsync(d_cnt.ptr, counts, C * 8, hipMemcpyHostToDevice, xs));
+        }
         KARMA_HIP(hipEventRecord(ev[3], xs));
     }
     {
@@ -583,6 +619,26 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
     *out = nullptr;
     KARMA_TRY(graph_eq_run(ctx, cls_off, members, counts, pair_skip, C, N, is_device, cap, &P, out));
     if (!*out) KARMA_TRY(graph_eq_run(ctx, cls_off, members, counts, pair_skip, C, N, is_device, 0, &P, out));
+    ctx->eq_pair_cap = std::max(cap, P);
+    return KARMA_OK;
+}
+
+int karma_graph_eq_compact(karma_ctx* ctx, const uint8_t* sizes, const uint32_t* members, const uint32_t* counts,
+                           int64_t C, int64_t N, karma_pairs** out) {
+    KARMA_TRY(ctx_begin(ctx));
+    KARMA_CHECK(out && (sizes || C == 0) && (counts || C == 0) && C >= 0 && N >= 0 && N < (int64_t(1) << 32),
+                KARMA_ERR_ARG, "karma_graph_eq_compact: bad arguments");
+    EqCompact cq;
+    static const uint8_t none = 0;
+    cq.sizes = C ? sizes : &none;
+    cq.counts32 = counts;
+    for (int64_t c = 0; c < C; ++c) cq.n_mem += sizes[c] & 0x7F;  // sizes the members' copy (host side)
+    KARMA_CHECK(cq.n_mem == 0 || members, KARMA_ERR_ARG, "karma_graph_eq_compact: no members");
+    const int64_t cap = ctx->eq_pair_cap;
+    int64_t P = 0;
+    *out = nullptr;
+    KARMA_TRY(graph_eq_run(ctx, nullptr, members, nullptr, nullptr, C, N, 0, cap, &P, out, cq));
+    if (!*out) KARMA_TRY(graph_eq_run(ctx, nullptr, members, nullptr, nullptr, C, N, 0, 0, &P, out, cq));
     ctx->eq_pair_cap = std::max(cap, P);
     return KARMA_OK;
 }

@@ -667,6 +667,30 @@ extern "C" int karma_eq_get(karma_eq* q, char* names, int64_t* name_off, int64_t
     return KARMA_OK;
 }
 
+extern "C" int karma_eq_get_compact(karma_eq* q, char* names, int64_t* name_off, uint8_t* sizes, uint32_t* members,
+                                    uint32_t* counts) {
+    if (!q) {
+        set_error("karma_eq_get_compact: null handle");
+        return KARMA_ERR_ARG;
+    }
+    const int64_t C = (int64_t)q->counts.size();
+    for (int64_t c = 0; c < C; ++c) {  // checked first: nothing is written when a class does not fit
+        if (q->cls_off[c + 1] - q->cls_off[c] > 127 || q->counts[c] < 0 || q->counts[c] > (int64_t)UINT32_MAX) {
+            set_error("karma_eq_get_compact: class %lld does not fit (%lld members, count %lld)", (long long)c,
+                      (long long)(q->cls_off[c + 1] - q->cls_off[c]), (long long)q->counts[c]);
+            return KARMA_ERR_ARG;
+        }
+    }
+    copy_out(names, q->names.data(), q->names.size());
+    copy_out(name_off, q->name_off.data(), q->name_off.size() * sizeof(int64_t));
+    copy_out(members, q->members.data(), q->members.size() * sizeof(uint32_t));
+    for (int64_t c = 0; c < C; ++c) {
+        sizes[c] = (uint8_t)((q->cls_off[c + 1] - q->cls_off[c]) | (q->pair_skip[c] ? 0x80 : 0));
+        counts[c] = (uint32_t)q->counts[c];
+    }
+    return KARMA_OK;
+}
+
 extern "C" int karma_eq_destroy(karma_eq* q) {
     delete q;
     return KARMA_OK;

@@ -212,6 +212,8 @@ int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);
 int scan_excl_u32(karma_ctx* ctx, const uint32_t* in, int64_t* out, int64_t n);
 // out[c] = sum over classes before c of m (m - 1) / 2 (0 where skip[c]), c <= C
 int scan_excl_pairs(karma_ctx* ctx, const int64_t* off, const uint8_t* skip, int64_t C, int64_t* out);
+// compact eq classes: off[c] = sum of (sizes & 0x7F) before c (c <= C), skip[c] = sizes[c] >> 7
+int scan_excl_sizes(karma_ctx* ctx, const uint8_t* sizes, uint8_t* skip, int64_t C, int64_t* off);
 int radix_sort_u64(karma_ctx* ctx, const uint64_t* kin, const uint32_t* vin, int64_t n, int key_bits,
                    uint64_t* kout, uint32_t* vout);
 int radix_sort_u32(karma_ctx* ctx, const uint32_t* kin, const uint32_t* vin, int64_t n, int key_bits,

@@ -75,6 +75,20 @@ struct PairCountIn {  // m (m - 1) / 2 for class i of m members, 0 when skipped 
     }
 };
 
+// compact eq classes (karma_graph_eq_compact): the member count in bits 0-6,
+// the size token "1" in bit 7, unpacked into skip as the sizes are scanned
+struct SizeIn {
+    const uint8_t* __restrict__ sz;
+    uint8_t* __restrict__ skip;
+    int64_t C;
+    __device__ int64_t operator()(int64_t i) const {
+        if (i >= C) return 0;
+        const uint32_t v = sz[i];
+        skip[i] = (uint8_t)(v >> 7);
+        return v & 0x7Fu;
+    }
+};
+
 template <typename In>
 __global__ void __launch_bounds__(kST) scan_lb_kernel(In in, int64_t n, int64_t* __restrict__ out,
                                                       uint64_t* __restrict__ st, unsigned* __restrict__ ticket) {
@@ -319,6 +333,11 @@ int scan_excl_i64(karma_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
 
 int scan_excl_u32(karma_ctx* ctx, const uint32_t* in, int64_t* out, int64_t n) {
     return scan_excl(ctx, ArrayIn<uint32_t>{in}, out, n);
+}
+
+// off[c] = members of the compact classes before c (c <= C), skip[c] = bit 7
+int scan_excl_sizes(karma_ctx* ctx, const uint8_t* sizes, uint8_t* skip, int64_t C, int64_t* off) {
+    return scan_excl(ctx, SizeIn{sizes, skip, C}, off, C + 1);
 }
 
 // out[c] = pairs of the eq classes before c (c <= C; out[C] = all pairs)

@@ -376,6 +376,19 @@ class Pairs:
         return cls(ctx, h)
 
     @classmethod
+    def from_eq_compact(cls, ctx, sizes, members, counts32, n_contigs):
+        """karma_graph_eq_compact: sizes uint8[C] (member count | 0x80 for the
+        size token "1"), members uint32, counts uint32[C]."""
+        h = ctypes.c_void_p()
+        sizes = np.ascontiguousarray(sizes, np.uint8)
+        members = np.ascontiguousarray(members, np.uint32)
+        counts32 = np.ascontiguousarray(counts32, np.uint32)
+        call("karma_graph_eq_compact", ctx.h, ptr(sizes) if len(sizes) else None,
+             ptr(members) if len(members) else None, ptr(counts32) if len(counts32) else None, len(sizes),
+             n_contigs, ctypes.byref(h))
+        return cls(ctx, h)
+
+    @classmethod
     def merge_runs_kc(cls, ctx, kc_dev_ptr, runs):
         """Merge received runs of interleaved (key, count) int64 pairs in device memory."""
         off = np.zeros(len(runs) + 1, np.int64)
@@ -599,6 +612,34 @@ def graph_from_eq_ordered(cls_off, members, counts, pair_skip, n_contigs, ctx=No
     insertion order (read_graph.py:96-131), ordered on the device."""
     ctx = ctx or _lib.default_context()
     p = Pairs.from_eq(ctx, cls_off, members, counts, pair_skip, n_contigs)
+    try:
+        e = p.edges(_lib.KARMA_MODE_EQ, n_contigs)
+        try:
+            return e.get_ordered()
+        finally:
+            e.close()
+    finally:
+        p.close()
+
+
+def eq_compact(cls_off, counts, pair_skip):
+    """(sizes uint8, counts uint32) of wide eq arrays for karma_graph_eq_compact,
+    or None when a class has > 127 members or a count past 2^32 - 1 (the form
+    the C++ parser emits directly, ingest.parse_eq(compact=True))."""
+    m = np.diff(np.asarray(cls_off, np.int64))
+    counts = np.asarray(counts, np.int64)
+    if len(m) and (m.max() > 127 or counts.min() < 0 or counts.max() > 0xFFFFFFFF):
+        return None
+    sizes = m.astype(np.uint8)
+    if pair_skip is not None and len(pair_skip):
+        sizes |= (np.asarray(pair_skip, np.uint8) != 0).astype(np.uint8) << 7
+    return sizes, counts.astype(np.uint32)
+
+
+def graph_from_eq_compact_ordered(sizes, members, counts32, n_contigs, ctx=None):
+    """graph_from_eq_ordered from the compact inputs (karma_graph_eq_compact)."""
+    ctx = ctx or _lib.default_context()
+    p = Pairs.from_eq_compact(ctx, sizes, members, counts32, n_contigs)
     try:
         e = p.edges(_lib.KARMA_MODE_EQ, n_contigs)
         try:

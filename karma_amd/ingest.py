@@ -115,13 +115,18 @@ def parse_fasta(data: bytes, threads=0) -> FastaRecords:
 @dataclass
 class EqClasses:
     names: list
-    cls_off: np.ndarray   # int64[C + 1]
+    cls_off: np.ndarray   # int64[C + 1]            (None in the compact form)
     members: np.ndarray   # uint32
-    counts: np.ndarray    # int64[C]
-    pair_skip: np.ndarray  # uint8[C], eq_size token == "1"
+    counts: np.ndarray    # int64[C]                (None in the compact form)
+    pair_skip: np.ndarray  # uint8[C], eq_size token == "1" (None in the compact form)
+    sizes: np.ndarray = None     # compact: uint8[C] member count | 0x80 for the token "1"
+    counts32: np.ndarray = None  # compact: uint32[C]
 
 
-def parse_eq(data: bytes, threads=0) -> EqClasses:
+def parse_eq(data: bytes, threads=0, compact=False) -> EqClasses:
+    """compact=True: the karma_graph_eq_compact form when every class fits it
+    (<= 127 members, counts < 2^32), in pinned host memory (the device copies
+    run at the full PCIe rate); otherwise the wide form."""
     if not _utf8_locale():
         raise ParseDeferred("locale encoding is not UTF-8")
     h = _parse("karma_eq_parse", data, threads)
@@ -131,6 +136,18 @@ def parse_eq(data: bytes, threads=0) -> EqClasses:
         n, C, nm, nb = (x.value for x in v)
         names = ctypes.create_string_buffer(max(nb, 1))
         name_off = np.empty(n + 1, np.int64)
+        if compact:
+            try:
+                sizes, mem, c32 = _lib.pinned_empty(C, np.uint8), _lib.pinned_empty(nm, np.uint32), \
+                    _lib.pinned_empty(C, np.uint32)
+            except KarmaError:  # no device to pin for (the parse itself is host code)
+                sizes, mem, c32 = _buf(C, np.uint8), _buf(nm, np.uint32), _buf(C, np.uint32)
+            rc = _lib.load().karma_eq_get_compact(h, names, _lib.ptr(name_off), _lib.ptr(sizes), _lib.ptr(mem),
+                                                  _lib.ptr(c32))
+            if rc == 0:
+                raw, o = names.raw[:nb], name_off.tolist()
+                return EqClasses([raw[o[i]:o[i + 1]].decode("utf-8") for i in range(n)], None, mem[:nm], None, None,
+                                 sizes[:C], c32[:C])
         cls_off = np.empty(C + 1, np.int64)
         members = _buf(nm, np.uint32)
         counts = _buf(C, np.int64)

@@ -263,13 +263,23 @@ class ReadGraph(nx.Graph):
     @classmethod
     def from_equivalence_classes(cls, equivalence_class_file: str, sequences_from_fasta: dict) -> "ReadGraph":
         """read_graph.py:61-148 with the pair sums and weights on the GPU."""
-        names, off, members, counts, skip = parse_eq_classes(equivalence_class_file)
-        return cls._from_eq_arrays(names, off, members, counts, skip, sequences_from_fasta)
+        try:
+            # the compact form (1 + 4 bytes per class instead of 17 over PCIe)
+            # when every class fits it, straight from the C++ parser
+            q = ingest.parse_eq(ingest._read(equivalence_class_file), 0, compact=True)
+        except ingest.ParseDeferred:
+            names, off, members, counts, skip = _parse_eq_text(equivalence_class_file)
+            return cls._from_eq_arrays(names, off, members, counts, skip, sequences_from_fasta)
+        if q.sizes is not None:
+            return cls._from_eq_arrays(q.names, None, q.members, None, None, sequences_from_fasta,
+                                       compact=(q.sizes, q.counts32))
+        return cls._from_eq_arrays(q.names, q.cls_off, q.members, q.counts, q.pair_skip, sequences_from_fasta)
 
     @classmethod
-    def _from_eq_arrays(cls, names, off, members, counts, skip, sequences_from_fasta):
+    def _from_eq_arrays(cls, names, off, members, counts, skip, sequences_from_fasta, compact=None):
         """from_equivalence_classes after the parse (read_graph.py:86-148): eq
-        names, class offsets/members/counts and the size-token-"1" flags."""
+        names, class offsets/members/counts and the size-token-"1" flags (or
+        compact = (sizes, counts32), karma_graph_eq_compact's form)."""
         n = len(names)
         ea = eb = np.zeros(0, np.uint32)
         ew = np.zeros(0, np.float64)
@@ -277,7 +287,11 @@ class ReadGraph(nx.Graph):
             # the reference's intermediate graph (read_graph.py:96-131) gets edge
             # (u, v) from its lower-index endpoint u, in first-insertion order:
             # that order comes from the device
-            ea, eb, ew = _edges_or_zero_div(engine.graph_from_eq_ordered, off, members, counts, skip, n)
+            if compact is not None:
+                ea, eb, ew = _edges_or_zero_div(engine.graph_from_eq_compact_ordered, compact[0], members, compact[1],
+                                                n)
+            else:
+                ea, eb, ew = _edges_or_zero_div(engine.graph_from_eq_ordered, off, members, counts, skip, n)
         # read_graph.py:136-143: FASTA names missing from the eq file become
         # isolated nodes, in the order of this set difference (hash seed
         # dependent, as in the reference); eq names are distinct (:93 assert)

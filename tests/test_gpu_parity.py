@@ -337,6 +337,36 @@ def test_eq_ordered_edges_are_the_insertion_order(hub):
         assert int(np.sum(a == 0)) >= hub
 
 
+def test_eq_compact_inputs_match_wide():
+    """karma_graph_eq_compact (sizes u8 with the size token "1" in bit 7, u32
+    counts; offsets and skip flags rebuilt on the device by one scan) against
+    the oracle: classes up to 127 members, token-"1" classes of several
+    members, counts near 2^32, an empty class list; a member out of range
+    fails it as on the wide path."""
+    rng = np.random.default_rng(41)
+    n = 2500
+    cl = [rng.integers(0, n, int(m)).astype(np.uint32) for m in list(rng.integers(1, 6, 4000)) + [127, 90, 2, 1]]
+    off = np.r_[0, np.cumsum([len(c) for c in cl])].astype(np.int64)
+    mem = np.concatenate(cl).astype(np.uint32)
+    cnt = rng.integers(1, 2**32 - 1, len(cl)).astype(np.int64)
+    skip = (rng.random(len(cl)) < 0.05).astype(np.uint8)
+    skip[-4] = 1  # the 127-member class with size token "1"
+    sz, c32 = engine.eq_compact(off, cnt, skip)
+    a, b, w = engine.graph_from_eq_compact_ordered(sz, mem, c32, n)
+    o = oracle.graph_groups(off, mem, cnt, skip, n, dedup=False)
+    order = np.lexsort((o["first"], o["a"]))
+    assert np.array_equal(a, o["a"][order]) and np.array_equal(b, o["b"][order])
+    assert np.array_equal(w.view(np.uint64), o["weight"][order].view(np.uint64))
+    a0, _, _ = engine.graph_from_eq_compact_ordered(np.zeros(0, np.uint8), np.zeros(0, np.uint32),
+                                                    np.zeros(0, np.uint32), n)
+    assert len(a0) == 0
+    m2 = mem.copy()
+    m2[int(off[7])] = n + 1
+    with pytest.raises(_lib.KarmaError) as ei:
+        engine.graph_from_eq_compact_ordered(sz, m2, c32, n)
+    assert ei.value.code == _lib.KARMA_ERR_ARG, str(ei.value)
+
+
 def test_eq_big_classes_device_inputs_and_errors():
     """Classes past the per-thread size (a block each in eq_rank), duplicate
     members, size-token-"1" classes of several members, the skip array absent,

@@ -9,7 +9,7 @@ import random
 import numpy as np
 import pytest
 
-from karma_amd import contig, fasta, ingest, read_graph
+from karma_amd import contig, engine, fasta, ingest, read_graph
 from oracle import oracle
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ingest.json")))
@@ -102,6 +102,22 @@ def test_fasta_threads_and_packed(tmp_path):
 
 
 # ------------------------------------------------------------- eq classes ----
+def _eq_compact_matches(data, wide):
+    """ingest.parse_eq(compact=True): the karma_graph_eq_compact form of the
+    same classes when every class fits it, else the wide form."""
+    names, off, mem, cnt, skip = wide
+    q = ingest.parse_eq(data, compact=True)
+    want = engine.eq_compact(off, cnt, skip)
+    if want is None:
+        assert q.sizes is None
+        _eq_arrays_equal((q.names, q.cls_off, q.members, q.counts, q.pair_skip), wide)
+        return False
+    assert q.cls_off is None and list(q.names) == list(names)
+    assert np.array_equal(q.sizes, want[0]) and np.array_equal(q.counts32, want[1])
+    assert np.array_equal(q.members, mem[:off[-1]])
+    return True
+
+
 def _eq_arrays_equal(a, b):
     names_a, off_a, mem_a, cnt_a, skip_a = a
     names_b, off_b, mem_b, cnt_b, skip_b = b
@@ -128,6 +144,7 @@ def test_eq_parse_golden(tmp_path, case):
     _eq_arrays_equal(read_graph.parse_eq_classes(path), want)
     q = ingest.parse_eq(data)  # accepted by the C++ parser itself
     _eq_arrays_equal((q.names, q.cls_off, q.members, q.counts, q.pair_skip), want)
+    _eq_compact_matches(data, want)
     if raises is None:
         assert q.names == [n for n in g["out"]["nodes"][:len(q.names)]]
 
@@ -153,6 +170,29 @@ def test_eq_random_vs_oracle(tmp_path, seed):
     want = oracle.parse_eq_file(path)
     q = ingest.parse_eq(data, threads=1 + seed % 8)
     _eq_arrays_equal((q.names, q.cls_off, q.members, q.counts, q.pair_skip), want)
+
+
+@pytest.mark.parametrize("big", [0, 127, 128])
+def test_eq_compact_form(tmp_path, big):
+    """The parser's compact form (karma_eq_get_compact): sizes with the size
+    token "1" in bit 7 and u32 counts, equal to the wide form's; a class of
+    128 members or a count past 2^32 - 1 falls back to the wide form."""
+    rng = random.Random(7 + big)
+    n = 300
+    lines = [str(n), "0"] + [f"t{i}" for i in range(n)]
+    for c in range(2000):
+        k = rng.randrange(1, 6)
+        ids = [str(rng.randrange(n)) for _ in range(k)]
+        size = "1" if rng.random() < 0.05 else str(k)
+        lines.append("\t".join([size] + ids + [str(rng.randrange(0, 4_000_000_000))]))
+    if big:
+        lines.append("\t".join([str(big)] + [str(rng.randrange(n)) for _ in range(big)] + ["3"]))
+    data = ("\n".join(lines) + "\n").encode()
+    path = _write(tmp_path, "eq.txt", data)
+    want = oracle.parse_eq_file(path)
+    assert _eq_compact_matches(data, want) == (big <= 127)
+    big_count = data.replace(b"\t3\n", b"\t4294967296\n") if big else data + b"1\t0\t4294967296\n"
+    assert not _eq_compact_matches(big_count, oracle.parse_eq_file(_write(tmp_path, "eq2.txt", big_count)))
 
 
 def test_eq_threads_large():

@@ -55,6 +55,14 @@ def main():
     out["whole_ms"] = best(whole, a.reps)
     out["whole_ordered_ms"] = best(lambda: engine.graph_from_eq_ordered(cls_off, members, counts, skip, n, ctx=ctx),
                                    a.reps)
+    cq = engine.eq_compact(cls_off, counts, skip)
+    c_sz, c_mem, c_cnt = (_lib.pinned_empty(len(x), x.dtype) for x in (cq[0], members, cq[1]))
+    c_sz[:], c_mem[:], c_cnt[:] = cq[0], members, cq[1]
+    out["compact_h2d_bytes"] = int(c_sz.nbytes + c_mem.nbytes + c_cnt.nbytes)
+    out["whole_compact_pinned_ms"] = best(
+        lambda: engine.graph_from_eq_compact_ordered(c_sz, c_mem, c_cnt, n, ctx=ctx), a.reps)
+    out["whole_compact_pageable_ms"] = best(
+        lambda: engine.graph_from_eq_compact_ordered(cq[0], members, cq[1], n, ctx=ctx), a.reps)
 
     def from_eq():
         p = engine.Pairs.from_eq(ctx, cls_off, members, counts, skip, n)
@@ -101,7 +109,7 @@ def main():
     out["d2h_pinned_ms"] = best(d2h_pinned, a.reps)
     ctx.timing(True)
     ctx.timing_reset()
-    whole()
+    engine.graph_from_eq_compact_ordered(c_sz, c_mem, c_cnt, n, ctx=ctx)
     out["kernels_ms"] = {k: round(ms, 4) for k, (ms, nl) in sorted(ctx.timing_read().items())}
     ctx.timing(False)
     print(json.dumps(out))
