@@ -254,9 +254,10 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
                    const uint8_t* pair_skip, int64_t n_classes, int64_t n_contigs, int is_device, karma_pairs** out);
 /* karma_graph_eq from compact host inputs (10 bytes per class fewer over PCIe):
  * sizes[C] = member count (<= 127) | 0x80 when the class's eq_size token is
- * "1" (pair_skip), counts[C] as u32.  Same pairs, firsts and totals. */
-int karma_graph_eq_compact(karma_ctx* ctx, const uint8_t* sizes, const uint32_t* members, const uint32_t* counts,
-                           int64_t C, int64_t n_contigs, karma_pairs** out);
+ * "1" (pair_skip), counts[C] as u32; n_members = the sizes' sum (KARMA_ERR_ARG
+ * when they disagree, checked on the device).  Same pairs, firsts and totals. */
+int karma_graph_eq_compact(karma_ctx* ctx, const uint8_t* sizes, const uint32_t* members, int64_t n_members,
+                           const uint32_t* counts, int64_t C, int64_t n_contigs, karma_pairs** out);
 /* Merge (key, count) lists in any order into one sorted unique list (exchange merge). */
 int karma_pairs_merge(karma_ctx* ctx, const uint64_t* keys, const int64_t* counts, int64_t n, int is_device,
                       karma_pairs** out);

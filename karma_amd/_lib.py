@@ -111,7 +111,7 @@ _SIGS = {
     "karma_graph_records_end": [_c_p, _PP],
     "karma_graph_split_hint": [_c_p, _c_p, _i32],
     "karma_graph_eq": [_c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i64, _i32, _PP],
-    "karma_graph_eq_compact": [_c_p, _c_p, _c_p, _c_p, _i64, _i64, _PP],
+    "karma_graph_eq_compact": [_c_p, _c_p, _c_p, _i64, _c_p, _i64, _i64, _PP],
     "karma_pairs_merge": [_c_p, _c_p, _c_p, _i64, _i32, _PP],
     "karma_pairs_merge_runs": [_c_p, _c_p, _c_p, _c_p, _i32, _i32, _PP],
     "karma_pairs_merge_runs_kc": [_c_p, _c_p, _c_p, _i32, _PP],

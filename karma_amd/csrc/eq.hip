@@ -64,6 +64,7 @@ struct EqIn {
     const uint8_t* skip;
     int64_t C;
     uint32_t N;
+    int64_t n_mem;  // members readable: a class past it fails the call (bad |= 2), nothing reads beyond
 };
 
 // ---- 1. each pair's rank inside its lower contig's segment ------------------------
@@ -99,8 +100,15 @@ __global__ void __launch_bounds__(kEqT) eq_rank_kernel(EqIn in, const int64_t* _
                                                        uint32_t* __restrict__ segcnt, Pairs3 P3,
                                                        uint32_t* __restrict__ big, unsigned* __restrict__ n_big,
                                                        int* __restrict__ bad) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && in.off[in.C] != in.n_mem) atomicOr(bad, 2);
     for (int64_t c = (int64_t)blockIdx.x * kEqT + threadIdx.x; c < in.C; c += (int64_t)gridDim.x * kEqT) {
         const int64_t s = in.off[c], e = in.off[c + 1], m = e - s;
+        if (s < 0 || e < s || e > in.n_mem) {  // offsets past the members (or decreasing ones)
+            atomicOr(bad, 2);
+            // the class's pair slots as sentinels the placement skips (never left unwritten)
+            for (int64_t t = poff[c]; t < min(poff[c + 1], P3.cap); ++t) P3.rank[t] = ~0u;
+            continue;
+        }
         if (m < 2 || (in.skip && in.skip[c])) continue;
         if (m > kSmallM) {
             big[atomicAdd(n_big, 1u)] = (uint32_t)c;
@@ -134,6 +142,7 @@ __global__ void __launch_bounds__(kEqT) eq_rank_big_kernel(EqIn in, const int64_
 __global__ void __launch_bounds__(kEqT) eq_totals_kernel(EqIn in, int64_t n_mem,
                                                          unsigned long long* __restrict__ totals,
                                                          int* __restrict__ bad) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && in.off[in.C] != in.n_mem) atomicOr(bad, 2);
     for (int64_t j = (int64_t)blockIdx.x * kEqT + threadIdx.x; j < n_mem; j += (int64_t)gridDim.x * kEqT) {
         int64_t lo = 0, hi = in.C;  // the last class with off[c] <= j
         while (hi - lo > 1) {
@@ -509,7 +518,7 @@ int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members
         if (n_mem) KARMA_HIP(hipMemcpyAsync(d_mem.ptr, members, n_mem * 4, hipMemcpyHostToDevice, xs));
         KARMA_HIP(hipEventRecord(ev[2], xs));
     }
-    const EqIn in{off, mem, cnt, skip, C, (uint32_t)N};
+    const EqIn in{off, mem, cnt, skip, C, (uint32_t)N, n_mem};
     const int bg = std::max(1, ctx->cu_count);
     // the pair total sizes the scratch: the one readback before the end
     // (none when the previous call's total is taken as the capacity)
@@ -571,7 +580,7 @@ int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members
     {
         ctx->stream = xs;
         if (N) KARMA_HIP(hipMemsetAsync(p->totals.ptr, 0, N * 8, xs));
-        if (n_mem)
+        if (n_mem || compact)  // (compact: also checks the sizes' sum against n_mem)
             KARMA_LAUNCH(ctx, "eq_totals", eq_totals_kernel, grid_of(n_mem, kEqT), kEqT, 0, in, n_mem,
                          (unsigned long long*)p->totals.ptr, bad);
         ctx->stream = ms;
@@ -596,6 +605,8 @@ int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members
     *P_out = hp[0];
     KARMA_CHECK(hp[0] >= 0 && hp[0] < (int64_t(1) << 32), KARMA_ERR_ARG, "karma_graph_eq: %lld pairs exceed 2^32",
                 (long long)hp[0]);
+    KARMA_CHECK(!((int)hp[2] & 2), KARMA_ERR_ARG, "eq class offsets / sizes disagree with the member count (%lld)",
+                (long long)n_mem);
     KARMA_CHECK(!(int)hp[2], KARMA_ERR_ARG, "eq class member index >= n_contigs");
     if (spec && hp[0] > cap) return KARMA_OK;  // *out untouched: run again, sized
     p->n = hp[1];
@@ -623,17 +634,17 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
     return KARMA_OK;
 }
 
-int karma_graph_eq_compact(karma_ctx* ctx, const uint8_t* sizes, const uint32_t* members, const uint32_t* counts,
-                           int64_t C, int64_t N, karma_pairs** out) {
+int karma_graph_eq_compact(karma_ctx* ctx, const uint8_t* sizes, const uint32_t* members, int64_t n_members,
+                           const uint32_t* counts, int64_t C, int64_t N, karma_pairs** out) {
     KARMA_TRY(ctx_begin(ctx));
-    KARMA_CHECK(out && (sizes || C == 0) && (counts || C == 0) && C >= 0 && N >= 0 && N < (int64_t(1) << 32),
+    KARMA_CHECK(out && (sizes || C == 0) && (counts || C == 0) && (members || n_members == 0) && C >= 0 &&
+                    n_members >= 0 && N >= 0 && N < (int64_t(1) << 32),
                 KARMA_ERR_ARG, "karma_graph_eq_compact: bad arguments");
     EqCompact cq;
     static const uint8_t none = 0;
     cq.sizes = C ? sizes : &none;
     cq.counts32 = counts;
-    for (int64_t c = 0; c < C; ++c) cq.n_mem += sizes[c] & 0x7F;  // sizes the members' copy (host side)
-    KARMA_CHECK(cq.n_mem == 0 || members, KARMA_ERR_ARG, "karma_graph_eq_compact: no members");
+    cq.n_mem = n_members;  // the sizes' sum is checked on the device (eq_rank)
     const int64_t cap = ctx->eq_pair_cap;
     int64_t P = 0;
     *out = nullptr;

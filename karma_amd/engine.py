@@ -384,8 +384,8 @@ class Pairs:
         members = np.ascontiguousarray(members, np.uint32)
         counts32 = np.ascontiguousarray(counts32, np.uint32)
         call("karma_graph_eq_compact", ctx.h, ptr(sizes) if len(sizes) else None,
-             ptr(members) if len(members) else None, ptr(counts32) if len(counts32) else None, len(sizes),
-             n_contigs, ctypes.byref(h))
+             ptr(members) if len(members) else None, len(members), ptr(counts32) if len(counts32) else None,
+             len(sizes), n_contigs, ctypes.byref(h))
         return cls(ctx, h)
 
     @classmethod

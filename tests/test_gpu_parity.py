@@ -365,6 +365,17 @@ def test_eq_compact_inputs_match_wide():
     with pytest.raises(_lib.KarmaError) as ei:
         engine.graph_from_eq_compact_ordered(sz, m2, c32, n)
     assert ei.value.code == _lib.KARMA_ERR_ARG, str(ei.value)
+    # sizes that disagree with the members' length: an error, no read past them
+    for short in (mem[:-5], mem[:10]):
+        with pytest.raises(_lib.KarmaError) as ei:
+            engine.graph_from_eq_compact_ordered(sz, short, c32, n)
+        assert ei.value.code == _lib.KARMA_ERR_ARG and "disagree" in str(ei.value), str(ei.value)
+    one = np.array([1, 1, 1], np.uint8)  # three single-member classes, two members given (no pairs)
+    with pytest.raises(_lib.KarmaError) as ei:
+        engine.graph_from_eq_compact_ordered(one, np.array([3, 4], np.uint32), np.ones(3, np.uint32), n)
+    assert "disagree" in str(ei.value), str(ei.value)
+    a, _, _ = engine.graph_from_eq_compact_ordered(sz, mem, c32, n)  # the context still works
+    assert len(a) > 0
 
 
 def test_eq_big_classes_device_inputs_and_errors():
