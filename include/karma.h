@@ -356,10 +356,11 @@ typedef struct karma_step karma_step;
 #define KARMA_STEP_DEFER 4      /* outputs not read: the step returns without waiting for anything (its
                                  * checks arrive through mapped memory and are read <= 3 steps later; a
                                  * step needing the general path runs again synchronously).  Several ranks:
-                                 * once a synchronous step has sized the exchange's slots and the store is
-                                 * ACGT-only on every rank (else the step runs synchronously, its edge
-                                 * count not read back); the slow verdict is summed over the ranks, so all
-                                 * of them re-run the same steps.  Every rank must pass the same flags.
+                                 * with a side communicator, once a synchronous step has sized the
+                                 * exchange's slots and the store is ACGT-only on every rank (else the
+                                 * step runs synchronously, its edge count not read back); every rank
+                                 * learns every rank's re-run verdict from the exchange, so all of them
+                                 * re-run the same steps.  Every rank must pass the same flags.
                                  * Inputs must stay valid until the next non-deferred step or
                                  * karma_step_sync. */
 int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, int kmode, int64_t n_glob,

@@ -1221,7 +1221,8 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
     // deferred: one process (no collective needs a host count), nothing read back
     // several processes: once a synchronous step has sized the exchange's
     // slots and every rank's store is known to be ACGT-only
-    const bool ranks_ok = s->world == 1 || (s->defer_ranks && s->kc > 0 && s->acgt_store == store);
+    // (and with a side communicator: the main one's operations then stay on one stream)
+    const bool ranks_ok = s->world == 1 || (s->defer_ranks && s->scomm && s->kc > 0 && s->acgt_store == store);
     const bool defer = (flags & KARMA_STEP_DEFER) && !keep && ranks_ok && s->n_glob <= sets_max_contigs();
     int rc = KARMA_OK;
     if (defer && s->sticky_sync > 0) {
