@@ -110,7 +110,10 @@ int make_geo(int64_t N, Geo* g) {
     while ((int64_t(1) << bbits) < N) ++bbits;
     auto nb = [&](int w) { return (N + (int64_t(1) << w) - 1) >> w; };
     int bw = 4;
-    while (nb(bw) > 256 && bw < kMaxBwCompact) ++bw;
+#ifndef KARMA_GEO_B
+#define KARMA_GEO_B 256  // pair buckets aimed at (A/B builds: more, smaller buckets)
+#endif
+    while (nb(bw) > KARMA_GEO_B && bw < kMaxBwCompact) ++bw;
     while (nb(bw) > kMaxB) ++bw;
     KARMA_CHECK(bw + bbits <= 31, KARMA_ERR_ARG, "n_contigs too large for 32-bit pair keys");
     g->bw = bw;
