@@ -123,6 +123,13 @@ def test_config_eq_path_digests(gold, name):
     skip = (np.diff(cls_off) == 1).astype(np.uint8)
     e = engine.graph_from_eq(cls_off, mem, cnt, skip, inp["n_glob"])
     assert edge_digest_of(e) == gold[name]["edges"]
+    # the drop-in's form: compact inputs, (a, b, w) in insertion order (by a,
+    # then first emission) -- the same edges, that order of the wide result
+    sz, c32 = engine.eq_compact(cls_off, cnt, skip)
+    a, b, w = engine.graph_from_eq_compact_ordered(sz, mem, c32, inp["n_glob"])
+    order = np.lexsort((e.first, e.a))
+    assert np.array_equal(a, e.a[order]) and np.array_equal(b, e.b[order])
+    assert np.array_equal(w.view(np.uint64), e.weight[order].view(np.uint64))
 
 
 def test_config3_shuffled_contig_ids(gold):
