@@ -2066,12 +2066,14 @@ int64_t chunk_records(const karma_ctx* ctx, int64_t A) {
     const int64_t slots = (int64_t)ctx->cu_count * 16;
     return ceil_div(A, kCChunk) < 4 * slots ? kCChunk / 2 : kCChunk;
 }
-int mark_at() {
-    static const int at = [] {
+// KARMA_MARK_AT in the environment wins; else the caller's choice
+// (ctx->mark_pos, the native step's deferred batches), else the default
+int mark_at(const karma_ctx* ctx) {
+    static const int env = [] {
         const char* e = std::getenv("KARMA_MARK_AT");
-        return e ? std::atoi(e) : KARMA_MARK_AT;
+        return e ? std::atoi(e) : -1;
     }();
-    return at;
+    return env >= 0 ? env : ctx->mark_pos >= 0 ? ctx->mark_pos : KARMA_MARK_AT;
 }
 struct SetsJob {
     karma_ctx* ctx = nullptr;
@@ -2216,7 +2218,7 @@ int SetsJob::launch() {
     const bool probe = A > 0 && !relabeled;  // the probe kernel clears the control block
     if (!probe) KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk + B) * 8, ctx->stream));
     if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
-    if (mark_at() == 3 && attempt == 0 && !relabeled) {  // side-stream work may start beside classify
+    if (mark_at(ctx) == 3 && attempt == 0 && !relabeled) {  // side-stream work may start beside classify
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
         KARMA_HIP(hipEventRecord(ctx->mark_ev, ctx->stream));
         ctx->mark_set = true;
@@ -2258,7 +2260,7 @@ int SetsJob::launch() {
     // 2 stretches the profile to 0.60 ms beside the reduce (1.43 vs 1.35);
     // 3 stretches classify 0.54 -> 0.74 ms (1.35 vs 1.25): HBM is already full
     auto mark = [&](int at) -> int {
-        if (mark_at() != at || attempt != 0) return KARMA_OK;
+        if (mark_at(ctx) != at || attempt != 0) return KARMA_OK;
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
         KARMA_HIP(hipEventRecord(ctx->mark_ev, ctx->stream));
         ctx->mark_set = true;

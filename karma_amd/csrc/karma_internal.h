@@ -90,6 +90,7 @@ struct karma_ctx {
     int side_headroom = 0;         // grid_headroom of karma_kmer_profile_side (karma_ctx_set_side_headroom)
     hipEvent_t mark_ev = nullptr;  // recorded by an open graph job after its classify kernel
     bool mark_set = false;
+    int mark_pos = -1;  // where an open graph job records mark_ev (SetsJob::launch); -1: the default
     int64_t* fin_pinned = nullptr;  // M of an in-flight karma_kmer_plan_finalize_async
     // mapped, coherent pinned host memory that kernels read and write directly
     // (one-launch consumers of small views: no copy launches)

@@ -200,6 +200,13 @@ __global__ void __launch_bounds__(kET) step_edge_write_kernel(
 // 5 dependent loads), stages the windows in LDS, and places every element at
 // its rank in its own run plus its rank in each other run (stable: equal keys
 // of different runs end up adjacent, in run order).
+#ifndef KARMA_MARK_ONE
+#define KARMA_MARK_ONE 2  // deferred batches on one main stream (SetsJob::launch positions)
+#endif
+#ifndef KARMA_MARK_TWO
+#define KARMA_MARK_TWO 5  // deferred batches alternating two main streams
+#endif
+constexpr int kMarkOne = KARMA_MARK_ONE, kMarkTwo = KARMA_MARK_TWO;
 constexpr int64_t kAltMaxRecords = int64_t(1) << 27;  // batches below this alternate main streams
 constexpr int kMT = 1024;       // tile elements (one round of tiles at the 8-rank preview's ~300k keys)
 constexpr int kMLds = 8192;     // staged window keys
@@ -1014,7 +1021,14 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // stream; kept on the main stream with two (see side_alt_s)
     ctx->no_fork = two && s->sides == 2;
     ctx->fork_use = two ? nullptr : s->alt_s;
+    // where the side stream's profile may start (SetsJob::launch): with one main
+    // stream, after the code partition -- the profile's writes then share HBM
+    // with the LDS-bound code reduce and final kernel instead of the next
+    // batch's classify (config 3: 1.15 against 1.20-1.22 ms per step,
+    // profiles/r04/ab_mark3/); with two, after the final kernel
+    ctx->mark_pos = two ? kMarkTwo : kMarkOne;
     const int jrc = sets_begin_deferred(ctx, reinterpret_cast<const uint2*>(rec), A, s->n_glob, &job, &v);
+    ctx->mark_pos = -1;
     ctx->no_fork = false;
     ctx->fork_use = nullptr;
     KARMA_TRY(jrc);
