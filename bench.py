@@ -361,9 +361,9 @@ def main():
             roof["solo_launch_ms"] = round(solo[0] / solo[1], 4)
             roof["solo_achieved"] = round(b / solo_s / 1e9, 1)
             roof["solo_frac"] = round(b / solo_s / 1e9 / PEAK_HBM_GBS, 4)
-            roof["note"] = ("achieved/frac: live launches of the timed stream (deferred batches overlap: this kernel "
-                            "shares HBM with the previous batch's profile); solo_*: the sequential pass, alone on "
-                            "the chip")
+            roof["note"] = ("achieved/frac: live launches of the timed stream (deferred batches overlap: beside the "
+                            "other stream's batch with two main streams, beside nothing of the profile with one); "
+                            "solo_*: the sequential pass, alone on the chip")
     write_ceiling = profile_write_ceiling(ctx, leg, n_loc, M, kern, args.steps)
     step_bytes = leg.packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
     host_us, api_calls = leg.host_us_per_step, leg.api_calls_per_step
