@@ -1195,8 +1195,10 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     // blocks dispatch first when CUs free up beside the side-stream profile
     KARMA_HIP(hipStreamCreateWithPriority(&s->main_s, hipStreamNonBlocking, hi));
     KARMA_HIP(hipStreamCreateWithPriority(&s->alt_s, hipStreamNonBlocking, hi));
-    KARMA_HIP(hipStreamCreateWithPriority(&s->side_s, hipStreamNonBlocking, 0));
-    KARMA_HIP(hipStreamCreateWithPriority(&s->side_alt_s, hipStreamNonBlocking, 0));
+    // KARMA_STEP_SIDE_PRIO=1 (A/B): the side streams at the main streams' priority
+    const int side_prio = getenv("KARMA_STEP_SIDE_PRIO") && atoi(getenv("KARMA_STEP_SIDE_PRIO")) ? hi : 0;
+    KARMA_HIP(hipStreamCreateWithPriority(&s->side_s, hipStreamNonBlocking, side_prio));
+    KARMA_HIP(hipStreamCreateWithPriority(&s->side_alt_s, hipStreamNonBlocking, side_prio));
     void *hm = nullptr, *dm = nullptr;
     KARMA_TRY(ctx_mapped(ctx, kMapStep, kRing * sizeof(StepStatus) + kRing * 8, &hm, &dm));
     s->mring_h = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(hm) + kRing * sizeof(StepStatus));
