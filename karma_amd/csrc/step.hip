@@ -1050,7 +1050,14 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
         rc = hipStreamWaitEvent(side, ctx->mark_ev, 0) == hipSuccess ? KARMA_OK : KARMA_ERR_HIP;
     }
-    if (!rc && s->n_loc) rc = kmer_profile_device_m(plan, tl.prof.ptr, m_dev);
+    if (!rc && s->n_loc) {
+        // KARMA_STEP_HEADROOM (A/B): profile blocks per CU left free for the
+        // main stream's kernels (one main stream only)
+        static const int headroom = getenv("KARMA_STEP_HEADROOM") ? atoi(getenv("KARMA_STEP_HEADROOM")) : 0;
+        ctx->grid_headroom = two || sequential ? 0 : headroom;
+        rc = kmer_profile_device_m(plan, tl.prof.ptr, m_dev);
+        ctx->grid_headroom = 0;
+    }
     if (!rc && !two && !sequential && s->join) {
         if (!s->ev && hipEventCreateWithFlags(&s->ev, hipEventDisableTiming) != hipSuccess) rc = KARMA_ERR_HIP;
         if (counted_call("hipEventRecord")) ++t_hip_calls;
