@@ -282,6 +282,9 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 #ifndef KARMA_CLS_STAGE
 #define KARMA_CLS_STAGE 0
 #endif
+#ifndef KARMA_CLS_DIRECT
+#define KARMA_CLS_DIRECT 0  // A/B: each lane loads its own 8 records (no LDS transpose)
+#endif
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
@@ -370,8 +373,26 @@ classify2_kernel(ClassArgs P) {
     }
 
     // records [t0, hi) of a step, coalesced: unit u of lane l = records t0 + 128u + 2l, + 1.
+    // (KARMA_CLS_DIRECT: unit u of lane l = records t0 + 8l + 2u, + 1 -- each
+    // lane its own 64 bytes, no LDS transpose.)
     // Past the chunk: read id kEmpty (a read of its own that is never emitted), contig 0.
     auto prefetch = [&](u32x4 (&dst)[kCPer], int64_t t0, int64_t hi) {
+#if KARMA_CLS_DIRECT
+        const int64_t gd = t0 + 8 * lane;
+        if (t0 + kCIter <= hi) {
+#pragma unroll
+            for (int u = 0; u < kCPer; ++u) dst[u] = *reinterpret_cast<const u32x4*>(P.rec + gd + 2 * u);
+        } else {
+#pragma unroll
+            for (int u = 0; u < kCPer; ++u) {
+                const int64_t gi = gd + 2 * u;
+                const uint2 r0 = gi < hi ? P.rec[gi] : make_uint2(kEmpty, 0u);
+                const uint2 r1 = gi + 1 < hi ? P.rec[gi + 1] : make_uint2(kEmpty, 0u);
+                dst[u] = u32x4{r0.x, r0.y, r1.x, r1.y};
+            }
+        }
+        return;
+#endif
         const int64_t gb = t0 + 2 * lane;
         if (t0 + kCIter <= hi) {
 #pragma unroll
@@ -418,6 +439,15 @@ classify2_kernel(ClassArgs P) {
         // a step emits <= kCIter codes, the chunk tail one more
         if (kStaged && ncs + kCIter + 1 > (uint32_t)kStage) flush_stage();
         uint32_t rid[8], ctg[8];
+#if KARMA_CLS_DIRECT
+#pragma unroll
+        for (int u = 0; u < kCPer; ++u) {
+            rid[2 * u] = buf[u].x;
+            ctg[2 * u] = buf[u].y;
+            rid[2 * u + 1] = buf[u].z;
+            ctg[2 * u + 1] = buf[u].w;
+        }
+#else
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
 #pragma unroll
         for (int u = 0; u < kCPer; ++u) {
@@ -434,6 +464,7 @@ classify2_kernel(ClassArgs P) {
             ctg[2 * u + 1] = q.w;
         }
         wave_sync();
+#endif
         if (REMAP) {
             if (t0 + kCIter < c_hi) remap_units(nxt);
             if (t0 + 2 * kCIter < c_hi) prefetch(buf, t0 + 2 * kCIter, c_hi);
