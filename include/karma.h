@@ -372,7 +372,9 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records_
 /* Waits for every enqueued step and checks the deferred ones. */
 int karma_step_sync(karma_step* s);
 /* [M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending, host ns inside
- * karma_step_run, of which ns waiting for a deferred step's status] (first n). */
+ * karma_step_run, of which ns waiting for a deferred step's status] (first n).  After
+ * karma_step_sync, M and E are the newest step's also when it was deferred (E: this rank's
+ * edges). */
 int karma_step_info(karma_step* s, int64_t* info, int n);
 /* Outputs (valid until the next run).  _profile: the newest step's profile
  * (device, rows x M dense f64; a deferred step's once karma_step_sync has read

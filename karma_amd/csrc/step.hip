@@ -1285,8 +1285,12 @@ int karma_step_sync(karma_step* s) {
     KARMA_HIP(hipStreamSynchronize(s->alt_s));
     KARMA_HIP(hipStreamSynchronize(s->main_s));
     KARMA_TRY(bury(s, true));
-    if (s->prof_seq)  // every stream is idle: the newest deferred step's column count has landed
+    if (s->prof_seq) {  // every stream is idle: the newest deferred step's column count has landed
         s->prof_M = __atomic_load_n(&s->mring_h[s->prof_seq % kRing], __ATOMIC_ACQUIRE);
+        // ... and its status: M and the local edge count read as of a synchronous step
+        s->M = s->prof_M;
+        s->E = const_cast<const StepStatus&>(s->ring_h[s->prof_seq % kRing]).E;
+    }
     if (s->edges && s->E < 0) KARMA_TRY(karma_edges_count(s->edges, &s->E));
     return KARMA_OK;
 }

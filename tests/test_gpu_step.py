@@ -101,6 +101,10 @@ def test_deferred_steps_then_kept_step_match_oracle(emulate, n_rate):
         assert np.array_equal(res["profile"].numpy().view(np.uint64), prof_o.view(np.uint64))
         check_edges(res["edges"], oracle_graph(rec, n))
         assert res["E_local"] == len(res["edges"].a)
+        # after sync, the newest deferred step's M and edge count (its status words)
+        assert int(info[0]) == len(cols_o)
+        if not emulate:
+            assert int(info[1]) == len(res["edges"].a), (info.tolist(), len(res["edges"].a))
     finally:
         r.close()
 
