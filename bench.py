@@ -85,6 +85,133 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class Watchdog:
+    """Ends the process (non-zero, without teardown) when no phase or step
+    has ticked for `limit` seconds: a rank whose peer stopped issuing
+    collectives would otherwise wait in a device synchronisation until the
+    driver's own timeout.  os._exit, because teardown would wait on the same
+    stalled streams."""
+
+    def __init__(self):
+        self.limit = float(os.environ.get("KARMA_BENCH_STALL_S", "300"))
+        self.what, self.t = "start", time.monotonic()
+        self.rank = 0
+        self._thread = None
+
+    def start(self, rank):
+        import threading
+
+        self.rank = rank
+        if self.limit > 0 and self._thread is None:
+            self._thread = threading.Thread(target=self._run, daemon=True, name="bench-watchdog")
+            self._thread.start()
+
+    def tick(self, what):
+        self.what, self.t = what, time.monotonic()
+
+    def _run(self):
+        while True:
+            time.sleep(min(5.0, self.limit / 4))
+            idle = time.monotonic() - self.t
+            if idle > self.limit:
+                log(f"bench.py: rank {self.rank} made no progress for {idle:.0f} s after '{self.what}' "
+                    f"(KARMA_BENCH_STALL_S={self.limit:g}); exiting without teardown")
+                os._exit(5)
+
+
+WATCHDOG = Watchdog()
+
+
+def stalled_exit(rank, err):
+    """A deferred step's status never arrived (KARMA_ERR_STALL: a peer's or the
+    device's collectives stalled): report it and leave at once -- destroying the
+    streams would wait on the stalled work."""
+    log(f"bench.py: rank {rank}: {err}")
+    os._exit(4)
+
+
+def visible_devices():
+    """HIP devices visible to a child process (this process must not touch HIP
+    before it starts the ranks: karma_device_count runs in a child)."""
+    import subprocess
+
+    code = ("import ctypes, sys; sys.path.insert(0, %r); from karma_amd import _lib; n = ctypes.c_int(0); "
+            "rc = _lib.load().karma_device_count(ctypes.byref(n)); print(n.value if rc == 0 else 0)" % REPO)
+    try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else 0
+    except (subprocess.TimeoutExpired, ValueError, OSError):
+        return 0
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_envs(n, port, base=None):
+    """The environment of each of n self-launched ranks (what torchrun would set)."""
+    base = dict(os.environ if base is None else base)
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), KARMA_BENCH_LAUNCHER="self")
+        out.append(e)
+    return out
+
+
+def launch_ranks(n, cmd, envs, poll=0.2):
+    """Start one child per rank (never exec: the parent stays a plain waiter),
+    wait for all; when one fails, stop the others (their exact PIDs) and
+    return its exit code.  Rank 0's stdout is the line (inherited)."""
+    import subprocess
+
+    procs = [subprocess.Popen(cmd, env=envs[r]) for r in range(n)]
+    rc = 0
+    try:
+        live = set(range(n))
+        while live:
+            for r in sorted(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c
+                    log(f"bench.py: rank {r} exited with {c}; stopping the other ranks")
+                    for q in live:
+                        procs[q].terminate()
+            time.sleep(poll)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc
+
+
+def self_launch(args):
+    """--gpus N > 1 with no launcher (WORLD_SIZE unset): start N rank
+    processes as torchrun would (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR
+    127.0.0.1, MASTER_PORT), one per device, and return the first failing
+    exit code (0 when all succeed).  Fewer visible devices than N is an error,
+    unless KARMA_FORCE_DEVICE pins every rank to one device (the host-staged
+    rehearsal on a one-GPU box: KARMA_DIST_BACKEND=host)."""
+    n = args.gpus
+    if os.environ.get("KARMA_FORCE_DEVICE") is None:
+        nd = visible_devices()
+        if nd < n:
+            log(f"bench.py: --gpus {n} but {nd} HIP device(s) visible; refusing to report an {n}-GPU line")
+            return 2
+    log(f"bench.py: launching {n} ranks (no WORLD_SIZE in the environment)")
+    return launch_ranks(n, [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:],
+                        rank_envs(n, free_port()))
+
+
 def shard(total, world, rank):
     return total * rank // world, total * (rank + 1) // world
 
@@ -128,6 +255,7 @@ class Leg:
         t_gen = time.time()
         self.args, self.comm, self.rank, self.world = args, comm, rank, world
         self.inp = inp = make_inputs(args, rank, world)
+        WATCHDOG.tick("inputs generated")
         self.A = len(inp["rec"])
         log(f"[rank {rank}] {'strong' if args.strong else 'weak'}: generated {inp['n_loc']} contigs "
             f"({int(inp['offs'][-1])} bases), {inp['f_loc']} fragments, {self.A} records in "
@@ -151,9 +279,11 @@ class Leg:
         barrier + device sync; returns (max-over-ranks seconds, last result,
         per-kernel totals, dominant kernel, its live (ms, launches))."""
         comm = self.comm
-        for _ in range(warmup):
+        for i in range(warmup):
             self.step()
+            WATCHDOG.tick(f"warmup step {i}")
         self.sync_all()
+        WATCHDOG.tick("warmup synced")
         # Per-kernel breakdown, outside the timed region, with every launch timed
         # and the profile on the main stream (sequential): kernels do not share the
         # chip, so no launch is charged for time it spent queued behind another.
@@ -165,6 +295,7 @@ class Leg:
             for _ in range(steps):  # the same kernels as the timed steps (deferred where they are)
                 self.step(sequential=True, count=False)
             self.sync_all()
+            WATCHDOG.tick("per-kernel pass")
             for c in self.ctxs:
                 for name, (ms, nl) in c.timing_read().items():
                     prev = kern.get(name, (0.0, 0))
@@ -200,9 +331,15 @@ class Leg:
             h0 = time.perf_counter()
             res = self.step(count=i == steps - 1 and not native)
             host += time.perf_counter() - h0
+            WATCHDOG.tick(f"timed step {i}")
+        info_loop = self.build.native.info() if self.build.native is not None else None
+        d0 = time.perf_counter()
         self.sync_all()
         comm.barrier()
         t1 = time.perf_counter()
+        # the drain after the loop (every step still in flight, its checks, the
+        # barrier): part of the timed region, not of the step calls
+        self.drain_us = (t1 - d0) * 1e6
         if native:
             info = self.build.native.info()
             res = dict(res, M=int(info[0]), E_local=int(info[1]))
@@ -211,9 +348,12 @@ class Leg:
         self.api_calls_per_step = (_lib.api_calls() - calls0) / steps
         self.step_info = self.build.native.info().tolist() if self.build.native is not None else None
         # of the host time inside the step calls: waiting for the device (a
-        # deferred step's status kLag steps back) vs enqueueing the step
-        self.host_wait_us_per_step = ((self.step_info[9] - int(info0[9])) / steps / 1e3
+        # deferred step's status kLag steps back) vs enqueueing the step; the
+        # drain's waits (karma_step_sync after the loop) are reported apart
+        self.host_wait_us_per_step = ((int(info_loop[9]) - int(info0[9])) / steps / 1e3
                                       if info0 is not None else None)
+        self.drain_wait_us = (self.step_info[9] - int(info_loop[9])) / 1e3 if info0 is not None else None
+        self.step_mode = self.build.native.mode() if self.build.native is not None else None
         dom_live = None
         if dom:
             for c in self.ctxs:
@@ -307,12 +447,33 @@ def parity_check(leg, key):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args)  # before anything here touches HIP
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    launcher = os.environ.get("KARMA_BENCH_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ else
+                              ("env" if "WORLD_SIZE" in os.environ else "none"))
+    WATCHDOG.start(rank)
+    from karma_amd import _lib
 
+    try:
+        return run(args, rank, world, local_rank, launcher)
+    except _lib.KarmaError as e:
+        if e.code == _lib.KARMA_ERR_STALL:
+            stalled_exit(rank, e)
+        if world > 1:  # a failed rank leaves its peers inside collectives: no teardown
+            import traceback
+
+            traceback.print_exc()
+            log(f"bench.py: rank {rank} failed; exiting without teardown")
+            os._exit(1)
+        raise
+
+
+def run(args, rank, world, local_rank, launcher):
     from karma_amd import _lib, comm as comm_mod
 
     # KARMA_FORCE_DEVICE pins every rank to one device (multi-rank rehearsal on
@@ -320,12 +481,19 @@ def main():
     dev_index = int(os.environ.get("KARMA_FORCE_DEVICE", local_rank if world > 1 else 0))
     ctx = _lib.Context(dev_index)
     comm = comm_mod.create(ctx, world, rank)
+    WATCHDOG.tick("communicator")
+    # what joined: the processes (a host-side sum) and, for RCCL, the
+    # communicator's own size as RCCL reports it
+    transport = {"launcher": launcher, "backend": type(comm).__name__,
+                 "ranks_joined": comm.sum_int(1) if world > 1 else 1,
+                 "rccl_ranks": comm.info()[0] if hasattr(comm, "info") else None}
     build_info = _lib.build_info()
     if build_info.get("defines") and not os.environ.get("KARMA_ALLOW_VARIANT"):
         raise SystemExit(f"bench.py: libkarma_hip.so was built with non-default defines {build_info['defines']}; "
                          f"rebuild with `make -C karma_amd/csrc` (KARMA_ALLOW_VARIANT=1 to time a variant)")
 
     leg = Leg(args, ctx, comm, rank, world)
+    WATCHDOG.tick("inputs resident")
     inp, A = leg.inp, leg.A
     n_loc, f_loc = inp["n_loc"], inp["f_loc"]
     dt, res, kern, dom, dom_live = leg.timed(args.steps, args.warmup, not args.no_timing)
@@ -377,20 +545,28 @@ def main():
     si = leg.step_info
     step_driver = ({"native": True, "deferred_steps": si[5], "synchronous_steps": si[4], "rerun_steps": si[6],
                     "host_wait_us_per_step": round(leg.host_wait_us_per_step, 1),
+                    "drain_us": round(leg.drain_us, 1), "drain_wait_us": round(leg.drain_wait_us, 1),
+                    "mode": leg.step_mode,
                     "note": "karma_step (csrc/step.hip): one C ABI call per step; host_us_per_step is the time "
                             "inside those calls (host_wait_us_per_step of it waiting for the device: the status "
-                            "of the step kLag = 3 back), api_calls_per_step the HIP/RCCL calls they made"}
+                            "of the step kLag = 3 back), api_calls_per_step the HIP/RCCL calls they made; "
+                            "drain_us: the sync + barrier after the last step call (inside the timed region), "
+                            "drain_wait_us of it waiting for deferred statuses"}
                    if si else {"native": False})
     step_s = dt / args.steps
+    WATCHDOG.tick("timed loop done")
     parity = None
     if not args.no_parity:
         parity = parity_check(leg, digest_key(args, world, inp["emu"]))
+        WATCHDOG.tick("parity")
     extra = {}
     if rank == 0 and world == 1 and not args.no_e2e and inp["emu"] == 1 and not args.shuffle_contigs:
         extra = end_to_end_legs(args, inp, ctx, leg.build, leg.store)
+        WATCHDOG.tick("end-to-end legs")
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline != "off":
         cpu = cpu_baseline(inp)
+        WATCHDOG.tick("cpu baseline")
     leg.close()
     del leg
 
@@ -419,6 +595,7 @@ def main():
             "value": round(value, 1),
             "unit": "(contigs+fragments)/s",
             "n_gpus": world,
+            "transport": transport,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(step_s * 1e3, 3),
@@ -458,6 +635,7 @@ def main():
         print(json.dumps(line), flush=True)
     comm.close()
     ctx.close()
+    return 0
 
 
 def profile_write_ceiling(ctx, leg, n_loc, M, kern, steps):
@@ -489,10 +667,11 @@ def profile_write_ceiling(ctx, leg, n_loc, M, kern, steps):
 
 def reference_measured(config):
     """The reference Python timed on this exact workload in the build container
-    (tests/golden/time_reference.py -> profiles/r03/reference_<config>.json):
-    read_fasta_file + __calc_kmer_profile + from_equivalence_classes."""
+    (tests/golden/time_reference.py -> tests/golden/reference_<config>.json,
+    which ships to the GPU box): read_fasta_file + __calc_kmer_profile +
+    from_equivalence_classes."""
     try:
-        with open(os.path.join(REPO, "profiles", "r03", f"reference_{config}.json")) as f:
+        with open(os.path.join(REPO, "tests", "golden", f"reference_{config}.json")) as f:
             r = json.load(f)
     except (OSError, ValueError):
         return None
@@ -501,7 +680,7 @@ def reference_measured(config):
     return {"units_per_s": r["units_per_s"], "seconds": r["total_s"],
             "split_s": {k: r[k] for k in ("read_fasta_file_s", "calc_kmer_profile_s", "from_equivalence_classes_s")},
             "threads": r["threads"], "host": "build container (8 vCPU Xeon), not the GPU box",
-            "source": f"profiles/r03/reference_{config}.json"}
+            "source": f"tests/golden/reference_{config}.json"}
 
 
 def pmc_traffic(args, world, kernel):
@@ -712,4 +891,4 @@ def cpu_baseline(inp):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -51,6 +51,7 @@ extern "C" {
 #define KARMA_ERR_STATE (-7)     /* call out of order (e.g. profile before finalize)          */
 #define KARMA_ERR_PARSE (-8)     /* input text outside what the C++ parser reproduces exactly */
 #define KARMA_ERR_COMM (-9)      /* RCCL communicator error                                   */
+#define KARMA_ERR_STALL (-10)    /* a deferred step's status did not arrive (stalled peer/device) */
 
 #define KARMA_KMER_5P6 (-1) /* kmer.py:69 "5p6": all 5-mers + string-palindromic 6-mers */
 
@@ -342,8 +343,10 @@ int karma_edges_get_ordered(karma_edges* e, uint32_t* a, uint32_t* b, double* w,
  * owner's merge and the edge stage around the totals all-gather.  Replaces the
  * Python per-step sequence of karma_amd/distributed.py (which stays for the
  * host-staged rehearsal transport).
- * comm: the main-stream communicator (NULL or world 1: one process);
- * side_comm: the column-set exchange's communicator (KARMA_COMM_SIDE; NULL: comm).
+ * comm: the communicator (NULL or world 1: one process); by default every
+ * collective of a step goes to it on ONE stream, in the same order on every rank.
+ * side_comm: NULL (or comm) for that default; a distinct KARMA_COMM_SIDE
+ * communicator puts the column-set exchange on it, on the side stream.
  * bounds[nranks + 1]: owner contig ranges tiling [0, n_glob); this rank's store
  * holds [bounds[rank], bounds[rank + 1]) (nranks = 1: any shard of the n_glob
  * contig ids, no exchange).  One process with nranks > 1 emulates
@@ -355,8 +358,9 @@ typedef struct karma_step karma_step;
 #define KARMA_STEP_SEQUENTIAL 2 /* every kernel on the main stream (per-kernel timing) */
 #define KARMA_STEP_DEFER 4      /* outputs not read: the step returns without waiting for anything (its
                                  * checks arrive through mapped memory and are read <= 3 steps later; a
-                                 * step needing the general path runs again synchronously).  Several ranks:
-                                 * with a side communicator, once a synchronous step has sized the
+                                 * step needing the general path runs again synchronously; a status later
+                                 * than KARMA_STEP_STALL_S seconds (120) is KARMA_ERR_STALL).  Several ranks:
+                                 * once a synchronous step has sized the
                                  * exchange's slots and the store is ACGT-only on every rank (else the
                                  * step runs synchronously, its edge count not read back); every rank
                                  * learns every rank's re-run verdict from the exchange, so all of them
@@ -372,7 +376,9 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records_
 /* Waits for every enqueued step and checks the deferred ones. */
 int karma_step_sync(karma_step* s);
 /* [M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending, host ns inside
- * karma_step_run, of which ns waiting for a deferred step's status] (first n).  After
+ * karma_step_run, of which ns waiting for a deferred step's status, deferred steps on two main
+ * streams, deferred steps whose tail ran on the exchange stream, mode bits (1 one communicator,
+ * 2 exchange stream allowed, 4 deferral across ranks allowed), ranks] (first n).  After
  * karma_step_sync, M and E are the newest step's also when it was deferred (E: this rank's
  * edges). */
 int karma_step_info(karma_step* s, int64_t* info, int n);

@@ -27,6 +27,7 @@ KARMA_ERR_UNSORTED = -6
 KARMA_ERR_STATE = -7
 KARMA_ERR_PARSE = -8
 KARMA_ERR_COMM = -9
+KARMA_ERR_STALL = -10
 
 KARMA_DT_U8, KARMA_DT_I32, KARMA_DT_I64, KARMA_DT_U64, KARMA_DT_F64 = 0, 1, 2, 3, 4
 KARMA_OP_SUM, KARMA_OP_MAX, KARMA_OP_MIN = 0, 1, 2

@@ -143,13 +143,16 @@ class HostComm:
 class RcclComm:
     """The library's RCCL communicator on one device (karma_comm_*).
 
-    With several ranks it holds two communicators over the same ranks: this
-    one for the main stream and `side` (KARMA_COMM_SIDE, its own unique id) for
-    the column set's exchange on the side stream.  One communicator's
-    operations must be issued in the same order on every rank; with one per
-    stream, how the two streams interleave on a rank cannot matter."""
+    One communicator by default: the native step (csrc/step.hip) issues every
+    collective of a step on one stream in the same order on every rank, so no
+    two collectives are ever in flight at once.  with_side=True (or
+    KARMA_STEP_SIDE_COMM=1) adds a second communicator over the same ranks,
+    `side` (KARMA_COMM_SIDE, its own unique id), for the column set's exchange
+    on the side stream beside the main one's operations (round 4's mode)."""
 
-    def __init__(self, group, ctx, with_side=True):
+    def __init__(self, group, ctx, with_side=None):
+        if with_side is None:
+            with_side = os.environ.get("KARMA_STEP_SIDE_COMM", "0") == "1"
         self.group, self.world, self.rank, self.ctx = group, group.world, group.rank, ctx
         lib = _lib.load()
         nb = lib.karma_comm_id_bytes()
@@ -173,6 +176,12 @@ class RcclComm:
         call("karma_comm_create_ex", self.ctx.h, ptr(np.ascontiguousarray(uid)), self.world, self.rank, flags,
              ctypes.byref(h))
         return h
+
+    def info(self):
+        """(ranks, rank) as the RCCL communicator itself reports them."""
+        w, r = ctypes.c_int(0), ctypes.c_int(0)
+        call("karma_comm_info", self.h, ctypes.byref(w), ctypes.byref(r))
+        return w.value, r.value
 
     # -- host scalars --
     def _reduce_host(self, arr, op):

@@ -616,6 +616,11 @@ int graph_eq_run(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members
 
 }  // namespace
 
+// The next call's speculative pair capacity: this call's total + 1/8, not the
+// largest ever seen (one large call would otherwise size -- and launch -- every
+// later small call's scratch at its size).
+static int64_t eq_next_cap(int64_t P) { return P + P / 8; }
+
 extern "C" {
 
 int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* members, const int64_t* counts,
@@ -623,14 +628,14 @@ int karma_graph_eq(karma_ctx* ctx, const int64_t* cls_off, const uint32_t* membe
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(out && cls_off && C >= 0 && N >= 0 && N < (int64_t(1) << 32), KARMA_ERR_ARG,
                 "karma_graph_eq: bad arguments");
-    // the previous call's pair total as the scratch capacity: a stream of
-    // similar calls never waits for the pair total
+    // the previous call's pair total (+ 1/8) as the scratch capacity: a
+    // stream of similar calls never waits for the pair total
     const int64_t cap = ctx->eq_pair_cap;
     int64_t P = 0;
     *out = nullptr;
     KARMA_TRY(graph_eq_run(ctx, cls_off, members, counts, pair_skip, C, N, is_device, cap, &P, out));
     if (!*out) KARMA_TRY(graph_eq_run(ctx, cls_off, members, counts, pair_skip, C, N, is_device, 0, &P, out));
-    ctx->eq_pair_cap = std::max(cap, P);
+    ctx->eq_pair_cap = eq_next_cap(P);
     return KARMA_OK;
 }
 
@@ -650,7 +655,7 @@ int karma_graph_eq_compact(karma_ctx* ctx, const uint8_t* sizes, const uint32_t*
     *out = nullptr;
     KARMA_TRY(graph_eq_run(ctx, nullptr, members, nullptr, nullptr, C, N, 0, cap, &P, out, cq));
     if (!*out) KARMA_TRY(graph_eq_run(ctx, nullptr, members, nullptr, nullptr, C, N, 0, 0, &P, out, cq));
-    ctx->eq_pair_cap = std::max(cap, P);
+    ctx->eq_pair_cap = eq_next_cap(P);
     return KARMA_OK;
 }
 

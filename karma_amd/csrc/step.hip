@@ -564,7 +564,7 @@ struct karma_step {
     };
     std::deque<Pending> pending;
     uint64_t seq = 0;
-    StepStatus* ring_h = nullptr;  // mapped host memory (kMapStep): per step its status words ...
+    StepStatus* ring_h = nullptr;  // mapped host memory (ring_mem): per step its status words ...
     StepStatus* ring_d = nullptr;
     int64_t* mring_h = nullptr;    // ... and its column count, written by its column table
     int64_t* mring_d = nullptr;
@@ -632,6 +632,21 @@ struct karma_step {
     hipEvent_t ev_rec = nullptr, ev_sync = nullptr, ev_tail[2] = {};
     bool tail_set[2] = {}, sync_set = false;
     int tail_last = -1;
+    // One communicator (no distinct side communicator passed, the default):
+    // every collective of a step -- the presence all-gather included -- is
+    // issued on ONE stream in the same order on every rank: the exchange
+    // stream for deferred steps, and a synchronous step's side-stream column
+    // exchange only after every earlier collective has completed.  No two
+    // collectives are ever in flight at once, the usage RCCL guarantees to be
+    // deadlock-free.  With a distinct side communicator (KARMA_STEP_SIDE_COMM=1
+    // in karma_amd/comm.py) the presence all-gather runs on the side stream
+    // beside the main communicator's operations (round 4's mode).
+    bool one_comm = true;
+    hipEvent_t ev_pres = nullptr, ev_pres2 = nullptr, ev_pre = nullptr;
+    // deferred steps by mode (karma_step_info): two main streams, tail on the exchange stream
+    int64_t n_two = 0, n_xs = 0;
+    int stall_s = 120;             // KARMA_STEP_STALL_S: a deferred status this late is KARMA_ERR_STALL
+    void* ring_mem = nullptr;      // this step's own mapped status ring (two steps on one context never share it)
 };
 
 namespace {
@@ -806,6 +821,13 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
         if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
         KARMA_HIP(hipStreamWaitEvent(s->main_s, s->ev_tail[s->tail_last], 0));
     }
+    if (s->world > 1 && s->one_comm && !sequential) {
+        // the column exchange below (side stream, the one communicator) after
+        // every collective issued so far: the main stream's (an earlier
+        // synchronous step's totals all-gather) and, through the wait above,
+        // the exchange stream's
+        KARMA_TRY(stream_after(&s->ev_pre, s->main_s, s->side_s));
+    }
     if (s->exchange) KARMA_TRY(karma_graph_split_hint(ctx, s->bounds.data(), s->nranks));
     int64_t M = 0;
     if (!sequential) {
@@ -930,7 +952,9 @@ bool entry_done(const karma_step* s, uint64_t seq) {
 
 // Checks deferred steps: every finished one (wait = false), or all of them
 // after waiting (wait = true), or down to kLag - 1 outstanding (lag = true).
-// A step whose words call for the general path runs again synchronously.
+// A step whose words call for the general path runs again synchronously;
+// the newest deferred step's profile, M and E stay the ones karma_step_sync
+// and karma_step_profile report (a re-run of an older step does not replace them).
 int drain(karma_step* s, bool wait, bool lag) {
     while (!s->pending.empty()) {
         karma_step::Pending p = s->pending.front();
@@ -950,12 +974,15 @@ int drain(karma_step* s, bool wait, bool lag) {
                     set_error("karma_step: a deferred step's status never arrived");
                     return KARMA_ERR_STATE;
                 }
-                // a step takes milliseconds: two minutes means a peer that
+                // a step takes milliseconds: this long means a peer that
                 // stopped issuing collectives; an error beats a silent hang
-                if (spin % 65536 == 65535 && std::chrono::steady_clock::now() - w0 > std::chrono::seconds(120)) {
-                    set_error("karma_step: a deferred step's status did not arrive within 120 s (%s)",
-                              s->world > 1 ? "a rank's collectives stalled?" : "device stalled?");
-                    return KARMA_ERR_STATE;
+                if (spin % 65536 == 65535 && std::chrono::steady_clock::now() - w0 > std::chrono::seconds(s->stall_s)) {
+                    set_error("karma_step: deferred step %llu's status did not arrive within %d s (rank %d of %d; %s)",
+                              (unsigned long long)p.seq, s->stall_s, s->rank, s->world,
+                              s->world == 1 ? "one process: device stalled?"
+                              : s->one_comm ? "collectives of the main communicator on the exchange stream stalled"
+                                            : "collectives of the main or side communicator stalled");
+                    return KARMA_ERR_STALL;
                 }
             }
             s->wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0)
@@ -969,7 +996,16 @@ int drain(karma_step* s, bool wait, bool lag) {
             // an overflowed bucket): the step's work again, synchronously
             ++s->n_redone;
             s->sticky_sync = 8;
+            const uint64_t newest = s->prof_seq;
+            const int newest_par = s->prof_par;
+            const int64_t newest_M = s->prof_M;
             KARMA_TRY(run_sync(s, p.store, p.rec, p.A, false, false, true));
+            if (newest > p.seq) {  // a newer deferred step is pending: its outputs stay the newest
+                s->prof_seq = newest;
+                s->prof_par = newest_par;
+                s->prof_M = newest_M;
+                s->M = s->E = -1;
+            }
         }
     }
     return KARMA_OK;
@@ -989,7 +1025,12 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // (the main communicator's operations then all go to side_alt_s)
     const bool two = (s->world == 1 || (s->xstream && !sequential)) &&
                      (s->streams ? s->streams == 2 : A < kAltMaxRecords);
-    const bool xs_on = s->world > 1 && two;
+    // the exchange stream carries the tail: with two main streams, and with
+    // one communicator also behind one main stream (it then holds every
+    // collective of the step, the presence all-gather included)
+    const bool xs_on = s->world > 1 && !sequential && s->xstream && (two || s->one_comm);
+    if (two) ++s->n_two;
+    if (xs_on) ++s->n_xs;
     const int par = sequential || !two ? 0 : (int)(seq & 1);
     hipStream_t const ms = par ? s->alt_s : s->main_s;
     hipStream_t const xs = s->side_alt_s;
@@ -1040,7 +1081,25 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     ctx->stream = side;
     karma_kmer_plan* plan = nullptr;
     int rc = karma_kmer_plan_create(ctx, store, s->kmode, &plan);
-    if (!rc && s->world > 1) rc = exchange_presence(s, plan, s->scomm ? s->scomm : s->comm);
+    if (!rc && s->world > 1) {
+        if (xs_on && s->one_comm) {
+            // the presence all-gather on the exchange stream (behind the previous
+            // batch's tail and a synchronous step's collectives), the column
+            // table back on the side stream behind it
+            rc = stream_after(&s->ev_pres, side, xs);
+            if (!rc && s->sync_set) {
+                rc = stream_after(&s->ev_sync, s->main_s, xs);
+                s->sync_set = false;
+            }
+            ctx->stream = xs;
+            if (!rc) rc = exchange_presence(s, plan, s->comm);
+            if (!rc) rc = stream_after(&s->ev_pres2, xs, side);
+            ctx->stream = side;
+        } else {
+            // sequential (one stream), or the side communicator on the side stream
+            rc = exchange_presence(s, plan, s->scomm ? s->scomm : s->comm);
+        }
+    }
     // M: into the device ring (the profile reads it) and the mapped ring (the
     // host reads it once the step is done); nothing on the main streams waits for it
     int64_t* const m_dev = s->m_ring.ptr + seq % kRing;
@@ -1069,6 +1128,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     KARMA_TRY(rc);
     if (xs_on) {  // the tail on the exchange stream, behind this records job (and a synchronous step's collectives)
         KARMA_TRY(stream_after(&s->ev_rec, ms, xs));
+        // (one communicator: the presence all-gather above already waited for them)
         if (s->sync_set) {
             KARMA_TRY(stream_after(&s->ev_sync, s->main_s, xs));
             s->sync_set = false;
@@ -1180,7 +1240,10 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     std::unique_ptr<karma_step> s(new karma_step());
     s->ctx = ctx;
     s->comm = world > 1 ? comm : nullptr;
-    s->scomm = world > 1 ? side_comm : nullptr;
+    // a side communicator equal to the main one is none (its operations would
+    // otherwise go on two streams at once)
+    s->scomm = world > 1 && side_comm != comm ? side_comm : nullptr;
+    s->one_comm = s->scomm == nullptr;
     s->kmode = kmode;
     s->world = world;
     s->rank = rank;
@@ -1191,6 +1254,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     if (const char* e = getenv("KARMA_STEP_SIDES")) s->sides = atoi(e) == 1 ? 1 : 2;
     if (const char* e = getenv("KARMA_STEP_DEFER_RANKS")) s->defer_ranks = atoi(e) != 0;
     if (const char* e = getenv("KARMA_STEP_XSTREAM")) s->xstream = atoi(e) != 0;
+    if (const char* e = getenv("KARMA_STEP_STALL_S")) s->stall_s = std::max(1, atoi(e));
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
@@ -1206,8 +1270,14 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     const int side_prio = getenv("KARMA_STEP_SIDE_PRIO") && atoi(getenv("KARMA_STEP_SIDE_PRIO")) ? hi : 0;
     KARMA_HIP(hipStreamCreateWithPriority(&s->side_s, hipStreamNonBlocking, side_prio));
     KARMA_HIP(hipStreamCreateWithPriority(&s->side_alt_s, hipStreamNonBlocking, side_prio));
+    // the status ring in mapped coherent host memory of this step's own: a
+    // second live step on the context numbers its steps from 1 too, and a
+    // shared ring would hand it this step's verdicts
     void *hm = nullptr, *dm = nullptr;
-    KARMA_TRY(ctx_mapped(ctx, kMapStep, kRing * sizeof(StepStatus) + kRing * 8, &hm, &dm));
+    KARMA_HIP(hipHostMalloc(&s->ring_mem, kRing * sizeof(StepStatus) + kRing * 8,
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    hm = s->ring_mem;
+    KARMA_HIP(hipHostGetDevicePointer(&dm, hm, 0));
     s->mring_h = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(hm) + kRing * sizeof(StepStatus));
     s->mring_d = reinterpret_cast<int64_t*>(static_cast<uint8_t*>(dm) + kRing * sizeof(StepStatus));
     KARMA_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->graves_h), kRing * 4 * 8, hipHostMallocDefault));
@@ -1244,8 +1314,10 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
     // deferred: one process (no collective needs a host count), nothing read back
     // several processes: once a synchronous step has sized the exchange's
     // slots and every rank's store is known to be ACGT-only
-    // (and with a side communicator: the main one's operations then stay on one stream)
-    const bool ranks_ok = s->world == 1 || (s->defer_ranks && s->scomm && s->kc > 0 && s->acgt_store == store);
+    // (one communicator: with the exchange stream, which then carries every
+    // collective; a side communicator: the main one's operations stay on one stream)
+    const bool ranks_ok = s->world == 1 || (s->defer_ranks && (s->one_comm ? s->xstream : s->scomm != nullptr) &&
+                                            s->kc > 0 && s->acgt_store == store);
     const bool defer = (flags & KARMA_STEP_DEFER) && !keep && ranks_ok && s->n_glob <= sets_max_contigs();
     int rc = KARMA_OK;
     if (defer && s->sticky_sync > 0) {
@@ -1297,9 +1369,11 @@ int karma_step_sync(karma_step* s) {
 
 int karma_step_info(karma_step* s, int64_t* info, int n) {
     KARMA_CHECK(s && info && n >= 0, KARMA_ERR_ARG, "karma_step_info: bad arguments");
+    const int64_t mode = (s->one_comm ? 1 : 0) | (s->xstream ? 2 : 0) | (s->defer_ranks ? 4 : 0);
     const int64_t v[] = {s->M,          s->E,        s->pairs_local, s->entries,
                          s->n_sync,     s->n_deferred, s->n_redone,  (int64_t)s->pending.size(),
-                         s->run_ns,     s->wait_ns};
+                         s->run_ns,     s->wait_ns,  s->n_two,       s->n_xs,
+                         mode,          s->world};
     for (int i = 0; i < n && i < (int)(sizeof v / sizeof v[0]); ++i) info[i] = v[i];
     return KARMA_OK;
 }
@@ -1343,9 +1417,11 @@ int karma_step_destroy(karma_step* s) {
     bury(s, true);
     for (auto& ev : s->grave_ev)
         if (ev) hipEventDestroy(ev);
-    for (hipEvent_t ev : {s->ev, s->ev_rec, s->ev_sync, s->ev_tail[0], s->ev_tail[1]})
+    for (hipEvent_t ev : {s->ev, s->ev_rec, s->ev_sync, s->ev_tail[0], s->ev_tail[1], s->ev_pres, s->ev_pres2,
+                          s->ev_pre})
         if (ev) hipEventDestroy(ev);
     if (s->graves_h) hipHostFree(s->graves_h);
+    if (s->ring_mem) hipHostFree(s->ring_mem);
     // the step's buffers return to the context's cache under streams about to
     // be destroyed: release them first, then hand cached blocks to the context
     s->prof.release();

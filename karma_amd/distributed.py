@@ -230,8 +230,11 @@ class NativeStep:
         b = np.ascontiguousarray(bounds, np.int64)
         assert int(b[rank + 1] - b[rank]) == n_loc, "the owner bounds disagree with this rank's contig shard"
         multi = comm.world > 1
+        # a distinct side communicator only (one that is the main one is none:
+        # its operations would go on two streams at once)
+        side = comm.side.h if multi and comm.side is not comm else None
         h = ctypes.c_void_p()
-        call("karma_step_create", ctx.h, comm.h if multi else None, comm.side.h if multi else None, int(kmode),
+        call("karma_step_create", ctx.h, comm.h if multi else None, side, int(kmode),
              int(n_glob), ptr(b), len(b) - 1, int(rank), ctypes.byref(h))
         self.h = h
         self._info = np.zeros(4, np.int64)
@@ -274,10 +277,20 @@ class NativeStep:
 
     def info(self):
         """[M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending,
-        host ns inside karma_step_run, of which ns waiting for deferred statuses]."""
-        v = np.zeros(10, np.int64)
-        call("karma_step_info", self.h, ptr(v), 10)
+        host ns inside karma_step_run, of which ns waiting for deferred statuses, deferred steps on
+        two main streams, deferred tails on the exchange stream, mode bits, ranks]."""
+        v = np.zeros(14, np.int64)
+        call("karma_step_info", self.h, ptr(v), 14)
         return v
+
+    def mode(self):
+        """How the steps ran (the bench line's step_driver.mode)."""
+        v = self.info()
+        bits, ranks = int(v[12]), int(v[13])
+        return {"ranks": ranks, "one_communicator": bool(bits & 1), "exchange_stream": bool(bits & 2),
+                "defer_across_ranks": bool(bits & 4), "deferred_two_main_streams": int(v[10]),
+                "deferred_tail_on_exchange_stream": int(v[11]), "synchronous": int(v[4]), "deferred": int(v[5]),
+                "rerun": int(v[6])}
 
     def close(self):
         if getattr(self, "h", None):

@@ -6,8 +6,9 @@ csrc/comm.hip) -- the communicator code a real multi-GPU job runs.  RCCL itself
 refuses several ranks on one device, so the parent starts this process with
 LD_LIBRARY_PATH pointing at tools/fake_rccl/ (a host-staged test double of the
 RCCL entry points the library binds, ahead of ROCm's librccl in the search
-order).  Everything else is the product: the presence all-gather on the side
-communicator, the padded variable all-gather of the exception keys, the count
+order).  Everything else is the product: the presence all-gather (one
+communicator on the exchange stream by default, the side communicator with
+KARMA_STEP_SIDE_COMM=1), the padded variable all-gather of the exception keys, the count
 exchange, the grouped key/count all-to-all-v, the owners' merge, the totals
 all-gather (in place for equal shards, padded otherwise).
 
@@ -237,7 +238,12 @@ def main():
     ap.add_argument("--sizes", default="")
     ap.add_argument("--frags", type=int, default=0)
     ap.add_argument("--seed", type=int, default=29)
+    ap.add_argument("--env", action="append", default=[],
+                    help="KEY=VALUE set before the communicators and steps are created (mode A/B)")
     a = ap.parse_args()
+    for kv in a.env:
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
     _lib.load()
     summary = {"fake_rccl_loaded": fake_loaded(), "case": a.case, "world": a.world}
     if not summary["fake_rccl_loaded"]:

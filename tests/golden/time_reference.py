@@ -16,7 +16,7 @@ encodings; they must equal the oracle's config-3 digests, which pins the
 config-3 digests by the reference itself (key "reference_config3").
 
 Usage: python tests/golden/time_reference.py [--config config3] [--threads 8]
-Writes profiles/r03/reference_<config>.json and adds reference_<config> to
+Writes tests/golden/reference_<config>.json and adds reference_<config> to
 tests/golden/digests.json.
 """
 
@@ -117,7 +117,7 @@ def main():
         out["units_per_s"] = round((inp["n_loc"] + inp["f_loc"]) / tot, 1)
 
     os.makedirs(os.path.join(REPO, "profiles", "r03"), exist_ok=True)
-    with open(os.path.join(REPO, "profiles", "r03", f"reference_{args.config}.json"), "w") as f:
+    with open(os.path.join(REPO, "tests", "golden", f"reference_{args.config}.json"), "w") as f:
         json.dump(out, f, indent=1)
     if not args.skip_profile:
         allw = D.load()

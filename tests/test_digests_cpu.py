@@ -44,7 +44,7 @@ def test_oracle_config2_matches_reference_digests():
 def test_config3_digests_are_the_reference_outputs():
     """reference_config3: lmfaber/karma's own config-3 outputs (profile 424 s,
     eq graph 10 s in the build container, tests/golden/time_reference.py,
-    profiles/r03/reference_config3.json).  The oracle digests that the GPU tests
+    tests/golden/reference_config3.json).  The oracle digests that the GPU tests
     and bench.py's in-run parity check use for config 3 are the same bytes."""
     gold = D.load()
     ref, orc = gold["reference_config3"], gold["config3"]

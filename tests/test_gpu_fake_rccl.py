@@ -5,8 +5,8 @@ RCCL refuses several ranks on one device, so these tests start a child process
 librccl.so.1 is tools/fake_rccl/ (a host-staged test double of the RCCL entry
 points, ahead of ROCm's in LD_LIBRARY_PATH; libkarma_hip.so itself is the
 shipped build, unchanged).  What runs is the product's multi-GPU code --
-karma_amd/comm.py RcclComm and csrc/comm.hip, the side-stream communicator,
-the sharded driver -- so the only piece left unverified before a real
+karma_amd/comm.py RcclComm and csrc/comm.hip, the one-communicator exchange
+stream (and the optional side-stream communicator), the sharded driver -- so the only piece left unverified before a real
 multi-GPU run is RCCL's own transport.  The child refuses to run (exit 3) if
 the fake is not the librccl it loaded."""
 import json
@@ -99,8 +99,19 @@ def test_rccl_sharded_build_three_unequal_ranks_match_oracle(tmp_path):
     check_graph(parts, o)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world):
+DEFER_MODES = {
+    # default: one communicator, every collective on the exchange stream
+    "one_comm": ([], 1, 3),
+    # one main stream (the config-3 batch size's mode): the tail still on the exchange stream
+    "one_comm_one_stream": (["KARMA_STEP_STREAMS=1"], 1, 3),
+    # round 4's mode: the presence all-gather on a side communicator, on the side stream
+    "side_comm": (["KARMA_STEP_SIDE_COMM=1"], 0, 3),
+}
+
+
+@pytest.mark.parametrize("world,mode", [(2, "one_comm"), (3, "one_comm"), (2, "one_comm_one_stream"),
+                                        (3, "side_comm")])
+def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world, mode):
     """Deferred steps with several processes (csrc/step.hip run_deferred: the
     padded fixed-slot all-to-all, the merge from slots, the totals all-gather
     and the summed slow flag).  A first synchronous step on 1 % of the
@@ -113,8 +124,9 @@ def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world):
     contigs: the deferred path needs no exception keys)."""
     sizes = [5000, 6000, 5500][:world]  # ~5000 distinct pairs per owner's slice
     frags, seed = 200_000, 31
+    env, one_comm, xs = DEFER_MODES[mode]
     run_child("--case", "defer", "--world", str(world), "--sizes", ",".join(map(str, sizes)), "--frags",
-              str(frags), "--seed", str(seed), "--out", str(tmp_path))
+              str(frags), "--seed", str(seed), "--out", str(tmp_path), *[x for e in env for x in ("--env", e)])
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     prof, _, o = oracle_of(sizes, frags, seed, n_rate=0, len_span=100)
     # rank 0's batches in the third build carry one more read, of 12 records
@@ -129,6 +141,8 @@ def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world):
         for i in infos:
             assert i[5] == 3 and i[7] == 0, (tag, i.tolist())
             assert i[6] == (0 if tag == "fit" else 3), (tag, i.tolist())
+            # the mode that ran: one communicator or not, tails on the exchange stream, the ranks
+            assert (int(i[12]) & 1) == one_comm and i[11] == xs and i[13] == world, (mode, tag, i.tolist())
         got = np.concatenate([p[f"{tag}_profile"] for p in parts])
         assert np.array_equal(got.view(np.uint64), prof.view(np.uint64)), tag
         check_graph(parts, o_peer if tag == "peer" else o, tag + "_")

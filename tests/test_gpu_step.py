@@ -193,3 +193,69 @@ def test_native_step_equals_python_driver():
             ctx.close()
         for x, y in zip(*outs):
             assert x.shape == y.shape and np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+
+
+def test_two_steps_on_one_context_keep_their_own_status():
+    """Two live native steps on one context (two ShardedBuilds of different
+    shapes) interleave deferred steps: each has its own mapped status ring, so
+    neither reads the other's verdicts, and each one's newest profile, M and
+    edge count are its own (csrc/step.hip karma_step::ring_mem)."""
+    ctx = _lib.Context(0)
+    objs = []
+    try:
+        runs = []
+        for n, nf, seed in ((2000, 120_000, SEED), (3500, 200_000, SEED + 7)):
+            blob, offs, kl = engine.synth_contigs(seed, n, 30, 900, 0)
+            rec = np.ascontiguousarray(engine.synth_records(seed, n, 0, nf, True))
+            b = ShardedBuild(ctx, SoloComm(), -1, n, 0, n)
+            st = engine.ContigStore(ctx, blob, offs, kl)
+            d = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))
+            objs += [b, st, d]
+            runs.append((b, st, d, rec, n, blob, offs))
+        for _ in range(4):
+            for b, st, d, rec, *_ in runs:
+                b.run(st, d.ptr, len(rec), count=False)
+        for b, st, d, rec, n, blob, offs in runs:
+            b.sync()
+            info = b.native.info()
+            assert info[5] == 4 and info[6] == 0, info.tolist()  # 4 deferred, none run again
+            prof_o, cols_o = oracle_profile(blob, offs, 0, n)
+            assert int(info[0]) == len(cols_o)
+            assert int(info[1]) == len(oracle_graph(rec, n)["a"])
+            got = b.native.profile().numpy()
+            assert np.array_equal(got.view(np.uint64), prof_o.view(np.uint64))
+    finally:
+        for o in objs:
+            o.close()
+        ctx.close()
+
+
+def test_middle_deferred_step_rerun_keeps_newest_outputs():
+    """Three deferred steps of which the middle one holds reads of > 8 records
+    (its status calls for the general path, so karma_step_sync runs it again
+    synchronously): the newest step's M and edge count stay the ones reported
+    after sync, not the re-run's."""
+    n = 3000
+    rec = np.ascontiguousarray(engine.synth_records(SEED, n, 0, 150_000, True))
+    rng = np.random.default_rng(9)
+    r0 = int(rec[-1, 0]) + 1
+    big = np.array([(r0 + i, int(c)) for i in range(50) for c in rng.integers(0, n, 12)], np.uint32)
+    rec_big = np.concatenate([rec, big])
+    r = Run(n, rec, n_rate=0)
+    d_big = _lib.DevBuf.from_numpy(r.ctx, rec_big.view(np.int64).reshape(-1))
+    try:
+        r.step(count=False)
+        r.build.run(r.store, d_big.ptr, len(rec_big), count=False)
+        r.step(count=False)
+        r.build.sync()
+        info = r.build.native.info()
+        assert info[6] == 1, info.tolist()  # the middle step ran again
+        e_new = len(oracle_graph(rec, n)["a"])
+        assert len(oracle_graph(rec_big, n)["a"]) != e_new  # the big reads add edges
+        assert int(info[1]) == e_new, (info.tolist(), e_new)
+        prof_o, cols_o = oracle_profile(r.blob, r.offs, 0, n)
+        assert int(info[0]) == len(cols_o)
+        assert np.array_equal(r.build.native.profile().numpy().view(np.uint64), prof_o.view(np.uint64))
+    finally:
+        d_big.close()
+        r.close()

@@ -3,7 +3,7 @@
 # emulated ranks, each rank's share of config 3) and the 8-rank weak preview
 # (no tests); gpurun_out/quick/*.json.  STEPS / LEGS override the defaults.
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$REPO/gpurun_out/quick
+OUT=${QUICK_OUT:-$REPO/gpurun_out/quick}
 mkdir -p $OUT
 cd $REPO
 run() {
