@@ -186,7 +186,7 @@ int ctx_mapped(karma_ctx* ctx, int slot, size_t bytes, void** host, void** dev) 
 
 // ---- pinned host blocks for results (karma_host_alloc) ---------------------------
 // A D2H copy into pageable memory runs at about half the rate of one into
-// pinned memory (8 MB of eq edges: 0.257 against 0.152 ms, profiles/r04/meas_c),
+// pinned memory (8 MB of eq edges: 0.257 against 0.152 ms, profiles/r04/measurements.md (meas_c)),
 // and hipHostMalloc itself costs far more than the copy, so freed blocks are
 // kept by size class (powers of two from 4 KiB) for the next caller.
 namespace {

@@ -741,7 +741,7 @@ template <bool P56, bool C16>
 // 6 waves per SIMD (3 blocks per CU): fewer rows written at once write faster
 // than 8 waves (4 blocks) do, and the counting still hides under the writes:
 // profile 0.345-0.355 -> 0.335-0.337 ms at config 3 (round 3,
-// profiles/r03/ab_profwaves/; 7 waves: 0.407, 5: 0.497, 4: 0.499 ms)
+// profiles/r03/measurements.md (ab_profwaves); 7 waves: 0.407, 5: 0.497, 4: 0.499 ms)
 #ifndef KARMA_PROF_WAVES
 #define KARMA_PROF_WAVES 6
 #endif

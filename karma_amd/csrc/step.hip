@@ -1043,7 +1043,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // One main stream (large batches): the records job does not wait for the
     // previous batch's profile.  With KARMA_STEP_JOIN=1 it does (classify then
     // never shares HBM with a profile): config 3 1.29-1.31 against 1.16-1.21 ms
-    // per step without the join (profiles/r04/ab_join/).
+    // per step without the join (profiles/r04/measurements.md (ab_join)).
     if (!two && !sequential && s->ev_set && s->join) {
         if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;
         KARMA_HIP(hipStreamWaitEvent(ms, s->ev, 0));
@@ -1066,7 +1066,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // stream, after the code partition -- the profile's writes then share HBM
     // with the LDS-bound code reduce and final kernel instead of the next
     // batch's classify (config 3: 1.15 against 1.20-1.22 ms per step,
-    // profiles/r04/ab_mark3/); with two, after the final kernel
+    // profiles/r04/measurements.md (ab_mark3)); with two, after the final kernel
     ctx->mark_pos = two ? kMarkTwo : kMarkOne;
     const int jrc = sets_begin_deferred(ctx, reinterpret_cast<const uint2*>(rec), A, s->n_glob, &job, &v);
     ctx->mark_pos = -1;

@@ -393,7 +393,7 @@ class ShardedBuild:
             # queue behind its blocks.  Leaving a block slot free for them
             # (round 2's default with an exchange) halves the profile's blocks
             # now: 8-rank strong preview 0.244 (none free) vs 0.256 ms, weak
-            # 1.35-1.37 vs 1.40-1.42 ms (profiles/r03/ab_headroom/)
+            # 1.35-1.37 vs 1.40-1.42 ms (profiles/r03/measurements.md (ab_headroom))
             hr = os.environ.get("KARMA_SIDE_HEADROOM")  # measurement override (blocks per CU)
             ops.ctx.set_side_headroom(int(hr) if hr else 0)
         try:

@@ -5,7 +5,7 @@
 set -e
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 CFG=${1:-config3}
-OUT=$REPO/gpurun_out
+OUT=${PROF_OUT:-$REPO/gpurun_out}
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_trace -o trace --output-format csv -- \
     python3 $REPO/bench.py --config $CFG --steps 5 --warmup 2 --cpu-baseline off --no-e2e --no-timing > $OUT/prof_trace.log 2>&1
