@@ -268,32 +268,45 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-// KARMA_CLS_SORT (A/B build): classify stages its codes
-// in a wave-private LDS buffer of this many codes and writes each buffer
-// counting-sorted by code bucket (runs of one bucket back to back), as a
-// classify that feeds a reducer directly would; the partition still consumes
-// the chunk's codes (order inside a chunk is free), so results are unchanged.
-#ifndef KARMA_CLS_SORT
-#define KARMA_CLS_SORT 0
-#endif
-// KARMA_CLS_STAGE (A/B build): the same LDS staging without the sort -- each
-// stage written out as one contiguous, coalesced copy (are the scattered
-// per-emit buffer stores what keeps classify off the read rate?)
-#ifndef KARMA_CLS_STAGE
-#define KARMA_CLS_STAGE 0
-#endif
-#ifndef KARMA_CLS_DIRECT
-#define KARMA_CLS_DIRECT 0  // A/B: each lane loads its own 8 records (no LDS transpose)
-#endif
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
+
+// ---- binned classify (BIN): compact codes straight into bucket runs --------------
+// With few code buckets (Bc <= kBinMaxBc: n_contigs <= 229,376 at bwc = 12)
+// each wave keeps one LDS queue of kBinQ u16 codes (m0_local << 3 | M) per
+// code bucket.  A code goes to its bucket's queue (one returning LDS add for
+// its slot, one 2-byte LDS store); a queue that fills is written out as one
+// 128-byte segment (8 lanes x 16 B) at the BACK of the chunk's segment region,
+// its bucket id in the chunk's directory; at the chunk's end every non-empty
+// queue is written at the FRONT, in bucket order, as a run of 16-byte
+// granules (its last one padded with 0xFFFF).  The chunk's header holds each
+// bucket's front granule count (a nibble: bucket b's run starts at the sum of
+// the nibbles below b), the back count, the back mask and the first 16
+// directory bytes.  The code reduce then reads each bucket's runs directly:
+// the u32 code stream, the partition kernel and its u16 runs (1.2 GB of
+// intermediate traffic at config 3) are gone.
+constexpr int kBinQ = 64;        // codes per queue and per back segment (128 B)
+constexpr int kBinMaxBc = 56;    // code buckets with a queue (LDS: 56 x 128 B per wave; 7 nibble words)
+// header (4 x uint4 per chunk): x0..x6 granule nibbles of buckets 0..55, x7
+// back count, x8-x9 back mask, x10-x13 directory bytes 0..15, x14 codes
+constexpr int kBinHdr = 4;
+struct BinArgs {
+    uint16_t* segs;     // per chunk: seg_cap x kBinQ codes (front runs, then back segments from the end)
+    uint4* hdr;         // per chunk: kBinHdr uint4 (above)
+    uint8_t* dir;       // per chunk: dir_cap bucket ids of the back segments (in flush order)
+    int64_t seg_cap;    // segments per chunk: chunk / kBinQ + Bc
+    int dir_cap;        // chunk / kBinQ
+};
+
 // HIST: per-block code-bucket histograms for code_append_kernel; COMPACT: the
 // compact-code path exists (n_contigs <= 2^21); REMAP: contig ids relabelled
-// through P.remap as they are read (contig order without locality, see relabel)
-template <bool HIST, bool COMPACT, bool REMAP = false>
+// through P.remap as they are read (contig order without locality, see
+// relabel); BIN: codes into bucket segments (see above; not with HIST)
+template <bool HIST, bool COMPACT, bool REMAP = false, bool BIN = false>
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
-classify2_kernel(ClassArgs P) {
+classify2_kernel(ClassArgs P, BinArgs Q) {
+    static_assert(!(HIST && BIN), "the binned classify has no partition block histograms");
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
@@ -303,6 +316,8 @@ classify2_kernel(ClassArgs P) {
         if (lane == 0) {
             P.n_codes[chunk] = 0;
             P.n_gen[chunk] = 0;
+            if (BIN)
+                for (int i = 0; i < kBinHdr; ++i) Q.hdr[kBinHdr * chunk + i] = uint4{0u, 0u, 0u, 0u};
         }
         return;
     }
@@ -317,83 +332,94 @@ classify2_kernel(ClassArgs P) {
     // transpose buffer: lane l's 8 records in row l (4 units of 16 bytes), the
     // unit index XOR-ed with (l >> 2) & 3: conflict-free for the 16-byte stores
     // (8-lane groups, banks mod 32) and for the row reads (16-lane groups,
-    // banks mod 64) alike
-    __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][64 * 4];
+    // banks mod 64) alike.  BIN: half of it (rows of lanes 0-31, then of lanes
+    // 32-63), to leave LDS for the bucket queues at 4 blocks per CU.
+    constexpr int kRows = BIN ? 32 : 64;
+    __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][kRows * 4];
     u32x4* tb = tbuf[wave];
     // the chunk's codes per code bucket, added to its partition block's row at the end
     __shared__ uint32_t whist[kCW / 64][HIST ? kMaxBc : 1];
     uint32_t* wh = whist[wave];
-    constexpr int kStage = KARMA_CLS_SORT > 0 ? KARMA_CLS_SORT : (KARMA_CLS_STAGE > 0 ? KARMA_CLS_STAGE : 1);
-    constexpr bool kStaged = KARMA_CLS_SORT > 0 || KARMA_CLS_STAGE > 0;
-    __shared__ uint32_t cstage[kCW / 64][kStage];
-    __shared__ uint32_t chist[kCW / 64][KARMA_CLS_SORT > 0 ? kMaxBc : 1];
-    uint32_t* stg = cstage[wave];
-    uint32_t* shh = chist[wave];
-    uint32_t ncs = 0, nc_out = 0;  // codes staged; codes written (the chunk region's fill)
-    // the staged codes to the chunk region, counting-sorted by code bucket
-    auto flush_stage = [&]() {
-        if (!kStaged || ncs == 0) return;
-        if (KARMA_CLS_STAGE > 0) {  // a contiguous copy, 64 codes per store instruction
-            wave_sync();
-            for (uint32_t j = lane; j < ncs; j += 64) out[nc_out + j] = stg[j];
-            nc_out += ncs;
-            ncs = 0;
-            wave_sync();
-            return;
-        }
-        for (int b = lane; b < P.Bc; b += 64) shh[b] = 0;
-        wave_sync();
-        for (uint32_t j = lane; j < ncs; j += 64) atomicAdd(&shh[(stg[j] & 0xFFFFFFu) >> P.bwc], 1u);
-        wave_sync();
-        // exclusive scan of the bucket counts (lane l: buckets 2l, 2l + 1)
-        const uint32_t c0 = 2 * lane < P.Bc ? shh[2 * lane] : 0u, c1 = 2 * lane + 1 < P.Bc ? shh[2 * lane + 1] : 0u;
-        uint32_t x = c0 + c1;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        const uint32_t ex = x - c0 - c1;
-        wave_sync();
-        if (2 * lane < P.Bc) shh[2 * lane] = ex;
-        if (2 * lane + 1 < P.Bc) shh[2 * lane + 1] = ex + c0;
-        wave_sync();
-        for (uint32_t j = lane; j < ncs; j += 64) {
-            const uint32_t code = stg[j];
-            const uint32_t pos = atomicAdd(&shh[(code & 0xFFFFFFu) >> P.bwc], 1u);
-            out[nc_out + pos] = code;
-        }
-        nc_out += ncs;
-        ncs = 0;
-        wave_sync();
-    };
+    // BIN: the bucket queues, their fill counts, and rank -> bucket of the end flush
+    __shared__ __attribute__((aligned(16))) uint16_t bq[kCW / 64][BIN ? kBinMaxBc * kBinQ : 8];
+    __shared__ uint32_t bcnt[kCW / 64][BIN ? kBinMaxBc : 1];
+    uint16_t* const q = bq[wave];
+    uint32_t* const qn = bcnt[wave];
+    uint16_t* const seg_out = BIN ? Q.segs + chunk * Q.seg_cap * kBinQ : nullptr;
+    // back-segment bookkeeping, touched only when a queue fills (kept in LDS,
+    // not in registers across the walk): [0] back count, [1..2] back mask,
+    // [3..6] the first 16 directory bytes (for the header)
+    __shared__ uint32_t bback[kCW / 64][BIN ? 8 : 1];
+    uint32_t* const bst = bback[wave];
     constexpr bool hist_on = HIST;
     if (hist_on) {
         for (int b = lane; b < P.Bc; b += 64) wh[b] = 0;
         wave_sync();
     }
+    if (BIN) {
+        if (lane < P.Bc) qn[lane] = 0;
+        if (lane < 8) bst[lane] = 0;
+        wave_sync();
+    }
+    // BIN: codes of the lanes in `m` into their queues; a queue that fills is
+    // written as a back segment, and the codes that found it full go into the
+    // emptied queue (a queue holds < kBinQ codes between calls, so the lane
+    // that took slot kBinQ - 1 exists whenever one overflowed)
+    auto bin_emit = [&](uint64_t m, uint32_t code) {
+        const uint32_t m0 = code & 0xFFFFFFu, bk = m0 >> P.bwc;
+        const uint16_t val = (uint16_t)(((m0 & ((1u << P.bwc) - 1u)) << 3) | (code >> 24));
+        uint32_t pos = 0;
+        if (in_mask(m)) {
+            pos = __hip_atomic_fetch_add(&qn[bk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (pos < (uint32_t)kBinQ) q[bk * kBinQ + pos] = val;
+        }
+        uint64_t full = m & lanes(pos == (uint32_t)kBinQ - 1u);
+        if (!full) return;
+        const uint64_t over = m & lanes(pos >= (uint32_t)kBinQ);
+        while (full) {  // rare: ~1 per kBinQ codes of a bucket (uniform loop)
+            const int L = __builtin_ctzll(full);
+            full &= full - 1;
+            const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)bk, L);
+            wave_lds_order();
+            const uint32_t nbk = (uint32_t)__builtin_amdgcn_readfirstlane((int)bst[0]);
+            uint16_t* const dst = seg_out + (Q.seg_cap - 1 - (int64_t)nbk) * kBinQ;
+            if (lane < 8) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(q + fb * kBinQ + 8 * lane);
+                *reinterpret_cast<u32x4*>(dst + 8 * lane) = v;
+            }
+            if (lane == 0) {
+                Q.dir[chunk * Q.dir_cap + nbk] = (uint8_t)fb;
+                bst[0] = nbk + 1;
+                bst[1 + (fb >> 5)] |= 1u << (fb & 31);
+                if (nbk < 16) bst[3 + (nbk >> 2)] |= fb << (8 * (nbk & 3));
+            }
+            wave_lds_order();
+            if (in_mask(over) && bk == fb) q[fb * kBinQ + pos - kBinQ] = val;
+            if (lane == 0) qn[fb] -= (uint32_t)kBinQ;  // was kBinQ + the overflowed codes
+            wave_lds_order();
+        }
+    };
+    // BIN: a step's codes are staged (ballot-compacted u32) in the transpose
+    // buffer, idle during the walk (a step ends <= 512 reads: 2 KB), and go
+    // into the queues once per step, 64 at a time, instead of at each of the
+    // walk's 8 emit points
+    uint32_t* const stg = reinterpret_cast<uint32_t*>(tb);
+    uint32_t ns = 0;  // staged codes (uniform)
+    auto bin_stage = [&]() {
+        if (!ns) return;
+        wave_lds_order();
+        for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
+            const bool on = j0 + lane < ns;
+            const uint32_t code = on ? stg[j0 + lane] : 0u;
+            bin_emit(lanes(on), code);
+        }
+        ns = 0;
+        wave_lds_order();
+    };
 
     // records [t0, hi) of a step, coalesced: unit u of lane l = records t0 + 128u + 2l, + 1.
-    // (KARMA_CLS_DIRECT: unit u of lane l = records t0 + 8l + 2u, + 1 -- each
-    // lane its own 64 bytes, no LDS transpose.)
     // Past the chunk: read id kEmpty (a read of its own that is never emitted), contig 0.
     auto prefetch = [&](u32x4 (&dst)[kCPer], int64_t t0, int64_t hi) {
-#if KARMA_CLS_DIRECT
-        const int64_t gd = t0 + 8 * lane;
-        if (t0 + kCIter <= hi) {
-#pragma unroll
-            for (int u = 0; u < kCPer; ++u)  // plain loads: the 4 loads share lines (non-temporal: 0.757 ms)
-                dst[u] = *reinterpret_cast<const u32x4*>(P.rec + gd + 2 * u);
-        } else {
-#pragma unroll
-            for (int u = 0; u < kCPer; ++u) {
-                const int64_t gi = gd + 2 * u;
-                const uint2 r0 = gi < hi ? P.rec[gi] : make_uint2(kEmpty, 0u);
-                const uint2 r1 = gi + 1 < hi ? P.rec[gi + 1] : make_uint2(kEmpty, 0u);
-                dst[u] = u32x4{r0.x, r0.y, r1.x, r1.y};
-            }
-        }
-        return;
-#endif
         const int64_t gb = t0 + 2 * lane;
         if (t0 + kCIter <= hi) {
 #pragma unroll
@@ -437,35 +463,50 @@ classify2_kernel(ClassArgs P) {
     };
     auto step = [&](auto full_tag, u32x4 (&buf)[kCPer], u32x4 (&nxt)[kCPer], int64_t t0) {
         constexpr bool FULL = decltype(full_tag)::value;
-        // a step emits <= kCIter codes, the chunk tail one more
-        if (kStaged && ncs + kCIter + 1 > (uint32_t)kStage) flush_stage();
         uint32_t rid[8], ctg[8];
-#if KARMA_CLS_DIRECT
-#pragma unroll
-        for (int u = 0; u < kCPer; ++u) {
-            rid[2 * u] = buf[u].x;
-            ctg[2 * u] = buf[u].y;
-            rid[2 * u + 1] = buf[u].z;
-            ctg[2 * u + 1] = buf[u].w;
-        }
-#else
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
+        if (!BIN) {
 #pragma unroll
-        for (int u = 0; u < kCPer; ++u) {
-            const int row = 16 * u + (lane >> 2);
-            tb[4 * row + ((lane & 3) ^ ((row >> 2) & 3))] = buf[u];
-        }
-        wave_sync();
+            for (int u = 0; u < kCPer; ++u) {
+                const int row = 16 * u + (lane >> 2);
+                tb[4 * row + ((lane & 3) ^ ((row >> 2) & 3))] = buf[u];
+            }
+            wave_sync();
 #pragma unroll
-        for (int u = 0; u < kCPer; ++u) {
-            const u32x4 q = tb[4 * lane + (u ^ ((lane >> 2) & 3))];
-            rid[2 * u] = q.x;
-            ctg[2 * u] = q.y;
-            rid[2 * u + 1] = q.z;
-            ctg[2 * u + 1] = q.w;
+            for (int u = 0; u < kCPer; ++u) {
+                const u32x4 qv = tb[4 * lane + (u ^ ((lane >> 2) & 3))];
+                rid[2 * u] = qv.x;
+                ctg[2 * u] = qv.y;
+                rid[2 * u + 1] = qv.z;
+                ctg[2 * u + 1] = qv.w;
+            }
+            wave_sync();
+        } else {
+            // two halves through 32 rows: units 0-1 hold lanes 0-31's records,
+            // units 2-3 lanes 32-63's; every lane reads row (lane & 31) in both
+            // halves and keeps the one of its own
+            const int rl = lane & 31;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int row = 16 * u + (lane >> 2);
+                    tb[4 * row + ((lane & 3) ^ ((row >> 2) & 3))] = buf[2 * h + u];
+                }
+                wave_sync();
+                if ((lane >> 5) == h) {
+#pragma unroll
+                    for (int u = 0; u < kCPer; ++u) {
+                        const u32x4 qv = tb[4 * rl + (u ^ ((rl >> 2) & 3))];
+                        rid[2 * u] = qv.x;
+                        ctg[2 * u] = qv.y;
+                        rid[2 * u + 1] = qv.z;
+                        ctg[2 * u + 1] = qv.w;
+                    }
+                }
+                wave_sync();
+            }
         }
-        wave_sync();
-#endif
         if (REMAP) {
             if (t0 + kCIter < c_hi) remap_units(nxt);
             if (t0 + 2 * kCIter < c_hi) prefetch(buf, t0 + 2 * kCIter, c_hi);
@@ -483,11 +524,12 @@ classify2_kernel(ClassArgs P) {
         const uint32_t ubase = (uint32_t)(t0 - c_lo) + 8u * lane;
         // The lane's walk (branch-free: no lane predicate lives across a branch,
         // so the compiler keeps them as SGPR lane masks).  Emission: codes from
-        // the front of the chunk's region, general read starts (chunk-relative)
-        // from the back, big reads to the big list.  The walk runs once for the
-        // codes; only when some lane met a general or a big read does it run
-        // again to emit those (rare on assembled transcriptomes).  Codes go out
-        // through a buffer store whose range check drops the lanes without one.
+        // the front of the chunk's region (BIN: into the bucket queues),
+        // general read starts (chunk-relative) from the back, big reads to the
+        // big list.  The walk runs once for the codes; only when some lane met
+        // a general or a big read does it run again to emit those (rare on
+        // assembled transcriptomes).  Codes go out through a buffer store whose
+        // range check drops the lanes without one.
         // Outputs: the lane's last read (st, spos), whether one started in the
         // lane, and the mask of lanes with a general or big read.
         auto walk = [&](auto rare_pass, RState& st, uint32_t& spos, uint64_t& started) -> uint64_t {
@@ -497,9 +539,9 @@ classify2_kernel(ClassArgs P) {
             auto emit = [&](uint64_t e, uint64_t ok, uint32_t code, uint32_t pos, uint64_t big) {
                 if (!RARE) {
                     const uint64_t b = e & ok & ~big;
-                    if (kStaged) {
-                        if (in_mask(b)) stg[ncs + (uint32_t)rank_below(b)] = code;
-                        ncs += __popcll(b);
+                    if (BIN) {
+                        if (in_mask(b)) stg[ns + (uint32_t)rank_below(b)] = code;
+                        ns += __popcll(b);
                     } else {
                         // lanes without a code store past the region (bit 31): dropped
                         const uint32_t boff =
@@ -605,6 +647,7 @@ classify2_kernel(ClassArgs P) {
             uint64_t started2;
             walk(std::true_type{}, st2, spos2, started2);
         }
+        if (BIN) bin_stage();  // before the next step's transpose reuses the buffer
         ct_ok = ct_ok_next;
         ct = ct_next;
         ct_len = ct_len_next;
@@ -647,26 +690,73 @@ classify2_kernel(ClassArgs P) {
         const bool big = ct_len + hl > (uint32_t)kMaxFast;
         uint32_t code;
         const bool ok = !big && (hl ? rs_code2<COMPACT>(ct, h, P.N, &code) : rs_code<COMPACT>(ct, P.N, &code));
+        if (BIN && ok) bin_emit(1ull, code);  // lane 0's code (uniform values)
         if (lane == 0) {
             if (big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + ct_pos;
             else if (ok) {
-                if (kStaged) stg[ncs] = code;
-                else out[nc] = code;
+                if (!BIN) out[nc] = code;
                 if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
             } else out[P.chunk - 1 - ng] = ct_pos;
         }
-        if (kStaged && !big && ok) ++ncs;
         nc += ok ? 1u : 0u;
         ng += !big && !ok ? 1u : 0u;
     }
-    if (kStaged) {
-        wave_sync();
-        flush_stage();
+    if (BIN) {
+        // the front runs: every non-empty queue, in bucket order, as 16-byte
+        // granules; granule k of the chunk is found through a table in the
+        // (now idle) transpose buffer: k -> bucket << 3 | granule
+        wave_lds_order();
+        const uint32_t cnt = lane < P.Bc ? qn[lane] : 0u;
+        const uint32_t g = (cnt + 7u) >> 3;
+        const uint32_t incl = wave_scan_incl(g), excl = incl - g;
+        const uint32_t G = lane63(incl);
+        uint16_t* const gt = reinterpret_cast<uint16_t*>(tb);  // <= 56 x 8 entries
+        uint8_t* const gb = reinterpret_cast<uint8_t*>(tb) + 1024;  // granule count per bucket
+        for (uint32_t i = 0; i < g; ++i) gt[excl + i] = (uint16_t)(lane << 3 | i);
+        gb[lane] = (uint8_t)g;
+        wave_lds_order();
+        for (uint32_t k0 = 0; k0 < G; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            if (k < G) {
+                const uint32_t e = gt[k], bk = e >> 3, i = e & 7u;
+                const uint32_t n = qn[bk];
+                u32x4 v = *reinterpret_cast<const u32x4*>(q + bk * kBinQ + 8 * i);
+                // codes at index >= n are stale: 0xFFFF
+                const int k0c = 8 * (int)i;
+                auto pad = [&](uint32_t w, int c) -> uint32_t {
+                    const uint32_t lo = k0c + c < (int)n ? (w & 0xFFFFu) : 0xFFFFu;
+                    const uint32_t hi = k0c + c + 1 < (int)n ? (w >> 16) : 0xFFFFu;
+                    return lo | hi << 16;
+                };
+                v.x = pad(v.x, 0), v.y = pad(v.y, 2), v.z = pad(v.z, 4), v.w = pad(v.w, 6);
+                *reinterpret_cast<u32x4*>(seg_out + (int64_t)k * 8) = v;
+            }
+        }
+        // the header: lane w < 7 packs the nibbles of buckets 8w .. 8w + 7
+        uint32_t nib = 0;
+        if (lane < 7) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) nib |= (uint32_t)(8 * lane + j < P.Bc ? gb[8 * lane + j] : 0u) << (4 * j);
+        }
+        const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 0);
+        const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 1);
+        const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 2);
+        const uint32_t w3 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 3);
+        const uint32_t w4 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 4);
+        const uint32_t w5 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 5);
+        const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 6);
+        if (lane == 0) {
+            uint4* const h = Q.hdr + kBinHdr * chunk;
+            h[0] = uint4{w0, w1, w2, w3};
+            h[1] = uint4{w4, w5, w6, bst[0]};
+            h[2] = uint4{bst[1], bst[2], bst[3], bst[4]};
+            h[3] = uint4{bst[5], bst[6], nc, 0u};
+        }
     }
     if (lane == 0) {
         P.n_codes[chunk] = nc;
         P.n_gen[chunk] = ng;
-        if (nc) atomicAdd(P.blk_items + chunk / P.lists_per_block, (unsigned long long)nc);
+        if (nc && !BIN) atomicAdd(P.blk_items + chunk / P.lists_per_block, (unsigned long long)nc);
     }
     if (hist_on && nc) {
         wave_sync();
@@ -1348,6 +1438,144 @@ __global__ void __launch_bounds__(kCRT) code_reduce_kernel(const uint16_t* __res
     for (int i = threadIdx.x; i < hn; i += kCRT) out[i] = h[slot(i)];
 }
 
+// One block per (code bucket, group of chunks) of the binned classify: the
+// bucket's runs of the group's chunks into the same direct-mapped LDS
+// histogram (same part_ch layout as code_reduce_kernel).
+//   front runs   one per chunk (its granule count and offset from the header's
+//                nibbles), streamed with stream_runs: batches of 64 chunks,
+//                the next batch's headers in flight while one is counted;
+//   back segments (a queue that filled mid-chunk; ~10 % of the chunks at
+//                config 3) found from the header's first 16 directory bytes
+//                (the directory array past them), read 8 per load
+//                instruction (8 lanes x 16 B).
+__device__ __forceinline__ uint32_t nibble_sum(uint32_t x) {  // sum of the 8 nibbles
+    x = (x & 0x0F0F0F0Fu) + ((x >> 4) & 0x0F0F0F0Fu);
+    return (x * 0x01010101u) >> 24;
+}
+constexpr int kBackList = 2048;  // chunks with back segments of the block's bucket, listed in LDS
+__global__ void __launch_bounds__(kCRT) code_seg_reduce_kernel(const uint16_t* __restrict__ segs,
+                                                               const uint4* __restrict__ hdr,
+                                                               const uint8_t* __restrict__ dir, int64_t n_chunks,
+                                                               uint32_t seg_cap, int dir_cap, int bwc, int n_cg,
+                                                               uint32_t* __restrict__ part_ch, uint32_t list_cap) {
+    __shared__ uint32_t h[kHistMax];
+    __shared__ int slots[kCRT];
+    __shared__ uint32_t blist[kBackList];
+    __shared__ uint32_t nlist;
+    const int bucket = blockIdx.x / n_cg, grp = blockIdx.x % n_cg;
+    const int hn = 1 << (bwc + 3);
+    for (int i = threadIdx.x; i < hn; i += kCRT) h[i] = 0;
+    if (threadIdx.x == 0) nlist = 0;
+    __syncthreads();
+    const int64_t per = (n_chunks + n_cg - 1) / n_cg;
+    const int64_t c_lo = min(n_chunks, (int64_t)grp * per), c_hi = min(n_chunks, c_lo + per);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    auto slot = [](uint32_t c) { return c ^ ((c >> 5) & 31u); };
+    auto add = [&](uint32_t c) {
+        if (c != 0xFFFFu) __hip_atomic_fetch_add(&h[slot(c)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto add8 = [&](const u32x4 v) {
+        add(v.x & 0xFFFFu), add(v.x >> 16), add(v.y & 0xFFFFu), add(v.y >> 16);
+        add(v.z & 0xFFFFu), add(v.z >> 16), add(v.w & 0xFFFFu), add(v.w >> 16);
+    };
+    const int bw_ = bucket >> 3, bs = 4 * (bucket & 7);
+    // front runs: run r = chunk r's granules of this bucket; a chunk whose
+    // back mask holds the bucket is listed for the back pass on the way
+    stream_runs(
+        reinterpret_cast<const u32x4*>(segs), c_lo, c_hi, kCRT,
+        [&](int64_t c, int64_t* beg, uint32_t* len) {
+            const uint4 h0 = hdr[kBinHdr * c], h1 = hdr[kBinHdr * c + 1], h2 = hdr[kBinHdr * c + 2];
+            const uint32_t w[7] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z};
+            uint32_t pre = 0, mine = 0;
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                pre += i < bw_ ? nibble_sum(w[i]) : 0u;
+                if (i == bw_) {
+                    pre += nibble_sum(w[i] & ((1u << bs) - 1u));
+                    mine = (w[i] >> bs) & 15u;
+                }
+            }
+            *beg = c * (int64_t)seg_cap * (kBinQ / 8) + pre;
+            *len = mine;
+            const uint32_t bmw = bucket < 32 ? h2.x : h2.y;
+            if ((bmw >> (bucket & 31)) & 1u) {
+                const uint32_t i = __hip_atomic_fetch_add(&nlist, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (i < list_cap) blist[i] = (uint32_t)(c - c_lo);
+            }
+        },
+        add8, nullptr, slots);
+    __syncthreads();
+    // back segments of the listed chunks (every chunk of the group when the
+    // list overflowed: a skewed input), a chunk per lane
+    uint32_t* const wt = reinterpret_cast<uint32_t*>(slots) + wave * 64;
+    auto stream8 = [&](uint64_t m, uint32_t seg) {  // one whole segment per lane in m
+        const int n = __popcll(m);
+        wave_lds_order();
+        if (in_mask(m)) wt[rank_below(m)] = seg;
+        wave_lds_order();
+        u32x4 v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int j = 8 * t + (lane >> 3);
+            if (8 * t < n && j < n) v[t] = *reinterpret_cast<const u32x4*>(segs + (int64_t)wt[j] * kBinQ + 8 * (lane & 7));
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            if (8 * t < n && 8 * t + (lane >> 3) < n) add8(v[t]);
+    };
+    const uint8_t bb = (uint8_t)bucket;
+    const uint32_t nl = nlist;
+    const bool listed = nl <= list_cap;
+    const int64_t n_items = listed ? (int64_t)nl : c_hi - c_lo;
+    for (int64_t i0 = (int64_t)wave * 64; i0 < n_items; i0 += kCRT) {
+        const int64_t i = i0 + lane;
+        const int64_t c = i < n_items ? c_lo + (listed ? (int64_t)blist[i] : i) : c_hi;
+        uint4 h1 = {0u, 0u, 0u, 0u}, h2 = {0u, 0u, 0u, 0u}, h3 = {0u, 0u, 0u, 0u};
+        if (c < c_hi) {
+            h2 = hdr[kBinHdr * c + 2];
+            h1 = hdr[kBinHdr * c + 1];
+            h3 = hdr[kBinHdr * c + 3];
+        }
+        const uint64_t bm = h2.x | (uint64_t)h2.y << 32;
+        uint64_t mb = lanes((bm >> bucket) & 1ull);
+        if (!mb) continue;
+        const uint32_t nb = h1.w;
+        // matches among the first 16 directory bytes
+        const uint32_t d[4] = {h2.z, h2.w, h3.x, h3.y};
+        uint32_t hit = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            hit |= (((d[k >> 2] >> (8 * (k & 3))) & 0xFFu) == bb && (uint32_t)k < nb) ? 1u << k : 0u;
+        for (uint32_t base = 0;;) {
+            // this lane's matches in [base, base + 16), one segment per round
+            for (;;) {
+                const uint64_t mm = lanes(in_mask(mb) && hit != 0u);
+                if (!mm) break;
+                uint32_t sg = 0;
+                if (hit) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(hit);
+                    hit &= hit - 1u;
+                    sg = (uint32_t)c * seg_cap + seg_cap - 1u - (base + k);
+                }
+                stream8(mm, sg);
+            }
+            base += 16;
+            mb &= lanes(base < nb);
+            if (!mb) break;
+            if (in_mask(mb)) {  // directory bytes past the header's 16 (a skewed chunk)
+                const u32x4 q = *reinterpret_cast<const u32x4*>(dir + c * (int64_t)dir_cap + base);
+                const uint32_t e[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    hit |= (((e[k >> 2] >> (8 * (k & 3))) & 0xFFu) == bb && base + k < nb) ? 1u << k : 0u;
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t* out = part_ch + (int64_t)blockIdx.x * hn;
+    for (int i = threadIdx.x; i < hn; i += kCRT) out[i] = h[slot(i)];
+}
+
 // ---- pair reduce --------------------------------------------------------------------
 // A pair (a, b), b >= a, of a bucket is counted in one of two LDS structures:
 //   band   dense counters band[a_local * D + (b - a)] for b - a < D = 2^dbits
@@ -1903,7 +2131,8 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
             ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags,
                         nullptr,   0,         0,       nullptr, 0, nullptr, kCChunk};
-            KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false>), ceil_div(n_chunks, kCW / 64), kCW, 0, C);
+            KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false>), ceil_div(n_chunks, kCW / 64), kCW, 0, C,
+                         BinArgs{});
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, general_grid(ctx, n_chunks), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags,
@@ -2074,6 +2303,19 @@ __global__ void relabel_back_kernel(uint64_t* __restrict__ keys, int64_t n, cons
 // the general-read branch on the context's fork stream beside the code branch
 // (KARMA_FORK=0 in the environment: both branches in order on one stream;
 // scheduling only, the same kernels run)
+// the binned classify where it applies (KARMA_BIN=0 in the environment: the
+// code partition instead, A/B and tests; read per job)
+bool bin_on() {
+    const char* e = std::getenv("KARMA_BIN");
+    return e ? std::atoi(e) != 0 : true;
+}
+// the code reduce's LDS list of chunks with back segments (KARMA_BACKLIST in
+// the environment lowers it, so tests reach the overflow path; read per job)
+uint32_t back_list_cap() {
+    const char* e = std::getenv("KARMA_BACKLIST");
+    const int v = e ? std::atoi(e) : kBackList;
+    return (uint32_t)std::max(0, std::min(v, kBackList));
+}
 bool fork_on() {
     static const bool on = [] {
         const char* e = std::getenv("KARMA_FORK");
@@ -2087,7 +2329,7 @@ bool fork_on() {
 // chunks while 8192-record chunks would fill fewer than 4 rounds: classify
 // 0.0755 -> 0.070 ms there, 0.139 -> 0.128 ms at 4 ranks; at config 3 on one
 // GPU (9.2 rounds) 8192 stays, 4096 measured 0.536 -> 0.549 ms
-// (profiles/r03/ab_chunk/).
+// (profiles/r03/measurements.md (ab_chunk)).
 // KARMA_CHUNK=4096|8192 in the environment pins the size (tests run both
 // sizes on the same small inputs; read per call).
 int64_t chunk_records(const karma_ctx* ctx, int64_t A) {
@@ -2135,6 +2377,13 @@ struct SetsJob {
     uint8_t* ovf = nullptr;
     const int64_t* hctrl = nullptr;  // pinned copy of the control block
     int64_t max_cflush = 0, ccap = 0;
+    // binned classify (Bc <= kBinMaxBc, not append): segments, headers, back directories
+    bool bin = false;
+    uint32_t seg_cap = 0;
+    int dir_cap = 0;
+    DevArray<uint16_t> bsegs;
+    DevArray<uint32_t> bhdr;  // kBinHdr uint4 per chunk
+    DevArray<uint8_t> bdir;
     DevArray<uint16_t> cent;
     DevArray<int64_t> cf_base;
     DevArray<uint32_t> cf_off;
@@ -2208,7 +2457,18 @@ int SetsJob::setup() {
     max_cflush = n_pblk + ceil_div(A, CodeStream::kCap) + 1;
     ccap = A + max_cflush * (8 * (int64_t)g.Bc + 8);
     if (append) KARMA_TRY(blk_hist.alloc(ctx, n_pblk * g.Bc));
-    if (g.Bc > 0) {
+    // the binned classify (no code partition) while the code buckets' queues
+    // fit its LDS; KARMA_BIN=0 in the environment keeps the partition (A/B)
+    bin = !append && g.Bc > 0 && g.Bc <= kBinMaxBc && bin_on();
+    if (bin) {
+        dir_cap = (int)(chunk / kBinQ);
+        seg_cap = (uint32_t)(dir_cap + g.Bc);
+        KARMA_CHECK(n_chunks * (int64_t)seg_cap < (int64_t(1) << 32), KARMA_ERR_ARG,
+                    "binned classify: %lld chunks exceed 32-bit segment indices", (long long)n_chunks);
+        KARMA_TRY(bsegs.alloc(ctx, n_chunks * (int64_t)seg_cap * kBinQ));
+        KARMA_TRY(bhdr.alloc(ctx, n_chunks * 4 * kBinHdr));
+        KARMA_TRY(bdir.alloc(ctx, n_chunks * (int64_t)dir_cap));
+    } else if (g.Bc > 0) {
         KARMA_TRY(cent.alloc(ctx, ccap + 16));
         KARMA_TRY(cf_base.alloc(ctx, max_cflush));
         KARMA_TRY(cf_off.alloc(ctx, max_cflush * (g.Bc + 1)));
@@ -2222,6 +2482,8 @@ int SetsJob::setup() {
     n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>({ctx->cu_count / g.Bc, ceil_div(max_cflush, 4),
                                                                      ceil_div(A, (int64_t)g.Bc << KARMA_CG_SHIFT)}))
                     : 0;
+    // binned: one group per ~64 chunks at most (a wave's batch), up to one block per CU
+    if (bin) n_cg = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count / g.Bc, ceil_div(n_chunks, 64)));
     // pair-reduce groups per bucket: enough blocks to fill the chip while
     // buckets are few; one group from KARMA_ONE_GROUP_B buckets on, so the
     // final kernel copies the bucket's single list instead of re-hashing
@@ -2260,18 +2522,25 @@ int SetsJob::launch() {
                     n_gen.ptr, blk_items, lpb, big_list.ptr, counters, flags,
                     append ? blk_hist.ptr : nullptr, g.bwc, g.Bc, relabeled ? remap_map.ptr : nullptr, 0, nullptr,
                     chunk};
+        const BinArgs Bn = bin ? BinArgs{bsegs.ptr, reinterpret_cast<uint4*>(bhdr.ptr), bdir.ptr, (int64_t)seg_cap,
+                                         dir_cap}
+                               : BinArgs{};
         auto classify = [&](int64_t c_from, int64_t c_to) -> int {
             C.c0 = c_from;
             const int64_t cg = ceil_div(c_to - c_from, kCW / 64);
             if (cg <= 0) return KARMA_OK;
-            if (append && relabeled)
-                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true, true>), cg, kCW, 0, C);
+            if (bin && relabeled)
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, true, true>), cg, kCW, 0, C, Bn);
+            else if (bin)
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, false, true>), cg, kCW, 0, C, Bn);
+            else if (append && relabeled)
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true, true>), cg, kCW, 0, C, Bn);
             else if (append)
-                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true>), cg, kCW, 0, C);
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true>), cg, kCW, 0, C, Bn);
             else if (relabeled)
-                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, true>), cg, kCW, 0, C);
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, true>), cg, kCW, 0, C, Bn);
             else
-                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true>), cg, kCW, 0, C);
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true>), cg, kCW, 0, C, Bn);
             return KARMA_OK;
         };
         if (!relabeled) {
@@ -2285,7 +2554,7 @@ int SetsJob::launch() {
     }
     // where side-stream work (the k-mer profile) may start: 5 = after the final
     // kernel, beside the control-block readback (default; 0.283 against 0.291
-    // ms for the 8-rank strong preview, equal on one GPU, profiles/r03/ab_mark5/),
+    // ms for the 8-rank strong preview, equal on one GPU, profiles/r03/measurements.md (ab_mark5)),
     // 0 = after the whole pipeline, 1 = after classify, 2 = after the code
     // partition, 3 = at once (beside classify), 4 = after the code reduce.
     // Measured: 1 slows the code partition 0.19 -> 0.5 ms (1.46 vs 1.37 ms/step);
@@ -2302,6 +2571,7 @@ int SetsJob::launch() {
     if (A == 0) {
         KARMA_HIP(hipMemsetAsync(n_codes.ptr, 0, n_chunks * 4, ctx->stream));
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
+        if (bin) KARMA_HIP(hipMemsetAsync(bhdr.ptr, 0, n_chunks * 16 * kBinHdr, ctx->stream));
     }
     const RunDir cdir{cf_base.ptr, cf_off.ptr, counters + 1, blk_items};
     pdir = RunDir{pf_base.ptr, pf_off.ptr, counters + 2, blk_items + n_pblk};
@@ -2338,7 +2608,12 @@ int SetsJob::launch() {
     }();
     ctx->stream = main_stream;
     KARMA_TRY(rc_pair);
-    if (g.Bc > 0) {
+    if (bin) {
+        KARMA_TRY(mark(2));  // where the code partition would end
+        KARMA_LAUNCH(ctx, "graph_code_reduce", code_seg_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, bsegs.ptr,
+                     reinterpret_cast<const uint4*>(bhdr.ptr), bdir.ptr, n_chunks, seg_cap, dir_cap, g.bwc, n_cg,
+                     part_ch.ptr, back_list_cap());
+    } else if (g.Bc > 0) {
         uint16_t* const trash = cent.ptr + (ccap + 7) / 8 * 8;
         if (append && wide_c)
             KARMA_LAUNCH(ctx, "graph_code_partition", code_append_kernel<kMaxBc>, n_pblk, kPT, 0, codes.ptr, chunk,

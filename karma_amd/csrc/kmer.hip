@@ -600,7 +600,14 @@ __device__ __forceinline__ void hist_add(uint32_t* counts, uint32_t col) {
 // word (l mod 16) is fixed and its 16-base window is one alignbit of the word
 // pair staged in LDS as a u64 (one 8-byte read per position).  The k-mer code
 // is the window's top 2k bits; for 5p6 the 5-mer is the 6-mer's top 10 bits.
-template <bool P56, bool C16>
+// ORD (5p6, KARMA_PROF_ORD): count by compact table index (the 5-mer code, or
+// 1024 + the first three bases of a palindromic 6-mer) instead of by column:
+// no table lookup per window; the row phase gathers each column's count
+// through the inverse table (write_row_ord)
+#ifndef KARMA_PROF_ORD
+#define KARMA_PROF_ORD 0
+#endif
+template <bool P56, bool C16, bool ORD = false>
 __device__ __forceinline__ void count_clean(const Stage& first, const uint32_t* __restrict__ packed, int64_t w0,
                                             int64_t L, int kmin, int k, const uint16_t* __restrict__ tab,
                                             uint32_t* __restrict__ counts, uint32_t* __restrict__ win, int lane,
@@ -628,12 +635,12 @@ __device__ __forceinline__ void count_clean(const Stage& first, const uint32_t* 
                 const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
                 const uint32_t W = o ? __builtin_amdgcn_alignbit(hi, lo, sh) : hi;
                 if (P56) {
-                    hist_add<C16>(counts, tab[W >> 22]);  // kmer.py:72-73
+                    hist_add<C16>(counts, ORD ? W >> 22 : tab[W >> 22]);  // kmer.py:72-73
                     ++my;
                     const uint32_t c6 = W >> 20;
                     // palindromic 6-mers that fit in the contig, kmer.py:76-80
                     if ((c6 >> 6) == rev3(c6 & 63u) && 64 * t + 1 < lim) {
-                        hist_add<C16>(counts, tab[1024u + (c6 >> 6)]);
+                        hist_add<C16>(counts, ORD ? 1024u + (c6 >> 6) : tab[1024u + (c6 >> 6)]);
                         ++my;
                     }
                 } else {
@@ -717,6 +724,47 @@ __device__ __forceinline__ void write_row_wave(double* __restrict__ row, uint32_
     }
 }
 
+// ORD: the row from a histogram indexed by compact table index (u16
+// counters, C16): column j's count is counts16[inv[j]]; the histogram is
+// cleared afterwards with whole-word stores (1088 entries)
+__device__ __forceinline__ void write_row_ord(double* __restrict__ row, uint32_t* __restrict__ counts, int64_t M,
+                                              int32_t klen, int* __restrict__ err, double* __restrict__ lut,
+                                              const uint16_t* __restrict__ inv, int lane) {
+    const double len = (double)klen;
+    lut[lane] = lane ? (double)lane / len : 0.0;  // IEEE correctly rounded (kmer.py:120)
+    wave_lds_sync();
+    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(counts);
+    auto val = [&](uint32_t a) {
+        double v = lut[min(a, 63u)];
+        if (a >= 64u) v = (double)a / len;
+        return v;
+    };
+    const uint64_t u = (uint64_t)row;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u)),
+        0, (int)(M * 8), 0x00020000);
+    const bool al = (u & 15) == 0;
+    for (int64_t j = lane; 2 * j < M; j += 64) {
+        const uint32_t ii = reinterpret_cast<const uint32_t*>(inv)[j];
+        const uint32_t a = c16[ii & 0xFFFFu];
+        const uint32_t b = 2 * j + 1 < M ? (uint32_t)c16[ii >> 16] : 0u;
+        if ((a | b) && klen == 0) *err = 1;
+        const double x = val(a), y = val(b);
+        if (al && 2 * j + 1 < M) {
+            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+            const u32x4_t w = {(uint32_t)__double2loint(x), (uint32_t)__double2hiint(x), (uint32_t)__double2loint(y),
+                               (uint32_t)__double2hiint(y)};
+            __builtin_amdgcn_raw_buffer_store_b128(w, rr, (int)(j * 16), 0, KARMA_ROW_AUX >= 0 ? KARMA_ROW_AUX : 0);
+        } else {
+            row_store(x, row + 2 * j);
+            if (2 * j + 1 < M) row_store(y, row + 2 * j + 1);
+        }
+    }
+    wave_lds_sync();
+    for (int j = lane; j < 544; j += 64) counts[j] = 0;  // 1088 u16 counters
+}
+
 // Sum over the wave's 64 lanes, in every lane: DPP row shifts and row
 // broadcasts (no ds_bpermute address registers, which stayed live across the
 // contig loop and spilled), then lane 63's value read as a scalar.
@@ -752,20 +800,23 @@ profile_wave_kernel(
     const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
     const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
     double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
-    int64_t exc0, const int64_t* __restrict__ m_dev) {
+    int64_t exc0, const int64_t* __restrict__ m_dev, int ord_on) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     // wave index in an SGPR: contig offsets and lengths load with scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
     const int t_pad = (int)((tab_entries(P56, S) + 7) & ~7);
+    // ORD (no exception k-mers, 5p6, u16 counters): the inverse table follows tab
+    const bool ord_m = KARMA_PROF_ORD && P56 && C16 && ord_on;
+    uint16_t* inv = tab + t_pad;
     // LDS is laid out for M; with m_dev (the column table's count, not read
     // back to the host first) M is its capacity and the rows are dense
-    const int h_words = (int)hist_words(M, C16);
+    const int h_words = (int)hist_words(ord_m ? max<int64_t>(M, 1088) : M, C16);
     if (m_dev) {
         M = *m_dev;
         ld = M;
     }
-    uint32_t* counts = lds + t_pad / 2 + wave * (h_words + kProfWin);
+    uint32_t* counts = lds + (t_pad + (ord_m ? t_pad : 0)) / 2 + wave * (h_words + kProfWin);
     uint32_t* win = counts + h_words;
     uint16_t* mbuf = reinterpret_cast<uint16_t*>(win + 80);
     double* lut = reinterpret_cast<double*>(win);
@@ -779,6 +830,7 @@ profile_wave_kernel(
                 ord = (c6 >> 2) * 5u + 1u + (c6 & 3u);
             }
             tab[o] = (uint16_t)col_of_ord[ord];
+            if (KARMA_PROF_ORD && ord_on && (uint32_t)col_of_ord[ord] < (uint32_t)M) inv[col_of_ord[ord]] = (uint16_t)o;
         }
     } else {
         for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
@@ -820,7 +872,8 @@ profile_wave_kernel(
         const int64_t L = cur.L;
         unsigned my = 0;
         if (!cur.exc) {
-            count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
+            if (KARMA_PROF_ORD && ord_m) count_clean<P56, C16, true>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
+            else count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
         } else {
             // a contig with exception bases: windows that touch one are keyed by
             // their bytes and looked up among the sorted exception keys
@@ -852,7 +905,8 @@ profile_wave_kernel(
         // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
         my = wave_total(my);
         if (lane == 0) row_tot[c] = (int64_t)my;
-        write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
+        if (KARMA_PROF_ORD && ord_m) write_row_ord(out + c * ld, counts, M, cur.klen, err, lut, inv, lane);
+        else write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         cur = nxt;
@@ -1503,8 +1557,11 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         // counters when no contig reaches 2^16 bases (a count is <= L)
         const bool p56 = p->kmode == KARMA_KMER_5P6;
         const bool c16 = KARMA_PROF_C16 && c->max_len < 65536;
-        const size_t lds = (size_t)((tab_entries(p56, p->S) + 7) & ~7) * 2 +
-                           (kPBlock / 64) * (size_t)(hist_words(M, c16) + kProfWin) * 4;
+        // KARMA_PROF_ORD builds: count by compact index when no exception k-mer exists
+        const int ord_on = KARMA_PROF_ORD && p56 && c16 && p->n_exc == 0;
+        const size_t lds = (size_t)((tab_entries(p56, p->S) + 7) & ~7) * 2 * (ord_on ? 2 : 1) +
+                           (kPBlock / 64) * (size_t)(hist_words(ord_on ? std::max<int64_t>(M, 1088) : M, c16) +
+                                                     kProfWin) * 4;
 #define KARMA_WAVE_LAUNCH(P56, C16)                                                                              \
     do {                                                                                                         \
         const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_wave_kernel<P56, C16>), kPBlock, \
@@ -1512,7 +1569,7 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16>), g_, kPBlock, lds, c->packed.ptr,      \
                      c->mask.ptr, c->has_exc.ptr, woff, off, c->raw, keylen, n, k, with_len,                     \
                      p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err,       \
-                     (int)p->S, row_tot, lo, m_dev);                                                             \
+                     (int)p->S, row_tot, lo, m_dev, ord_on);                                                     \
     } while (0)
         if (KARMA_PROF_SPLIT > 0 && p56 && c16) {
             const size_t lds_s = (size_t)((tab_entries(true, p->S) + 7) & ~7) * 2 +

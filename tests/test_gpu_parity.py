@@ -685,3 +685,35 @@ def test_records_both_chunk_sizes(chunk, monkeypatch):
     rec = np.ascontiguousarray(engine.synth_records(21, 20_000, 0, 400_000, True))
     rec[:, 1] = np.random.default_rng(3).permutation(20_000).astype(np.uint32)[rec[:, 1]]
     check_records(rec, 20_000)
+
+
+@pytest.mark.parametrize("binned", ["1", "0"])
+def test_records_binned_classify_and_partition_paths(binned, monkeypatch):
+    """The binned classify (codes straight into per-bucket segments, no code
+    partition; graph_sets.hip classify2_kernel<.., BIN>, code_seg_reduce_kernel)
+    and the partition path it replaces (KARMA_BIN=0) give the oracle's graph:
+    a skewed input whose codes all fall in one bucket (dozens of back segments
+    per chunk), the bucket-count limit of the binned path (56 code buckets at
+    229,376 contigs; 57 takes the partition), reads across chunk boundaries at
+    every chunk size, and the relabelled rerun."""
+    monkeypatch.setenv("KARMA_BIN", binned)
+    rng = np.random.default_rng(31)
+    R = 120_000
+    m0 = rng.integers(0, 4093, R)  # every compact code in code bucket 0
+    span = rng.integers(0, 4, R)
+    rows = np.stack([np.repeat(np.arange(R, dtype=np.uint32), 2),
+                     np.stack([m0, m0 + span], 1).reshape(-1).astype(np.uint32)], 1)
+    check_records(rows, 50_000)
+    monkeypatch.setenv("KARMA_BACKLIST", "3")  # the code reduce's back-segment list overflows: full scan
+    check_records(rows, 50_000)
+    monkeypatch.delenv("KARMA_BACKLIST")
+    for n in (229_376, 229_377):
+        check_records(engine.synth_records(33, n, 0, 300_000, True), n)
+    for chunk in ("2048", "8192"):
+        monkeypatch.setenv("KARMA_CHUNK", chunk)
+        check_records(engine.synth_records(34, 30_000, 0, 250_000, True), 30_000)
+        check_records(rows, 50_000)
+    monkeypatch.delenv("KARMA_CHUNK")
+    rec = np.ascontiguousarray(engine.synth_records(21, 20_000, 0, 400_000, True))
+    rec[:, 1] = np.random.default_rng(3).permutation(20_000).astype(np.uint32)[rec[:, 1]]
+    check_records(rec, 20_000)
