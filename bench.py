@@ -510,9 +510,14 @@ def run(args, rank, world, local_rank, launcher):
         "kmer_presence": leg.packed_bytes,
         "graph_classify": 8 * A,  # the records, read once
     }
+    # intermediate (not in the roofline bytes): the binned classify (<= 56 code
+    # buckets) writes one 2-byte code per compact read into bucket runs, which
+    # the code reduce reads; otherwise a 4-byte code per read, partitioned into
+    # 2-byte runs (graph_sets.hip)
+    binned = "graph_code_partition" not in kern
     intermediate_bytes = {
-        "graph_classify": 4 * n_reads,  # one 4-byte code per compact read written
-        "graph_code_partition": 6 * n_reads,  # codes read, 2-byte bucket-local codes written
+        "graph_classify": (2 if binned else 4) * n_reads,
+        "graph_code_partition": 6 * n_reads,
         "graph_code_reduce": 2 * n_reads,
     }
     roof = None

@@ -184,9 +184,17 @@ struct ClassArgs {
     int bwc, Bc;
     const uint32_t* remap;  // contig relabelling (classify2_kernel<.., REMAP>), new id by old id
     int64_t c0;             // first chunk of this launch
-    const unsigned* skip;   // set: leave the chunks empty (a relabelled rerun follows)
+    unsigned* skip;         // set: leave the chunks empty (a relabelled rerun follows)
     int64_t chunk;          // records per chunk (chunk_records)
+    unsigned* vote = nullptr;  // classify decides the relabel itself (no probe kernel): chunks' votes
 };
+// In-classify relabel decision (a job without the probe kernel): every
+// kVoteStride-th chunk votes when more than 1/8 of its reads are general
+// (span > 4 contig ids; the probe's threshold); the kVotes-th vote sets the
+// relabel word, and chunks that start later skip (their wave reads the word
+// as it starts).  The pass is then wasted and reruns relabelled, as after a
+// probe; without votes every chunk runs.
+constexpr int kVoteStride = 16, kVotes = 4;
 
 // lanes below this one with their bit set in a wave mask
 __device__ __forceinline__ int rank_below(unsigned long long m) {
@@ -312,7 +320,9 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
     const int64_t c_lo = chunk * P.chunk;
     if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
-    if (P.skip && *P.skip) {  // the sample chunks asked for a relabelled rerun
+    // the relabel word (set by the probe kernel, or by this kernel's votes:
+    // read past the L2 of this XCD)
+    if (P.skip && __hip_atomic_load(P.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         if (lane == 0) {
             P.n_codes[chunk] = 0;
             P.n_gen[chunk] = 0;
@@ -769,6 +779,9 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     if (lane == 0) {
         if (bad_order) P.flags[0] = 1;
         if (bad_contig) P.flags[1] = 1;
+        if (P.vote && chunk % kVoteStride == 0 && 8 * ng > nc + ng && nc + ng >= 64 &&
+            atomicAdd(P.vote, 1u) + 1 == (unsigned)kVotes)
+            __hip_atomic_store(P.skip, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2367,6 +2380,8 @@ struct SetsJob {
     // | pairs per bucket[B+1] | their exclusive scan[B+1] | overflow[B]
     int64_t ctrl_words = 0;
     DevArray<int64_t> ctrl;
+    int64_t* cb = nullptr;  // the control block: ctrl, or the caller's zeroed one (ext)
+    bool ext = false;
     std::vector<int64_t> split_b;  // owner bounds (karma_graph_split_hint), found by the final kernel
     int64_t* split_loc = nullptr;   // in the control block: per bound, keys of its bucket below it
     int* flags = nullptr;
@@ -2438,12 +2453,20 @@ int SetsJob::setup() {
     ctrl_words = 6 + 2 * (int64_t)(B + 1) + ceil_div(B, 8) + (int64_t)split_b.size();
     // one allocation (and one memset per attempt) for the control block and
     // the per-partition-block item counts behind it
-    KARMA_TRY(ctrl.alloc(ctx, ctrl_words + 2 * n_pblk + B));
-    blk_items = reinterpret_cast<unsigned long long*>(ctrl.ptr + ctrl_words);
-    lb = reinterpret_cast<uint64_t*>(ctrl.ptr + ctrl_words + 2 * n_pblk);
-    flags = reinterpret_cast<int*>(ctrl.ptr);
-    counters = reinterpret_cast<unsigned*>(ctrl.ptr + 2);
-    n_per = ctrl.ptr + 6;
+    const int64_t cw_total = ctrl_words + 2 * n_pblk + B;
+    // a deferred job may take the caller's zeroed block (ctx->job_ctrl)
+    ext = deferred && ctx->job_ctrl && ctx->job_ctrl_words >= cw_total;
+    if (ext) {
+        cb = ctx->job_ctrl;
+    } else {
+        KARMA_TRY(ctrl.alloc(ctx, cw_total));
+        cb = ctrl.ptr;
+    }
+    blk_items = reinterpret_cast<unsigned long long*>(cb + ctrl_words);
+    lb = reinterpret_cast<uint64_t*>(cb + ctrl_words + 2 * n_pblk);
+    flags = reinterpret_cast<int*>(cb);
+    counters = reinterpret_cast<unsigned*>(cb + 2);
+    n_per = cb + 6;
     dst = n_per + (B + 1);
     ovf = reinterpret_cast<uint8_t*>(dst + (B + 1));
     split_loc = dst + (B + 1) + ceil_div(B, 8);
@@ -2509,8 +2532,11 @@ int SetsJob::launch() {
     KARMA_TRY(pent.alloc(ctx, pscap + 8));
     KARMA_TRY(pf_base.alloc(ctx, max_pflush));
     KARMA_TRY(pf_off.alloc(ctx, max_pflush * (B + 1)));
-    const bool probe = A > 0 && !relabeled;  // the probe kernel clears the control block
-    if (!probe) KARMA_HIP(hipMemsetAsync(ctrl.ptr, 0, (ctrl_words + 2 * n_pblk + B) * 8, ctx->stream));
+    // the probe kernel clears the control block; a caller's block (ext) is zero
+    // already on the first attempt, and classify decides the relabel itself
+    const bool fresh_ext = ext && attempt == 0 && !relabeled;
+    const bool probe = A > 0 && !relabeled && !fresh_ext;
+    if (!probe && !fresh_ext) KARMA_HIP(hipMemsetAsync(cb, 0, (ctrl_words + 2 * n_pblk + B) * 8, ctx->stream));
     if (append) KARMA_HIP(hipMemsetAsync(blk_hist.ptr, 0, n_pblk * g.Bc * 4, ctx->stream));
     if (mark_at(ctx) == 3 && attempt == 0 && !relabeled) {  // side-stream work may start beside classify
         if (!ctx->mark_ev) KARMA_HIP(hipEventCreateWithFlags(&ctx->mark_ev, hipEventDisableTiming));
@@ -2547,8 +2573,11 @@ int SetsJob::launch() {
             // a probe of the reads decides: when many span more than 4 contig
             // ids, this pass is skipped and a relabelled rerun follows
             KARMA_LAUNCH(ctx, "relabel_probe", relabel_probe_kernel, 1, kRelabelProbes, 0, rec, A, (uint32_t)N,
-                         counters + 3, reinterpret_cast<uint64_t*>(ctrl.ptr), (int64_t)(ctrl_words + 2 * n_pblk + B));
+                         counters + 3, reinterpret_cast<uint64_t*>(cb), (int64_t)(ctrl_words + 2 * n_pblk + B));
             C.skip = counters + 3;
+        } else if (fresh_ext) {
+            C.skip = counters + 3;
+            C.vote = counters + 4;
         }
         KARMA_TRY(classify(0, n_chunks));
     }
@@ -2647,7 +2676,7 @@ int SetsJob::launch() {
                      ovf, sa, lb, dst);
     KARMA_TRY(mark(5));  // after the final kernel, before the control-block readback
     if (!deferred)
-        KARMA_HIP(hipMemcpyAsync(const_cast<int64_t*>(hctrl), ctrl.ptr, ctrl_words * 8, hipMemcpyDeviceToHost,
+        KARMA_HIP(hipMemcpyAsync(const_cast<int64_t*>(hctrl), cb, ctrl_words * 8, hipMemcpyDeviceToHost,
                                  ctx->stream));
     return KARMA_OK;
 }
@@ -2873,6 +2902,8 @@ int sets_begin_deferred(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, 
     v->flags = j->flags;
     v->counters = j->counters;
     v->ovf = j->ovf;
+    v->ctrl = j->ext ? j->cb : nullptr;
+    v->ctrl_need = j->ctrl_words + 2 * j->n_pblk + j->B;
     ctx->job_open = true;
     *job = j.release();
     return KARMA_OK;

@@ -116,6 +116,11 @@ struct karma_ctx {
     // records job's main stream (config 3: 1.52 against 1.2 ms per step)
     hipStream_t fork_use = nullptr;
     int64_t eq_pair_cap = 0;     // the eq path's previous pair total (its speculative scratch size)
+    // a zeroed control block the next deferred records job may use instead of
+    // its own (a native step's, kept zero by the step's status kernel): no
+    // clearing launch ahead of classify, no relabel probe (classify votes)
+    int64_t* job_ctrl = nullptr;
+    int64_t job_ctrl_words = 0;
 };
 
 namespace karma {
@@ -279,6 +284,8 @@ struct SetsDeferred {
     const int* flags = nullptr;       // [0] unsorted, [1] contig range, [2] pair capacity, [3] partition check
     const unsigned* counters = nullptr;  // [0] big reads, [3] relabel vote
     const uint8_t* ovf = nullptr;     // per bucket: overflowed the LDS tables (generic path needed)
+    int64_t* ctrl = nullptr;          // the caller's control block when the job used it (ctx->job_ctrl), else null
+    int64_t ctrl_need = 0;            // words of control block the job needed (a larger ctx->job_ctrl next time)
 };
 int sets_begin_deferred(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job, SetsDeferred* view);
 // Frees a deferred job's buffers to the allocator (stream-ordered; no wait).

@@ -607,6 +607,9 @@ __device__ __forceinline__ void hist_add(uint32_t* counts, uint32_t col) {
 #ifndef KARMA_PROF_ORD
 #define KARMA_PROF_ORD 0
 #endif
+#ifndef KARMA_PROF_BLOCKROW
+#define KARMA_PROF_BLOCKROW 0  // A/B: the block writes its waves' rows as one linear stream (profile_wave_kernel)
+#endif
 template <bool P56, bool C16, bool ORD = false>
 __device__ __forceinline__ void count_clean(const Stage& first, const uint32_t* __restrict__ packed, int64_t w0,
                                             int64_t L, int kmin, int k, const uint16_t* __restrict__ tab,
@@ -867,6 +870,92 @@ profile_wave_kernel(
     Stage st0;
     meta(c, cur);
     if (c < n) st0.load(packed, mask, cur.exc, cur.w0, lane);
+    // BLOCKROW (A/B build, KARMA_PROF_BLOCKROW): the block's waves count their
+    // consecutive contigs, then the whole block writes the rows as ONE linear
+    // stream (dense rows: the block's rows are contiguous), 3 streams per CU
+    // instead of 24 row writers (the write rate of few streams, MI355X
+    // micro-benchmarks in DESIGN.md §4.1)
+    if (KARMA_PROF_BLOCKROW && C16 && !ord_m && (M & 1) == 0 && ld == M &&
+        (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+        __shared__ int32_t bklen[16];
+        const int64_t M2 = M >> 1;
+        for (int64_t base = (int64_t)blockIdx.x * wpb; base < n; base += stride, c += stride) {
+            if (c < n) {
+                meta(c + stride, nxt);
+                const int64_t L = cur.L;
+                unsigned my = 0;
+                if (!cur.exc) {
+                    count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
+                } else {
+                    const uint8_t* craw = raw + cur.s;
+                    auto add = [&](uint32_t cl) {
+                        hist_add<C16>(counts, cl);
+                        ++my;
+                    };
+                    for_each_window(packed, mask, true, cur.w0, L - kmin + 1, win, mbuf, lane,
+                                    [&](int64_t i, const Window& v) {
+                        if (P56) {
+                            if (v.clean(5)) add(tab[v.code(5)]);
+                            else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 5, true))]);
+                            if (i + 6 <= L) {
+                                if (v.clean(6)) {
+                                    const uint32_t c6 = v.code(6);
+                                    if (pal6_code(c6)) add(tab[1024u + (c6 >> 6)]);
+                                } else if (pal_bytes(craw + i, 6)) {
+                                    add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 6, true))]);
+                                }
+                            }
+                        } else {
+                            if (v.clean(k)) add(tab[v.code(k)]);
+                            else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
+                        }
+                    }, &st0);
+                }
+                if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
+                my = wave_total(my);
+                if (lane == 0) {
+                    row_tot[c] = (int64_t)my;
+                    bklen[wave] = cur.klen;
+                }
+                wave_lds_sync();
+                lut[lane] = lane ? (double)lane / (double)cur.klen : 0.0;  // IEEE correctly rounded (kmer.py:120)
+                cur = nxt;
+            }
+            __syncthreads();
+            // rows [base, base + nr): pair q = (row r, columns 2j, 2j + 1)
+            const int nr = (int)min<int64_t>(wpb, n - base);
+            const int64_t np = (int64_t)nr * M2;
+            const uint64_t u = (uint64_t)(out + base * M);
+            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+            const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u)),
+                0, (int)(np * 16), 0x00020000);
+            int r = (int)((int64_t)threadIdx.x / M2);
+            int64_t j = (int64_t)threadIdx.x - (int64_t)r * M2;
+            for (int64_t q = threadIdx.x; q < np; q += blockDim.x) {
+                uint32_t* cr = lds + (t_pad / 2) + r * (h_words + kProfWin);
+                const double* lr = reinterpret_cast<const double*>(cr + h_words);
+                const uint32_t ab = cr[j];
+                cr[j] = 0;
+                const uint32_t a = ab & 0xFFFFu, b = ab >> 16;
+                const int32_t kl = bklen[r];
+                if ((a | b) && kl == 0) *err = 1;
+                const double x = a < 64u ? lr[a] : (double)a / (double)kl;
+                const double y = b < 64u ? lr[b] : (double)b / (double)kl;
+                const u32x4_t w = {(uint32_t)__double2loint(x), (uint32_t)__double2hiint(x), (uint32_t)__double2loint(y),
+                                   (uint32_t)__double2hiint(y)};
+                __builtin_amdgcn_raw_buffer_store_b128(w, rr, (int)(q * 16), 0, KARMA_ROW_AUX >= 0 ? KARMA_ROW_AUX : 0);
+                j += blockDim.x;
+                while (j >= M2) {
+                    j -= M2;
+                    ++r;
+                }
+            }
+            __syncthreads();  // histograms clear, tables free for the next contigs
+        }
+        return;
+    }
     for (; c < n; c += stride) {
         meta(c + stride, nxt);
         const int64_t L = cur.L;

@@ -487,25 +487,40 @@ __global__ void __launch_bounds__(256) step_pack_kernel(const uint64_t* __restri
 // entry (seq written last, released to the host).  With several processes the
 // merge's word carries the other ranks' verdicts (step_pack_kernel), so every
 // rank's entry asks for the same re-runs and the collectives stay matched.
+// ctrl (n_ctrl words): the records job's control block when it was the
+// step's own (SetsDeferred::ctrl): zeroed once every word is read, for the
+// next records job of this tail (no clearing launch ahead of its classify).
 __global__ void step_status_kernel(const int* __restrict__ flags, const unsigned* __restrict__ counters,
                                    const uint8_t* __restrict__ ovf, int B, const int64_t* __restrict__ dst,
                                    int64_t* __restrict__ merge_bad, const int64_t* __restrict__ est,
-                                   StepStatus* __restrict__ out, uint64_t seq) {
+                                   StepStatus* __restrict__ out, uint64_t seq, int64_t* __restrict__ ctrl,
+                                   int64_t n_ctrl) {
     __shared__ int any_ovf;
+    __shared__ int64_t words[4];
     if (threadIdx.x == 0) any_ovf = 0;
     __syncthreads();
     for (int b = threadIdx.x; b < B; b += blockDim.x)
         if (ovf[b]) any_ovf = 1;
+    if (threadIdx.x == 0) {
+        words[0] = (int64_t)flags[0] | (int64_t)flags[1] << 8 | (int64_t)flags[2] << 16 | (int64_t)flags[3] << 24;
+        words[1] = (int64_t)(counters[0] != 0) | (int64_t)(counters[3] != 0) << 1;
+        words[2] = dst[B];
+    }
     __syncthreads();
+    if (ctrl)
+        for (int64_t i = threadIdx.x; i < n_ctrl; i += blockDim.x) ctrl[i] = 0;
     if (threadIdx.x != 0) return;
+    const int fw = (int)words[0];
+    const int f0 = fw & 255, f1 = (fw >> 8) & 255, f2 = (fw >> 16) & 255, f3 = (fw >> 24) & 255;
+    const bool c0 = words[1] & 1, c3 = (words[1] >> 1) & 1;
     int64_t slow = 0, err = 0;
-    if (counters[3]) slow |= 1;
-    if (flags[2]) slow |= 2;
-    if (counters[0]) slow |= 4;
+    if (c3) slow |= 1;
+    if (f2) slow |= 2;
+    if (c0) slow |= 4;
     if (any_ovf) slow |= 8;
-    if (flags[0]) err |= 1;
-    if (flags[1]) err |= 2;
-    if (flags[3]) err |= 4;
+    if (f0) err |= 1;
+    if (f1) err |= 2;
+    if (f3) err |= 4;
     if (est[0]) err |= 8;
     if (est[1]) err |= 2;  // a key past the contig range
     if (merge_bad) {
@@ -516,7 +531,7 @@ __global__ void step_status_kernel(const int* __restrict__ flags, const unsigned
     }
     out->slow = slow;
     out->err = err;
-    out->U = dst[B];
+    out->U = words[2];
     out->E = est[2];
     __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -579,7 +594,9 @@ struct karma_step {
         DevArray<uint32_t> ea, eb;
         DevArray<int64_t> es;
         DevArray<double> ew;
+        DevArray<int64_t> ctrl;        // the records job's control block, kept zero by the status kernel
         void release() {
+            ctrl.release();
             prof.release();
             sk.release();
             rk.release();
@@ -646,6 +663,11 @@ struct karma_step {
     // deferred steps by mode (karma_step_info): two main streams, tail on the exchange stream
     int64_t n_two = 0, n_xs = 0;
     int stall_s = 120;             // KARMA_STEP_STALL_S: a deferred status this late is KARMA_ERR_STALL
+    // deferred records jobs use this step's own control blocks (tail[par].ctrl),
+    // kept zero by the status kernel: no probe / clearing launch at their head,
+    // the relabel decided in classify (KARMA_STEP_OWN_CTRL=0: the job's own
+    // block and the probe kernel)
+    bool own_ctrl = true;
     void* ring_mem = nullptr;      // this step's own mapped status ring (two steps on one context never share it)
 };
 
@@ -1068,12 +1090,27 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // batch's classify (config 3: 1.15 against 1.20-1.22 ms per step,
     // profiles/r04/measurements.md (ab_mark3)); with two, after the final kernel
     ctx->mark_pos = two ? kMarkTwo : kMarkOne;
+    ctx->job_ctrl = s->own_ctrl ? tl.ctrl.ptr : nullptr;  // zero: the last status kernel of this tail cleared it
+    ctx->job_ctrl_words = s->own_ctrl ? (int64_t)tl.ctrl.n : 0;
     const int jrc = sets_begin_deferred(ctx, reinterpret_cast<const uint2*>(rec), A, s->n_glob, &job, &v);
+    ctx->job_ctrl = nullptr;
+    ctx->job_ctrl_words = 0;
     ctx->mark_pos = -1;
     ctx->no_fork = false;
     ctx->fork_use = nullptr;
     KARMA_TRY(jrc);
     std::unique_ptr<SetsJob, void (*)(SetsJob*)> jg(job, sets_release);
+    if (s->own_ctrl && !v.ctrl) {
+        // the job needed a larger block than this tail's: grow it for the next
+        // job on this tail (with every stream idle: the old block may still
+        // be cleared by a status kernel), zeroed in stream order
+        KARMA_HIP(hipStreamSynchronize(s->side_s));
+        KARMA_HIP(hipStreamSynchronize(s->side_alt_s));
+        KARMA_HIP(hipStreamSynchronize(s->main_s));
+        KARMA_HIP(hipStreamSynchronize(s->alt_s));
+        KARMA_TRY(tl.ctrl.alloc(ctx, (size_t)(v.ctrl_need + v.ctrl_need / 4 + 64)));
+        KARMA_HIP(hipMemsetAsync(tl.ctrl.ptr, 0, tl.ctrl.n * 8, ms));
+    }
     // side stream: presence, column table (M stays on the device), then the
     // profile behind the graph's final kernel (sequential: all on the main
     // stream, every kernel alone on the chip -- the per-kernel timing pass)
@@ -1182,7 +1219,9 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         KARMA_TRY(ensure_arr(ctx, tl.mk, cap));
         KARMA_TRY(ensure_arr(ctx, tl.mc, cap));
         const int64_t tiles_cap = (cap + kMT - 1) / kMT + s->nranks;
-        KARMA_LAUNCH(ctx, "merge_rank", step_merge_kernel, (int)std::min<int64_t>(tiles_cap, 2 * cu), 256, 0, mkeys,
+        // a tile per block up to 8 blocks per CU (the tiles' searches are
+        // dependent loads: more tiles in flight, not more tiles per block)
+        KARMA_LAUNCH(ctx, "merge_rank", step_merge_kernel, (int)std::min<int64_t>(tiles_cap, 8 * cu), 256, 0, mkeys,
                      mcounts, v.dst, v.split_loc, rs, tl.mk.ptr, tl.mc.ptr, tl.mbad.ptr);
         lk = tl.mk.ptr;
         lc = tl.mc.ptr;
@@ -1195,7 +1234,10 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     KARMA_TRY(ensure_arr(ctx, tl.eb, cap));
     KARMA_TRY(ensure_arr(ctx, tl.es, cap));
     KARMA_TRY(ensure_arr(ctx, tl.ew, cap));
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((cap + kET - 1) / kET, cu));
+    // the edge stage's tiles are chains of dependent loads (keys, totals): up
+    // to 4 blocks per CU take a tile each (one block per CU striding over 12
+    // tiles at the 8-rank weak preview's 3.2M keys took 29 + 46 us)
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((cap + kET - 1) / kET, 4 * cu));
     KARMA_LAUNCH(ctx, "edge_count", step_edge_count_kernel, grid, kET, 0, lk, lc, n_dev, s->n_glob, tl.tot.ptr,
                  tl.tile_cnt.ptr, tl.est.ptr);
     // the owners' readset totals from every owner (fixed sizes: no host wait)
@@ -1203,7 +1245,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     KARMA_LAUNCH(ctx, "edge_weights", step_edge_write_kernel, grid, kET, 0, lk, lc, n_dev, tl.tot.ptr,
                  tl.tile_cnt.ptr, tl.ea.ptr, tl.eb.ptr, tl.es.ptr, tl.ew.ptr, tl.est.ptr, s->n_glob);
     KARMA_LAUNCH(ctx, "step_status", step_status_kernel, 1, 256, 0, v.flags, v.counters, v.ovf, v.B, v.dst, mbad,
-                 tl.est.ptr, s->ring_d + seq % kRing, seq);
+                 tl.est.ptr, s->ring_d + seq % kRing, seq, v.ctrl, v.ctrl ? v.ctrl_need : (int64_t)0);
     if (xs_on) {
         if (!s->ev_tail[par]) KARMA_HIP(hipEventCreateWithFlags(&s->ev_tail[par], hipEventDisableTiming));
         if (counted_call("hipEventRecord")) ++t_hip_calls;
@@ -1255,6 +1297,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     if (const char* e = getenv("KARMA_STEP_DEFER_RANKS")) s->defer_ranks = atoi(e) != 0;
     if (const char* e = getenv("KARMA_STEP_XSTREAM")) s->xstream = atoi(e) != 0;
     if (const char* e = getenv("KARMA_STEP_STALL_S")) s->stall_s = std::max(1, atoi(e));
+    if (const char* e = getenv("KARMA_STEP_OWN_CTRL")) s->own_ctrl = atoi(e) != 0;
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
