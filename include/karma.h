@@ -378,7 +378,8 @@ int karma_step_sync(karma_step* s);
 /* [M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending, host ns inside
  * karma_step_run, of which ns waiting for a deferred step's status, deferred steps on two main
  * streams, deferred steps whose tail ran on the exchange stream, mode bits (1 one communicator,
- * 2 exchange stream allowed, 4 deferral across ranks allowed), ranks] (first n).  After
+ * 2 exchange stream allowed, 4 deferral across ranks allowed), ranks, deferred records jobs on the
+ * step's own (pre-zeroed) control block] (first n).  After
  * karma_step_sync, M and E are the newest step's also when it was deferred (E: this rank's
  * edges). */
 int karma_step_info(karma_step* s, int64_t* info, int n);

@@ -276,6 +276,12 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
+#ifndef KARMA_KARG_REREAD
+#define KARMA_KARG_REREAD 1  // classify reads its rarely used arguments from the argument segment where used
+#endif
+#ifndef KARMA_SKIP_PLAIN
+#define KARMA_SKIP_PLAIN 0  // A/B: the relabel word read with a plain load (a vote seen late or not at all)
+#endif
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
@@ -315,22 +321,28 @@ template <bool HIST, bool COMPACT, bool REMAP = false, bool BIN = false>
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
 classify2_kernel(ClassArgs P, BinArgs Q) {
     static_assert(!(HIST && BIN), "the binned classify has no partition block histograms");
+    // BIN's arguments are read where used, straight from the kernel argument
+    // segment behind an opaque pointer (Q follows P at its natural alignment):
+    // held in SGPRs across the walk they pushed its mask registers into spills
+    constexpr size_t kQOff = (sizeof(ClassArgs) + alignof(BinArgs) - 1) / alignof(BinArgs) * alignof(BinArgs);
+    auto QA = [&]() -> const BinArgs& {
+        if (!KARMA_KARG_REREAD) return Q;
+        const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        return *reinterpret_cast<const BinArgs*>(ka + kQOff);
+    };
+    // the same for P's fields the walk does not use (the rare pass, the chunk's end)
+    auto PA = [&]() -> const ClassArgs& {
+        if (!KARMA_KARG_REREAD) return P;
+        const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        return *reinterpret_cast<const ClassArgs*>(ka);
+    };
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
     const int64_t c_lo = chunk * P.chunk;
     if (c_lo >= P.A) return;  // waves are independent (wave-private LDS only)
-    // the relabel word (set by the probe kernel, or by this kernel's votes:
-    // read past the L2 of this XCD)
-    if (P.skip && __hip_atomic_load(P.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        if (lane == 0) {
-            P.n_codes[chunk] = 0;
-            P.n_gen[chunk] = 0;
-            if (BIN)
-                for (int i = 0; i < kBinHdr; ++i) Q.hdr[kBinHdr * chunk + i] = uint4{0u, 0u, 0u, 0u};
-        }
-        return;
-    }
     const int64_t c_hi = min(P.A, c_lo + P.chunk);
     uint32_t* out = P.codes + c_lo;
     // the chunk's region as a buffer resource built from wave-uniform values
@@ -355,7 +367,6 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     __shared__ uint32_t bcnt[kCW / 64][BIN ? kBinMaxBc : 1];
     uint16_t* const q = bq[wave];
     uint32_t* const qn = bcnt[wave];
-    uint16_t* const seg_out = BIN ? Q.segs + chunk * Q.seg_cap * kBinQ : nullptr;
     // back-segment bookkeeping, touched only when a queue fills (kept in LDS,
     // not in registers across the walk): [0] back count, [1..2] back mask,
     // [3..6] the first 16 directory bytes (for the header)
@@ -392,13 +403,14 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)bk, L);
             wave_lds_order();
             const uint32_t nbk = (uint32_t)__builtin_amdgcn_readfirstlane((int)bst[0]);
-            uint16_t* const dst = seg_out + (Q.seg_cap - 1 - (int64_t)nbk) * kBinQ;
+            const BinArgs& Qa = QA();
+            uint16_t* const dst = Qa.segs + (chunk * Qa.seg_cap + Qa.seg_cap - 1 - (int64_t)nbk) * kBinQ;
             if (lane < 8) {
                 const u32x4 v = *reinterpret_cast<const u32x4*>(q + fb * kBinQ + 8 * lane);
                 *reinterpret_cast<u32x4*>(dst + 8 * lane) = v;
             }
             if (lane == 0) {
-                Q.dir[chunk * Q.dir_cap + nbk] = (uint8_t)fb;
+                Qa.dir[chunk * Qa.dir_cap + nbk] = (uint8_t)fb;
                 bst[0] = nbk + 1;
                 bst[1 + (fb >> 5)] |= 1u << (fb & 31);
                 if (nbk < 16) bst[3 + (nbk >> 2)] |= fb << (8 * (nbk & 3));
@@ -564,12 +576,15 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                 } else {
                     const uint64_t g = e & ~big & ~ok;
                     if (g) {
-                        if (in_mask(g)) out[P.chunk - 1 - (ng + rank_below(g))] = pos;
+                        if (in_mask(g)) (BIN ? PA().codes + c_lo : out)[P.chunk - 1 - (ng + rank_below(g))] = pos;
                         ng += __popcll(g);
                     }
                     const uint64_t bg = e & big;
                     if (bg) {
-                        if (in_mask(bg)) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + pos;
+                        if (in_mask(bg)) {
+                            const ClassArgs& Pa = PA();
+                            Pa.big_list[atomicAdd(Pa.big_n, 1u)] = c_lo + pos;
+                        }
                     }
                 }
             };
@@ -667,6 +682,19 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     };
     u32x4 buf[kCPer];
     prefetch(buf, c_lo, c_hi);
+    // the relabel word (set by the probe kernel, or by this kernel's votes:
+    // read past the L2 of this XCD), once the chunk's first records are in
+    // flight (its latency hides under theirs)
+    if (P.skip && (KARMA_SKIP_PLAIN ? *P.skip : __hip_atomic_load(P.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        if (lane == 0) {
+            const ClassArgs& Pa = PA();
+            Pa.n_codes[chunk] = 0;
+            Pa.n_gen[chunk] = 0;
+            if (BIN)
+                for (int i = 0; i < kBinHdr; ++i) QA().hdr[kBinHdr * chunk + i] = uint4{0u, 0u, 0u, 0u};
+        }
+        return;
+    }
     if (!REMAP) {
         int64_t t0 = c_lo;
         for (; t0 + kCIter <= c_hi; t0 += kCIter) step(std::true_type{}, buf, buf, t0);
@@ -702,11 +730,12 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         const bool ok = !big && (hl ? rs_code2<COMPACT>(ct, h, P.N, &code) : rs_code<COMPACT>(ct, P.N, &code));
         if (BIN && ok) bin_emit(1ull, code);  // lane 0's code (uniform values)
         if (lane == 0) {
-            if (big) P.big_list[atomicAdd(P.big_n, 1u)] = c_lo + ct_pos;
+            const ClassArgs& Pa = PA();
+            if (big) Pa.big_list[atomicAdd(Pa.big_n, 1u)] = c_lo + ct_pos;
             else if (ok) {
                 if (!BIN) out[nc] = code;
                 if (hist_on) atomicAdd(&wh[(code & 0xFFFFFFu) >> P.bwc], 1u);
-            } else out[P.chunk - 1 - ng] = ct_pos;
+            } else (BIN ? Pa.codes + c_lo : out)[P.chunk - 1 - ng] = ct_pos;
         }
         nc += ok ? 1u : 0u;
         ng += !big && !ok ? 1u : 0u;
@@ -739,7 +768,8 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     return lo | hi << 16;
                 };
                 v.x = pad(v.x, 0), v.y = pad(v.y, 2), v.z = pad(v.z, 4), v.w = pad(v.w, 6);
-                *reinterpret_cast<u32x4*>(seg_out + (int64_t)k * 8) = v;
+                const BinArgs& Qa = QA();
+                *reinterpret_cast<u32x4*>(Qa.segs + chunk * Qa.seg_cap * kBinQ + (int64_t)k * 8) = v;
             }
         }
         // the header: lane w < 7 packs the nibbles of buckets 8w .. 8w + 7
@@ -756,7 +786,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         const uint32_t w5 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 5);
         const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 6);
         if (lane == 0) {
-            uint4* const h = Q.hdr + kBinHdr * chunk;
+            uint4* const h = QA().hdr + kBinHdr * chunk;
             h[0] = uint4{w0, w1, w2, w3};
             h[1] = uint4{w4, w5, w6, bst[0]};
             h[2] = uint4{bst[1], bst[2], bst[3], bst[4]};
@@ -764,9 +794,10 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         }
     }
     if (lane == 0) {
-        P.n_codes[chunk] = nc;
-        P.n_gen[chunk] = ng;
-        if (nc && !BIN) atomicAdd(P.blk_items + chunk / P.lists_per_block, (unsigned long long)nc);
+        const ClassArgs& Pa = PA();
+        Pa.n_codes[chunk] = nc;
+        Pa.n_gen[chunk] = ng;
+        if (nc && !BIN) atomicAdd(Pa.blk_items + chunk / Pa.lists_per_block, (unsigned long long)nc);
     }
     if (hist_on && nc) {
         wave_sync();
@@ -777,11 +808,12 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         }
     }
     if (lane == 0) {
-        if (bad_order) P.flags[0] = 1;
-        if (bad_contig) P.flags[1] = 1;
-        if (P.vote && chunk % kVoteStride == 0 && 8 * ng > nc + ng && nc + ng >= 64 &&
-            atomicAdd(P.vote, 1u) + 1 == (unsigned)kVotes)
-            __hip_atomic_store(P.skip, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const ClassArgs& Pa = PA();
+        if (bad_order) Pa.flags[0] = 1;
+        if (bad_contig) Pa.flags[1] = 1;
+        if (Pa.vote && chunk % kVoteStride == 0 && 8 * ng > nc + ng && nc + ng >= 64 &&
+            atomicAdd(Pa.vote, 1u) + 1 == (unsigned)kVotes)
+            __hip_atomic_store(Pa.skip, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -2456,6 +2488,10 @@ int SetsJob::setup() {
     const int64_t cw_total = ctrl_words + 2 * n_pblk + B;
     // a deferred job may take the caller's zeroed block (ctx->job_ctrl)
     ext = deferred && ctx->job_ctrl && ctx->job_ctrl_words >= cw_total;
+    if (std::getenv("KARMA_DEBUG_CTRL"))
+        std::fprintf(stderr, "[karma] records job: deferred %d, caller block %p (%lld words), needs %lld: %s\n",
+                     (int)deferred, (void*)ctx->job_ctrl, (long long)ctx->job_ctrl_words, (long long)cw_total,
+                     ext ? "caller's" : "own");
     if (ext) {
         cb = ctx->job_ctrl;
     } else {
@@ -2638,10 +2674,15 @@ int SetsJob::launch() {
     ctx->stream = main_stream;
     KARMA_TRY(rc_pair);
     if (bin) {
-        KARMA_TRY(mark(2));  // where the code partition would end
         KARMA_LAUNCH(ctx, "graph_code_reduce", code_seg_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, bsegs.ptr,
                      reinterpret_cast<const uint4*>(bhdr.ptr), bdir.ptr, n_chunks, seg_cap, dir_cap, g.bwc, n_cg,
                      part_ch.ptr, back_list_cap());
+        // position 2 ("after the code partition": the profile beside the
+        // LDS-bound reduce) is after the reduce here: its 132 KB blocks
+        // cannot share a CU with the profile's, so a profile started after
+        // classify ran first and the reduce after it (config 3 1.13 against
+        // 1.05 ms per step)
+        KARMA_TRY(mark(2));
     } else if (g.Bc > 0) {
         uint16_t* const trash = cent.ptr + (ccap + 7) / 8 * 8;
         if (append && wide_c)

@@ -204,7 +204,8 @@ __global__ void __launch_bounds__(kET) step_edge_write_kernel(
 #define KARMA_MARK_ONE 2  // deferred batches on one main stream (SetsJob::launch positions)
 #endif
 #ifndef KARMA_MARK_TWO
-#define KARMA_MARK_TWO 5  // deferred batches alternating two main streams
+#define KARMA_MARK_TWO 4  // deferred batches alternating two main streams (5, after the final kernel: 8-rank
+                          // strong preview 0.196 against 0.188 ms with the binned classify)
 #endif
 constexpr int kMarkOne = KARMA_MARK_ONE, kMarkTwo = KARMA_MARK_TWO;
 constexpr int64_t kAltMaxRecords = int64_t(1) << 27;  // batches below this alternate main streams
@@ -661,7 +662,7 @@ struct karma_step {
     bool one_comm = true;
     hipEvent_t ev_pres = nullptr, ev_pres2 = nullptr, ev_pre = nullptr;
     // deferred steps by mode (karma_step_info): two main streams, tail on the exchange stream
-    int64_t n_two = 0, n_xs = 0;
+    int64_t n_two = 0, n_xs = 0, n_own = 0;  // ... and records jobs on the step's own control block
     int stall_s = 120;             // KARMA_STEP_STALL_S: a deferred status this late is KARMA_ERR_STALL
     // deferred records jobs use this step's own control blocks (tail[par].ctrl),
     // kept zero by the status kernel: no probe / clearing launch at their head,
@@ -1100,6 +1101,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     ctx->fork_use = nullptr;
     KARMA_TRY(jrc);
     std::unique_ptr<SetsJob, void (*)(SetsJob*)> jg(job, sets_release);
+    if (v.ctrl) ++s->n_own;
     if (s->own_ctrl && !v.ctrl) {
         // the job needed a larger block than this tail's: grow it for the next
         // job on this tail (with every stream idle: the old block may still
@@ -1416,7 +1418,7 @@ int karma_step_info(karma_step* s, int64_t* info, int n) {
     const int64_t v[] = {s->M,          s->E,        s->pairs_local, s->entries,
                          s->n_sync,     s->n_deferred, s->n_redone,  (int64_t)s->pending.size(),
                          s->run_ns,     s->wait_ns,  s->n_two,       s->n_xs,
-                         mode,          s->world};
+                         mode,          s->world,    s->n_own};
     for (int i = 0; i < n && i < (int)(sizeof v / sizeof v[0]); ++i) info[i] = v[i];
     return KARMA_OK;
 }

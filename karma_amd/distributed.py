@@ -279,8 +279,8 @@ class NativeStep:
         """[M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending,
         host ns inside karma_step_run, of which ns waiting for deferred statuses, deferred steps on
         two main streams, deferred tails on the exchange stream, mode bits, ranks]."""
-        v = np.zeros(14, np.int64)
-        call("karma_step_info", self.h, ptr(v), 14)
+        v = np.zeros(15, np.int64)
+        call("karma_step_info", self.h, ptr(v), 15)
         return v
 
     def mode(self):
@@ -290,7 +290,7 @@ class NativeStep:
         return {"ranks": ranks, "one_communicator": bool(bits & 1), "exchange_stream": bool(bits & 2),
                 "defer_across_ranks": bool(bits & 4), "deferred_two_main_streams": int(v[10]),
                 "deferred_tail_on_exchange_stream": int(v[11]), "synchronous": int(v[4]), "deferred": int(v[5]),
-                "rerun": int(v[6])}
+                "rerun": int(v[6]), "deferred_on_own_control_block": int(v[14])}
 
     def close(self):
         if getattr(self, "h", None):

@@ -1,1 +1,5 @@
-bash tools/gpu_run.sh r05f tests quick=config3,strong_emu8,weak_emu8 trace=--emulate-ranks,8 && KARMA_MARK_AT=4 bash tools/gpu_run.sh r05f_m4 quick=config3,strong_emu8 && KARMA_LIB=$PWD/karma_amd/variants/libkarma_ord.so KARMA_ALLOW_VARIANT=1 bash tools/gpu_run.sh r05f_ord tests=tests/test_gpu_parity.py,tests/test_gpu_device_profile.py quick=config3,strong_emu8
+bash tools/gpu_run.sh r05h tests=tests/test_gpu_step.py quick=config3,strong_emu8 || exit 1
+for v in plainskip nokarg both; do
+  KARMA_LIB=$PWD/karma_amd/variants/libkarma_$v.so KARMA_ALLOW_VARIANT=1 bash tools/gpu_run.sh r05h_$v quick=config3,strong_emu8 || exit 1
+done
+KARMA_STEP_OWN_CTRL=0 bash tools/gpu_run.sh r05h_noown quick=config3,strong_emu8

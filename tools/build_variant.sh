@@ -16,10 +16,12 @@ HASH=$(cat $(ls $SRC/*.hip $SRC/*.h $SRC/*.cpp $REPO/include/karma.h | sort) | s
 # the variant's -D flags are recorded in karma_build_info() (bench.py refuses
 # a variant unless KARMA_ALLOW_VARIANT=1)
 /opt/rocm/bin/hipcc $FLAGS $EXTRA -DKARMA_BUILD_DEFINES="\"$EXTRA\"" -DKARMA_SRC_HASH="\"$HASH\"" -c $SRC/core.hip -o $B/core.o &
+pids="$!"
 for f in kmer graph graph_sets eq consumers comm step sort; do
   /opt/rocm/bin/hipcc $FLAGS $EXTRA -c $SRC/$f.hip -o $B/$f.o &
+  pids="$pids $!"
 done
-wait
+for p in $pids; do wait $p || { echo "compile failed"; exit 1; }; done
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fopenmp -x c++ -c $SRC/synth.cpp -o $B/synth.o
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -pthread -x c++ -c $SRC/ingest.cpp -o $B/ingest.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fopenmp -o $OUT/libkarma_$NAME.so $B/*.o -L/opt/rocm/lib/llvm/lib -Wl,-rpath,/opt/rocm/lib/llvm/lib \
