@@ -276,12 +276,6 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-#ifndef KARMA_KARG_REREAD
-#define KARMA_KARG_REREAD 1  // classify reads its rarely used arguments from the argument segment where used
-#endif
-#ifndef KARMA_SKIP_PLAIN
-#define KARMA_SKIP_PLAIN 0  // A/B: the relabel word read with a plain load (a vote seen late or not at all)
-#endif
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
@@ -321,23 +315,6 @@ template <bool HIST, bool COMPACT, bool REMAP = false, bool BIN = false>
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
 classify2_kernel(ClassArgs P, BinArgs Q) {
     static_assert(!(HIST && BIN), "the binned classify has no partition block histograms");
-    // BIN's arguments are read where used, straight from the kernel argument
-    // segment behind an opaque pointer (Q follows P at its natural alignment):
-    // held in SGPRs across the walk they pushed its mask registers into spills
-    constexpr size_t kQOff = (sizeof(ClassArgs) + alignof(BinArgs) - 1) / alignof(BinArgs) * alignof(BinArgs);
-    auto QA = [&]() -> const BinArgs& {
-        if (!KARMA_KARG_REREAD) return Q;
-        const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ka));
-        return *reinterpret_cast<const BinArgs*>(ka + kQOff);
-    };
-    // the same for P's fields the walk does not use (the rare pass, the chunk's end)
-    auto PA = [&]() -> const ClassArgs& {
-        if (!KARMA_KARG_REREAD) return P;
-        const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ka));
-        return *reinterpret_cast<const ClassArgs*>(ka);
-    };
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
@@ -403,7 +380,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)bk, L);
             wave_lds_order();
             const uint32_t nbk = (uint32_t)__builtin_amdgcn_readfirstlane((int)bst[0]);
-            const BinArgs& Qa = QA();
+            const BinArgs& Qa = Q;
             uint16_t* const dst = Qa.segs + (chunk * Qa.seg_cap + Qa.seg_cap - 1 - (int64_t)nbk) * kBinQ;
             if (lane < 8) {
                 const u32x4 v = *reinterpret_cast<const u32x4*>(q + fb * kBinQ + 8 * lane);
@@ -576,13 +553,13 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                 } else {
                     const uint64_t g = e & ~big & ~ok;
                     if (g) {
-                        if (in_mask(g)) (BIN ? PA().codes + c_lo : out)[P.chunk - 1 - (ng + rank_below(g))] = pos;
+                        if (in_mask(g)) (BIN ? P.codes + c_lo : out)[P.chunk - 1 - (ng + rank_below(g))] = pos;
                         ng += __popcll(g);
                     }
                     const uint64_t bg = e & big;
                     if (bg) {
                         if (in_mask(bg)) {
-                            const ClassArgs& Pa = PA();
+                            const ClassArgs& Pa = P;
                             Pa.big_list[atomicAdd(Pa.big_n, 1u)] = c_lo + pos;
                         }
                     }
@@ -685,13 +662,13 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // the relabel word (set by the probe kernel, or by this kernel's votes:
     // read past the L2 of this XCD), once the chunk's first records are in
     // flight (its latency hides under theirs)
-    if (P.skip && (KARMA_SKIP_PLAIN ? *P.skip : __hip_atomic_load(P.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+    if (P.skip && __hip_atomic_load(P.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         if (lane == 0) {
-            const ClassArgs& Pa = PA();
+            const ClassArgs& Pa = P;
             Pa.n_codes[chunk] = 0;
             Pa.n_gen[chunk] = 0;
             if (BIN)
-                for (int i = 0; i < kBinHdr; ++i) QA().hdr[kBinHdr * chunk + i] = uint4{0u, 0u, 0u, 0u};
+                for (int i = 0; i < kBinHdr; ++i) Q.hdr[kBinHdr * chunk + i] = uint4{0u, 0u, 0u, 0u};
         }
         return;
     }
@@ -730,7 +707,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         const bool ok = !big && (hl ? rs_code2<COMPACT>(ct, h, P.N, &code) : rs_code<COMPACT>(ct, P.N, &code));
         if (BIN && ok) bin_emit(1ull, code);  // lane 0's code (uniform values)
         if (lane == 0) {
-            const ClassArgs& Pa = PA();
+            const ClassArgs& Pa = P;
             if (big) Pa.big_list[atomicAdd(Pa.big_n, 1u)] = c_lo + ct_pos;
             else if (ok) {
                 if (!BIN) out[nc] = code;
@@ -768,7 +745,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     return lo | hi << 16;
                 };
                 v.x = pad(v.x, 0), v.y = pad(v.y, 2), v.z = pad(v.z, 4), v.w = pad(v.w, 6);
-                const BinArgs& Qa = QA();
+                const BinArgs& Qa = Q;
                 *reinterpret_cast<u32x4*>(Qa.segs + chunk * Qa.seg_cap * kBinQ + (int64_t)k * 8) = v;
             }
         }
@@ -786,7 +763,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         const uint32_t w5 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 5);
         const uint32_t w6 = (uint32_t)__builtin_amdgcn_readlane((int)nib, 6);
         if (lane == 0) {
-            uint4* const h = QA().hdr + kBinHdr * chunk;
+            uint4* const h = Q.hdr + kBinHdr * chunk;
             h[0] = uint4{w0, w1, w2, w3};
             h[1] = uint4{w4, w5, w6, bst[0]};
             h[2] = uint4{bst[1], bst[2], bst[3], bst[4]};
@@ -794,7 +771,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         }
     }
     if (lane == 0) {
-        const ClassArgs& Pa = PA();
+        const ClassArgs& Pa = P;
         Pa.n_codes[chunk] = nc;
         Pa.n_gen[chunk] = ng;
         if (nc && !BIN) atomicAdd(Pa.blk_items + chunk / Pa.lists_per_block, (unsigned long long)nc);
@@ -808,7 +785,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         }
     }
     if (lane == 0) {
-        const ClassArgs& Pa = PA();
+        const ClassArgs& Pa = P;
         if (bad_order) Pa.flags[0] = 1;
         if (bad_contig) Pa.flags[1] = 1;
         if (Pa.vote && chunk % kVoteStride == 0 && 8 * ng > nc + ng && nc + ng >= 64 &&
