@@ -190,8 +190,8 @@ struct ClassArgs {
 };
 // In-classify relabel decision (a job without the probe kernel): every
 // kVoteStride-th chunk votes when more than 1/8 of its reads are general
-// (span > 4 contig ids; the probe's threshold); the kVotes-th vote sets the
-// relabel word, and chunks that start later skip (their wave reads the word
+// (span > 4 contig ids; the probe's threshold); the kVotes-th vote (half the
+// voting chunks' in a small job) sets the relabel word, and chunks that start later skip (their wave reads the word
 // as it starts).  The pass is then wasted and reruns relabelled, as after a
 // probe; without votes every chunk runs.
 constexpr int kVoteStride = 16, kVotes = 4;
@@ -788,8 +788,11 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         const ClassArgs& Pa = P;
         if (bad_order) Pa.flags[0] = 1;
         if (bad_contig) Pa.flags[1] = 1;
+        // kVotes, or half the voting chunks of a small job
+        const int64_t voters = ((Pa.A + Pa.chunk - 1) / Pa.chunk + kVoteStride - 1) / kVoteStride;
+        const unsigned need = (unsigned)min<int64_t>(kVotes, (voters + 1) / 2);
         if (Pa.vote && chunk % kVoteStride == 0 && 8 * ng > nc + ng && nc + ng >= 64 &&
-            atomicAdd(Pa.vote, 1u) + 1 == (unsigned)kVotes)
+            atomicAdd(Pa.vote, 1u) + 1 == need)
             __hip_atomic_store(Pa.skip, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -2582,7 +2585,7 @@ int SetsJob::launch() {
                 KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true>), cg, kCW, 0, C, Bn);
             return KARMA_OK;
         };
-        if (!relabeled) {
+        if (probe) {
             // a probe of the reads decides: when many span more than 4 contig
             // ids, this pass is skipped and a relabelled rerun follows
             KARMA_LAUNCH(ctx, "relabel_probe", relabel_probe_kernel, 1, kRelabelProbes, 0, rec, A, (uint32_t)N,

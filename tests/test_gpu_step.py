@@ -109,26 +109,62 @@ def test_deferred_steps_then_kept_step_match_oracle(emulate, n_rate):
         r.close()
 
 
-def test_deferred_steps_slow_path_runs_again():
+@pytest.mark.parametrize("big", [True, False])
+def test_deferred_steps_slow_path_runs_again(big):
     """Shuffled contig ids (most reads leave the compact path: the relabel vote)
-    plus reads of > 8 records: the deferred step's status calls for the general
-    path and the step runs again synchronously; the next deferred steps run
-    synchronously for a while; results stay exact."""
+    plus (big) reads of > 8 records: the deferred step's status calls for the
+    general path and the step runs again synchronously; the next deferred steps
+    run synchronously for a while; results stay exact.  Without big reads the
+    relabel verdict alone calls for the rerun: on the step's own control block
+    (from the second deferred step of each main stream) it comes from
+    classify's chunk votes, not from the probe kernel."""
     n = 4000
     rec = np.ascontiguousarray(engine.synth_records(SEED, n, 0, 200_000, True))
     perm = np.random.default_rng(3).permutation(n).astype(np.uint32)
     rec[:, 1] = perm[rec[:, 1]]
-    rng = np.random.default_rng(4)
-    r0 = int(rec[-1, 0]) + 1
-    big = np.array([(r0 + i, int(c)) for i in range(200) for c in rng.integers(0, n, 12)], np.uint32)
-    rec = np.concatenate([rec, big])
+    if big:
+        rng = np.random.default_rng(4)
+        r0 = int(rec[-1, 0]) + 1
+        extra = np.array([(r0 + i, int(c)) for i in range(200) for c in rng.integers(0, n, 12)], np.uint32)
+        rec = np.concatenate([rec, extra])
     r = Run(n, rec)
     try:
-        for _ in range(3):
+        for _ in range(3 if big else 12):
             r.step(count=False)
         r.build.sync()
         info = r.build.native.info()
         assert info[6] >= 1, info  # run again on the general path
+        if not big:
+            assert info[14] >= 1, info  # some verdicts came from the votes on the step's own block
+        res = r.step(keep=True)
+        check_edges(res["edges"], oracle_graph(rec, n))
+    finally:
+        r.close()
+
+
+def test_deferred_steps_on_own_control_block_launch_no_probe():
+    """From the second deferred step of each main stream on, the records job
+    takes the step's own zeroed control block: no relabel probe launch ahead of
+    classify (the relabel verdict comes from classify's votes); results exact."""
+    n = 3000
+    rec = engine.synth_records(SEED, n, 0, 300_000, True)
+    r = Run(n, rec)
+    try:
+        for _ in range(3):
+            r.step(count=False)  # each main stream's first job sizes its control block
+        r.build.sync()
+        own0 = int(r.build.native.info()[14])
+        r.ctx.timing(True, "relabel_probe")
+        r.ctx.timing_reset()
+        for _ in range(6):
+            r.step(count=False)
+        r.build.sync()
+        probes = r.ctx.timing_read().get("relabel_probe", (0.0, 0))[1]
+        r.ctx.timing(False)
+        info = r.build.native.info()
+        assert int(info[14]) - own0 == 6, info
+        assert probes == 0, probes
+        assert info[6] == 0, info
         res = r.step(keep=True)
         check_edges(res["edges"], oracle_graph(rec, n))
     finally:

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--prefix", default="tr")
     ap.add_argument("--last-ms", type=float, default=1.0)
     ap.add_argument("--min-api-us", type=float, default=2.0)
+    ap.add_argument("--back-ms", type=float, default=0.0, help="end the window this long before the last kernel")
     a = ap.parse_args()
     ev = []
     for r in load(os.path.join(a.dir, f"{a.prefix}_kernel_trace.csv")):
@@ -37,11 +38,13 @@ def main():
         if (e - s) / 1e3 >= a.min_api_us:
             ev.append(("A", s, e, r["Function"], r["Thread_Id"]))
     ev.sort(key=lambda x: x[1])
-    t_end = max(x[2] for x in ev if x[0] == "K")
+    t_end = max(x[2] for x in ev if x[0] == "K") - int(a.back_ms * 1e6)
     t0 = t_end - int(a.last_ms * 1e6)
     gpu_busy_until = None
     busy = 0
     for kind, s, e, name, sid in ev:
+        if s > t_end:
+            break
         if e < t0:
             if kind != "A":
                 gpu_busy_until = max(gpu_busy_until or 0, e)
