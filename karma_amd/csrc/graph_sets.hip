@@ -1348,7 +1348,7 @@ constexpr int kWin = 16;
 // slots: 64 ints of LDS per wave of the block.
 template <typename Bounds, typename Count>
 __device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int64_t r_lo, int64_t r_hi, int threads,
-                                            Bounds bounds, Count count, bool* stop, int* slots) {
+                                            Bounds bounds, Count count, const int* stop, int* slots) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int* const wslot = slots + wave * 64;
     // stop == nullptr: nothing stops the block early, so the waves run without
@@ -1400,7 +1400,7 @@ __device__ __forceinline__ void stream_runs(const u32x4* __restrict__ data, int6
         }
         if (pipe) {
             if (r0 + threads >= r_hi) break;  // this wave's last batch
-        } else if (__syncthreads_or(stop != nullptr && *stop)) {
+        } else if (__syncthreads_or(stop != nullptr && *stop != 0)) {
             return;
         }
     }
@@ -1698,14 +1698,15 @@ __global__ void __launch_bounds__(kRT) pair_reduce_kernel(const uint32_t* __rest
     if (threadIdx.x == 0) ovf = 0;
     __syncthreads();
     const uint32_t bmask = (1u << bbits) - 1u, abase = (uint32_t)bucket << bw;
-    bool full = false;
+    // a full table (rare) is flagged in LDS: a local flag whose address the
+    // stream's stop check takes lived in scratch (a scratch access per pair)
     auto add = [&](uint32_t e) {
         if (e == kEmpty) return;
         const uint32_t al = e >> bbits, d = (e & bmask) - (abase + al);
         if (d < D)
             __hip_atomic_fetch_add(&band[(al << dbits) | d], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        else
-            full |= !t.insert(e, 1u);
+        else if (!t.insert(e, 1u))
+            ovf = 1;
     };
     stream_runs(
         reinterpret_cast<const u32x4*>(pent), f_lo, f_hi, kRT,
@@ -1716,10 +1717,9 @@ __global__ void __launch_bounds__(kRT) pair_reduce_kernel(const uint32_t* __rest
         },
         [&](const u32x4 v) {
             add(v.x), add(v.y), add(v.z), add(v.w);
-            if (nuniq > kHashR - kHashR / 8) full = true;  // early out: the bucket goes generic
+            if (nuniq > kHashR - kHashR / 8) ovf = 1;  // early out: the bucket goes generic
         },
-        &full, slots);
-    if (full) ovf = 1;
+        &ovf, slots);
     __syncthreads();
     if (ovf) {
         if (threadIdx.x == 0) overflow[bucket] = 1;

@@ -669,6 +669,8 @@ struct karma_step {
     // the relabel decided in classify (KARMA_STEP_OWN_CTRL=0: the job's own
     // block and the probe kernel)
     bool own_ctrl = true;
+    bool emu_xs = false;  // KARMA_STEP_EMU_XS=1 (A/B; see run_deferred)
+    int lag = kLag;      // KARMA_STEP_LAG (A/B): deferred steps in flight before the host waits
     void* ring_mem = nullptr;      // this step's own mapped status ring (two steps on one context never share it)
 };
 
@@ -981,7 +983,7 @@ bool entry_done(const karma_step* s, uint64_t seq) {
 int drain(karma_step* s, bool wait, bool lag) {
     while (!s->pending.empty()) {
         karma_step::Pending p = s->pending.front();
-        const bool must = wait || (lag && (int)s->pending.size() >= kLag);
+        const bool must = wait || (lag && (int)s->pending.size() >= s->lag);
         // several processes: a step's entry is read at the same point of the
         // step sequence on every rank (a rerun issues collectives)
         if (s->world > 1 && !must) break;
@@ -1051,7 +1053,12 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // the exchange stream carries the tail: with two main streams, and with
     // one communicator also behind one main stream (it then holds every
     // collective of the step, the presence all-gather included)
-    const bool xs_on = s->world > 1 && !sequential && s->xstream && (two || s->one_comm);
+    // (emulated ranks, KARMA_STEP_EMU_XS=1: the same stream layout as several
+    // processes, the tail on the exchange stream; its 8 more event calls per
+    // step cost more than the overlap gains: 8-rank strong preview 0.200 /
+    // 0.204 against 0.193 / 0.186 ms with the tail on the main stream, same box)
+    const bool xs_on = !sequential && s->xstream &&
+                       ((s->world > 1 && (two || s->one_comm)) || (s->world == 1 && s->emulate && s->emu_xs && two));
     if (two) ++s->n_two;
     if (xs_on) ++s->n_xs;
     const int par = sequential || !two ? 0 : (int)(seq & 1);
@@ -1152,7 +1159,11 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         // KARMA_STEP_HEADROOM (A/B): profile blocks per CU left free for the
         // main stream's kernels (one main stream only)
         static const int headroom = getenv("KARMA_STEP_HEADROOM") ? atoi(getenv("KARMA_STEP_HEADROOM")) : 0;
-        ctx->grid_headroom = two || sequential ? 0 : headroom;
+        // two main streams: KARMA_STEP_PROF_SPREAD=1 (A/B) launches one block per
+        // 8 contigs instead of a resident grid, so the other streams' blocks
+        // dispatch as the profile's retire
+        static const int spread = getenv("KARMA_STEP_PROF_SPREAD") ? atoi(getenv("KARMA_STEP_PROF_SPREAD")) : 0;
+        ctx->grid_headroom = sequential ? 0 : two ? (spread ? -64 : 0) : headroom;
         rc = kmer_profile_device_m(plan, tl.prof.ptr, m_dev);
         ctx->grid_headroom = 0;
     }
@@ -1300,6 +1311,8 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     if (const char* e = getenv("KARMA_STEP_XSTREAM")) s->xstream = atoi(e) != 0;
     if (const char* e = getenv("KARMA_STEP_STALL_S")) s->stall_s = std::max(1, atoi(e));
     if (const char* e = getenv("KARMA_STEP_OWN_CTRL")) s->own_ctrl = atoi(e) != 0;
+    if (const char* e = getenv("KARMA_STEP_EMU_XS")) s->emu_xs = atoi(e) != 0;
+    if (const char* e = getenv("KARMA_STEP_LAG")) s->lag = std::max(1, std::min(kRing / 2, atoi(e)));
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
