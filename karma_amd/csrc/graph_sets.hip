@@ -2523,6 +2523,10 @@ int SetsJob::setup() {
                     : 0;
     // binned: one group per ~64 chunks at most (a wave's batch), up to one block per CU
     if (bin) n_cg = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count / g.Bc, ceil_div(n_chunks, 64)));
+    if (bin) {  // KARMA_BIN_CG (A/B): at most this many groups per bucket
+        static const int cap = std::getenv("KARMA_BIN_CG") ? std::atoi(std::getenv("KARMA_BIN_CG")) : 0;
+        if (cap > 0) n_cg = std::min(n_cg, cap);
+    }
     // pair-reduce groups per bucket: enough blocks to fill the chip while
     // buckets are few; one group from KARMA_ONE_GROUP_B buckets on, so the
     // final kernel copies the bucket's single list instead of re-hashing

@@ -121,6 +121,11 @@ struct karma_ctx {
     // clearing launch ahead of classify, no relabel probe (classify votes)
     int64_t* job_ctrl = nullptr;
     int64_t job_ctrl_words = 0;
+    // the next k-mer plan may take this zeroed block for its presence bitmap
+    // and exception counter (no clearing memset); its column table kernel
+    // clears it again (karma_step, per side stream)
+    uint32_t* plan_zeroed = nullptr;
+    int64_t plan_zeroed_words = 0;
 };
 
 namespace karma {

@@ -52,6 +52,11 @@ struct karma_kmer_plan {
     uint32_t S = 0;  // ordinal space
     int64_t nwords = 0;
     DevArray<uint32_t> presence;
+    // the bitmap (nwords, padded to even) then the exception k-mer counter (2
+    // words): inside `presence`, or the caller's zeroed block (bits_ext:
+    // ctx->plan_zeroed, karma_step's; the column table kernel clears it again)
+    uint32_t* bits = nullptr;
+    bool bits_ext = false;
     DevArray<uint64_t> exc_keys;  // sorted unique
     int64_t n_exc = 0;
     DevArray<int32_t> col_of_ord;
@@ -340,18 +345,28 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
                                                           int nwords, bool with_len, uint32_t* __restrict__ presence,
                                                           uint64_t* __restrict__ exc_buf, int64_t exc_cap,
                                                           unsigned long long* __restrict__ exc_cnt,
-                                                          int64_t c_begin, const int* __restrict__ full,
+                                                          int64_t c_begin, uint32_t n_can,
                                                           const uint32_t* __restrict__ exc_list,
                                                           const unsigned* __restrict__ exc_n) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_bits[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
-    // once every ACGT ordinal is present, only contigs with exception bases can
-    // still add columns (tested between the two launches, see saturation_kernel)
-    const bool saturated = full != nullptr && *full != 0;
     uint32_t* wbuf = lds_bits + nwords + wave * 80;
     uint16_t* mbuf = reinterpret_cast<uint16_t*>(lds_bits + nwords + wpb * 80) + wave * 80;
+    // the second pass (n_can = the ACGT ordinals that can occur: 4^k, or
+    // 1,024 + 64 for 5p6): once all are present, only contigs with exception
+    // bases can still add columns.  Each block counts the bitmap's bits itself
+    // (no saturation launch between the passes)
+    __shared__ unsigned present;
+    if (threadIdx.x == 0) present = 0;
+    __syncthreads();
+    if (n_can) {
+        unsigned c = 0;
+        for (int w = threadIdx.x; w < nwords; w += blockDim.x) c += __popc(presence[w]);
+        if (c) atomicAdd(&present, c);
+    }
     for (int w = threadIdx.x; w < nwords; w += blockDim.x) lds_bits[w] = 0;
     __syncthreads();
+    const bool saturated = n_can != 0 && present >= n_can;
     const int kmin = P56 ? 5 : k;
     auto push_exc = [&](uint64_t key) {
         const unsigned long long slot = atomicAdd(exc_cnt, 1ull);
@@ -380,14 +395,22 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
         });
     };
     const int64_t w0 = (int64_t)blockIdx.x * wpb + wave, ws = (int64_t)gridDim.x * wpb;
-    if (saturated) {  // only the listed contigs past the prefix (scanned before)
+    if (!n_can) {  // the first pass: every contig of the prefix
+        for (int64_t c = c_begin + w0; c < n; c += ws) scan(c);
+    } else {
+        // Blocks may see different verdicts (a late block can find the set
+        // completed by other blocks' flushes), so the contigs with exception
+        // bases are listed out independently of it (slots of the store's
+        // list) and an unsaturated block adds the ACGT-only contigs of its
+        // contig slots: a saturated set gains nothing from those
         const int64_t ne = *exc_n;
         for (int64_t i = w0; i < ne; i += ws) {
             const int64_t c = exc_list[i];
             if (c >= c_begin && c < n) scan(c);
         }
-    } else {
-        for (int64_t c = c_begin + w0; c < n; c += ws) scan(c);
+        if (!saturated)
+            for (int64_t c = c_begin + w0; c < n; c += ws)
+                if (!has_exc[c]) scan(c);
     }
     __syncthreads();
     // OR-flush only the bits the global bitmap lacks: every block of the
@@ -399,33 +422,19 @@ __global__ void __launch_bounds__(kBlock) presence_kernel(const uint32_t* __rest
     }
 }
 
-// Sets *full when every ACGT ordinal that can occur is present: all 4^k codes,
-// or for 5p6 the 1024 5-mers and the 64 palindromic 6-mers.
-__global__ void saturation_kernel(const uint32_t* __restrict__ presence, uint32_t S, bool p56, int* __restrict__ full) {
-    __shared__ int missing;
-    if (threadIdx.x == 0) missing = 0;
-    __syncthreads();
-    for (uint32_t o = threadIdx.x; o < S; o += blockDim.x) {
-        bool can = true;
-        if (p56 && o % 5 != 0) can = pal6_code(((o / 5) << 2) | (o % 5 - 1));
-        if (can && !((presence[o >> 5] >> (o & 31)) & 1u)) missing = 1;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) *full = missing ? 0 : 1;
-}
-
 // ----------------------------------------------------------- column table ---
 // One block: merges present ACGT ordinals with the sorted exception keys in
 // byte-key order (= Python sorted() over str, kmer.py:172).
 constexpr int kColBlock = 1024;
 
-__global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* __restrict__ presence, int nwords,
+__global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* presence, int nwords,
                                                             uint32_t S, bool p56, int k, bool with_len,
                                                             const uint64_t* __restrict__ exc, int64_t X,
                                                             int32_t* __restrict__ col_of_ord,
                                                             int32_t* __restrict__ col_of_exc,
                                                             uint64_t* __restrict__ col_keys, int64_t* __restrict__ M_out,
-                                                            int64_t* __restrict__ M_host) {
+                                                            int64_t* __restrict__ M_host, uint32_t* clear,
+                                                            int clear_words) {
     extern __shared__ __attribute__((aligned(16))) uint32_t prefix[];  // nwords + 1
     // exclusive popcount prefix over the bitmap (nwords <= 2048)
     __shared__ uint32_t chunk_sum[kColBlock];
@@ -493,6 +502,12 @@ __global__ void __launch_bounds__(kColBlock) columns_kernel(const uint32_t* __re
         *M_out = (int64_t)n_present + X;
         // karma_step: also into mapped host memory, read there once the step is done
         if (M_host) __hip_atomic_store(M_host, (int64_t)n_present + X, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // a caller's bitmap block (karma_step): cleared for the next plan on this
+    // stream once every read above is done
+    if (clear) {
+        __syncthreads();
+        for (int w = threadIdx.x; w < clear_words; w += blockDim.x) clear[w] = 0;
     }
 }
 
@@ -1370,47 +1385,43 @@ int karma_kmer_plan_create(karma_ctx* ctx, karma_contigs* c, int kmode, karma_km
     // k-mer counter, the row totals (8-byte aligned behind the bitmap)
     const int64_t pw = (p->nwords + 1) & ~int64_t(1);
     const int64_t nrow = c->n ? c->n : 1;
-    if ((rc = p->presence.alloc(ctx, pw + 2 + 2 * nrow)) || (rc = p->err.alloc(ctx, 1)) ||
+    // a caller's zeroed bitmap block (karma_step): no clearing memset; the
+    // row totals need none (every profile launch writes or clears its rows)
+    p->bits_ext = ctx->plan_zeroed && ctx->plan_zeroed_words >= pw + 2;
+    if ((rc = p->presence.alloc(ctx, (p->bits_ext ? 0 : pw + 2) + 2 * nrow)) || (rc = p->err.alloc(ctx, 1)) ||
         (rc = exc_buf.alloc(ctx, exc_cap))) {
         delete p;
         return rc;
     }
-    KARMA_HIP(hipMemsetAsync(p->presence.ptr, 0, (pw + 2 + 2 * nrow) * 4, ctx->stream));
+    p->bits = p->bits_ext ? ctx->plan_zeroed : p->presence.ptr;
+    if (!p->bits_ext) KARMA_HIP(hipMemsetAsync(p->presence.ptr, 0, (pw + 2 + 2 * nrow) * 4, ctx->stream));
     struct {
         unsigned long long* ptr;
-    } exc_cnt{reinterpret_cast<unsigned long long*>(p->presence.ptr + pw)};
-    p->row_tot = reinterpret_cast<int64_t*>(p->presence.ptr + pw + 2);
-    DevArray<int> full;
-    if ((rc = full.alloc(ctx, 1))) {
-        delete p;
-        return rc;
-    }
+    } exc_cnt{reinterpret_cast<unsigned long long*>(p->bits + pw)};
+    p->row_tot = reinterpret_cast<int64_t*>(p->presence.ptr + (p->bits_ext ? 0 : pw + 2));
     if (c->n) {
         // phase A over a prefix, saturation test, phase B over the rest (only
         // contigs with exception bases once the ACGT ordinals are saturated)
         const int64_t nA = std::min<int64_t>(c->n, 4096);
         const size_t lds = p->nwords * 4 + (kBlock / 64) * 80 * (4 + 2);
         const bool p56 = kmode == KARMA_KMER_5P6;
-        auto launch = [&](int64_t lo, int64_t hi, const int* f) -> int {
+        auto launch = [&](int64_t lo, int64_t hi, uint32_t n_can) -> int {
             if (hi <= lo) return KARMA_OK;
             const int grid = grid_for(ceil_div(hi - lo, kBlock / 64), 2048);
             if (p56)
                 KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<true>, grid, kBlock, lds, c->packed.ptr,
                              c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, hi, kmode, (int)p->nwords,
-                             with_len, p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, f, c->exc_list.ptr,
+                             with_len, p->bits, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, n_can, c->exc_list.ptr,
                              c->exc_n.ptr);
             else
                 KARMA_LAUNCH(ctx, "kmer_presence", presence_kernel<false>, grid, kBlock, lds, c->packed.ptr,
                              c->mask.ptr, c->has_exc.ptr, c->woff.ptr, c->off, c->raw, hi, kmode, (int)p->nwords,
-                             with_len, p->presence.ptr, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, f, c->exc_list.ptr,
+                             with_len, p->bits, exc_buf.ptr, exc_cap, exc_cnt.ptr, lo, n_can, c->exc_list.ptr,
                              c->exc_n.ptr);
             return KARMA_OK;
         };
-        KARMA_TRY(launch(0, nA, nullptr));
-        if (nA < c->n) {
-            KARMA_LAUNCH(ctx, "kmer_saturation", saturation_kernel, 1, 1024, 0, p->presence.ptr, S, p56, full.ptr);
-            KARMA_TRY(launch(nA, c->n, full.ptr));
-        }
+        KARMA_TRY(launch(0, nA, 0u));
+        if (nA < c->n) KARMA_TRY(launch(nA, c->n, p56 ? 1088u : S));
     }
     unsigned long long ninst = 0;
     if (c->exc_bases) {  // exception k-mers exist only in contigs with non-ACGT bases
@@ -1443,14 +1454,14 @@ int karma_kmer_presence_words(karma_kmer_plan* p, int64_t* nwords) {
 int karma_kmer_presence_get(karma_kmer_plan* p, uint32_t* dst) {
     KARMA_CHECK(p && dst, KARMA_ERR_ARG, "null argument");
     KARMA_TRY(ctx_begin(p->ctx));
-    KARMA_HIP(hipMemcpyAsync(dst, p->presence.ptr, p->nwords * 4, hipMemcpyDeviceToDevice, p->ctx->stream));
+    KARMA_HIP(hipMemcpyAsync(dst, p->bits, p->nwords * 4, hipMemcpyDeviceToDevice, p->ctx->stream));
     return KARMA_OK;
 }
 
 int karma_kmer_presence_set(karma_kmer_plan* p, const uint32_t* src) {
     KARMA_CHECK(p && src, KARMA_ERR_ARG, "null argument");
     KARMA_TRY(ctx_begin(p->ctx));
-    KARMA_HIP(hipMemcpyAsync(p->presence.ptr, src, p->nwords * 4, hipMemcpyDeviceToDevice, p->ctx->stream));
+    KARMA_HIP(hipMemcpyAsync(p->bits, src, p->nwords * 4, hipMemcpyDeviceToDevice, p->ctx->stream));
     p->M = -1;
     return KARMA_OK;
 }
@@ -1461,7 +1472,7 @@ int karma_kmer_presence_merge(karma_kmer_plan* p, const uint32_t* all, int n_set
     KARMA_TRY(ctx_begin(ctx));
     const int64_t nw = p->nwords;
     KARMA_LAUNCH(ctx, "kmer_presence_merge", presence_or_kernel, (int)ceil_div(nw, 256), 256, 0, all, n_sets, nw,
-                 p->presence.ptr);
+                 p->bits);
     p->M = -1;
     return KARMA_OK;
 }
@@ -1506,9 +1517,10 @@ int karma_kmer_plan_finalize_async(karma_kmer_plan* p) {
         (rc = p->col_keys.alloc(ctx, S + p->n_exc)) || (rc = p->m_dev.alloc(ctx, 1)))
         return rc;
     const size_t lds = (p->nwords + 1) * 4;
-    KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->presence.ptr, (int)p->nwords, S,
+    KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->bits, (int)p->nwords, S,
                  p->kmode == KARMA_KMER_5P6, p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode, with_len, p->exc_keys.ptr,
-                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, p->m_dev.ptr, (int64_t*)nullptr);
+                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, p->m_dev.ptr, (int64_t*)nullptr,
+                 p->bits_ext ? p->bits : nullptr, (int)(((p->nwords + 1) & ~int64_t(1)) + 2));
     if (!ctx->fin_pinned) KARMA_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->fin_pinned), 64, hipHostMallocDefault));
     KARMA_HIP(hipMemcpyAsync(ctx->fin_pinned, p->m_dev.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
     if (!p->fin_ev) KARMA_HIP(hipEventCreateWithFlags(&p->fin_ev, hipEventDisableTiming));
@@ -1538,9 +1550,10 @@ int kmer_finalize_device(karma_kmer_plan* p, int64_t* m_out, int64_t* m_host) {
         (rc = p->col_keys.alloc(ctx, S + p->n_exc)))
         return rc;
     const size_t lds = (p->nwords + 1) * 4;
-    KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->presence.ptr, (int)p->nwords, S,
+    KARMA_LAUNCH(ctx, "kmer_columns", columns_kernel, 1, kColBlock, lds, p->bits, (int)p->nwords, S,
                  p->kmode == KARMA_KMER_5P6, p->kmode == KARMA_KMER_5P6 ? 5 : p->kmode, with_len, p->exc_keys.ptr,
-                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, m_out, m_host);
+                 p->n_exc, p->col_of_ord.ptr, p->col_of_exc.ptr, p->col_keys.ptr, m_out, m_host,
+                 p->bits_ext ? p->bits : nullptr, (int)(((p->nwords + 1) & ~int64_t(1)) + 2));
     return KARMA_OK;
 }
 

@@ -588,6 +588,9 @@ struct karma_step {
     // deferred steps' device buffers, one set per main stream (kept across
     // steps: identical shapes reuse them)
     DevArray<int64_t> m_ring;      // per ring entry: the step's column count, written by its column table
+    // per side stream: the k-mer plan's presence bitmap block, zero between
+    // plans (ctx->plan_zeroed; the column table kernel clears it after use)
+    DevArray<uint32_t> plan_zero[2];
     struct Tail {
         DevArray<double> prof;         // the step's profile
         DevArray<uint64_t> mk, sk, rk;  // merged keys; the exchange's send and receive slots
@@ -1125,8 +1128,20 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // stream, every kernel alone on the chip -- the per-kernel timing pass)
     hipStream_t const side = sequential ? ms : (par && s->sides == 2 && !xs_on ? s->side_alt_s : s->side_s);
     ctx->stream = side;
+    DevArray<uint32_t>& pz = s->plan_zero[side == s->side_alt_s ? 1 : 0];
+    if (!sequential) {
+        // 2,048 + 2 words: the bitmap of every k <= 8 and the exception counter
+        if (!pz.ptr) {
+            KARMA_TRY(pz.alloc(ctx, 2048 + 2));
+            KARMA_HIP(hipMemsetAsync(pz.ptr, 0, pz.n * 4, side));
+        }
+        ctx->plan_zeroed = pz.ptr;
+        ctx->plan_zeroed_words = (int64_t)pz.n;
+    }
     karma_kmer_plan* plan = nullptr;
     int rc = karma_kmer_plan_create(ctx, store, s->kmode, &plan);
+    ctx->plan_zeroed = nullptr;
+    ctx->plan_zeroed_words = 0;
     if (!rc && s->world > 1) {
         if (xs_on && s->one_comm) {
             // the presence all-gather on the exchange stream (behind the previous
@@ -1150,6 +1165,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // host reads it once the step is done); nothing on the main streams waits for it
     int64_t* const m_dev = s->m_ring.ptr + seq % kRing;
     if (!rc) rc = kmer_finalize_device(plan, m_dev, s->mring_d + seq % kRing);
+    if (rc && !sequential && pz.ptr) (void)hipMemsetAsync(pz.ptr, 0, pz.n * 4, side);  // not cleared by a column table
     if (!rc) rc = ensure_prof(s, tl.prof, (size_t)std::max<int64_t>(1, s->n_loc * kmer_m_cap(plan)));
     if (!rc && ctx->mark_set && !sequential) {
         if (counted_call("hipStreamWaitEvent")) ++t_hip_calls;

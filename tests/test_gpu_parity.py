@@ -485,10 +485,13 @@ def test_eq_path_equals_readset_path():
     assert np.array_equal(er.totals, ee.totals)
 
 
-@pytest.mark.parametrize("kmer,n_rate", [("5p6", 700), (3, 300), (7, 0), (6, 2000)])
+@pytest.mark.parametrize("kmer,n_rate", [("5p6", 700), (3, 300), (7, 0), (6, 2000), (8, 0), (8, 250)])
 def test_profile_presence_two_phase(kmer, n_rate):
     # > 4096 contigs: phase B of the presence pass runs (saturated or not),
-    # exception k-mers appear only in late contigs for the high n_rate cases
+    # exception k-mers appear only in late contigs for the high n_rate cases;
+    # at k = 8 the first 4,096 contigs miss some of the 65,536 8-mers, so phase
+    # B's blocks start unsaturated and the late ones may see the set completed
+    # by the early ones' flushes (each block decides for its own contigs)
     n = 6000
     blob, offs, key_len = engine.synth_contigs(900 + n_rate, n, 40, 200, n_rate)
     seqs = OrderedDict((f">ctg{i}", bytes(blob[offs[i]:offs[i + 1]]).decode()) for i in range(n))
