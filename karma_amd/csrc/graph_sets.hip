@@ -2521,12 +2521,14 @@ int SetsJob::setup() {
     n_cg = g.Bc > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>({ctx->cu_count / g.Bc, ceil_div(max_cflush, 4),
                                                                      ceil_div(A, (int64_t)g.Bc << KARMA_CG_SHIFT)}))
                     : 0;
-    // binned: one group per ~64 chunks at most (a wave's batch), up to one block per CU
-    if (bin) n_cg = (int)std::max<int64_t>(1, std::min<int64_t>(ctx->cu_count / g.Bc, ceil_div(n_chunks, 64)));
-    if (bin) {  // KARMA_BIN_CG (A/B): at most this many groups per bucket
-        static const int cap = std::getenv("KARMA_BIN_CG") ? std::atoi(std::getenv("KARMA_BIN_CG")) : 0;
-        if (cap > 0) n_cg = std::min(n_cg, cap);
-    }
+    // binned: one group per ~64 chunks at most (a wave's batch), up to one block
+    // per CU, and one per 2^19 records a bucket may hold (each group clears and
+    // writes back a 128 KB histogram the final kernel sums: at the 8-rank
+    // strong preview's 38.6M records 2 groups per bucket instead of 5 took
+    // 0.183-0.184 against 0.190-0.192 ms per step; 1: 0.185, 3: 0.188)
+    if (bin)
+        n_cg = (int)std::max<int64_t>(1, std::min<int64_t>({ctx->cu_count / g.Bc, ceil_div(n_chunks, 64),
+                                                            ceil_div(A, (int64_t)g.Bc << 19)}));
     // pair-reduce groups per bucket: enough blocks to fill the chip while
     // buckets are few; one group from KARMA_ONE_GROUP_B buckets on, so the
     // final kernel copies the bucket's single list instead of re-hashing

@@ -622,6 +622,9 @@ __device__ __forceinline__ void hist_add(uint32_t* counts, uint32_t col) {
 #ifndef KARMA_PROF_ORD
 #define KARMA_PROF_ORD 0
 #endif
+#ifndef KARMA_PROF_WRITERS
+#define KARMA_PROF_WRITERS 0  // A/B: row writers per block at once (0: no limit)
+#endif
 #ifndef KARMA_PROF_BLOCKROW
 #define KARMA_PROF_BLOCKROW 0  // A/B: the block writes its waves' rows as one linear stream (profile_wave_kernel)
 #endif
@@ -854,6 +857,10 @@ profile_wave_kernel(
         for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
     }
     for (int j = lane; j < h_words; j += 64) counts[j] = 0;  // write_row_wave clears it after each row
+#if KARMA_PROF_WRITERS > 0
+    __shared__ unsigned w_ticket, w_served;
+    if (threadIdx.x == 0) w_ticket = w_served = 0;
+#endif
     __syncthreads();
     const int kmin = P56 ? 5 : k;
     // software pipeline over this wave's contigs: the next contig's offsets
@@ -1009,8 +1016,21 @@ profile_wave_kernel(
         // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
         my = wave_total(my);
         if (lane == 0) row_tot[c] = (int64_t)my;
+#if KARMA_PROF_WRITERS > 0
+        // at most KARMA_PROF_WRITERS of the block's waves write rows at once:
+        // a monotonic ticket per row, served in order (no retry loop)
+        unsigned tk = 0;
+        if (lane == 0) tk = __hip_atomic_fetch_add(&w_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        tk = (unsigned)__builtin_amdgcn_readfirstlane((int)tk);
+        while (tk >= __hip_atomic_load(&w_served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) +
+                         (unsigned)KARMA_PROF_WRITERS)
+            __builtin_amdgcn_s_sleep(2);
+#endif
         if (KARMA_PROF_ORD && ord_m) write_row_ord(out + c * ld, counts, M, cur.klen, err, lut, inv, lane);
         else write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
+#if KARMA_PROF_WRITERS > 0
+        if (lane == 0) __hip_atomic_fetch_add(&w_served, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         cur = nxt;

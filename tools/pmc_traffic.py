@@ -23,6 +23,7 @@ NAMES = {
     "code_append_kernel": "graph_code_partition",
     "partition_kernel<CodeStream": "graph_code_partition",
     "code_reduce_kernel": "graph_code_reduce",
+    "code_seg_reduce_kernel": "graph_code_reduce",
     "profile_kernel": "kmer_profile",
     "profile_wave_kernel": "kmer_profile",
     "presence_kernel": "kmer_presence",
