@@ -86,7 +86,7 @@ struct karma_ctx {
     size_t job_pinned_bytes = 0;
     bool job_open = false;
     hipEvent_t side_ev = nullptr;  // main -> side stream ordering (karma_kmer_profile_side)
-    int grid_headroom = 0;         // blocks per CU resident_grid leaves free (a side-stream launch; < 0: more)
+    int grid_headroom = 0;         // blocks per CU resident_grid leaves free (a side-stream launch)
     int side_headroom = 0;         // grid_headroom of karma_kmer_profile_side (karma_ctx_set_side_headroom)
     hipEvent_t mark_ev = nullptr;  // recorded by an open graph job after its classify kernel
     bool mark_set = false;

@@ -615,20 +615,7 @@ __device__ __forceinline__ void hist_add(uint32_t* counts, uint32_t col) {
 // word (l mod 16) is fixed and its 16-base window is one alignbit of the word
 // pair staged in LDS as a u64 (one 8-byte read per position).  The k-mer code
 // is the window's top 2k bits; for 5p6 the 5-mer is the 6-mer's top 10 bits.
-// ORD (5p6, KARMA_PROF_ORD): count by compact table index (the 5-mer code, or
-// 1024 + the first three bases of a palindromic 6-mer) instead of by column:
-// no table lookup per window; the row phase gathers each column's count
-// through the inverse table (write_row_ord)
-#ifndef KARMA_PROF_ORD
-#define KARMA_PROF_ORD 0
-#endif
-#ifndef KARMA_PROF_WRITERS
-#define KARMA_PROF_WRITERS 0  // A/B: row writers per block at once (0: no limit)
-#endif
-#ifndef KARMA_PROF_BLOCKROW
-#define KARMA_PROF_BLOCKROW 0  // A/B: the block writes its waves' rows as one linear stream (profile_wave_kernel)
-#endif
-template <bool P56, bool C16, bool ORD = false>
+template <bool P56, bool C16>
 __device__ __forceinline__ void count_clean(const Stage& first, const uint32_t* __restrict__ packed, int64_t w0,
                                             int64_t L, int kmin, int k, const uint16_t* __restrict__ tab,
                                             uint32_t* __restrict__ counts, uint32_t* __restrict__ win, int lane,
@@ -656,12 +643,12 @@ __device__ __forceinline__ void count_clean(const Stage& first, const uint32_t* 
                 const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
                 const uint32_t W = o ? __builtin_amdgcn_alignbit(hi, lo, sh) : hi;
                 if (P56) {
-                    hist_add<C16>(counts, ORD ? W >> 22 : tab[W >> 22]);  // kmer.py:72-73
+                    hist_add<C16>(counts, tab[W >> 22]);  // kmer.py:72-73
                     ++my;
                     const uint32_t c6 = W >> 20;
                     // palindromic 6-mers that fit in the contig, kmer.py:76-80
                     if ((c6 >> 6) == rev3(c6 & 63u) && 64 * t + 1 < lim) {
-                        hist_add<C16>(counts, ORD ? 1024u + (c6 >> 6) : tab[1024u + (c6 >> 6)]);
+                        hist_add<C16>(counts, tab[1024u + (c6 >> 6)]);
                         ++my;
                     }
                 } else {
@@ -745,47 +732,6 @@ __device__ __forceinline__ void write_row_wave(double* __restrict__ row, uint32_
     }
 }
 
-// ORD: the row from a histogram indexed by compact table index (u16
-// counters, C16): column j's count is counts16[inv[j]]; the histogram is
-// cleared afterwards with whole-word stores (1088 entries)
-__device__ __forceinline__ void write_row_ord(double* __restrict__ row, uint32_t* __restrict__ counts, int64_t M,
-                                              int32_t klen, int* __restrict__ err, double* __restrict__ lut,
-                                              const uint16_t* __restrict__ inv, int lane) {
-    const double len = (double)klen;
-    lut[lane] = lane ? (double)lane / len : 0.0;  // IEEE correctly rounded (kmer.py:120)
-    wave_lds_sync();
-    const uint16_t* c16 = reinterpret_cast<const uint16_t*>(counts);
-    auto val = [&](uint32_t a) {
-        double v = lut[min(a, 63u)];
-        if (a >= 64u) v = (double)a / len;
-        return v;
-    };
-    const uint64_t u = (uint64_t)row;
-    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
-                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u)),
-        0, (int)(M * 8), 0x00020000);
-    const bool al = (u & 15) == 0;
-    for (int64_t j = lane; 2 * j < M; j += 64) {
-        const uint32_t ii = reinterpret_cast<const uint32_t*>(inv)[j];
-        const uint32_t a = c16[ii & 0xFFFFu];
-        const uint32_t b = 2 * j + 1 < M ? (uint32_t)c16[ii >> 16] : 0u;
-        if ((a | b) && klen == 0) *err = 1;
-        const double x = val(a), y = val(b);
-        if (al && 2 * j + 1 < M) {
-            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-            const u32x4_t w = {(uint32_t)__double2loint(x), (uint32_t)__double2hiint(x), (uint32_t)__double2loint(y),
-                               (uint32_t)__double2hiint(y)};
-            __builtin_amdgcn_raw_buffer_store_b128(w, rr, (int)(j * 16), 0, KARMA_ROW_AUX >= 0 ? KARMA_ROW_AUX : 0);
-        } else {
-            row_store(x, row + 2 * j);
-            if (2 * j + 1 < M) row_store(y, row + 2 * j + 1);
-        }
-    }
-    wave_lds_sync();
-    for (int j = lane; j < 544; j += 64) counts[j] = 0;  // 1088 u16 counters
-}
-
 // Sum over the wave's 64 lanes, in every lane: DPP row shifts and row
 // broadcasts (no ds_bpermute address registers, which stayed live across the
 // contig loop and spilled), then lane 63's value read as a scalar.
@@ -821,23 +767,20 @@ profile_wave_kernel(
     const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
     const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
     double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
-    int64_t exc0, const int64_t* __restrict__ m_dev, int ord_on) {
+    int64_t exc0, const int64_t* __restrict__ m_dev) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     // wave index in an SGPR: contig offsets and lengths load with scalar loads
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
     const int t_pad = (int)((tab_entries(P56, S) + 7) & ~7);
-    // ORD (no exception k-mers, 5p6, u16 counters): the inverse table follows tab
-    const bool ord_m = KARMA_PROF_ORD && P56 && C16 && ord_on;
-    uint16_t* inv = tab + t_pad;
     // LDS is laid out for M; with m_dev (the column table's count, not read
     // back to the host first) M is its capacity and the rows are dense
-    const int h_words = (int)hist_words(ord_m ? max<int64_t>(M, 1088) : M, C16);
+    const int h_words = (int)hist_words(M, C16);
     if (m_dev) {
         M = *m_dev;
         ld = M;
     }
-    uint32_t* counts = lds + (t_pad + (ord_m ? t_pad : 0)) / 2 + wave * (h_words + kProfWin);
+    uint32_t* counts = lds + t_pad / 2 + wave * (h_words + kProfWin);
     uint32_t* win = counts + h_words;
     uint16_t* mbuf = reinterpret_cast<uint16_t*>(win + 80);
     double* lut = reinterpret_cast<double*>(win);
@@ -851,16 +794,11 @@ profile_wave_kernel(
                 ord = (c6 >> 2) * 5u + 1u + (c6 & 3u);
             }
             tab[o] = (uint16_t)col_of_ord[ord];
-            if (KARMA_PROF_ORD && ord_on && (uint32_t)col_of_ord[ord] < (uint32_t)M) inv[col_of_ord[ord]] = (uint16_t)o;
         }
     } else {
         for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
     }
     for (int j = lane; j < h_words; j += 64) counts[j] = 0;  // write_row_wave clears it after each row
-#if KARMA_PROF_WRITERS > 0
-    __shared__ unsigned w_ticket, w_served;
-    if (threadIdx.x == 0) w_ticket = w_served = 0;
-#endif
     __syncthreads();
     const int kmin = P56 ? 5 : k;
     // software pipeline over this wave's contigs: the next contig's offsets
@@ -892,99 +830,12 @@ profile_wave_kernel(
     Stage st0;
     meta(c, cur);
     if (c < n) st0.load(packed, mask, cur.exc, cur.w0, lane);
-    // BLOCKROW (A/B build, KARMA_PROF_BLOCKROW): the block's waves count their
-    // consecutive contigs, then the whole block writes the rows as ONE linear
-    // stream (dense rows: the block's rows are contiguous), 3 streams per CU
-    // instead of 24 row writers (the write rate of few streams, MI355X
-    // micro-benchmarks in DESIGN.md §4.1)
-    if (KARMA_PROF_BLOCKROW && C16 && !ord_m && (M & 1) == 0 && ld == M &&
-        (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
-        __shared__ int32_t bklen[16];
-        const int64_t M2 = M >> 1;
-        for (int64_t base = (int64_t)blockIdx.x * wpb; base < n; base += stride, c += stride) {
-            if (c < n) {
-                meta(c + stride, nxt);
-                const int64_t L = cur.L;
-                unsigned my = 0;
-                if (!cur.exc) {
-                    count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
-                } else {
-                    const uint8_t* craw = raw + cur.s;
-                    auto add = [&](uint32_t cl) {
-                        hist_add<C16>(counts, cl);
-                        ++my;
-                    };
-                    for_each_window(packed, mask, true, cur.w0, L - kmin + 1, win, mbuf, lane,
-                                    [&](int64_t i, const Window& v) {
-                        if (P56) {
-                            if (v.clean(5)) add(tab[v.code(5)]);
-                            else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 5, true))]);
-                            if (i + 6 <= L) {
-                                if (v.clean(6)) {
-                                    const uint32_t c6 = v.code(6);
-                                    if (pal6_code(c6)) add(tab[1024u + (c6 >> 6)]);
-                                } else if (pal_bytes(craw + i, 6)) {
-                                    add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 6, true))]);
-                                }
-                            }
-                        } else {
-                            if (v.clean(k)) add(tab[v.code(k)]);
-                            else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
-                        }
-                    }, &st0);
-                }
-                if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
-                my = wave_total(my);
-                if (lane == 0) {
-                    row_tot[c] = (int64_t)my;
-                    bklen[wave] = cur.klen;
-                }
-                wave_lds_sync();
-                lut[lane] = lane ? (double)lane / (double)cur.klen : 0.0;  // IEEE correctly rounded (kmer.py:120)
-                cur = nxt;
-            }
-            __syncthreads();
-            // rows [base, base + nr): pair q = (row r, columns 2j, 2j + 1)
-            const int nr = (int)min<int64_t>(wpb, n - base);
-            const int64_t np = (int64_t)nr * M2;
-            const uint64_t u = (uint64_t)(out + base * M);
-            typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-            const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<void*>(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u)),
-                0, (int)(np * 16), 0x00020000);
-            int r = (int)((int64_t)threadIdx.x / M2);
-            int64_t j = (int64_t)threadIdx.x - (int64_t)r * M2;
-            for (int64_t q = threadIdx.x; q < np; q += blockDim.x) {
-                uint32_t* cr = lds + (t_pad / 2) + r * (h_words + kProfWin);
-                const double* lr = reinterpret_cast<const double*>(cr + h_words);
-                const uint32_t ab = cr[j];
-                cr[j] = 0;
-                const uint32_t a = ab & 0xFFFFu, b = ab >> 16;
-                const int32_t kl = bklen[r];
-                if ((a | b) && kl == 0) *err = 1;
-                const double x = a < 64u ? lr[a] : (double)a / (double)kl;
-                const double y = b < 64u ? lr[b] : (double)b / (double)kl;
-                const u32x4_t w = {(uint32_t)__double2loint(x), (uint32_t)__double2hiint(x), (uint32_t)__double2loint(y),
-                                   (uint32_t)__double2hiint(y)};
-                __builtin_amdgcn_raw_buffer_store_b128(w, rr, (int)(q * 16), 0, KARMA_ROW_AUX >= 0 ? KARMA_ROW_AUX : 0);
-                j += blockDim.x;
-                while (j >= M2) {
-                    j -= M2;
-                    ++r;
-                }
-            }
-            __syncthreads();  // histograms clear, tables free for the next contigs
-        }
-        return;
-    }
     for (; c < n; c += stride) {
         meta(c + stride, nxt);
         const int64_t L = cur.L;
         unsigned my = 0;
         if (!cur.exc) {
-            if (KARMA_PROF_ORD && ord_m) count_clean<P56, C16, true>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
-            else count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
+            count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
         } else {
             // a contig with exception bases: windows that touch one are keyed by
             // their bytes and looked up among the sorted exception keys
@@ -1016,195 +867,10 @@ profile_wave_kernel(
         // k-mer occurrences of the contig (0 = the all-zero row of kmer.py:250-258)
         my = wave_total(my);
         if (lane == 0) row_tot[c] = (int64_t)my;
-#if KARMA_PROF_WRITERS > 0
-        // at most KARMA_PROF_WRITERS of the block's waves write rows at once:
-        // a monotonic ticket per row, served in order (no retry loop)
-        unsigned tk = 0;
-        if (lane == 0) tk = __hip_atomic_fetch_add(&w_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        tk = (unsigned)__builtin_amdgcn_readfirstlane((int)tk);
-        while (tk >= __hip_atomic_load(&w_served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) +
-                         (unsigned)KARMA_PROF_WRITERS)
-            __builtin_amdgcn_s_sleep(2);
-#endif
-        if (KARMA_PROF_ORD && ord_m) write_row_ord(out + c * ld, counts, M, cur.klen, err, lut, inv, lane);
-        else write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
-#if KARMA_PROF_WRITERS > 0
-        if (lane == 0) __hip_atomic_fetch_add(&w_served, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
+        write_row_wave<C16>(out + c * ld, counts, M, cur.klen, err, lut, lane);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         cur = nxt;
-    }
-}
-
-// ---- counting waves and writing waves (A/B build: KARMA_PROF_SPLIT writers) ----
-// The chip writes rows fastest from few waves per CU (tools/micro/write_bw7:
-// 6.5 TB/s from 4 streaming waves per CU, 5.2 TB/s from the 24 row-writing
-// waves the profile runs).  Here a 16-wave block splits into counting waves
-// (two LDS histograms each, ping-pong) and KARMA_PROF_SPLIT writing waves that
-// take full histograms from an LDS queue, write the row and clear it.  Every
-// wait has a partner that always progresses (writers leave only when every
-// counter has finished and no histogram is full), so the waits end.
-#ifndef KARMA_PROF_SPLIT
-#define KARMA_PROF_SPLIT 0
-#endif
-constexpr int kSplitW = KARMA_PROF_SPLIT > 0 ? KARMA_PROF_SPLIT : 1;
-constexpr int kSplitNC = 16 - kSplitW;
-
-template <bool P56, bool C16>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
-profile_split_kernel(
-    const uint32_t* __restrict__ packed, const uint16_t* __restrict__ mask, const uint8_t* __restrict__ has_exc,
-    const int64_t* __restrict__ woff, const int64_t* __restrict__ off, const uint8_t* __restrict__ raw,
-    const int32_t* __restrict__ keylen, int64_t n, int k, bool with_len, const int32_t* __restrict__ col_of_ord,
-    const uint64_t* __restrict__ exc, int64_t X, const int32_t* __restrict__ col_of_exc, int64_t M,
-    double* __restrict__ out, int64_t ld, int* __restrict__ err, int S, int64_t* __restrict__ row_tot,
-    int64_t exc0, const int64_t* __restrict__ m_dev) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    __shared__ int bstate[2 * kSplitNC];  // 0 free (its counter's), 1 full, 2 being written
-    __shared__ int64_t brow[2 * kSplitNC];
-    __shared__ int bklen[2 * kSplitNC];
-    __shared__ int ndone;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
-    const int t_pad = (int)((tab_entries(P56, S) + 7) & ~7);
-    const int h_words = (int)hist_words(M, C16);
-    if (m_dev) {
-        M = *m_dev;
-        ld = M;
-    }
-    uint32_t* cbase = lds + t_pad / 2;
-    const int per_c = 2 * h_words + kProfWin;
-    if (P56) {
-        for (int o = threadIdx.x; o < 1088; o += blockDim.x) {
-            uint32_t ord;
-            if (o < 1024) {
-                ord = 5u * o;
-            } else {
-                const uint32_t h3 = o - 1024, c6 = h3 << 6 | rev3(h3);
-                ord = (c6 >> 2) * 5u + 1u + (c6 & 3u);
-            }
-            tab[o] = (uint16_t)col_of_ord[ord];
-        }
-    } else {
-        for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
-    }
-    if (wave < kSplitNC)
-        for (int j = lane; j < 2 * h_words; j += 64) cbase[wave * per_c + j] = 0;
-    if (threadIdx.x < 2 * kSplitNC) bstate[threadIdx.x] = 0;
-    if (threadIdx.x == 0) ndone = 0;
-    __syncthreads();
-    if (wave < kSplitNC) {
-        const int kmin = P56 ? 5 : k;
-        uint32_t* win = cbase + wave * per_c + 2 * h_words;
-        uint16_t* mbuf = reinterpret_cast<uint16_t*>(win + 80);
-        struct Meta {
-            int64_t s = 0, L = 0, w0 = 0;
-            int32_t klen = 0;
-            bool exc = false;
-        };
-        auto meta = [&](int64_t cc, Meta& m) {
-            if (cc < n) {
-                m.s = off[cc];
-                m.L = off[cc + 1] - m.s;
-                m.w0 = woff[cc];
-                m.klen = keylen[cc];
-                const int64_t ce = exc0 + cc;
-                const uint32_t hw = reinterpret_cast<const uint32_t*>(has_exc)[ce >> 2];
-                m.exc = ((hw >> (8 * (ce & 3))) & 0xFFu) != 0;
-            }
-        };
-        const int64_t stride = (int64_t)gridDim.x * kSplitNC;
-        int64_t c = (int64_t)blockIdx.x * kSplitNC + wave;
-        Meta cur, nxt;
-        Stage st0;
-        meta(c, cur);
-        if (c < n) st0.load(packed, mask, cur.exc, cur.w0, lane);
-        int b = 0;
-        for (; c < n; c += stride) {
-            meta(c + stride, nxt);
-            const int slot = 2 * wave + b;
-            while (__hip_atomic_load(&bstate[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
-                __builtin_amdgcn_s_sleep(1);
-            uint32_t* counts = cbase + wave * per_c + b * h_words;
-            const int64_t L = cur.L;
-            unsigned my = 0;
-            if (!cur.exc) {
-                count_clean<P56, C16>(st0, packed, cur.w0, L, kmin, k, tab, counts, win, lane, my);
-            } else {
-                const uint8_t* craw = raw + cur.s;
-                auto add = [&](uint32_t cl) {
-                    hist_add<C16>(counts, cl);
-                    ++my;
-                };
-                for_each_window(packed, mask, true, cur.w0, L - kmin + 1, win, mbuf, lane,
-                                [&](int64_t i, const Window& v) {
-                    if (P56) {
-                        if (v.clean(5)) add(tab[v.code(5)]);
-                        else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 5, true))]);
-                        if (i + 6 <= L) {
-                            if (v.clean(6)) {
-                                const uint32_t c6 = v.code(6);
-                                if (pal6_code(c6)) add(tab[1024u + (c6 >> 6)]);
-                            } else if (pal_bytes(craw + i, 6)) {
-                                add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, 6, true))]);
-                            }
-                        }
-                    } else {
-                        if (v.clean(k)) add(tab[v.code(k)]);
-                        else add(col_of_exc[lower_bound_u64(exc, X, key_from_bytes(craw + i, k, with_len))]);
-                    }
-                }, &st0);
-            }
-            if (c + stride < n) st0.load(packed, mask, nxt.exc, nxt.w0, lane);
-            my = wave_total(my);
-            if (lane == 0) {
-                row_tot[c] = (int64_t)my;
-                brow[slot] = c;
-                bklen[slot] = cur.klen;
-                __hip_atomic_store(&bstate[slot], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            __builtin_amdgcn_wave_barrier();
-            b ^= 1;
-            cur = nxt;
-        }
-        if (lane == 0) __hip_atomic_fetch_add(&ndone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-        const int wi = wave - kSplitNC;
-        double* lut = reinterpret_cast<double*>(cbase + kSplitNC * per_c + wi * kProfWin);
-        for (;;) {
-            int st = lane < 2 * kSplitNC
-                         ? __hip_atomic_load(&bstate[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
-                         : 0;
-            unsigned long long full = __ballot(st == 1);
-            if (!full) {
-                if (__hip_atomic_load(&ndone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == kSplitNC) {
-                    st = lane < 2 * kSplitNC
-                             ? __hip_atomic_load(&bstate[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
-                             : 0;
-                    if (!__ballot(st == 1)) break;
-                    continue;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            // writers start their search at different slots
-            const int sh = (2 * wi) & 63;
-            const unsigned long long rot = sh ? ((full >> sh) | (full << (64 - sh))) : full;
-            const int pick = (__ffsll((long long)rot) - 1 + sh) & 63;
-            int got = 0;
-            if (lane == 0) got = atomicCAS(&bstate[pick], 1, 2) == 1;
-            got = __shfl(got, 0, 64);
-            if (!got) continue;
-            const int64_t row = brow[pick];
-            const int klen = bklen[pick];
-            uint32_t* counts = cbase + (pick >> 1) * per_c + (pick & 1) * h_words;
-            write_row_wave<C16>(out + row * ld, counts, M, klen, err, lut, lane);
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) __hip_atomic_store(&bstate[pick], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __builtin_amdgcn_wave_barrier();
-        }
     }
 }
 
@@ -1679,11 +1345,8 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         // counters when no contig reaches 2^16 bases (a count is <= L)
         const bool p56 = p->kmode == KARMA_KMER_5P6;
         const bool c16 = KARMA_PROF_C16 && c->max_len < 65536;
-        // KARMA_PROF_ORD builds: count by compact index when no exception k-mer exists
-        const int ord_on = KARMA_PROF_ORD && p56 && c16 && p->n_exc == 0;
-        const size_t lds = (size_t)((tab_entries(p56, p->S) + 7) & ~7) * 2 * (ord_on ? 2 : 1) +
-                           (kPBlock / 64) * (size_t)(hist_words(ord_on ? std::max<int64_t>(M, 1088) : M, c16) +
-                                                     kProfWin) * 4;
+        const size_t lds = (size_t)((tab_entries(p56, p->S) + 7) & ~7) * 2 +
+                           (kPBlock / 64) * (size_t)(hist_words(M, c16) + kProfWin) * 4;
 #define KARMA_WAVE_LAUNCH(P56, C16)                                                                              \
     do {                                                                                                         \
         const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_wave_kernel<P56, C16>), kPBlock, \
@@ -1691,18 +1354,9 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         KARMA_LAUNCH(ctx, "kmer_profile", (profile_wave_kernel<P56, C16>), g_, kPBlock, lds, c->packed.ptr,      \
                      c->mask.ptr, c->has_exc.ptr, woff, off, c->raw, keylen, n, k, with_len,                     \
                      p->col_of_ord.ptr, p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err,       \
-                     (int)p->S, row_tot, lo, m_dev, ord_on);                                                     \
+                     (int)p->S, row_tot, lo, m_dev);                                                             \
     } while (0)
-        if (KARMA_PROF_SPLIT > 0 && p56 && c16) {
-            const size_t lds_s = (size_t)((tab_entries(true, p->S) + 7) & ~7) * 2 +
-                                 (size_t)kSplitNC * (2 * hist_words(M, true) + kProfWin) * 4 +
-                                 (size_t)kSplitW * kProfWin * 4;
-            const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_split_kernel<true, true>), 1024,
-                                         lds_s, ceil_div(n, kSplitNC));
-            KARMA_LAUNCH(ctx, "kmer_profile", (profile_split_kernel<true, true>), g_, 1024, lds_s, c->packed.ptr,
-                         c->mask.ptr, c->has_exc.ptr, woff, off, c->raw, keylen, n, k, with_len, p->col_of_ord.ptr,
-                         p->exc_keys.ptr, p->n_exc, p->col_of_exc.ptr, M, dst, ld, err, (int)p->S, row_tot, lo, m_dev);
-        } else if (p56) {
+        if (p56) {
             if (c16) KARMA_WAVE_LAUNCH(true, true);
             else KARMA_WAVE_LAUNCH(true, false);
         } else {

@@ -1175,11 +1175,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         // KARMA_STEP_HEADROOM (A/B): profile blocks per CU left free for the
         // main stream's kernels (one main stream only)
         static const int headroom = getenv("KARMA_STEP_HEADROOM") ? atoi(getenv("KARMA_STEP_HEADROOM")) : 0;
-        // KARMA_STEP_PROF_SPREAD=1 (A/B) launches one block per 8 contigs
-        // instead of a resident grid, so the other streams' blocks dispatch as
-        // the profile's retire
-        static const int spread = getenv("KARMA_STEP_PROF_SPREAD") ? atoi(getenv("KARMA_STEP_PROF_SPREAD")) : 0;
-        ctx->grid_headroom = sequential ? 0 : spread ? -64 : two ? 0 : headroom;
+        ctx->grid_headroom = two || sequential ? 0 : headroom;
         rc = kmer_profile_device_m(plan, tl.prof.ptr, m_dev);
         ctx->grid_headroom = 0;
     }
