@@ -2468,7 +2468,8 @@ int SetsJob::setup() {
     const int64_t cw_total = ctrl_words + 2 * n_pblk + B;
     // a deferred job may take the caller's zeroed block (ctx->job_ctrl)
     ext = deferred && ctx->job_ctrl && ctx->job_ctrl_words >= cw_total;
-    if (std::getenv("KARMA_DEBUG_CTRL"))
+    static const bool debug_ctrl = std::getenv("KARMA_DEBUG_CTRL") != nullptr;
+    if (debug_ctrl)
         std::fprintf(stderr, "[karma] records job: deferred %d, caller block %p (%lld words), needs %lld: %s\n",
                      (int)deferred, (void*)ctx->job_ctrl, (long long)ctx->job_ctrl_words, (long long)cw_total,
                      ext ? "caller's" : "own");
