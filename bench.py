@@ -12,11 +12,12 @@ Inputs (2-bit packed contigs + records) are resident in HBM before timing.
 
 Multi-GPU (torchrun, one rank per GPU, the library's own RCCL communicator;
 no PyTorch in the process):
-  default (weak)  rank r owns contig rows [r*200k, (r+1)*200k) and fragments
-                  [r*100M, (r+1)*100M) of a global problem whose genes span all
-                  ranks;
-  --strong        BASELINE configs[3]: config 3 itself (200k contigs, 100M
-                  fragments) divided over the N ranks.
+  default (strong) BASELINE configs[3]: config 3 itself (200k contigs, 100M
+                  fragments) divided over the N ranks; a weak leg follows under
+                  "weak" (--no-weak-leg skips it);
+  --weak          headline = weak scaling: rank r owns contig rows
+                  [r*200k, (r+1)*200k) and fragments [r*100M, (r+1)*100M) of a
+                  global problem whose genes span all ranks.
 The step adds the presence all-gather, the exception-key all-gather, the edge
 partial all-to-all-v (pre-reduced pairs routed to the owner of contig a) and
 the totals all-gather (karma_amd/distributed.py, karma_amd/comm.py).
@@ -55,7 +56,9 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed batches; the two-stream pipeline's fill and drain are paid once per timed loop "
+                         "(DESIGN.md §5), so 100 batches measure the steady stream (20: +0.04 ms/step at 8 ranks)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="config3", choices=sorted(CONFIGS))
     ap.add_argument("--weak", action="store_true",
