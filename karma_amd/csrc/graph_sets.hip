@@ -1161,11 +1161,12 @@ __global__ void __launch_bounds__(kPT) code_append_kernel(const uint32_t* __rest
                                                            uint16_t* __restrict__ out, uint16_t* trash, RunDir dir,
                                                            int* err) {
     using T = CodeStreamT<NB>;
-    // codes per flush: 34 KB (narrow) / 70 KB (wide) of LDS, 4 / 2 blocks per CU;
+    // codes per flush: 34 KB (narrow) / 79 KB (wide) of LDS, 4 / 2 blocks per CU;
     // wide flushes of 8192 codes write ~20 codes per run instead of ~10
-    // (weak-scaled config 3: 0.26-0.27 vs 0.29 ms)
+    // (weak-scaled config 3: 0.26-0.27 vs 0.29 ms); 12288: ~30 per run, weak
+    // 8-rank preview 1.412 -> 1.397 ms; 16384 leaves one block per CU: 1.60 ms
 #ifndef KARMA_APPEND_WIDE_CAP
-#define KARMA_APPEND_WIDE_CAP 8192
+#define KARMA_APPEND_WIDE_CAP 12288
 #endif
     constexpr int kCap = NB > 128 ? KARMA_APPEND_WIDE_CAP : 4096;
     constexpr int kPer = kCap / kPT;
