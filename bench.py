@@ -282,8 +282,15 @@ class Leg:
         barrier + device sync; returns (max-over-ranks seconds, last result,
         per-kernel totals, dominant kernel, its live (ms, launches))."""
         comm = self.comm
+        # with the native step the timed batches are deferred ones (below): the
+        # warm-up runs that same kind of step, so both main streams' tail
+        # buffers, control blocks and events exist before the timed region (the
+        # sequential pass uses only the first; a first deferred batch on the
+        # second stream grew them with every stream synchronised, inside the
+        # timed loop: a fixed cost per loop that 20 short batches did not hide)
+        native = self.build.native is not None and os.environ.get("KARMA_BENCH_LAST_SYNC", "0") != "1"
         for i in range(warmup):
-            self.step()
+            self.step(count=not native)
             WATCHDOG.tick(f"warmup step {i}")
         self.sync_all()
         WATCHDOG.tick("warmup synced")
@@ -329,7 +336,6 @@ class Leg:
         # with the native step the last batch is deferred too: its column count
         # and edge count are read from its status after the sync (the same
         # kernels run; only the host's readback moves behind the sync)
-        native = self.build.native is not None and os.environ.get("KARMA_BENCH_LAST_SYNC", "0") != "1"
         for i in range(steps):
             h0 = time.perf_counter()
             res = self.step(count=i == steps - 1 and not native)
@@ -366,6 +372,26 @@ class Leg:
                 c.timing(False)
         return dt, res, kern, dom, dom_live
 
+    def single_batch(self, reps=5):
+        """One batch alone: from every stream idle (barrier + device sync) to
+        its checked status (karma_step_sync), the latency a karma run sees when
+        it builds this path once (karma.py:197-210, :240); a deferred step with
+        the native driver, as in the timed loop.  Median over reps of the max
+        over ranks (ms)."""
+        native = self.build.native is not None
+        ts = []
+        for _ in range(reps):
+            self.comm.barrier()
+            self.sync_all()
+            t0 = time.perf_counter()
+            self.step(count=not native)
+            self.sync_all()
+            ts.append(self.comm.max_float(time.perf_counter() - t0) * 1e3)
+        return {"ms": round(float(np.median(ts)), 4), "min_ms": round(min(ts), 4), "reps": reps,
+                "step": "deferred" if native else "synchronous",
+                "note": "one batch from idle streams to its synced, checked status (no pipelining with other "
+                        "batches); median over reps of the max over ranks"}
+
     def close(self):
         self.build.close()
         self.store.close()
@@ -381,35 +407,16 @@ def digest_key(args, world, emu):
     return {"config2": "config2", "config3": "config3", "config5_1gpu": "config5_1gpu"}.get(args.config)
 
 
-def parity_check(leg, key):
-    """In-run parity (outside the timed region): one more step with its outputs
-    kept; every rank hashes its own profile rows, rank 0 gathers the row digests
-    (32 B per row), edges (a < b owned by the rank of a), column digest and
-    totals, and compares the union with tests/golden/digests.json[key] (the
-    oracle's digests; config 3's profile and edges are also the reference's own,
-    tests/golden/time_reference.py).  A multi-GPU run is thereby its own RCCL
-    parity test.  Returns the JSON object for the bench line (rank 0)."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
+def _gather_compare(comm, inp, gold, M, rows, cols, e):
+    """Every rank's share of one step's outputs (profile row digests, edges it
+    owns, totals; the column digest when known) gathered to rank 0 and compared
+    with the digests.  Returns (mismatches, edge digests) on rank 0, None elsewhere."""
     import digests as D
-    from karma_amd import engine
 
-    comm, inp = leg.comm, leg.inp
-    gold = D.load().get(key) if key else None
-    if gold is None:
-        return {"parity": None, "reason": f"no digests for {key or 'this workload'}"}
-    t0 = time.perf_counter()
-    res = leg.step(keep=True)
-    leg.sync_all()
-    M = int(res["M"])
-    prof = res["profile"].numpy()  # this rank's rows, D2H
-    rows = D.row_digests(prof)
-    del prof
-    cols = D.columns_digest(engine.decode_keys(res["columns"], engine.kmode_of(inp["kmer"])))
-    e = res["edges"]
     meta = np.array([M, inp["c_lo"], inp["n_loc"], len(e.a)], np.int64)
     g_meta = comm.allgather_host(meta)
     g_rows = comm.allgather_host(np.frombuffer(rows, np.uint8))
-    g_cols = comm.allgather_host(np.frombuffer(cols.encode(), np.uint8))
+    g_cols = comm.allgather_host(np.frombuffer(cols.encode(), np.uint8)) if cols is not None else None
     g_a = comm.allgather_host(np.asarray(e.a, np.uint32))
     g_b = comm.allgather_host(np.asarray(e.b, np.uint32))
     g_w = comm.allgather_host(np.asarray(e.weight, np.float64))
@@ -421,7 +428,7 @@ def parity_check(leg, key):
     mism = []
     if any(int(m[0]) != gold["M"] for m in g_meta):
         mism.append("M")
-    if any(bytes(c).decode() != gold["columns"] for c in g_cols):
+    if g_cols is not None and any(bytes(c).decode() != gold["columns"] for c in g_cols):
         mism.append("columns")
     lo = 0
     for r in order:  # the shards tile [0, N) in rank order
@@ -442,15 +449,90 @@ def parity_check(leg, key):
             mism.append(f"edges.{k}")
     if any(not np.array_equal(t, g_t[0]) for t in g_t):
         mism.append("totals differ between ranks")
-    return {"parity": not mism, "against": f"tests/golden/digests.json[{key}]"
-            + (" (oracle; config 3 profile and edges also the reference's own)" if key == "config3" else " (oracle)"),
+    return mism, got
+
+
+def parity_check(leg, key):
+    """In-run parity (outside the timed region), of two steps:
+      timed_step  the LAST TIMED STEP itself, as the timed loop left it: with the
+                  native step a deferred one, whose profile (karma_step_profile)
+                  and edges (karma_step_newest_edges: the arrays its own tail
+                  kernels wrote -- step_edge_count / step_edge_write, and with an
+                  exchange step_pack / step_merge over the fixed slots) are the
+                  outputs of exactly the code path the headline times;
+      kept_step   one more, synchronous step with its outputs kept (the column
+                  keys too).
+    Every rank hashes its own profile rows, rank 0 gathers the row digests (32 B
+    per row), the edges (each owned by the rank of contig a), the column digest
+    and the totals, and compares the union with tests/golden/digests.json[key]
+    (the oracle's digests; config 3's profile and edges are also the
+    reference's own, tests/golden/time_reference.py).  A multi-GPU run is
+    thereby its own RCCL parity test.  Returns the JSON object for the bench
+    line (rank 0)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import digests as D
+    from karma_amd import engine
+
+    comm, inp = leg.comm, leg.inp
+    gold = D.load().get(key) if key else None
+    if gold is None:
+        return {"parity": None, "reason": f"no digests for {key or 'this workload'}"}
+    t0 = time.perf_counter()
+    timed = None
+    native = leg.build.native
+    if native is not None:
+        info = native.info()  # the timed loop ended with karma_step_sync
+        prof = native.profile().numpy()
+        rows = D.row_digests(prof)
+        del prof
+        e, deferred = native.newest_edges()
+        g_def = comm.allgather_host(np.array([int(deferred)], np.int64))
+        out = _gather_compare(comm, inp, gold, int(info[0]), rows, None, e)
+        if out is not None:
+            mism, got = out
+            timed = {"step": "last timed step", "deferred_on_every_rank": all(int(d[0]) for d in g_def),
+                     "outputs": "karma_step_profile + karma_step_newest_edges (the step's own tail buffers)",
+                     "checked": ["M", "profile_rows", "edges.ab", "edges.weight", "edges.shared", "edges.totals"],
+                     "mismatch": mism, "edges": got["E"]}
+    res = leg.step(keep=True)
+    leg.sync_all()
+    prof = res["profile"].numpy()  # this rank's rows, D2H
+    rows = D.row_digests(prof)
+    del prof
+    cols = D.columns_digest(engine.decode_keys(res["columns"], engine.kmode_of(inp["kmer"])))
+    out = _gather_compare(comm, inp, gold, int(res["M"]), rows, cols, res["edges"])
+    if comm.rank != 0:
+        return None
+    mism, got = out
+    kept = {"step": "one more synchronous step, outputs kept (KARMA_STEP_KEEP)",
             "checked": ["M", "columns", "profile_rows", "edges.ab", "edges.weight", "edges.shared", "edges.totals"],
-            "mismatch": mism, "edges": got["E"], "ranks": len(g_meta), "seconds": round(time.perf_counter() - t0, 2)}
+            "mismatch": mism, "edges": got["E"]}
+    ok = not mism and (timed is None or (not timed["mismatch"] and timed["deferred_on_every_rank"]))
+    src = " (oracle; config 3 profile and edges also the reference's own)" if key == "config3" else " (oracle)"
+    return {"parity": ok,
+            "against": ("the last timed (deferred) step's own outputs and a kept synchronous step, vs "
+                        if timed is not None else "a kept synchronous step, vs ") + f"tests/golden/digests.json[{key}]"
+                       + src,
+            "timed_step": timed, "kept_step": kept,
+            "mismatch": (timed["mismatch"] if timed else []) + mism, "edges": got["E"], "ranks": comm.world,
+            "seconds": round(time.perf_counter() - t0, 2)}
+
+
+def profiler_preloaded():
+    """True under rocprofv3 (its options reach the program as ROCPROF_*
+    variables, its tool library through LD_PRELOAD).  Its preload initialises
+    the GPU before this program starts, so self_launch's fork + exec of rank
+    processes would then come from a GPU-initialised process."""
+    return any(k.startswith("ROCPROF_") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", "")
 
 
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if profiler_preloaded():
+            log("bench.py: --gpus N > 1 under a profiler: start the ranks with the launcher (torchrun, or "
+                "RANK/WORLD_SIZE per process) and profile each rank, not bench.py's self-launch")
+            return 2
         return self_launch(args)  # before anything here touches HIP
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -567,6 +649,8 @@ def run(args, rank, world, local_rank, launcher):
     if not args.no_parity:
         parity = parity_check(leg, digest_key(args, world, inp["emu"]))
         WATCHDOG.tick("parity")
+    single = leg.single_batch()
+    WATCHDOG.tick("single batch")
     extra = {}
     if rank == 0 and world == 1 and not args.no_e2e and inp["emu"] == 1 and not args.shuffle_contigs:
         extra = end_to_end_legs(args, inp, ctx, leg.build, leg.store)
@@ -607,6 +691,8 @@ def run(args, rank, world, local_rank, launcher):
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(step_s * 1e3, 3),
+            "single_batch_ms": single["ms"],
+            "single_batch": single,
             "higher_is_better": True,
             "scaling": "strong" if args.strong else "weak",
             # BASELINE.md publishes no number for this metric

@@ -391,6 +391,18 @@ int karma_step_info(karma_step* s, int64_t* info, int n);
 int karma_step_profile(karma_step* s, double** dev, int64_t* rows, int64_t* M);
 int karma_step_columns(karma_step* s, uint64_t* keys_host);
 int karma_step_edges(karma_step* s, karma_edges** e);
+/* The newest step's graph as this rank owns it (edges with a in its owner
+ * range; one process: all), valid after karma_step_sync until the next run.
+ * A deferred step's come from its own tail buffers -- the outputs of the
+ * kernels a stream of deferred batches runs (step_edge_count / _write, and with
+ * an exchange step_pack / step_merge) -- a synchronous one's (a re-run
+ * included) from its karma_edges.  *n_edges = E; *deferred (may be NULL) = 1
+ * for a deferred step's.  a, b, shared, weight: E entries each (E <= cap, else
+ * KARMA_ERR_ARG), sorted by (a, b), a < b, weight (s/|A| + s/|B|)/2
+ * (read_graph.py:19-50, :34-42); totals: n_glob readset sizes.  Any pointer may
+ * be NULL (all NULL: only the count). */
+int karma_step_newest_edges(karma_step* s, uint32_t* a, uint32_t* b, int64_t* shared, double* weight,
+                            int64_t* totals, int64_t cap, int is_device, int64_t* n_edges, int* deferred);
 int karma_step_destroy(karma_step* s);
 
 /* ---- synthetic inputs (spec in karma_amd/synth.py) ------- */

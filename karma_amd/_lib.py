@@ -142,6 +142,7 @@ _SIGS = {
     "karma_step_profile": [_c_p, _PP, _I64P, _I64P],
     "karma_step_columns": [_c_p, _c_p],
     "karma_step_edges": [_c_p, _PP],
+    "karma_step_newest_edges": [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _i64, _i32, _I64P, _c_p],
     "karma_step_destroy": [_c_p],
     "karma_synth_contig_lengths": [_u64, _i64, _i32, _i32, _c_p],
     "karma_synth_contig_bases": [_u64, _c_p, _i64, _i32, _c_p],

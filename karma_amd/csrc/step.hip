@@ -491,11 +491,13 @@ __global__ void __launch_bounds__(256) step_pack_kernel(const uint64_t* __restri
 // ctrl (n_ctrl words): the records job's control block when it was the
 // step's own (SetsDeferred::ctrl): zeroed once every word is read, for the
 // next records job of this tail (no clearing launch ahead of its classify).
-__global__ void step_status_kernel(const int* __restrict__ flags, const unsigned* __restrict__ counters,
-                                   const uint8_t* __restrict__ ovf, int B, const int64_t* __restrict__ dst,
-                                   int64_t* __restrict__ merge_bad, const int64_t* __restrict__ est,
-                                   StepStatus* __restrict__ out, uint64_t seq, int64_t* __restrict__ ctrl,
-                                   int64_t n_ctrl) {
+// flags, counters, ovf and dst point into ctrl then, so none of the four (nor
+// ctrl) is __restrict__; every read of them is staged into LDS (any_ovf,
+// words[]) ahead of the __syncthreads that precedes the clear, and must stay so.
+__global__ void step_status_kernel(const int* flags, const unsigned* counters, const uint8_t* ovf, int B,
+                                   const int64_t* dst, int64_t* __restrict__ merge_bad,
+                                   const int64_t* __restrict__ est, StepStatus* __restrict__ out, uint64_t seq,
+                                   int64_t* ctrl, int64_t n_ctrl) {
     __shared__ int any_ovf;
     __shared__ int64_t words[4];
     if (threadIdx.x == 0) any_ovf = 0;
@@ -675,6 +677,7 @@ struct karma_step {
     bool emu_xs = false;  // KARMA_STEP_EMU_XS=1 (A/B; see run_deferred)
     int lag = kLag;      // KARMA_STEP_LAG (A/B): deferred steps in flight before the host waits
     void* ring_mem = nullptr;      // this step's own mapped status ring (two steps on one context never share it)
+    uint64_t fault_seq = 0;        // KARMA_STEP_FAULT_SEQ (tests only): this deferred step fails before its status
 };
 
 namespace {
@@ -1083,6 +1086,30 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         s->ev_set = false;
     }
     karma_step::Tail& tl = s->tail[par];
+    // A failure between here and the status kernel's launch leaves this job's
+    // flags, counters and block items in the tail's own control block (only
+    // the status kernel clears it), and the next job on this tail would take
+    // the block as zeroed (no probe, no memset): clear it once every stream is
+    // idle (a kernel of this step may still use it), and leave no newest
+    // deferred step without a status behind.
+    struct FailGuard {
+        karma_step* s;
+        karma_step::Tail& tl;
+        uint64_t seq;
+        bool armed = true;
+        ~FailGuard() {
+            if (!armed) return;
+            for (hipStream_t q : {s->side_s, s->side_alt_s, s->main_s, s->alt_s}) (void)hipStreamSynchronize(q);
+            if (s->own_ctrl && tl.ctrl.ptr) {
+                (void)hipMemsetAsync(tl.ctrl.ptr, 0, tl.ctrl.n * 8, s->main_s);
+                (void)hipStreamSynchronize(s->main_s);
+            }
+            if (s->prof_seq == seq) {
+                s->prof_seq = 0;
+                s->prof_M = -1;
+            }
+        }
+    } fail{s, tl, seq};
     ctx->stream = ms;
     s->prof_seq = seq;
     s->prof_par = par;
@@ -1269,6 +1296,10 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     if (s->world > 1) KARMA_TRY(allgather_slices(s, tl.tot.ptr));
     KARMA_LAUNCH(ctx, "edge_weights", step_edge_write_kernel, grid, kET, 0, lk, lc, n_dev, tl.tot.ptr,
                  tl.tile_cnt.ptr, tl.ea.ptr, tl.eb.ptr, tl.es.ptr, tl.ew.ptr, tl.est.ptr, s->n_glob);
+    // test hook (tests/test_gpu_step.py): fail deferred step `fault_seq` after
+    // its tail's kernels, before the status kernel (the control-block error path)
+    KARMA_CHECK(seq != s->fault_seq, KARMA_ERR_STATE, "karma_step: injected fault in deferred step %llu",
+                (unsigned long long)seq);
     KARMA_LAUNCH(ctx, "step_status", step_status_kernel, 1, 256, 0, v.flags, v.counters, v.ovf, v.B, v.dst, mbad,
                  tl.est.ptr, s->ring_d + seq % kRing, seq, v.ctrl, v.ctrl ? v.ctrl_need : (int64_t)0);
     if (xs_on) {
@@ -1279,6 +1310,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         s->tail_last = par;
         ctx->stream = ms;
     }
+    fail.armed = false;
     s->pending.push_back({seq, store, rec, A});
     return KARMA_OK;
 }
@@ -1325,6 +1357,7 @@ int karma_step_create(karma_ctx* ctx, karma_comm* comm, karma_comm* side_comm, i
     if (const char* e = getenv("KARMA_STEP_OWN_CTRL")) s->own_ctrl = atoi(e) != 0;
     if (const char* e = getenv("KARMA_STEP_EMU_XS")) s->emu_xs = atoi(e) != 0;
     if (const char* e = getenv("KARMA_STEP_LAG")) s->lag = std::max(1, std::min(kRing / 2, atoi(e)));
+    if (const char* e = getenv("KARMA_STEP_FAULT_SEQ")) s->fault_seq = strtoull(e, nullptr, 10);
     s->n_glob = n_glob;
     s->bounds.assign(bounds, bounds + nranks + 1);
     s->c_lo = bounds[rank];
@@ -1474,6 +1507,54 @@ int karma_step_edges(karma_step* s, karma_edges** e) {
     return KARMA_OK;
 }
 
+// The newest step's edges as this rank owns them, after karma_step_sync: a
+// deferred step's straight from its tail (the arrays step_edge_write_kernel
+// wrote, the code path a stream of deferred batches times), a synchronous
+// one's (a re-run included) from its karma_edges.
+int karma_step_newest_edges(karma_step* s, uint32_t* a, uint32_t* b, int64_t* shared, double* weight,
+                            int64_t* totals, int64_t cap, int is_device, int64_t* n_edges, int* deferred) {
+    KARMA_CHECK(s && n_edges && cap >= 0, KARMA_ERR_ARG, "karma_step_newest_edges: bad arguments");
+    KARMA_CHECK(s->pending.empty() && s->prof_M >= 0, KARMA_ERR_STATE,
+                "karma_step_newest_edges: no finished step (karma_step_sync first)");
+    KARMA_TRY(ctx_begin(s->ctx));
+    const hipMemcpyKind kind = is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (!s->prof_seq) {  // a synchronous step is the newest
+        KARMA_CHECK(s->edges, KARMA_ERR_STATE, "karma_step_newest_edges: the newest step kept no edges");
+        int64_t E = 0;
+        KARMA_TRY(karma_edges_count(s->edges, &E));
+        *n_edges = E;
+        if (deferred) *deferred = 0;
+        if (a || b || shared || weight) {
+            KARMA_CHECK(E <= cap, KARMA_ERR_ARG, "karma_step_newest_edges: %lld edges, room for %lld",
+                        (long long)E, (long long)cap);
+            KARMA_TRY(karma_edges_get(s->edges, a, b, shared, weight, nullptr, is_device));
+        }
+        if (totals) KARMA_TRY(karma_edges_totals(s->edges, totals, is_device));
+        if (is_device) KARMA_TRY(karma_ctx_sync(s->ctx));
+        return KARMA_OK;
+    }
+    const karma_step::Tail& tl = s->tail[s->prof_par];
+    const int64_t E = const_cast<const StepStatus&>(s->ring_h[s->prof_seq % kRing]).E;
+    KARMA_CHECK(E >= 0 && E <= (int64_t)tl.ea.n, KARMA_ERR_STATE, "karma_step_newest_edges: bad edge count %lld",
+                (long long)E);
+    *n_edges = E;
+    if (deferred) *deferred = 1;
+    if ((a || b || shared || weight) && E > cap) {
+        set_error("karma_step_newest_edges: %lld edges, room for %lld", (long long)E, (long long)cap);
+        return KARMA_ERR_ARG;
+    }
+    hipStream_t q = s->main_s;
+    if (E) {
+        if (a) KARMA_HIP(hipMemcpyAsync(a, tl.ea.ptr, E * 4, kind, q));
+        if (b) KARMA_HIP(hipMemcpyAsync(b, tl.eb.ptr, E * 4, kind, q));
+        if (shared) KARMA_HIP(hipMemcpyAsync(shared, tl.es.ptr, E * 8, kind, q));
+        if (weight) KARMA_HIP(hipMemcpyAsync(weight, tl.ew.ptr, E * 8, kind, q));
+    }
+    if (totals) KARMA_HIP(hipMemcpyAsync(totals, tl.tot.ptr, s->n_glob * 8, kind, q));
+    KARMA_HIP(hipStreamSynchronize(q));
+    return KARMA_OK;
+}
+
 int karma_step_destroy(karma_step* s) {
     if (!s) return KARMA_OK;
     hipSetDevice(s->ctx->device);
@@ -1496,6 +1577,8 @@ int karma_step_destroy(karma_step* s) {
     // be destroyed: release them first, then hand cached blocks to the context
     s->prof.release();
     s->m_ring.release();
+    s->plan_zero[0].release();  // allocated on side_s / side_alt_s
+    s->plan_zero[1].release();
     for (auto& tl : s->tail) tl.release();
     karma_ctx* ctx = s->ctx;
     hipStream_t prev = ctx->stream;

@@ -71,9 +71,15 @@ class HipOps:
         try:
             plan = self.engine.KmerPlan(self.ctx, store, kmode)
             if comm is not None and comm.world > 1:
-                # the side stream's own communicator (RcclComm.side): never the
-                # main stream's, whose operations interleave differently per rank
+                # the side stream's own communicator (RcclComm.side) when there
+                # is one.  RcclComm defaults to one communicator (comm.side is
+                # comm): the side stream then waits for everything enqueued on
+                # the main stream first (a previous step's totals all-gather may
+                # still be in flight there), so the communicator's operations
+                # never run on two streams at once
                 sc = getattr(comm, "side", comm)
+                if sc is comm:
+                    self.ctx.join(self.stream)
                 self.presence_merge(plan, sc.allgather_fixed(self.presence_words(plan)), comm.world)
                 self.set_exceptions(plan, sc.allgather_var(self.exceptions(plan)))
             plan.finalize_async()
@@ -274,6 +280,22 @@ class NativeStep:
         dev, rows, M = ctypes.c_void_p(), ctypes.c_int64(), ctypes.c_int64()
         call("karma_step_profile", self.h, ctypes.byref(dev), ctypes.byref(rows), ctypes.byref(M))
         return DevBuf(self.ctx, (rows.value, M.value), np.float64, _ptr=dev.value or 0, _owner=self)
+
+    def newest_edges(self):
+        """The newest step's edges after sync() (karma_step_newest_edges): a
+        deferred step's from the arrays its own tail kernels wrote.  Returns
+        (EdgeArrays, deferred)."""
+        from .engine import EdgeArrays
+
+        E, dfr = ctypes.c_int64(), ctypes.c_int()
+        call("karma_step_newest_edges", self.h, None, None, None, None, None, 0, 0, ctypes.byref(E), None)
+        n = E.value
+        a, b = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.uint32)
+        s, w = np.zeros(max(n, 1), np.int64), np.zeros(max(n, 1), np.float64)
+        tot = np.zeros(max(self.n_glob, 1), np.int64)
+        call("karma_step_newest_edges", self.h, ptr(a), ptr(b), ptr(s), ptr(w), ptr(tot), n, 0, ctypes.byref(E),
+             ctypes.byref(dfr))
+        return EdgeArrays(a[:n], b[:n], s[:n], w[:n], np.zeros(n, np.uint64), tot[:self.n_glob]), bool(dfr.value)
 
     def info(self):
         """[M, E, pairs, entries, synchronous steps, deferred steps, re-run steps, pending,

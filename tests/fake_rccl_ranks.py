@@ -187,6 +187,12 @@ def defer_rank(group, rank, sizes, frags, seed):
                     build.sync()
                     out[f"{tag}_info"] = build.native.info()
                     out[f"{tag}_profile"] = build.native.profile().numpy()
+                    # the newest step's edges: a deferred step's from its tail
+                    # (slots, step_merge_kernel, step_edge_*), a re-run's synchronous
+                    ne, dfr = build.native.newest_edges()
+                    out.update({f"{tag}_na": ne.a, f"{tag}_nb": ne.b, f"{tag}_nw": ne.weight,
+                                f"{tag}_ns": ne.shared, f"{tag}_ntot": ne.totals,
+                                f"{tag}_ndeferred": np.array(dfr)})
                     res = build.run(store, batch[0].ptr, batch[1], keep=True)
                     e = res["edges"]
                     out.update({f"{tag}_a": e.a, f"{tag}_b": e.b, f"{tag}_w": e.weight, f"{tag}_tot": e.totals})

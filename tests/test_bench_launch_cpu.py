@@ -62,3 +62,16 @@ def test_bench_refuses_more_gpus_than_visible():
     assert r.returncode != 0
     assert "HIP device(s) visible" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_refuses_self_launch_under_a_profiler():
+    """Under rocprofv3 (ROCPROF_* in the environment) the process may already
+    have initialised the GPU: `bench.py --gpus 2` must not fork + exec rank
+    processes from it, but exit with a message."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "KARMA_FORCE_DEVICE")}
+    env["ROCPROF_KERNEL_TRACE"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 2
+    assert "under a profiler" in r.stderr
+    assert "launching" not in r.stderr

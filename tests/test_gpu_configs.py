@@ -170,3 +170,40 @@ def test_config4_strong_8_ranks(gold):
         lo, hi = p["c_lo"], p["c_lo"] + p["n_loc"]
         assert np.all((p["edges"].a >= lo) & (p["edges"].a < hi)), "an edge left its owner (contig a's rank)"
     assert D.edge_digests(cat["a"], cat["b"], cat["weight"], cat["shared"], parts[0]["edges"].totals) == g["edges"]
+
+
+@pytest.mark.parametrize("name", ["config2", "config3"])
+def test_config_deferred_step_digests(gold, name):
+    """The code path bench.py TIMES at these sizes: a stream of deferred steps
+    (count=False: karma_step's run_deferred, two main streams at config 2's
+    size, one at config 3's), then sync.  The newest deferred step's own outputs
+    -- its profile (karma_step_profile) and its edges straight from the tail
+    buffers step_edge_count / step_edge_write filled (karma_step_newest_edges)
+    -- must hash to the same digests as the kept synchronous step above."""
+    g = gold[name]
+    inp = D.bench_inputs(name)
+    ctx = _lib.Context(0)
+    build = ShardedBuild(ctx, SoloComm(), engine.kmode_of(inp["kmer"]), inp["n_glob"], inp["c_lo"], inp["n_loc"])
+    store = engine.ContigStore(ctx, inp["blob"], inp["offs"], inp["key_len"])
+    rec_dev = _lib.DevBuf.from_numpy(ctx, inp["rec"].view(np.int64).reshape(-1))
+    try:
+        assert build.native is not None
+        for _ in range(4):
+            build.run(store, rec_dev.ptr, len(inp["rec"]), count=False)
+        build.sync()
+        info = build.native.info()
+        assert info[5] == 4 and info[6] == 0, info.tolist()  # 4 deferred steps, none run again
+        assert int(info[0]) == g["M"]
+        e, deferred = build.native.newest_edges()
+        assert deferred
+        assert int(info[1]) == len(e.a)
+        assert edge_digest_of(e) == g["edges"]
+        prof = build.native.profile()
+        assert tuple(prof.shape) == (g["N"], g["M"])
+        sha, blocks = device_profile_digests(prof)
+        assert blocks == g["profile_blocks"] and sha == g["profile"]
+    finally:
+        build.close()
+        store.close()
+        rec_dev.close()
+        ctx.close()

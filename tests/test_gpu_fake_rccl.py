@@ -146,6 +146,15 @@ def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world, mode):
         got = np.concatenate([p[f"{tag}_profile"] for p in parts])
         assert np.array_equal(got.view(np.uint64), prof.view(np.uint64)), tag
         check_graph(parts, o_peer if tag == "peer" else o, tag + "_")
+        # the newest step's own edges (karma_step_newest_edges): in "fit" the
+        # deferred step's tail outputs (fixed-slot all-to-all, merge from
+        # slots, device-sized edge stage), else the synchronous re-run's
+        og = o_peer if tag == "peer" else o
+        check_graph(parts, og, tag + "_n")
+        s_cat = np.concatenate([p[f"{tag}_ns"] for p in parts])
+        assert np.array_equal(s_cat, og["shared"]), tag
+        for p in parts:
+            assert bool(p[f"{tag}_ndeferred"]) == (tag == "fit"), tag
 
 
 def test_rccl_config4_strong_8_ranks_digests():

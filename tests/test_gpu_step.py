@@ -92,6 +92,13 @@ def test_deferred_steps_then_kept_step_match_oracle(emulate, n_rate):
         got = r.build.native.profile().numpy()
         assert got.shape == prof_o.shape
         assert np.array_equal(got.view(np.uint64), prof_o.view(np.uint64))
+        # ... and its edges, from the arrays the deferred tail kernels wrote
+        # (step_edge_count / step_edge_write; emulated: step_merge_kernel first)
+        o = oracle_graph(rec, n)
+        e_def, deferred = r.build.native.newest_edges()
+        assert deferred
+        check_edges(e_def, o)
+        assert int(info[1]) == len(o["a"]), (info.tolist(), len(o["a"]))
         # an ACGT-only store: a deferred step enqueues ~30 HIP calls and waits
         # for nothing (with non-ACGT bases the exception keys' count is read back)
         if n_rate == 0:
@@ -99,12 +106,15 @@ def test_deferred_steps_then_kept_step_match_oracle(emulate, n_rate):
         res = r.step(keep=True)
         assert engine.decode_keys(res["columns"], -1) == cols_o
         assert np.array_equal(res["profile"].numpy().view(np.uint64), prof_o.view(np.uint64))
-        check_edges(res["edges"], oracle_graph(rec, n))
+        check_edges(res["edges"], o)
         assert res["E_local"] == len(res["edges"].a)
         # after sync, the newest deferred step's M and edge count (its status words)
         assert int(info[0]) == len(cols_o)
-        if not emulate:
-            assert int(info[1]) == len(res["edges"].a), (info.tolist(), len(res["edges"].a))
+        assert int(info[1]) == len(res["edges"].a), (info.tolist(), len(res["edges"].a))
+        # after a kept (synchronous) step the accessor answers with its edges
+        e_sync, deferred = r.build.native.newest_edges()
+        assert not deferred
+        check_edges(e_sync, o)
     finally:
         r.close()
 
@@ -294,4 +304,37 @@ def test_middle_deferred_step_rerun_keeps_newest_outputs():
         assert np.array_equal(r.build.native.profile().numpy().view(np.uint64), prof_o.view(np.uint64))
     finally:
         d_big.close()
+        r.close()
+
+
+@pytest.mark.parametrize("fault_seq", [4, 5])
+def test_failed_deferred_step_leaves_control_block_zeroed(monkeypatch, fault_seq):
+    """A deferred step that fails after its records job and tail kernels ran
+    (KARMA_STEP_FAULT_SEQ: the error path before the status kernel, which is
+    what clears the tail's own control block) must leave that block zeroed:
+    the next deferred jobs on the same tail take it as such.  Later deferred
+    steps' profile and edges stay bit-exact (ADVICE r05, step.hip FailGuard)."""
+    monkeypatch.setenv("KARMA_STEP_FAULT_SEQ", str(fault_seq))
+    n = 3000
+    rec = engine.synth_records(SEED, n, 0, 200_000, True)
+    r = Run(n, rec, n_rate=0)
+    try:
+        failed = 0
+        for _ in range(fault_seq + 4):  # both main streams' tails run again after the failure
+            try:
+                r.step(count=False)
+            except _lib.KarmaError as e:
+                assert "injected fault" in str(e)
+                failed += 1
+        assert failed == 1
+        r.build.sync()
+        info = r.build.native.info()
+        assert info[6] == 0, info.tolist()  # no stale flag asked for a re-run
+        o = oracle_graph(rec, n)
+        e, deferred = r.build.native.newest_edges()
+        assert deferred
+        check_edges(e, o)
+        prof_o, _ = oracle_profile(r.blob, r.offs, 0, n)
+        assert np.array_equal(r.build.native.profile().numpy().view(np.uint64), prof_o.view(np.uint64))
+    finally:
         r.close()

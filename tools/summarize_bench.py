@@ -14,6 +14,9 @@ for path in sys.argv[1:]:
     sd = d.get("step_driver") or {}
     print(path, "ms/step", d["ms_per_step"], "n_gpus", d["n_gpus"], "parity", d.get("parity"),
           "frac", r.get("frac"), r.get("kernel"), r.get("avg_launch_ms"))
+    print("  single_batch_ms", d.get("single_batch_ms"), "parity_detail",
+          {x: (d.get("parity_detail") or {}).get(x) for x in ("against", "mismatch", "edges")},
+          "timed_step", ((d.get("parity_detail") or {}).get("timed_step") or {}).get("deferred_on_every_rank"))
     print("  transport", d.get("transport"))
     print("  host_us", d.get("host_us_per_step"), "calls", d.get("api_calls_per_step"), "wait_us",
           sd.get("host_wait_us_per_step"), "drain_us", sd.get("drain_us"), "mode", sd.get("mode"))
