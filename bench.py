@@ -79,6 +79,11 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP-event timing")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end, drop-in and eq-path legs")
     ap.add_argument("--no-parity", action="store_true", help="skip the in-run digest check")
+    ap.add_argument("--records", choices=("flagged", "pairs"), default="flagged",
+                    help="device format of the read->contig records the step takes: flagged (KARMA_REC_FLAGGED, "
+                         "u32 contig | read-start << 31: the graph depends only on which records share a read) or "
+                         "pairs ({u32 read id, u32 contig}); the other format is timed too, as records_other")
+    ap.add_argument("--no-other-format", action="store_true", help="skip the records_other leg")
     a = ap.parse_args()
     a.strong = not a.weak
     return a
@@ -263,10 +268,15 @@ class Leg:
         log(f"[rank {rank}] {'strong' if args.strong else 'weak'}: generated {inp['n_loc']} contigs "
             f"({int(inp['offs'][-1])} bases), {inp['f_loc']} fragments, {self.A} records in "
             f"{time.time() - t_gen:.1f}s")
+        # the records on the device in the step's format: KARMA_REC_FLAGGED words
+        # (4 bytes per record) or (read, contig) pairs (8), the same records
+        self.flagged = args.records == "flagged"
+        self.rec_bytes = 4 if self.flagged else 8
         self.build = ShardedBuild(ctx, comm, engine.kmode_of(inp["kmer"]), inp["n_glob"], inp["c_lo"], inp["n_loc"],
-                                  emulate_ranks=inp["emu"])  # sets the library-owned main + side streams
+                                  emulate_ranks=inp["emu"], flagged=self.flagged)  # library-owned streams
         self.store = engine.ContigStore(ctx, inp["blob"], inp["offs"], inp["key_len"])
-        self.rec_dev = _lib.DevBuf.from_numpy(ctx, inp["rec"].view(np.int64).reshape(-1))
+        self.rec_dev = _lib.DevBuf.from_numpy(ctx, engine.flag_records(inp["rec"]) if self.flagged
+                                              else inp["rec"].view(np.int64).reshape(-1))
         ctx.sync()
         self.packed_bytes = int(np.sum((np.diff(inp["offs"]) + 3) // 4))  # sum ceil(L/4)
         self.ctxs = self.build.contexts()  # main context (+ the concurrent graph build's)
@@ -391,6 +401,39 @@ class Leg:
                 "step": "deferred" if native else "synchronous",
                 "note": "one batch from idle streams to its synced, checked status (no pipelining with other "
                         "batches); median over reps of the max over ranks"}
+
+    def other_format(self, steps, warmup):
+        """The same workload with the records in the other device format (a
+        second build on the same store; same step kinds, no per-kernel pass):
+        {ms_per_step, value} so both formats are measured in one line."""
+        from karma_amd import _lib, engine
+        from karma_amd.distributed import ShardedBuild
+
+        inp, ctx = self.inp, self.rec_dev.ctx
+        flagged = not self.flagged
+        build = ShardedBuild(ctx, self.comm, engine.kmode_of(inp["kmer"]), inp["n_glob"], inp["c_lo"], inp["n_loc"],
+                             emulate_ranks=inp["emu"], flagged=flagged)
+        dev = _lib.DevBuf.from_numpy(ctx, engine.flag_records(inp["rec"]) if flagged
+                                     else inp["rec"].view(np.int64).reshape(-1))
+        try:
+            native = build.native is not None
+            run = lambda: build.run(self.store, dev.ptr, self.A, count=not native)  # noqa: E731
+            for _ in range(warmup):
+                run()
+            build.sync()
+            self.comm.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                run()
+            build.sync()
+            self.comm.barrier()
+            dt = self.comm.max_float(time.perf_counter() - t0)
+        finally:
+            build.close()
+            dev.close()
+        units = self.comm.sum_int(inp["n_loc"] + inp["f_loc"]) * steps
+        return {"format": "flagged" if flagged else "pairs", "bytes_per_record": 4 if flagged else 8,
+                "ms_per_step": round(dt / steps * 1e3, 3), "value": round(units / dt, 1), "steps": steps}
 
     def close(self):
         self.build.close()
@@ -578,6 +621,7 @@ def run(args, rank, world, local_rank, launcher):
                          f"rebuild with `make -C karma_amd/csrc` (KARMA_ALLOW_VARIANT=1 to time a variant)")
 
     leg = Leg(args, ctx, comm, rank, world)
+    rec_bytes, flagged = leg.rec_bytes, leg.flagged
     WATCHDOG.tick("inputs resident")
     inp, A = leg.inp, leg.A
     n_loc, f_loc = inp["n_loc"], inp["f_loc"]
@@ -593,7 +637,7 @@ def run(args, rank, world, local_rank, launcher):
     per_kernel_bytes = {
         "kmer_profile": leg.packed_bytes + 8 * n_loc * M,
         "kmer_presence": leg.packed_bytes,
-        "graph_classify": 8 * A,  # the records, read once
+        "graph_classify": leg.rec_bytes * A,  # the records, read once (4 or 8 bytes each by format)
     }
     # intermediate (not in the roofline bytes): the binned classify (<= 56 code
     # buckets) writes one 2-byte code per compact read into bucket runs, which
@@ -630,7 +674,7 @@ def run(args, rank, world, local_rank, launcher):
                             "other stream's batch with two main streams, beside nothing of the profile with one); "
                             "solo_*: the sequential pass, alone on the chip")
     write_ceiling = profile_write_ceiling(ctx, leg, n_loc, M, kern, args.steps)
-    step_bytes = leg.packed_bytes + 8 * n_loc * M + 8 * A + 16 * res["E_local"] + 8 * n_loc
+    step_bytes = leg.packed_bytes + 8 * n_loc * M + leg.rec_bytes * A + 16 * res["E_local"] + 8 * n_loc
     host_us, api_calls = leg.host_us_per_step, leg.api_calls_per_step
     si = leg.step_info
     step_driver = ({"native": True, "deferred_steps": si[5], "synchronous_steps": si[4], "rerun_steps": si[6],
@@ -651,6 +695,11 @@ def run(args, rank, world, local_rank, launcher):
         WATCHDOG.tick("parity")
     single = leg.single_batch()
     WATCHDOG.tick("single batch")
+    other = None
+    # (not for a profile of tens of GB: the second build would hold its own buffers beside the first's)
+    if not args.no_other_format and 8 * n_loc * M < (32 << 30):
+        other = leg.other_format(min(args.steps, 40), min(args.warmup, 5))
+        WATCHDOG.tick("other records format")
     extra = {}
     if rank == 0 and world == 1 and not args.no_e2e and inp["emu"] == 1 and not args.shuffle_contigs:
         extra = end_to_end_legs(args, inp, ctx, leg.build, leg.store)
@@ -713,7 +762,16 @@ def run(args, rank, world, local_rank, launcher):
             "profile_write_ceiling": write_ceiling,
             "step": {"hbm_bytes_per_gpu": step_bytes, "achieved_GBs": round(step_bytes / step_s / 1e9, 1),
                      "frac": round(step_bytes / step_s / 1e9 / PEAK_HBM_GBS, 4),
-                     "formula": "sum ceil(L/4) + 8*N*M + 8*A + 16*E + 8*N (SURVEY.md 8(d))"},
+                     "formula": f"sum ceil(L/4) + 8*N*M + {rec_bytes}*A + 16*E + 8*N (SURVEY.md 8(d); "
+                                f"{rec_bytes} bytes per record in the {args.records} format)"},
+            "records_format": {"format": args.records,
+                               "layout": ("u32 contig | (first record of its read) << 31 (KARMA_REC_FLAGGED)"
+                                          if flagged else "{u32 read id, u32 contig} (KARMA_REC_SORTED)"),
+                               "bytes_per_record": rec_bytes,
+                               "note": "the same records (config's fragments); the graph depends only on which "
+                                       "records share a read, so the read ids may be replaced by read-start flags; "
+                                       "records_other times the other format"},
+            **({"records_other": other} if other else {}),
             "host_us_per_step": round(host_us, 1),
             "api_calls_per_step": round(api_calls, 1),
             "step_driver": step_driver,
@@ -784,7 +842,7 @@ def pmc_traffic(args, world, kernel):
     ranks = world * max(1, args.emulate_ranks)
     # strong and weak are one workload on one rank (the table's config3_n1)
     key = f"{args.config}{'_strong' if args.strong and ranks > 1 else ''}" \
-          f"{'_shuffled' if args.shuffle_contigs else ''}_n{ranks}"
+          f"{'_shuffled' if args.shuffle_contigs else ''}{'_pairs' if args.records == 'pairs' else ''}_n{ranks}"
     try:
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
             return json.load(f).get(key, {}).get(kernel)

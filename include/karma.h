@@ -226,7 +226,13 @@ int karma_kmer_row_totals(karma_kmer_plan* p, int64_t* dst_host);
 typedef struct karma_pairs karma_pairs;
 #define KARMA_REC_SORTED 0   /* records grouped by read, read ids non-decreasing (SAM order) */
 #define KARMA_REC_UNSORTED 1 /* any order: sorted by read on the device first */
-/* records: n_records x {u32 read_id, u32 contig} interleaved.  Deduplicates
+#define KARMA_REC_FLAGGED 2  /* records as n_records x u32: contig | (first record of its read) << 31, grouped by
+                              * read.  The graph depends only on which records share a read (read_graph.py:31-49
+                              * intersects readsets), so the read ids give way to read-start flags: 4 bytes per
+                              * record instead of 8.  Record 0 always starts a read; contig ids < 2^31. */
+/* records: n_records x {u32 read_id, u32 contig} interleaved (or, flags =
+ * KARMA_REC_FLAGGED, n_records x u32 flagged contigs; records is then a
+ * uint32_t array of n_records entries).  Deduplicates
  * (read, contig) (contig.py:11 keeps QNAMEs in a set); emits for every read's
  * contig set S every pair a <= b of S: the diagonal (a, a) counts |readset(a)|,
  * (a, b) counts |R_a ∩ R_b| (read_graph.py:34). */
@@ -356,6 +362,7 @@ int karma_edges_get_ordered(karma_edges* e, uint32_t* a, uint32_t* b, double* w,
 typedef struct karma_step karma_step;
 #define KARMA_STEP_KEEP 1       /* outputs kept for karma_step_profile / _columns / _edges */
 #define KARMA_STEP_SEQUENTIAL 2 /* every kernel on the main stream (per-kernel timing) */
+#define KARMA_STEP_FLAGGED 8    /* records_dev in the KARMA_REC_FLAGGED format (n_records x u32) */
 #define KARMA_STEP_DEFER 4      /* outputs not read: the step returns without waiting for anything (its
                                  * checks arrive through mapped memory and are read <= 3 steps later; a
                                  * step needing the general path runs again synchronously; a status later

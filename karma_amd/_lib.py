@@ -38,6 +38,8 @@ _DTYPE_CODE = {np.dtype(np.uint8): KARMA_DT_U8, np.dtype(np.int32): KARMA_DT_I32
 KARMA_KMER_5P6 = -1
 KARMA_REC_SORTED = 0
 KARMA_REC_UNSORTED = 1
+KARMA_REC_FLAGGED = 2
+KARMA_STEP_FLAGGED = 8
 KARMA_MODE_READS = 0
 KARMA_MODE_EQ = 1
 KARMA_STEP_KEEP, KARMA_STEP_SEQUENTIAL, KARMA_STEP_DEFER = 1, 2, 4

@@ -593,6 +593,7 @@ int sort_reduce_pairs(karma_ctx* ctx, const uint64_t* keys_in, const int64_t* co
 struct karma_graph_job {
     karma_pairs* p = nullptr;
     karma::DevArray<uint2> own;      // copied / read-sorted records, read by the kernels until _end
+    karma::DevArray<uint32_t> ownw;  // copied flagged records (KARMA_REC_FLAGGED)
     karma::SetsJob* sets = nullptr;  // open compact-path call (null: p already complete)
     ~karma_graph_job() {
         if (sets) karma::sets_free(sets);
@@ -607,12 +608,39 @@ int karma_graph_records_begin(karma_ctx* ctx, const uint32_t* records, int64_t A
     KARMA_TRY(ctx_begin(ctx));
     KARMA_CHECK(out && (records || A == 0) && A >= 0, KARMA_ERR_ARG, "karma_graph_records: bad arguments");
     KARMA_CHECK(A < (int64_t(1) << 40), KARMA_ERR_ARG, "too many records");
+    KARMA_CHECK(flags == KARMA_REC_SORTED || flags == KARMA_REC_UNSORTED || flags == KARMA_REC_FLAGGED, KARMA_ERR_ARG,
+                "karma_graph_records: unknown record format %d", flags);
     // held until the job owns it, so every early return (KARMA_HIP / KARMA_CHECK) frees it
     std::unique_ptr<karma_pairs> ph(new karma_pairs());
     ph->ctx = ctx;
     DevArray<uint2> own;
+    DevArray<uint32_t> ownw;
     const uint2* rec = reinterpret_cast<const uint2*>(records);
     int rc = KARMA_OK;
+    if (flags == KARMA_REC_FLAGGED) {
+        // one u32 per record; the classify kernel streams 16-byte loads
+        const uint32_t* w = records;
+        if (!is_device || (reinterpret_cast<uintptr_t>(w) & 15)) {
+            if ((rc = ownw.alloc(ctx, std::max<int64_t>(A, 1)))) return rc;
+            if (A)
+                KARMA_HIP(hipMemcpyAsync(ownw.ptr, records, A * 4,
+                                         is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, ctx->stream));
+            w = ownw.ptr;
+        }
+        karma_pairs* p = ph.get();
+        auto* job = new karma_graph_job();
+        job->p = ph.release();
+        job->ownw.swap(ownw);
+        RecIn in;
+        in.fw = w;
+        rc = N > sets_max_contigs() ? records_to_pairs_sets(ctx, in, A, N, p) : sets_begin(ctx, in, A, N, &job->sets);
+        if (rc) {
+            delete job;
+            return rc;
+        }
+        *out = job;
+        return KARMA_OK;
+    }
     if (!is_device || flags == KARMA_REC_UNSORTED) {
         if ((rc = own.alloc(ctx, A))) return rc;
         if (A) {
@@ -642,10 +670,12 @@ int karma_graph_records_begin(karma_ctx* ctx, const uint32_t* records, int64_t A
     auto* job = new karma_graph_job();
     job->p = ph.release();
     job->own.swap(own);
+    RecIn in;
+    in.pr = rec;
     if (N > sets_max_contigs()) {  // wide path: runs to completion here
-        rc = records_to_pairs_sets(ctx, rec, A, N, p);
+        rc = records_to_pairs_sets(ctx, in, A, N, p);
     } else {
-        rc = sets_begin(ctx, rec, A, N, &job->sets);
+        rc = sets_begin(ctx, in, A, N, &job->sets);
     }
     if (rc) {
         delete job;

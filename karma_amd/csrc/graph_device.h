@@ -50,28 +50,22 @@ __device__ __forceinline__ void sort_dedup(ReadSet& s) {
 // global memory, one thread per read.
 // contig ids relabelled by map (a bijection of [0, N); the identity below)
 template <typename Map, typename Emit>
-__device__ inline void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_t i, Map map, Emit emit) {
-    const uint32_t rid = rec[i].x;
-    int64_t end = i;
-    while (end < A && rec[end].x == rid) ++end;
+__device__ inline void read_pairs_slow(karma::RecIn rec, int64_t A, int64_t i, Map map, Emit emit) {
+    int64_t end = i + 1;
+    while (end < A && rec.cont(end)) ++end;
     for (int64_t p = i; p < end; ++p) {
-        const uint32_t c = map(rec[p].y);
+        const uint32_t c = map(rec.contig(p));
         bool dup = false;
-        for (int64_t q = i; q < p && !dup; ++q) dup = map(rec[q].y) == c;
+        for (int64_t q = i; q < p && !dup; ++q) dup = map(rec.contig(q)) == c;
         if (dup) continue;
         for (int64_t q = i; q < end; ++q) {
-            const uint32_t d = map(rec[q].y);
+            const uint32_t d = map(rec.contig(q));
             if (d < c) continue;
             bool first = true;
-            for (int64_t r = i; r < q && first; ++r) first = map(rec[r].y) != d;
+            for (int64_t r = i; r < q && first; ++r) first = map(rec.contig(r)) != d;
             if (first) emit(c, d);
         }
     }
-}
-
-template <typename Emit>
-__device__ inline void read_pairs_slow(const uint2* __restrict__ rec, int64_t A, int64_t i, Emit emit) {
-    read_pairs_slow(rec, A, i, [](uint32_t c) { return c; }, emit);
 }
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {

@@ -165,6 +165,9 @@ __device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__buil
 constexpr int kCW = 256;                // classify threads per block (4 independent waves)
 constexpr int kCIter = 512;             // records per wave step (8 per lane)
 constexpr int kCPer = kCIter / 128;     // 16-byte units per lane per step
+constexpr int kFPer = kCIter / 256;     // ... of flagged records (4 bytes each)
+constexpr uint32_t kContigMask = 0x7FFFFFFFu;  // flagged record: contig id; bit 31 starts a read
+constexpr uint32_t kPadW = 0x80000000u;        // flagged padding past a chunk: a read of its own, never emitted
 constexpr int64_t kCChunk = 8192;       // records per wave chunk (16 steps; chunk_records may halve it)
 
 struct ClassArgs {
@@ -187,6 +190,7 @@ struct ClassArgs {
     unsigned* skip;         // set: leave the chunks empty (a relabelled rerun follows)
     int64_t chunk;          // records per chunk (chunk_records)
     unsigned* vote = nullptr;  // classify decides the relabel itself (no probe kernel): chunks' votes
+    const uint32_t* recw = nullptr;  // FLAG: the records as u32 contig | first-of-read << 31 (RecIn::fw)
 };
 // In-classify relabel decision (a job without the probe kernel): every
 // kVoteStride-th chunk votes when more than 1/8 of its reads are general
@@ -276,6 +280,15 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
+#ifndef KARMA_CLS_DEFER_RARE
+#define KARMA_CLS_DEFER_RARE 1  // general / big reads of a step emitted by a replay after the chunk's loop
+                                // (the second walk inside the loop spilled 158 SGPRs: 222M -> 183M VALU)
+#endif
+constexpr int kRareMax = int(kCChunk / kCIter);  // steps per chunk
+constexpr int kRareW = 5;                        // words per listed step
+#ifndef KARMA_CLS_NO_RARE
+#define KARMA_CLS_NO_RARE 0  // measurement only (A/B of the rare pass's register cost): no general / big reads emitted
+#endif
 #ifndef KARMA_CLS2_WAVES
 #define KARMA_CLS2_WAVES 4  // 4: 0.541 ms; 5 (84 VGPRs): 0.545; 6 (80 VGPRs, 7 spilled): 0.576
 #endif
@@ -311,10 +324,23 @@ struct BinArgs {
 // compact-code path exists (n_contigs <= 2^21); REMAP: contig ids relabelled
 // through P.remap as they are read (contig order without locality, see
 // relabel); BIN: codes into bucket segments (see above; not with HIST)
-template <bool HIST, bool COMPACT, bool REMAP = false, bool BIN = false>
+// FLAG: flagged records (4 bytes each, read starts flagged; RecIn): a
+// 512-record step is 2 KB (two 16-byte units per lane), no read ids to
+// compare or order-check
+template <bool HIST, bool COMPACT, bool REMAP = false, bool BIN = false, bool FLAG = false>
 __global__ void __launch_bounds__(kCW) __attribute__((amdgpu_waves_per_eu(KARMA_CLS2_WAVES, KARMA_CLS2_WAVES)))
 classify2_kernel(ClassArgs P, BinArgs Q) {
     static_assert(!(HIST && BIN), "the binned classify has no partition block histograms");
+    // P's fields only the rare steps' replay uses (after the chunk's loop),
+    // read there from the kernel argument segment behind an opaque pointer: so
+    // they are not held in SGPRs across the hot loop (r05 measured the same
+    // re-read INSIDE the loop 0.036 ms slower; here no load is in the loop)
+    auto PA = [&]() -> const ClassArgs& {
+        if (!KARMA_CLS_DEFER_RARE) return P;
+        const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        return *reinterpret_cast<const ClassArgs*>(ka);
+    };
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
@@ -349,6 +375,12 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // [3..6] the first 16 directory bytes (for the header)
     __shared__ uint32_t bback[kCW / 64][BIN ? 8 : 1];
     uint32_t* const bst = bback[wave];
+    // steps with a general or big read, replayed after the chunk's main loop
+    // (kRareW words each: step index | carry flags, the carried tail's state,
+    // the previous record's read id), so the hot loop holds no second walk
+    __shared__ uint32_t rlist[kCW / 64][KARMA_CLS_DEFER_RARE ? kRareMax * kRareW : 1];
+    uint32_t* const rl = rlist[wave];
+    uint32_t n_rare = 0;  // uniform
     constexpr bool hist_on = HIST;
     if (hist_on) {
         for (int b = lane; b < P.Bc; b += 64) wh[b] = 0;
@@ -419,6 +451,23 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // records [t0, hi) of a step, coalesced: unit u of lane l = records t0 + 128u + 2l, + 1.
     // Past the chunk: read id kEmpty (a read of its own that is never emitted), contig 0.
     auto prefetch = [&](u32x4 (&dst)[kCPer], int64_t t0, int64_t hi) {
+        if (FLAG) {  // unit u of lane l = records t0 + 256u + 4l .. + 3; past the chunk: a read start, contig 0
+            const int64_t gw = t0 + 4 * lane;
+            if (t0 + kCIter <= hi) {
+#pragma unroll
+                for (int u = 0; u < kFPer; ++u)
+                    dst[u] = KARMA_REC_NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.recw + gw + 256 * u))
+                                          : *reinterpret_cast<const u32x4*>(P.recw + gw + 256 * u);
+            } else {
+#pragma unroll
+                for (int u = 0; u < kFPer; ++u) {
+                    const int64_t gi = gw + 256 * u;
+                    dst[u] = u32x4{gi < hi ? P.recw[gi] : kPadW, gi + 1 < hi ? P.recw[gi + 1] : kPadW,
+                                   gi + 2 < hi ? P.recw[gi + 2] : kPadW, gi + 3 < hi ? P.recw[gi + 3] : kPadW};
+                }
+            }
+            return;
+        }
         const int64_t gb = t0 + 2 * lane;
         if (t0 + kCIter <= hi) {
 #pragma unroll
@@ -439,7 +488,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     };
     // carry from the previous lane 63: its last read id, and its tail read
     bool have_prev = c_lo > 0;
-    uint32_t prev_rid = have_prev ? P.rec[c_lo - 1].x : kEmpty;
+    uint32_t prev_rid = FLAG || !have_prev ? kEmpty : P.rec[c_lo - 1].x;
     bool ct_ok = false;  // a tail read (started in this chunk) is carried
     RState ct{};
     uint32_t ct_len = 0, ct_pos = 0;
@@ -454,17 +503,45 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // from the remap table into `nxt`, loaded a step earlier), a full step
     // before they are used; `buf` then takes the records two steps ahead
     auto remap_units = [&](u32x4 (&b)[kCPer]) {
+        if (FLAG) {  // the low 31 bits relabelled, the read-start flag kept
+            auto rm = [&](uint32_t w) {
+                const uint32_t c = w & kContigMask;
+                return c < P.N ? P.remap[c] | (w & ~kContigMask) : w;
+            };
+#pragma unroll
+            for (int u = 0; u < kFPer; ++u) b[u] = u32x4{rm(b[u].x), rm(b[u].y), rm(b[u].z), rm(b[u].w)};
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < kCPer; ++u) {  // ids out of range stay out of range (the range check fails the call)
             b[u].y = b[u].y < P.N ? P.remap[b[u].y] : b[u].y;
             b[u].w = b[u].w < P.N ? P.remap[b[u].w] : b[u].w;
         }
     };
-    auto step = [&](auto full_tag, u32x4 (&buf)[kCPer], u32x4 (&nxt)[kCPer], int64_t t0) {
+    // REPLAY: a rare step again, after the main loop: its records reloaded and
+    // its carry-in restored; only the general / big reads are emitted
+    auto step = [&](auto full_tag, auto replay_tag, u32x4 (&buf)[kCPer], u32x4 (&nxt)[kCPer], int64_t t0) {
         constexpr bool FULL = decltype(full_tag)::value;
-        uint32_t rid[8], ctg[8];
+        constexpr bool REPLAY = decltype(replay_tag)::value;
+        uint32_t rid[8], ctg[8];  // FLAG: rid holds the raw words (bit 31: a read starts here)
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
-        if (!BIN) {
+        if (FLAG) {
+            // 16-byte granule g = 64u + L (records 4g .. 4g + 3) at slot g ^ ((g >> 3) & 1): lane l
+            // reads granules 2l, 2l + 1 (conflict-free on both sides; 2 KB: BIN's half buffer)
+#pragma unroll
+            for (int u = 0; u < kFPer; ++u) {
+                const int g = 64 * u + lane;
+                tb[g ^ ((g >> 3) & 1)] = buf[u];
+            }
+            wave_sync();
+            const int sw = (lane >> 2) & 1;
+            const u32x4 q0 = tb[(2 * lane) ^ sw], q1 = tb[(2 * lane + 1) ^ sw];
+            rid[0] = q0.x, rid[1] = q0.y, rid[2] = q0.z, rid[3] = q0.w;
+            rid[4] = q1.x, rid[5] = q1.y, rid[6] = q1.z, rid[7] = q1.w;
+            wave_sync();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ctg[i] = rid[i] & kContigMask;
+        } else if (!BIN) {
 #pragma unroll
             for (int u = 0; u < kCPer; ++u) {
                 const int row = 16 * u + (lane >> 2);
@@ -506,7 +583,8 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                 wave_sync();
             }
         }
-        if (REMAP) {
+        if (REPLAY) {
+        } else if (REMAP) {
             if (t0 + kCIter < c_hi) remap_units(nxt);
             if (t0 + 2 * kCIter < c_hi) prefetch(buf, t0 + 2 * kCIter, c_hi);
         } else if (t0 + kCIter < c_hi) {
@@ -514,12 +592,14 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         }
         // valid records of this lane (own reads start at a valid record)
         const int nval = FULL ? 8 : (int)max<int64_t>(0, min<int64_t>(8, c_hi - (t0 + 8 * lane)));
-        const uint32_t prev_last = dpp_shr1(prev_rid, rid[7]);
+        const uint32_t prev_last = FLAG ? 0u : dpp_shr1(prev_rid, rid[7]);
         // order and range checks as lane masks (padding: read id kEmpty, contig
         // 0); the order of records inside the lane is checked during the walk
-        bad_order |= lanes(prev_last > rid[0]) & (have_prev ? ~0ull : ~1ull);
-        bad_contig |= lanes(max(max(max(ctg[0], ctg[1]), max(ctg[2], ctg[3])),
-                                max(max(ctg[4], ctg[5]), max(ctg[6], ctg[7]))) >= P.N);
+        if (!REPLAY) {
+            if (!FLAG) bad_order |= lanes(prev_last > rid[0]) & (have_prev ? ~0ull : ~1ull);
+            bad_contig |= lanes(max(max(max(ctg[0], ctg[1]), max(ctg[2], ctg[3])),
+                                    max(max(ctg[4], ctg[5]), max(ctg[6], ctg[7]))) >= P.N);
+        }
         const uint32_t ubase = (uint32_t)(t0 - c_lo) + 8u * lane;
         // The lane's walk (branch-free: no lane predicate lives across a branch,
         // so the compiler keeps them as SGPR lane masks).  Emission: codes from
@@ -553,13 +633,14 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                 } else {
                     const uint64_t g = e & ~big & ~ok;
                     if (g) {
-                        if (in_mask(g)) (BIN ? P.codes + c_lo : out)[P.chunk - 1 - (ng + rank_below(g))] = pos;
+                        const ClassArgs& Pa = PA();
+                        if (in_mask(g)) (Pa.codes + c_lo)[Pa.chunk - 1 - (ng + rank_below(g))] = pos;
                         ng += __popcll(g);
                     }
                     const uint64_t bg = e & big;
                     if (bg) {
                         if (in_mask(bg)) {
-                            const ClassArgs& Pa = P;
+                            const ClassArgs& Pa = PA();
                             Pa.big_list[atomicAdd(Pa.big_n, 1u)] = c_lo + pos;
                         }
                     }
@@ -568,6 +649,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             // S(i): lanes where a read starts at record i (lane 0 of a chunk's
             // first step: always); computed where used, so few masks are live
             auto S = [&](int i) -> uint64_t {
+                if (FLAG) return lanes((int)rid[i] < 0) | (i == 0 && !have_prev ? 1ull : 0ull);
                 return i == 0 ? lanes(rid[0] != prev_last) | (have_prev ? 0ull : 1ull) : lanes(rid[i] != rid[i - 1]);
             };
             const uint64_t S0 = S(0);
@@ -591,7 +673,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     // a new read: bit 3 alone (c - fm3 = 3)
                     st.win = (in_mask(Si) ? 0u : st.win) | (1u << min(c - fm3, 31u));
                     st.fm3 = fm3;
-                    if (!RARE) bad_order |= lanes(rid[i - 1] > rid[i]);
+                    if (!RARE && !FLAG) bad_order |= lanes(rid[i - 1] > rid[i]);
                 }
                 if (i < 7) {
                     // an own read ends at i (the next record starts one); it
@@ -629,6 +711,13 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             emit(have, ok, code, in_pos, big);
             return rare;
         };
+        if (REPLAY) {
+            RState st2;
+            uint32_t spos2;
+            uint64_t started2;
+            walk(std::true_type{}, st2, spos2, started2);
+            return;
+        }
         RState st;
         uint32_t spos;
         uint64_t started;
@@ -643,7 +732,18 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         ct_next.win = (uint32_t)__builtin_amdgcn_readlane((int)st.win, 63);
         const uint32_t ct_len_next = (uint32_t)__builtin_amdgcn_readlane((int)t_len, 63);
         const uint32_t ct_pos_next = (uint32_t)__builtin_amdgcn_readlane((int)t_pos, 63);
-        if (rare) {
+        if (KARMA_CLS_DEFER_RARE && rare) {
+            // listed with its carry-in (ct* and prev_rid still hold it here)
+            if (lane == 0) {
+                uint32_t* const e = rl + kRareW * n_rare;
+                e[0] = (uint32_t)((t0 - c_lo) / kCIter) | (ct_ok ? 256u : 0u) | (have_prev ? 512u : 0u);
+                e[1] = ct.fm3;
+                e[2] = ct.win;
+                e[3] = ct_len | ct_pos << 8;
+                e[4] = prev_rid;
+            }
+            ++n_rare;
+        } else if (!KARMA_CLS_DEFER_RARE && !KARMA_CLS_NO_RARE && rare) {
             RState st2;
             uint32_t spos2;
             uint64_t started2;
@@ -654,7 +754,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         ct = ct_next;
         ct_len = ct_len_next;
         ct_pos = ct_pos_next;
-        prev_rid = (uint32_t)__builtin_amdgcn_readlane((int)rid[7], 63);
+        if (!FLAG) prev_rid = (uint32_t)__builtin_amdgcn_readlane((int)rid[7], 63);
         have_prev = true;
     };
     u32x4 buf[kCPer];
@@ -672,23 +772,56 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         }
         return;
     }
+    const std::false_type main_pass{};
     if (!REMAP) {
         int64_t t0 = c_lo;
-        for (; t0 + kCIter <= c_hi; t0 += kCIter) step(std::true_type{}, buf, buf, t0);
-        if (t0 < c_hi) step(std::false_type{}, buf, buf, t0);
+        for (; t0 + kCIter <= c_hi; t0 += kCIter) step(std::true_type{}, main_pass, buf, buf, t0);
+        if (t0 < c_hi) step(std::false_type{}, main_pass, buf, buf, t0);
     } else {  // two register sets, alternating
         u32x4 buf2[kCPer];
         if (c_lo + kCIter < c_hi) prefetch(buf2, c_lo + kCIter, c_hi);
         remap_units(buf);
         for (int64_t t0 = c_lo; t0 < c_hi;) {
-            if (t0 + kCIter <= c_hi) step(std::true_type{}, buf, buf2, t0);
-            else step(std::false_type{}, buf, buf2, t0);
+            if (t0 + kCIter <= c_hi) step(std::true_type{}, main_pass, buf, buf2, t0);
+            else step(std::false_type{}, main_pass, buf, buf2, t0);
             t0 += kCIter;
             if (t0 >= c_hi) break;
-            if (t0 + kCIter <= c_hi) step(std::true_type{}, buf2, buf, t0);
-            else step(std::false_type{}, buf2, buf, t0);
+            if (t0 + kCIter <= c_hi) step(std::true_type{}, main_pass, buf2, buf, t0);
+            else step(std::false_type{}, main_pass, buf2, buf, t0);
             t0 += kCIter;
         }
+    }
+    if (KARMA_CLS_DEFER_RARE && n_rare) {
+        // the listed steps again (in step order: the general starts land in the
+        // chunk's region in the order the in-loop pass wrote them), each from
+        // its carry-in; the chunk's own carry is restored for the tail below
+        const bool s_ok = ct_ok, s_hp = have_prev;
+        const RState s_ct = ct;
+        const uint32_t s_len = ct_len, s_pos = ct_pos, s_rid = prev_rid;
+        wave_lds_order();
+        for (uint32_t k = 0; k < n_rare; ++k) {
+            const uint32_t* const e = rl + kRareW * k;
+            const uint32_t w0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[0]);
+            ct_ok = (w0 & 256u) != 0;
+            have_prev = (w0 & 512u) != 0;
+            ct.fm3 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[1]);
+            ct.win = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[2]);
+            const uint32_t w3 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[3]);
+            ct_len = w3 & 255u;
+            ct_pos = w3 >> 8;
+            prev_rid = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[4]);
+            const int64_t t0 = c_lo + (int64_t)(w0 & 255u) * kCIter;
+            prefetch(buf, t0, c_hi);
+            if (REMAP) remap_units(buf);
+            if (t0 + kCIter <= c_hi) step(std::true_type{}, std::true_type{}, buf, buf, t0);
+            else step(std::false_type{}, std::true_type{}, buf, buf, t0);
+        }
+        ct_ok = s_ok;
+        have_prev = s_hp;
+        ct = s_ct;
+        ct_len = s_len;
+        ct_pos = s_pos;
+        prev_rid = s_rid;
     }
     // the chunk's last tail read continues into the next chunk's first records
     // (at most 8 of them matter): uniform scalar walk
@@ -696,9 +829,17 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         RState h{};
         uint32_t hl = 0;
         for (; hl < (uint32_t)kMaxFast && c_hi + hl < P.A; ++hl) {
-            const uint2 r = P.rec[c_hi + hl];
-            if (r.x != prev_rid) break;
-            const uint32_t cy = REMAP && r.y < P.N ? P.remap[r.y] : r.y;
+            uint32_t y;
+            if (FLAG) {
+                const uint32_t w = P.recw[c_hi + hl];
+                if ((int)w < 0) break;  // the next read starts
+                y = w & kContigMask;
+            } else {
+                const uint2 r = P.rec[c_hi + hl];
+                if (r.x != prev_rid) break;
+                y = r.y;
+            }
+            const uint32_t cy = REMAP && y < P.N ? P.remap[y] : y;
             if (hl == 0) rs_reset(h, cy);
             else rs_add(h, cy);
         }
@@ -810,7 +951,7 @@ int general_grid(const karma_ctx* ctx, int64_t n_chunks) {
 // preview while the code partition waited for CU slots): every pair (p <= q)
 // of each general read's distinct contigs, as (a << 32 | b), appended to the
 // chunk's pair list.
-__global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ rec, int64_t A, uint32_t N,
+__global__ void __launch_bounds__(kGW) general_kernel(RecIn rec, int64_t A, uint32_t N,
                                                        const uint32_t* __restrict__ codes,
                                                        const uint32_t* __restrict__ n_gen, int64_t n_chunks,
                                                        uint64_t* __restrict__ pairs, int64_t pcap,
@@ -837,14 +978,12 @@ __global__ void __launch_bounds__(kGW) general_kernel(const uint2* __restrict__ 
         for (int t = 0; t < kMaxFast; ++t) rs.keep[t] = false;
         if (k < ng) {
             const int64_t s = c_lo + codes[c_lo + chunk_len - 1 - k];
-            const uint32_t rid = rec[s].x;
             bool v = true;
 #pragma unroll
             for (int t = 0; t < kMaxFast; ++t) {
-                uint2 r = make_uint2(kEmpty, kEmpty);
-                if (v && s + t < A) r = rec[s + t];
-                v = v && r.x == rid;
-                rs.m[t] = v && r.y < N ? (remap ? remap[r.y] : r.y) : kEmpty;
+                v = v && s + t < A && (t == 0 || rec.cont(s + t));
+                const uint32_t y = v ? rec.contig(s + t) : kEmpty;
+                rs.m[t] = v && y < N ? (remap ? remap[y] : y) : kEmpty;
             }
             sort_dedup(rs);
         }
@@ -2010,7 +2149,7 @@ __global__ void bucket_widen_kernel(const uint32_t* __restrict__ pent, RunDir di
 }
 
 // big reads (> 8 records): pair keys, one thread per read, O(m^3) dedup
-__global__ void big_pairs_kernel(const uint2* __restrict__ rec, int64_t A, const int64_t* __restrict__ big_list,
+__global__ void big_pairs_kernel(RecIn rec, int64_t A, const int64_t* __restrict__ big_list,
                                  int64_t n_big, uint32_t N, uint64_t* __restrict__ out,
                                  unsigned long long* __restrict__ n_out, int count_only,
                                  const uint32_t* __restrict__ remap) {
@@ -2060,7 +2199,7 @@ namespace karma {
 
 // The sorted unique list (mk, mc, U) plus the pairs of reads with > 8 records
 // (big_list) -> out.
-int finish_pairs(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, const int64_t* big_list, unsigned n_big,
+int finish_pairs(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, const int64_t* big_list, unsigned n_big,
                  DevArray<uint64_t>& mk, DevArray<int64_t>& mc, int64_t U, karma_pairs* out,
                  const uint32_t* remap = nullptr) {
     out->n_contigs = N;
@@ -2121,7 +2260,7 @@ __global__ void gather_lists_kernel(const uint64_t* __restrict__ lists, int64_t 
 // longer fit, so every read takes the general path (sorted distinct contigs,
 // per-chunk u64 pair lists, no atomics) and one 64-bit sort-reduce follows;
 // reads of > 8 records are merged as in the main path.
-int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
+int records_to_pairs_wide(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, karma_pairs* out) {
     KARMA_CHECK(N >= 1 && N <= (int64_t(1) << 24), KARMA_ERR_ARG, "n_contigs %lld out of range [1, 2^24]",
                 (long long)N);
     int bbits = 1;
@@ -2154,11 +2293,16 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
         KARMA_HIP(hipMemsetAsync(blk_items.ptr, 0, 2 * n_chunks * 8, ctx->stream));
         KARMA_HIP(hipMemsetAsync(n_gen.ptr, 0, n_chunks * 4, ctx->stream));
         if (A > 0) {
-            ClassArgs C{rec,       A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
+            ClassArgs C{rec.pr,    A,         (uint32_t)N, false,         codes.ptr, n_codes.ptr,
                         n_gen.ptr, blk_items.ptr, 1,     big_list.ptr, counters,  flags,
                         nullptr,   0,         0,       nullptr, 0, nullptr, kCChunk};
-            KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false>), ceil_div(n_chunks, kCW / 64), kCW, 0, C,
-                         BinArgs{});
+            C.recw = rec.fw;
+            if (rec.flagged())
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false, false, false, true>),
+                             ceil_div(n_chunks, kCW / 64), kCW, 0, C, BinArgs{});
+            else
+                KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, false>), ceil_div(n_chunks, kCW / 64), kCW,
+                             0, C, BinArgs{});
         }
         KARMA_LAUNCH(ctx, "graph_general", general_kernel, general_grid(ctx, n_chunks), kGW, 0, rec, A, (uint32_t)N,
                      codes.ptr, n_gen.ptr, n_chunks, plist.ptr, pcap, n_pl.ptr, blk_items.ptr + n_chunks, 1, flags,
@@ -2208,7 +2352,7 @@ int records_to_pairs_wide(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N
 // their distinct contigs span more than 4 ids.  One block, one round of loads.
 constexpr int kRelabelProbes = 256;
 
-__global__ void __launch_bounds__(kRelabelProbes) relabel_probe_kernel(const uint2* __restrict__ rec, int64_t A,
+__global__ void __launch_bounds__(kRelabelProbes) relabel_probe_kernel(RecIn rec, int64_t A,
                                                                        uint32_t N, unsigned* __restrict__ relabel,
                                                                        uint64_t* __restrict__ zero, int64_t n_zero) {
     __shared__ unsigned wide;
@@ -2229,17 +2373,22 @@ __global__ void __launch_bounds__(kRelabelProbes) relabel_probe_kernel(const uin
     const int64_t p = (A * (int64_t)threadIdx.x / kRelabelProbes) & ~int64_t(1);
     uint32_t rid[kW], ctg[kW];
     if (p + kW <= A) {
-        const u32x4* v = reinterpret_cast<const u32x4*>(rec + p);
+        if (rec.flagged()) {  // rid[j]: the raw word (bit 31 starts a read)
 #pragma unroll
-        for (int u = 0; u < kW / 2; ++u) {
-            const u32x4 q = v[u];
-            rid[2 * u] = q.x, ctg[2 * u] = q.y, rid[2 * u + 1] = q.z, ctg[2 * u + 1] = q.w;
+            for (int j = 0; j < kW; ++j) rid[j] = rec.fw[p + j], ctg[j] = rid[j] & kContigMask;
+        } else {
+            const u32x4* v = reinterpret_cast<const u32x4*>(rec.pr + p);
+#pragma unroll
+            for (int u = 0; u < kW / 2; ++u) {
+                const u32x4 q = v[u];
+                rid[2 * u] = q.x, ctg[2 * u] = q.y, rid[2 * u + 1] = q.z, ctg[2 * u + 1] = q.w;
+            }
         }
         // the first read that starts inside the window and ends inside it
         int s0 = -1, e0 = -1;
 #pragma unroll
         for (int j = 1; j < kW; ++j) {
-            const bool start = rid[j] != rid[j - 1];
+            const bool start = rec.flagged() ? (int)rid[j] < 0 : rid[j] != rid[j - 1];
             if (start && s0 >= 0 && e0 < 0) e0 = j;
             if (start && s0 < 0) s0 = j;
         }
@@ -2262,18 +2411,20 @@ __global__ void iota_u32_kernel(uint32_t* __restrict__ v, int64_t n) {
 
 // one thread per record; the thread at a read's first record hooks each of the
 // read's contigs to the read's smallest contig (test before the atomic)
-__global__ void relabel_hook_kernel(const uint2* __restrict__ rec, int64_t A, uint32_t N, uint32_t* __restrict__ rep) {
+__global__ void relabel_hook_kernel(RecIn rec, int64_t A, uint32_t N, uint32_t* __restrict__ rep) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A) return;
-    const uint32_t rid = rec[i].x;
-    if (i > 0 && rec[i - 1].x == rid) return;
+    if (i > 0 && rec.cont(i)) return;
     uint32_t m = kEmpty;
     int64_t e = i;
-    for (; e < A && rec[e].x == rid; ++e)
-        if (rec[e].y < N) m = min(m, rec[e].y);
+    do {
+        const uint32_t y = rec.contig(e);
+        if (y < N) m = min(m, y);
+        ++e;
+    } while (e < A && rec.cont(e));
     if (m == kEmpty) return;
     for (int64_t j = i; j < e; ++j) {
-        const uint32_t c = rec[j].y;
+        const uint32_t c = rec.contig(j);
         if (c < N && rep[c] > m) atomicMin(&rep[c], m);
     }
 }
@@ -2377,7 +2528,7 @@ int mark_at(const karma_ctx* ctx) {
 }
 struct SetsJob {
     karma_ctx* ctx = nullptr;
-    const uint2* rec = nullptr;
+    RecIn rec;
     int64_t A = 0, N = 0;
     Geo g{};
     int B = 0;
@@ -2568,10 +2719,11 @@ int SetsJob::launch() {
         ctx->mark_set = true;
     }
     if (A > 0) {
-        ClassArgs C{rec,       A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
+        ClassArgs C{rec.pr,    A,         (uint32_t)N,   g.Bc > 0,     codes.ptr, n_codes.ptr,
                     n_gen.ptr, blk_items, lpb, big_list.ptr, counters, flags,
                     append ? blk_hist.ptr : nullptr, g.bwc, g.Bc, relabeled ? remap_map.ptr : nullptr, 0, nullptr,
                     chunk};
+        C.recw = rec.fw;
         const BinArgs Bn = bin ? BinArgs{bsegs.ptr, reinterpret_cast<uint4*>(bhdr.ptr), bdir.ptr, (int64_t)seg_cap,
                                          dir_cap}
                                : BinArgs{};
@@ -2579,7 +2731,26 @@ int SetsJob::launch() {
             C.c0 = c_from;
             const int64_t cg = ceil_div(c_to - c_from, kCW / 64);
             if (cg <= 0) return KARMA_OK;
-            if (bin && relabeled)
+            if (rec.flagged()) {  // flagged records (4 bytes each)
+                if (bin && relabeled)
+                    KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, true, true, true>), cg, kCW, 0, C,
+                                 Bn);
+                else if (bin)
+                    KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, false, true, true>), cg, kCW, 0,
+                                 C, Bn);
+                else if (append && relabeled)
+                    KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true, true, false, true>), cg, kCW, 0,
+                                 C, Bn);
+                else if (append)
+                    KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<true, true, false, false, true>), cg, kCW, 0,
+                                 C, Bn);
+                else if (relabeled)
+                    KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, true, false, true>), cg, kCW, 0,
+                                 C, Bn);
+                else
+                    KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, false, false, true>), cg, kCW, 0,
+                                 C, Bn);
+            } else if (bin && relabeled)
                 KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, true, true>), cg, kCW, 0, C, Bn);
             else if (bin)
                 KARMA_LAUNCH(ctx, "graph_classify", (classify2_kernel<false, true, false, true>), cg, kCW, 0, C, Bn);
@@ -2867,7 +3038,7 @@ int SetsJob::finish(karma_pairs* out) {
 
 int64_t sets_max_contigs() { return kMaxCompactN; }
 
-int sets_begin(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job) {
+int sets_begin(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, SetsJob** job) {
     KARMA_CHECK(N <= kMaxCompactN, KARMA_ERR_ARG, "sets_begin: n_contigs above the compact path");
     KARMA_CHECK(!ctx->job_open, KARMA_ERR_STATE, "a split graph call is already open on this context");
     std::unique_ptr<SetsJob> j(new SetsJob());
@@ -2903,7 +3074,7 @@ void sets_free(SetsJob* job) {
     delete job;
 }
 
-int sets_begin_deferred(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job, SetsDeferred* v) {
+int sets_begin_deferred(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, SetsJob** job, SetsDeferred* v) {
     KARMA_CHECK(N <= kMaxCompactN, KARMA_ERR_ARG, "sets_begin: n_contigs above the compact path");
     KARMA_CHECK(!ctx->job_open, KARMA_ERR_STATE, "a split graph call is already open on this context");
     std::unique_ptr<SetsJob> j(new SetsJob());
@@ -2945,7 +3116,7 @@ void sets_release(SetsJob* job) {
     delete job;  // its buffers go back to the main stream's cache: later work there is ordered after its kernels
 }
 
-int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out) {
+int records_to_pairs_sets(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, karma_pairs* out) {
     if (N > kMaxCompactN) return records_to_pairs_wide(ctx, rec, A, N, out);
     SetsJob* job = nullptr;
     KARMA_TRY(sets_begin(ctx, rec, A, N, &job));

@@ -264,15 +264,28 @@ struct karma_pairs {
 };
 
 namespace karma {
+// The graph's input records (karma_graph_records, karma_step_run): either
+// interleaved {u32 read id, u32 contig} grouped by read (pr; KARMA_REC_SORTED),
+// or one u32 per record, contig | first-of-its-read << 31 (fw;
+// KARMA_REC_FLAGGED): the graph depends only on which records share a read, so
+// the read ids are replaced by read-start flags and the records take 4 bytes.
+struct RecIn {
+    const uint2* pr = nullptr;
+    const uint32_t* fw = nullptr;
+    __host__ __device__ bool flagged() const { return fw != nullptr; }
+    __device__ __forceinline__ uint32_t contig(int64_t i) const { return fw ? fw[i] & 0x7FFFFFFFu : pr[i].y; }
+    // record i (> 0) belongs to the read of record i - 1
+    __device__ __forceinline__ bool cont(int64_t i) const { return fw ? (int)fw[i] >= 0 : pr[i].x == pr[i - 1].x; }
+};
 // set-partition records pipeline (graph_sets.hip)
-int records_to_pairs_sets(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, karma_pairs* out);
+int records_to_pairs_sets(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, karma_pairs* out);
 // The same in two halves: sets_begin enqueues every kernel up to the control
 // block readback and returns; sets_end synchronises and assembles the list.
 // Only for N <= sets_max_contigs() (the compact path); `rec` must stay valid
 // until sets_end.
 struct SetsJob;
 int64_t sets_max_contigs();
-int sets_begin(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job);
+int sets_begin(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, SetsJob** job);
 int sets_end(SetsJob* job, karma_pairs* out);  // frees the job
 void sets_free(SetsJob* job);
 // A records job launched without its control-block readback (karma_step's
@@ -292,7 +305,7 @@ struct SetsDeferred {
     int64_t* ctrl = nullptr;          // the caller's control block when the job used it (ctx->job_ctrl), else null
     int64_t ctrl_need = 0;            // words of control block the job needed (a larger ctx->job_ctrl next time)
 };
-int sets_begin_deferred(karma_ctx* ctx, const uint2* rec, int64_t A, int64_t N, SetsJob** job, SetsDeferred* view);
+int sets_begin_deferred(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, SetsJob** job, SetsDeferred* view);
 // Frees a deferred job's buffers to the allocator (stream-ordered; no wait).
 void sets_release(SetsJob* job);
 }  // namespace karma

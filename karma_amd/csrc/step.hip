@@ -579,6 +579,7 @@ struct karma_step {
         karma_contigs* store;
         const uint32_t* rec;
         int64_t A;
+        bool flg;  // KARMA_STEP_FLAGGED records
     };
     std::deque<Pending> pending;
     uint64_t seq = 0;
@@ -840,8 +841,9 @@ int stream_after(hipEvent_t* ev, hipStream_t on, hipStream_t w) {
 }
 
 // ---- the synchronous step ------------------------------------------------------
-int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A, bool keep, bool sequential,
-             bool count) {
+int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A, bool flg, bool keep,
+             bool sequential, bool count) {
+    const int rfmt = flg ? KARMA_REC_FLAGGED : KARMA_REC_SORTED;
     karma_ctx* ctx = s->ctx;
     KARMA_TRY(drop_outputs(s));
     ++s->n_sync;
@@ -867,7 +869,7 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
         // stream; the profile behind the graph's kernels on the side stream
         karma_graph_job* job = nullptr;
         ctx->fork_use = s->alt_s;  // the general-read branch on the spare main stream (see karma_ctx::fork_use)
-        const int brc = karma_graph_records_begin(ctx, rec, A, s->n_glob, KARMA_REC_SORTED, 1, &job);
+        const int brc = karma_graph_records_begin(ctx, rec, A, s->n_glob, rfmt, 1, &job);
         ctx->fork_use = nullptr;
         KARMA_TRY(brc);
         int rc = KARMA_OK;
@@ -896,7 +898,7 @@ int run_sync(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A
         KARMA_TRY(karma_kmer_plan_finalize(s->plan, &M));
         KARMA_TRY(ensure_prof(s, s->prof, (size_t)std::max<int64_t>(1, s->n_loc * M)));
         if (s->n_loc * M) KARMA_TRY(karma_kmer_profile(s->plan, s->prof.ptr, M, 1));
-        KARMA_TRY(karma_graph_records(ctx, rec, A, s->n_glob, KARMA_REC_SORTED, 1, &s->local));
+        KARMA_TRY(karma_graph_records(ctx, rec, A, s->n_glob, rfmt, 1, &s->local));
     }
     s->M = M;
     s->prof_M = M;
@@ -1030,7 +1032,7 @@ int drain(karma_step* s, bool wait, bool lag) {
             const uint64_t newest = s->prof_seq;
             const int newest_par = s->prof_par;
             const int64_t newest_M = s->prof_M;
-            KARMA_TRY(run_sync(s, p.store, p.rec, p.A, false, false, true));
+            KARMA_TRY(run_sync(s, p.store, p.rec, p.A, p.flg, false, false, true));
             if (newest > p.seq) {  // a newer deferred step is pending: its outputs stay the newest
                 s->prof_seq = newest;
                 s->prof_par = newest_par;
@@ -1042,7 +1044,7 @@ int drain(karma_step* s, bool wait, bool lag) {
     return KARMA_OK;
 }
 
-int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A, bool sequential) {
+int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64_t A, bool flg, bool sequential) {
     karma_ctx* ctx = s->ctx;
     KARMA_TRY(drop_outputs(s));  // a deferred step has no outputs to read
     ++s->n_deferred;
@@ -1130,7 +1132,11 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     ctx->mark_pos = two ? kMarkTwo : kMarkOne;
     ctx->job_ctrl = s->own_ctrl ? tl.ctrl.ptr : nullptr;  // zero: the last status kernel of this tail cleared it
     ctx->job_ctrl_words = s->own_ctrl ? (int64_t)tl.ctrl.n : 0;
-    const int jrc = sets_begin_deferred(ctx, reinterpret_cast<const uint2*>(rec), A, s->n_glob, &job, &v);
+    RecIn rin;
+    if (flg) rin.fw = rec;
+    else rin.pr = reinterpret_cast<const uint2*>(rec);
+    KARMA_CHECK(!(reinterpret_cast<uintptr_t>(rec) & 15), KARMA_ERR_ARG, "karma_step_run: records must be 16-byte aligned");
+    const int jrc = sets_begin_deferred(ctx, rin, A, s->n_glob, &job, &v);
     ctx->job_ctrl = nullptr;
     ctx->job_ctrl_words = 0;
     ctx->mark_pos = -1;
@@ -1311,7 +1317,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
         ctx->stream = ms;
     }
     fail.armed = false;
-    s->pending.push_back({seq, store, rec, A});
+    s->pending.push_back({seq, store, rec, A, flg});
     return KARMA_OK;
 }
 
@@ -1402,7 +1408,8 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
                    int64_t* info) {
     KARMA_CHECK(s && store && (records || n_records == 0) && n_records >= 0, KARMA_ERR_ARG,
                 "karma_step_run: bad arguments");
-    KARMA_CHECK((flags & ~(KARMA_STEP_KEEP | KARMA_STEP_SEQUENTIAL | KARMA_STEP_DEFER)) == 0, KARMA_ERR_ARG,
+    KARMA_CHECK((flags & ~(KARMA_STEP_KEEP | KARMA_STEP_SEQUENTIAL | KARMA_STEP_DEFER | KARMA_STEP_FLAGGED)) == 0,
+                KARMA_ERR_ARG,
                 "karma_step_run: unknown flags %d", flags);
     karma_ctx* ctx = s->ctx;
     KARMA_TRY(ctx_begin(ctx));
@@ -1414,6 +1421,7 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
     hipStream_t prev = ctx->stream;
     ctx->stream = s->main_s;
     const bool keep = flags & KARMA_STEP_KEEP, seq = flags & KARMA_STEP_SEQUENTIAL;
+    const bool flg = flags & KARMA_STEP_FLAGGED;
     // deferred: one process (no collective needs a host count), nothing read back
     // several processes: once a synchronous step has sized the exchange's
     // slots and every rank's store is known to be ACGT-only
@@ -1426,13 +1434,13 @@ int karma_step_run(karma_step* s, karma_contigs* store, const uint32_t* records,
     if (defer && s->sticky_sync > 0) {
         --s->sticky_sync;
         rc = drain(s, false, true);
-        if (!rc) rc = run_sync(s, store, records, n_records, false, seq, false);
+        if (!rc) rc = run_sync(s, store, records, n_records, flg, false, seq, false);
     } else if (defer) {
         rc = drain(s, false, true);
-        if (!rc) rc = run_deferred(s, store, records, n_records, seq);
+        if (!rc) rc = run_deferred(s, store, records, n_records, flg, seq);
     } else {
         rc = drain(s, true, false);  // earlier deferred steps complete and checked first
-        if (!rc) rc = run_sync(s, store, records, n_records, keep, seq, !(flags & KARMA_STEP_DEFER));
+        if (!rc) rc = run_sync(s, store, records, n_records, flg, keep, seq, !(flags & KARMA_STEP_DEFER));
     }
     ctx->stream = prev;
     s->run_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();

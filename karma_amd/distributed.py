@@ -140,16 +140,16 @@ class HipOps:
         pairs.rebind(self.ctx)
         return pairs
 
-    def graph_begin(self, records, n_records, n_contigs, split_bounds=None):
+    def graph_begin(self, records, n_records, n_contigs, split_bounds=None, flagged=False):
         return self.engine.Pairs.from_records_begin(self.ctx, n_contigs, records, n_records,
-                                                    split_bounds=split_bounds)
+                                                    split_bounds=split_bounds, flagged=flagged)
 
     def graph_end(self, job):
         return job.end()
 
-    def graph_local(self, records, n_records, n_contigs):
+    def graph_local(self, records, n_records, n_contigs, flagged=False):
         return self.engine.Pairs.from_records(self.ctx, None, n_contigs, grouped=True, device_ptr=records,
-                                              n_records=n_records)
+                                              n_records=n_records, flagged=flagged)
 
     def pairs_kc_split(self, pairs, bounds):
         """The list as interleaved (key, count) int64 pairs (2n, the exchange's
@@ -245,9 +245,9 @@ class NativeStep:
         self.h = h
         self._info = np.zeros(4, np.int64)
 
-    def run(self, store, records, n_records, keep=False, sequential=False, count=True):
+    def run(self, store, records, n_records, keep=False, sequential=False, count=True, flagged=False):
         flags = (_lib.KARMA_STEP_KEEP if keep else 0) | (_lib.KARMA_STEP_SEQUENTIAL if sequential else 0) | \
-            (_lib.KARMA_STEP_DEFER if not count and not keep else 0)
+            (_lib.KARMA_STEP_DEFER if not count and not keep else 0) | (_lib.KARMA_STEP_FLAGGED if flagged else 0)
         info = self._info
         call("karma_step_run", self.h, store.h, ctypes.c_void_p(records), int(n_records), flags, ptr(info))
         M, E = int(info[0]), int(info[1])
@@ -333,8 +333,11 @@ def native_step_on(comm, ops, overlap):
 class ShardedBuild:
     """k-mer profile + shared-read graph over contig/fragment shards."""
 
-    def __init__(self, ctx, comm, kmode, n_glob, c_lo, n_loc, ops=None, overlap=None, emulate_ranks=1):
+    def __init__(self, ctx, comm, kmode, n_glob, c_lo, n_loc, ops=None, overlap=None, emulate_ranks=1, flagged=False):
         self.comm, self.kmode, self.n_glob, self.c_lo, self.n_loc = comm, kmode, n_glob, c_lo, n_loc
+        # the records this build's steps take: (read, contig) pairs, or
+        # KARMA_REC_FLAGGED words (engine.flag_records: 4 bytes per record)
+        self.flagged = bool(flagged)
         # one process standing in for a rank of a W-rank job (bench.py
         # --emulate-ranks W): the exchange's local work runs -- split at the W
         # owners' bounds, merge of W sorted slices, totals -- its collectives do not
@@ -401,7 +404,8 @@ class ShardedBuild:
         not read back, so the step ends without waiting for its last kernels,
         and stats["E_local"] is None."""
         if self.native is not None:
-            return self.native.run(store, records, n_records, keep=keep, sequential=sequential, count=count)
+            return self.native.run(store, records, n_records, keep=keep, sequential=sequential, count=count,
+                                   flagged=self.flagged)
         ops = self.ops
         # Default order (one stream pair): k-mer columns, then the graph's
         # kernels alone on the chip (classify .. final), then the profile on
@@ -426,15 +430,17 @@ class ShardedBuild:
 
     def _graph_begin(self, records, n_records):
         """The records job, told the exchange's owner bounds when there is one."""
+        kw = {"flagged": True} if self.flagged else {}
         if self.split_bounds is not None:
-            return self.ops.graph_begin(records, n_records, self.n_glob, split_bounds=self.split_bounds)
-        return self.ops.graph_begin(records, n_records, self.n_glob)
+            return self.ops.graph_begin(records, n_records, self.n_glob, split_bounds=self.split_bounds, **kw)
+        return self.ops.graph_begin(records, n_records, self.n_glob, **kw)
 
     def _run(self, store, records, n_records, keep, side, count=True):
         ops, comm = self.ops, self.comm
         fut = None
         if self._pool is not None:  # ---- shared-read graph, concurrent (read_graph.py:19-50) ----
-            fut = self._pool.submit(self.gops.graph_local, records, n_records, self.n_glob)
+            fut = self._pool.submit(self.gops.graph_local, records, n_records, self.n_glob,
+                                    **({"flagged": True} if self.flagged else {}))
         local = None
         try:
             # ---- k-mer profile (kmer.py:199-233) ----
@@ -486,7 +492,7 @@ class ShardedBuild:
         if fut is not None:
             local = ops.adopt(local)
         elif local is None:  # ---- shared-read graph (read_graph.py:19-50) ----
-            local = ops.graph_local(records, n_records, self.n_glob)
+            local = ops.graph_local(records, n_records, self.n_glob, **({"flagged": True} if self.flagged else {}))
         stats = {"M": M}
         if keep:
             stats["entries"] = ops.entries(local)

@@ -337,20 +337,23 @@ class Pairs:
         self.ctx, self.h = ctx, h
 
     @classmethod
-    def from_records(cls, ctx, records, n_contigs, grouped=True, device_ptr=None, n_records=None):
+    def from_records(cls, ctx, records, n_contigs, grouped=True, device_ptr=None, n_records=None, flagged=False):
+        """flagged: the records are KARMA_REC_FLAGGED words (flag_records), one u32 each."""
         h = ctypes.c_void_p()
-        flags = _lib.KARMA_REC_SORTED if grouped else _lib.KARMA_REC_UNSORTED
+        flags = _lib.KARMA_REC_FLAGGED if flagged else _lib.KARMA_REC_SORTED if grouped else _lib.KARMA_REC_UNSORTED
         if device_ptr is not None:
             call("karma_graph_records", ctx.h, ctypes.c_void_p(device_ptr), n_records, n_contigs, flags, 1,
                  ctypes.byref(h))
         else:
-            rec = np.ascontiguousarray(records, dtype=np.uint32).reshape(-1, 2)
+            rec = np.ascontiguousarray(records, dtype=np.uint32)
+            rec = rec.reshape(-1) if flagged else rec.reshape(-1, 2)
             call("karma_graph_records", ctx.h, ptr(rec) if len(rec) else None, len(rec), n_contigs, flags, 0,
                  ctypes.byref(h))
         return cls(ctx, h)
 
     @classmethod
-    def from_records_begin(cls, ctx, n_contigs, device_ptr, n_records, grouped=True, split_bounds=None):
+    def from_records_begin(cls, ctx, n_contigs, device_ptr, n_records, grouped=True, split_bounds=None,
+                           flagged=False):
         """First half of from_records on device records (karma_graph_records_begin):
         the pipeline is enqueued up to its host synchronisation; .end() finishes.
         split_bounds: owner bounds the list will be split at (karma_graph_split_hint)."""
@@ -358,7 +361,7 @@ class Pairs:
             b = np.ascontiguousarray(split_bounds, np.int64)
             call("karma_graph_split_hint", ctx.h, ptr(b), len(b) - 1)
         h = ctypes.c_void_p()
-        flags = _lib.KARMA_REC_SORTED if grouped else _lib.KARMA_REC_UNSORTED
+        flags = _lib.KARMA_REC_FLAGGED if flagged else _lib.KARMA_REC_SORTED if grouped else _lib.KARMA_REC_UNSORTED
         call("karma_graph_records_begin", ctx.h, ctypes.c_void_p(device_ptr), n_records, n_contigs, flags, 1,
              ctypes.byref(h))
         return GraphJob(cls, ctx, h)
@@ -579,10 +582,11 @@ class Edges:
         self.close()
 
 
-def graph_from_records(records, n_contigs, grouped=True, ctx=None) -> EdgeArrays:
-    """Shared-read edges from (read, contig) records (read_graph.py:19-50 semantics)."""
+def graph_from_records(records, n_contigs, grouped=True, ctx=None, flagged=False) -> EdgeArrays:
+    """Shared-read edges from (read, contig) records (read_graph.py:19-50 semantics);
+    flagged: records given as flag_records words."""
     ctx = ctx or _lib.default_context()
-    p = Pairs.from_records(ctx, records, n_contigs, grouped=grouped)
+    p = Pairs.from_records(ctx, records, n_contigs, grouped=grouped, flagged=flagged)
     try:
         e = p.edges(_lib.KARMA_MODE_READS, n_contigs)
         try:
@@ -687,6 +691,23 @@ def synth_genes(seed, n_contigs, gene_max=4):
     gs = np.zeros(ng.value, np.int32)
     call("karma_synth_genes", seed, n_contigs, gene_max, ptr(gf), ptr(gs))
     return gf, gs
+
+
+def flag_records(records):
+    """(read, contig) records grouped by read -> KARMA_REC_FLAGGED words (the
+    read ids replaced by read-start flags): contig | (first record of its read) << 31.
+    The graph depends only on which records share a read, so the two formats
+    give the same graph."""
+    rec = np.asarray(records, np.uint32).reshape(-1, 2)
+    if len(rec) and int(rec[:, 1].max()) >= 1 << 31:
+        raise ValueError("flagged records hold contig ids < 2^31")
+    out = rec[:, 1].copy()
+    if len(rec):
+        start = np.empty(len(rec), np.uint32)
+        start[0] = 1
+        np.not_equal(rec[1:, 0], rec[:-1, 0], out=start[1:], casting="unsafe")
+        out |= start << np.uint32(31)
+    return out
 
 
 def synth_records(seed, n_contigs, frag_lo, frag_hi, paired, gene_max=4, genes=None):

@@ -150,6 +150,14 @@ def oracle_rank(group, rank, sizes, frags, seed):
         ctx.close()
 
 
+FLAGGED = False  # --flagged: the deferred case's records as KARMA_REC_FLAGGED words
+
+
+def dev_records(ctx, rec):
+    return _lib.DevBuf.from_numpy(ctx, engine.flag_records(rec) if FLAGGED else
+                                  np.ascontiguousarray(rec).view(np.int64).reshape(-1))
+
+
 def defer_rank(group, rank, sizes, frags, seed):
     world = group.world
     n_glob, c_lo, n_loc = sum(sizes), sum(sizes[:rank]), sizes[rank]
@@ -164,8 +172,8 @@ def defer_rank(group, rank, sizes, frags, seed):
         # 1 % of the reads (records stay grouped by read)
         k = int(np.searchsorted(rec[:, 0], rec[len(rec) // 100, 0]))
         store = engine.ContigStore(ctx, blob, offs, key_len)
-        full = _lib.DevBuf.from_numpy(ctx, rec.view(np.int64).reshape(-1))
-        small = _lib.DevBuf.from_numpy(ctx, np.ascontiguousarray(rec[:k]).view(np.int64).reshape(-1))
+        full = dev_records(ctx, rec)
+        small = dev_records(ctx, rec[:k])
         try:
             # rank 0 alone gets a read of 12 records (the general path): every
             # rank must run the deferred steps again
@@ -175,10 +183,10 @@ def defer_rank(group, rank, sizes, frags, seed):
                                 (np.arange(12, dtype=np.uint32) * 37) % n_glob], axis=1)
                 rp = np.concatenate([rec, big])
             out["peer_rec"] = rp
-            peer = _lib.DevBuf.from_numpy(ctx, np.ascontiguousarray(rp).view(np.int64).reshape(-1))
+            peer = dev_records(ctx, rp)
             for tag, first, batch in (("over", (small, k), (full, len(rec))), ("fit", (full, len(rec)), (full, len(rec))),
                                       ("peer", (peer, len(rp)), (peer, len(rp)))):
-                build = ShardedBuild(ctx, comm, -1, n_glob, c_lo, n_loc)
+                build = ShardedBuild(ctx, comm, -1, n_glob, c_lo, n_loc, flagged=FLAGGED)
                 try:
                     assert build.native is not None
                     build.run(store, first[0].ptr, first[1], count=False)  # synchronous: sizes the slots
@@ -244,9 +252,12 @@ def main():
     ap.add_argument("--sizes", default="")
     ap.add_argument("--frags", type=int, default=0)
     ap.add_argument("--seed", type=int, default=29)
+    ap.add_argument("--flagged", action="store_true", help="defer case: KARMA_REC_FLAGGED records")
     ap.add_argument("--env", action="append", default=[],
                     help="KEY=VALUE set before the communicators and steps are created (mode A/B)")
     a = ap.parse_args()
+    global FLAGGED
+    FLAGGED = a.flagged
     for kv in a.env:
         k, v = kv.split("=", 1)
         os.environ[k] = v

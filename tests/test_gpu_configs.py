@@ -172,8 +172,9 @@ def test_config4_strong_8_ranks(gold):
     assert D.edge_digests(cat["a"], cat["b"], cat["weight"], cat["shared"], parts[0]["edges"].totals) == g["edges"]
 
 
-@pytest.mark.parametrize("name", ["config2", "config3"])
-def test_config_deferred_step_digests(gold, name):
+@pytest.mark.parametrize("name,flagged", [("config2", False), ("config3", False), ("config2", True),
+                                          ("config3", True)])
+def test_config_deferred_step_digests(gold, name, flagged):
     """The code path bench.py TIMES at these sizes: a stream of deferred steps
     (count=False: karma_step's run_deferred, two main streams at config 2's
     size, one at config 3's), then sync.  The newest deferred step's own outputs
@@ -183,9 +184,11 @@ def test_config_deferred_step_digests(gold, name):
     g = gold[name]
     inp = D.bench_inputs(name)
     ctx = _lib.Context(0)
-    build = ShardedBuild(ctx, SoloComm(), engine.kmode_of(inp["kmer"]), inp["n_glob"], inp["c_lo"], inp["n_loc"])
+    build = ShardedBuild(ctx, SoloComm(), engine.kmode_of(inp["kmer"]), inp["n_glob"], inp["c_lo"], inp["n_loc"],
+                         flagged=flagged)
     store = engine.ContigStore(ctx, inp["blob"], inp["offs"], inp["key_len"])
-    rec_dev = _lib.DevBuf.from_numpy(ctx, inp["rec"].view(np.int64).reshape(-1))
+    rec_dev = _lib.DevBuf.from_numpy(ctx, engine.flag_records(inp["rec"]) if flagged
+                                     else inp["rec"].view(np.int64).reshape(-1))
     try:
         assert build.native is not None
         for _ in range(4):

@@ -106,11 +106,13 @@ DEFER_MODES = {
     "one_comm_one_stream": (["KARMA_STEP_STREAMS=1"], 1, 3),
     # round 4's mode: the presence all-gather on a side communicator, on the side stream
     "side_comm": (["KARMA_STEP_SIDE_COMM=1"], 0, 3),
+    # the default mode on KARMA_REC_FLAGGED records (u32 contig | read-start flag)
+    "one_comm_flagged": ([], 1, 3),
 }
 
 
 @pytest.mark.parametrize("world,mode", [(2, "one_comm"), (3, "one_comm"), (2, "one_comm_one_stream"),
-                                        (3, "side_comm")])
+                                        (3, "side_comm"), (3, "one_comm_flagged")])
 def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world, mode):
     """Deferred steps with several processes (csrc/step.hip run_deferred: the
     padded fixed-slot all-to-all, the merge from slots, the totals all-gather
@@ -126,7 +128,8 @@ def test_rccl_deferred_steps_rerun_on_slot_overflow(tmp_path, world, mode):
     frags, seed = 200_000, 31
     env, one_comm, xs = DEFER_MODES[mode]
     run_child("--case", "defer", "--world", str(world), "--sizes", ",".join(map(str, sizes)), "--frags",
-              str(frags), "--seed", str(seed), "--out", str(tmp_path), *[x for e in env for x in ("--env", e)])
+              str(frags), "--seed", str(seed), "--out", str(tmp_path), *[x for e in env for x in ("--env", e)],
+              *(["--flagged"] if mode.endswith("_flagged") else []))
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     prof, _, o = oracle_of(sizes, frags, seed, n_rate=0, len_span=100)
     # rank 0's batches in the third build carry one more read, of 12 records

@@ -178,7 +178,11 @@ def test_update_graph_golden(golden):
         assert dump(g) == case["out"], name
 
 
-def check_records(rec, n, grouped=True):
+def check_records(rec, n, grouped=True, flagged=True):
+    """The HIP graph of (read, contig) records against the oracle; grouped
+    records also as KARMA_REC_FLAGGED words (engine.flag_records: read ids
+    replaced by read-start flags, 4 bytes per record), which must give the
+    same graph bit for bit."""
     e = engine.graph_from_records(rec, n, grouped=grouped)
     rs = np.asarray(rec, dtype=np.int64)
     order = np.argsort(rs[:, 0], kind="stable")
@@ -186,11 +190,15 @@ def check_records(rec, n, grouped=True):
     starts = np.flatnonzero(np.r_[True, rs[1:, 0] != rs[:-1, 0]]) if len(rs) else np.zeros(0, np.int64)
     off = np.r_[starts, len(rs)]
     o = oracle.graph_groups(off, rs[:, 1] if len(rs) else np.zeros(0), None, None, n, dedup=True)
-    assert np.array_equal(e.a, o["a"])
-    assert np.array_equal(e.b, o["b"])
-    assert np.array_equal(e.shared, o["shared"])
-    assert np.array_equal(e.weight.view(np.uint64), o["weight"].view(np.uint64))
-    assert np.array_equal(e.totals, o["totals"])
+    outs = [e]
+    if grouped and flagged:
+        outs.append(engine.graph_from_records(engine.flag_records(rec), n, flagged=True))
+    for x in outs:
+        assert np.array_equal(x.a, o["a"])
+        assert np.array_equal(x.b, o["b"])
+        assert np.array_equal(x.shared, o["shared"])
+        assert np.array_equal(x.weight.view(np.uint64), o["weight"].view(np.uint64))
+        assert np.array_equal(x.totals, o["totals"])
     return e
 
 
@@ -292,6 +300,47 @@ def test_records_empty_and_bad_contig():
     assert len(e.a) == 0 and e.totals.tolist() == [0] * 10
     with pytest.raises(_lib.KarmaError):
         engine.graph_from_records(np.array([[0, 12]], np.uint32), 10)
+    e = engine.graph_from_records(np.zeros(0, np.uint32), 10, flagged=True)
+    assert len(e.a) == 0 and e.totals.tolist() == [0] * 10
+    with pytest.raises(_lib.KarmaError):
+        engine.graph_from_records(engine.flag_records(np.array([[0, 12]], np.uint32)), 10, flagged=True)
+
+
+def test_flagged_records_first_flag_and_chunk_edges():
+    """KARMA_REC_FLAGGED edge cases: record 0 without its start flag still
+    starts the first read; reads of 1..12 records placed across the 8,192- and
+    4,096-record chunk edges and the 512-record steps' lane edges (the carried
+    tail, the chunk-end walk, big reads at an edge); a device pointer that is
+    not 16-byte aligned (the library copies it)."""
+    rng = np.random.default_rng(17)
+    rows, r = [], 0
+    while len(rows) < 60_000:
+        near = len(rows) % 4096 > 4080 or len(rows) % 512 > 500
+        m = int(rng.choice([1, 2, 3, 5, 8, 9, 12])) if near else int(rng.integers(1, 5))
+        m0 = int(rng.integers(0, 2996))
+        for c in m0 + rng.integers(0, 5, m):
+            rows.append((r, int(c)))
+        r += 1
+    rec = np.array(rows, np.uint32)
+    check_records(rec, 3000)
+    w = engine.flag_records(rec)
+    w[0] &= np.uint32(0x7FFFFFFF)  # record 0 starts a read whatever its flag
+    e = engine.graph_from_records(w, 3000, flagged=True)
+    ref = engine.graph_from_records(rec, 3000)
+    assert np.array_equal(e.a, ref.a) and np.array_equal(e.weight.view(np.uint64), ref.weight.view(np.uint64))
+    ctx = _lib.default_context()
+    buf = _lib.DevBuf(ctx, (len(w) + 1,), np.uint32)
+    buf.view(1, len(w)).copy_from(w)
+    p = engine.Pairs.from_records(ctx, None, 3000, device_ptr=buf.ptr + 4, n_records=len(w), flagged=True)
+    q = engine.Pairs.from_records(ctx, rec, 3000)
+    try:
+        k, c, _ = p.get()
+        k2, c2, _ = q.get()
+        assert np.array_equal(k, k2) and np.array_equal(c, c2)
+    finally:
+        p.close()
+        q.close()
+        buf.close()
 
 
 def test_eq_vs_oracle_seeded():

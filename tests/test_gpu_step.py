@@ -42,17 +42,20 @@ def oracle_profile(blob, offs, c_lo, n):
 
 
 class Run:
-    def __init__(self, n_glob, rec, emulate=1, n_rate=300):
+    def __init__(self, n_glob, rec, emulate=1, n_rate=300, flagged=False):
         self.ctx = _lib.Context(0)
         self.n_glob = n_glob
         n_loc = n_glob // emulate if emulate > 1 else n_glob
         self.n_loc = n_loc
         self.blob, self.offs, kl = contigs(n_loc, n_rate=n_rate)
-        self.build = ShardedBuild(self.ctx, SoloComm(), -1, n_glob, 0, n_loc, emulate_ranks=emulate)
+        self.build = ShardedBuild(self.ctx, SoloComm(), -1, n_glob, 0, n_loc, emulate_ranks=emulate,
+                                  flagged=flagged)
         assert self.build.native is not None, "the native step drives the production path"
         self.store = engine.ContigStore(self.ctx, self.blob, self.offs, kl)
         self.rec = np.ascontiguousarray(rec)
-        self.dev = _lib.DevBuf.from_numpy(self.ctx, self.rec.view(np.int64).reshape(-1))
+        # the records as the step takes them: (read, contig) pairs or KARMA_REC_FLAGGED words
+        self.dev = _lib.DevBuf.from_numpy(self.ctx, engine.flag_records(self.rec) if flagged
+                                          else self.rec.view(np.int64).reshape(-1))
 
     def step(self, **kw):
         return self.build.run(self.store, self.dev.ptr, len(self.rec), **kw)
@@ -71,11 +74,12 @@ def check_edges(e, o):
     assert np.array_equal(e.totals, o["totals"])
 
 
-@pytest.mark.parametrize("emulate,n_rate", [(1, 300), (3, 300), (1, 0), (8, 0)])
-def test_deferred_steps_then_kept_step_match_oracle(emulate, n_rate):
+@pytest.mark.parametrize("emulate,n_rate,flagged", [(1, 300, False), (3, 300, False), (1, 0, False), (8, 0, False),
+                                                    (1, 300, True), (3, 0, True), (8, 300, True)])
+def test_deferred_steps_then_kept_step_match_oracle(emulate, n_rate, flagged):
     n = 3000 if emulate == 1 else 3001  # 3001 / 3: owner bounds that do not divide evenly
     rec = engine.synth_records(SEED, n, 0, 300_000, True)
-    r = Run(n, rec, emulate, n_rate)
+    r = Run(n, rec, emulate, n_rate, flagged)
     try:
         r.step(count=False)  # warm: allocations, events
         calls0 = _lib.api_calls()
@@ -119,8 +123,8 @@ def test_deferred_steps_then_kept_step_match_oracle(emulate, n_rate):
         r.close()
 
 
-@pytest.mark.parametrize("big", [True, False])
-def test_deferred_steps_slow_path_runs_again(big):
+@pytest.mark.parametrize("big,flagged", [(True, False), (False, False), (True, True), (False, True)])
+def test_deferred_steps_slow_path_runs_again(big, flagged):
     """Shuffled contig ids (most reads leave the compact path: the relabel vote)
     plus (big) reads of > 8 records: the deferred step's status calls for the
     general path and the step runs again synchronously; the next deferred steps
@@ -137,7 +141,7 @@ def test_deferred_steps_slow_path_runs_again(big):
         r0 = int(rec[-1, 0]) + 1
         extra = np.array([(r0 + i, int(c)) for i in range(200) for c in rng.integers(0, n, 12)], np.uint32)
         rec = np.concatenate([rec, extra])
-    r = Run(n, rec)
+    r = Run(n, rec, flagged=flagged)
     try:
         for _ in range(3 if big else 12):
             r.step(count=False)

@@ -12,7 +12,9 @@ for spec in "$@"; do
   label=${spec%%:*}; envs=${spec#*:}
   OUT=$REPO/gpurun_out/$TAG/$label
   mkdir -p $OUT
-  for pass in trace "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY"; do
+  # PASSES: counter passes separated by ';' (default: the traffic and SQ passes below)
+  IFS=';' read -ra PL <<< "${PASSES:-trace;FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY}"
+  for pass in "${PL[@]}"; do
     if [ "$pass" = trace ]; then
       env $envs timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- \
           python3 $REPO/bench.py $ARGS > $OUT/trace.log 2>&1 || { echo "$label trace failed"; tail -5 $OUT/trace.log; exit 1; }

@@ -6,6 +6,10 @@ WRITE_SIZE passes, KiB per dispatch, reported there as MB).  Correction as
 MI355X_MICROARCH.md §HBM prescribes: on gfx950 FETCH_SIZE reports 1/2 of a
 wide (16 B/lane) streaming read, so reads are doubled; WRITE_SIZE is exact for
 16-B stores.  graph_classify, the partition and kmer_profile move 16 B per lane.
+The code reduces read short runs (~110 B per chunk and bucket) for which
+FETCH_SIZE counts the bytes themselves (calibrated in round 6 with
+tools/micro/seg_read.hip: x 0.986 on a known byte count), so their reads are
+not doubled.
 
 The output is keyed by workload (bench.py pmc_traffic(): "<config>[_strong]
 [_shuffled]_n<ranks>"), so a number is only ever reported for the workload
@@ -43,7 +47,8 @@ def main():
     for k, v in src.items():
         name = bench_name(k)
         if name and v.get("fetch_MB") == v.get("fetch_MB"):  # skip NaN
-            out[name] = int(round((2 * v["fetch_MB"] + v["write_MB"]) * 1024 * 1024))
+            fx = 1 if name == "graph_code_reduce" else 2
+            out[name] = int(round((fx * v["fetch_MB"] + v["write_MB"]) * 1024 * 1024))
     dst, key = sys.argv[2], sys.argv[3]
     try:
         allw = json.load(open(dst))
