@@ -260,20 +260,27 @@ __device__ __forceinline__ bool rs_code2(const RState& a, const RState& b, uint3
 // masks, which feed selects through inverse ballots (no 0/1 VGPR round trips)
 __device__ __forceinline__ uint64_t lanes(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 __device__ __forceinline__ bool in_mask(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
-template <bool COMPACT>
+// K23 (the binned classify's staged codes): m0 | rel << 23, one shift-or;
+// rel's bit 0 (always set) lands on bit 23, so M = code >> 24 as in the
+// m0 | M << 24 form and m0 = code & 0x7FFFFF (m0 < 2^21 on the compact path).
+// K23 also drops the m0 < N test: m0 >= N needs a contig >= N, which the range
+// check reports (the call fails), and bin_emit clamps the bucket so that such
+// a code stays inside the queues meanwhile (one op per staged code instead of
+// one compare per record)
+template <bool COMPACT, bool K23 = false>
 __device__ __forceinline__ uint64_t rs_code_m(const RState& s, uint32_t N, uint32_t* code) {
     const uint32_t z = (uint32_t)__builtin_ctz(s.win);
     const uint32_t rel = s.win >> z, m0 = s.fm3 + z;
-    *code = m0 | (rel >> 1) << 24;
-    return COMPACT ? lanes(rel < 16u) & lanes(m0 < N) : 0ull;
+    *code = K23 ? m0 | rel << 23 : m0 | (rel >> 1) << 24;
+    return COMPACT ? lanes(rel < 16u) & (K23 ? ~0ull : lanes(m0 < N)) : 0ull;
 }
-template <bool COMPACT>
+template <bool COMPACT, bool K23 = false>
 __device__ __forceinline__ uint64_t rs_code2_m(const RState& a, const RState& b, uint32_t N, uint32_t* code) {
     const uint32_t za = (uint32_t)__builtin_ctz(a.win), zb = (uint32_t)__builtin_ctz(b.win);
     const uint32_t ma = a.fm3 + za, mb = b.fm3 + zb, m0 = min(ma, mb);
     const uint32_t rel = ((a.win >> za) << min(ma - m0, 31u)) | ((b.win >> zb) << min(mb - m0, 31u));
-    *code = m0 | (rel >> 1) << 24;
-    return COMPACT ? lanes(rel < 16u) & lanes(m0 < N) : 0ull;
+    *code = K23 ? m0 | rel << 23 : m0 | (rel >> 1) << 24;
+    return COMPACT ? lanes(rel < 16u) & (K23 ? ~0ull : lanes(m0 < N)) : 0ull;
 }
 
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lane l <- lane l - 1; lane 0 <- old
@@ -395,13 +402,14 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // written as a back segment, and the codes that found it full go into the
     // emptied queue (a queue holds < kBinQ codes between calls, so the lane
     // that took slot kBinQ - 1 exists whenever one overflowed)
+    // (code: m0 | M << 24 or the K23 form m0 | rel << 23; m0 < 2^21 either way)
     auto bin_emit = [&](uint64_t m, uint32_t code) {
-        const uint32_t m0 = code & 0xFFFFFFu, bk = m0 >> P.bwc;
+        const uint32_t m0 = code & 0x7FFFFFu, bk = min(m0 >> P.bwc, (uint32_t)P.Bc - 1u);
         const uint16_t val = (uint16_t)(((m0 & ((1u << P.bwc) - 1u)) << 3) | (code >> 24));
         uint32_t pos = 0;
         if (in_mask(m)) {
             pos = __hip_atomic_fetch_add(&qn[bk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (pos < (uint32_t)kBinQ) q[bk * kBinQ + pos] = val;
+            if (pos < (uint32_t)kBinQ) q[bk * kBinQ | pos] = val;
         }
         uint64_t full = m & lanes(pos == (uint32_t)kBinQ - 1u);
         if (!full) return;
@@ -440,9 +448,9 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         if (!ns) return;
         wave_lds_order();
         for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
-            const bool on = j0 + lane < ns;
-            const uint32_t code = on ? stg[j0 + lane] : 0u;
-            bin_emit(lanes(on), code);
+            // unpredicated read (ns <= 512 codes per step: the 2 KB buffer; past ns: masked off)
+            const uint32_t j = j0 + lane;
+            bin_emit(lanes(j < ns), stg[min(j, (uint32_t)(kRows * 16 - 1))]);
         }
         ns = 0;
         wave_lds_order();
@@ -682,7 +690,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     const uint64_t e = Sn & started & (FULL ? ~0ull : lanes(i < nval));
                     Si = Sn;
                     uint32_t code;
-                    const uint64_t ok = rs_code_m<COMPACT>(st, P.N, &code);
+                    const uint64_t ok = rs_code_m<COMPACT, BIN>(st, P.N, &code);
                     emit(e, ok, code, ubase + spos, 0ull);
                 }
             }
@@ -707,7 +715,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             hm.fm3 = in_mask(cont) ? hd.fm3 : in.fm3;
             hm.win = in_mask(cont) ? hd.win : in.win;
             uint32_t code;
-            const uint64_t ok = rs_code2_m<COMPACT>(in, hm, P.N, &code);
+            const uint64_t ok = rs_code2_m<COMPACT, BIN>(in, hm, P.N, &code);
             emit(have, ok, code, in_pos, big);
             return rare;
         };

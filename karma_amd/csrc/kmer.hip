@@ -751,6 +751,14 @@ __host__ __device__ constexpr int64_t hist_words(int64_t M, bool c16) {
 }
 // column-table entries (u16) in LDS
 __host__ __device__ constexpr int64_t tab_entries(bool p56, uint32_t S) { return p56 ? 1088 : (int64_t)S; }
+// KARMA_PROF_TABREP=1 (measurement variant): the column
+// table twice in LDS, lanes 32-63 reading the second copy, when it is small
+// (5p6's 1,088 entries), to test whether the lookup's bank collisions bound
+// the counting
+#ifndef KARMA_PROF_TABREP
+#define KARMA_PROF_TABREP 0
+#endif
+__host__ __device__ constexpr int tab_copies(int64_t t_pad) { return KARMA_PROF_TABREP && t_pad <= 4096 ? 2 : 1; }
 
 template <bool P56, bool C16>
 // 6 waves per SIMD (3 blocks per CU): fewer rows written at once write faster
@@ -773,6 +781,7 @@ profile_wave_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
     uint16_t* tab = reinterpret_cast<uint16_t*>(lds);
     const int t_pad = (int)((tab_entries(P56, S) + 7) & ~7);
+    const int t_rep = tab_copies(t_pad);
     // LDS is laid out for M; with m_dev (the column table's count, not read
     // back to the host first) M is its capacity and the rows are dense
     const int h_words = (int)hist_words(M, C16);
@@ -780,7 +789,7 @@ profile_wave_kernel(
         M = *m_dev;
         ld = M;
     }
-    uint32_t* counts = lds + t_pad / 2 + wave * (h_words + kProfWin);
+    uint32_t* counts = lds + t_rep * t_pad / 2 + wave * (h_words + kProfWin);
     uint32_t* win = counts + h_words;
     uint16_t* mbuf = reinterpret_cast<uint16_t*>(win + 80);
     double* lut = reinterpret_cast<double*>(win);
@@ -794,10 +803,15 @@ profile_wave_kernel(
                 ord = (c6 >> 2) * 5u + 1u + (c6 & 3u);
             }
             tab[o] = (uint16_t)col_of_ord[ord];
+            if (t_rep == 2) tab[t_pad + o] = (uint16_t)col_of_ord[ord];
         }
     } else {
-        for (int o = threadIdx.x; o < S; o += blockDim.x) tab[o] = (uint16_t)col_of_ord[o];
+        for (int o = threadIdx.x; o < S; o += blockDim.x) {
+            tab[o] = (uint16_t)col_of_ord[o];
+            if (t_rep == 2) tab[t_pad + o] = (uint16_t)col_of_ord[o];
+        }
     }
+    if (t_rep == 2 && lane >= 32) tab += t_pad;  // this lane's copy
     for (int j = lane; j < h_words; j += 64) counts[j] = 0;  // write_row_wave clears it after each row
     __syncthreads();
     const int kmin = P56 ? 5 : k;
@@ -1345,7 +1359,8 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         // counters when no contig reaches 2^16 bases (a count is <= L)
         const bool p56 = p->kmode == KARMA_KMER_5P6;
         const bool c16 = KARMA_PROF_C16 && c->max_len < 65536;
-        const size_t lds = (size_t)((tab_entries(p56, p->S) + 7) & ~7) * 2 +
+        const int64_t t_pad = (tab_entries(p56, p->S) + 7) & ~7;
+        const size_t lds = (size_t)(t_pad * tab_copies(t_pad)) * 2 +
                            (kPBlock / 64) * (size_t)(hist_words(M, c16) + kProfWin) * 4;
 #define KARMA_WAVE_LAUNCH(P56, C16)                                                                              \
     do {                                                                                                         \

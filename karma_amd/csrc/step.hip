@@ -207,7 +207,14 @@ __global__ void __launch_bounds__(kET) step_edge_write_kernel(
 #define KARMA_MARK_TWO 4  // deferred batches alternating two main streams (5, after the final kernel: 8-rank
                           // strong preview 0.196 against 0.188 ms with the binned classify)
 #endif
-constexpr int kMarkOne = KARMA_MARK_ONE, kMarkTwo = KARMA_MARK_TWO;
+#ifndef KARMA_MARK_ONE_FLAGGED
+#define KARMA_MARK_ONE_FLAGGED 2  // ... on flagged records too.  3 (at once, beside classify, which reads half the
+                                  // bytes and is VALU-bound) measured 0.849 against 0.860 ms at config 3 (three
+                                  // reps each; after classify 0.928, after the final kernel 0.911), but then
+                                  // neither kernel's live time is its own (classify 0.65 ms live beside the
+                                  // profile): not kept for 1 %, profiles/r06/measurements.md (r06h)
+#endif
+constexpr int kMarkOne = KARMA_MARK_ONE, kMarkTwo = KARMA_MARK_TWO, kMarkOneFlagged = KARMA_MARK_ONE_FLAGGED;
 constexpr int64_t kAltMaxRecords = int64_t(1) << 27;  // batches below this alternate main streams
 constexpr int kMT = 1024;       // tile elements (one round of tiles at the 8-rank preview's ~300k keys)
 constexpr int kMLds = 8192;     // staged window keys
@@ -1129,7 +1136,7 @@ int run_deferred(karma_step* s, karma_contigs* store, const uint32_t* rec, int64
     // with the LDS-bound code reduce and final kernel instead of the next
     // batch's classify (config 3: 1.15 against 1.20-1.22 ms per step,
     // profiles/r04/measurements.md (ab_mark3)); with two, after the final kernel
-    ctx->mark_pos = two ? kMarkTwo : kMarkOne;
+    ctx->mark_pos = two ? kMarkTwo : flg ? kMarkOneFlagged : kMarkOne;
     ctx->job_ctrl = s->own_ctrl ? tl.ctrl.ptr : nullptr;  // zero: the last status kernel of this tail cleared it
     ctx->job_ctrl_words = s->own_ctrl ? (int64_t)tl.ctrl.n : 0;
     RecIn rin;

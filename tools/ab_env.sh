@@ -14,7 +14,7 @@ for rep in ${REPS:-1 2}; do
         weak_emu*) extra="--weak --emulate-ranks ${leg#weak_emu}" ;;
       esac
       f=$OUT/${leg}_${name}_r${rep}
-      env $ev timeout -k 10 240 python bench.py --cpu-baseline off --no-e2e --no-parity \
+      env $ev timeout -k 10 240 python bench.py --cpu-baseline off --no-e2e --no-parity --no-other-format \
         --steps ${STEPS:-30} $extra > $f.json 2> $f.err || { echo "$leg $name failed"; tail -5 $f.err; exit 1; }
       python -c "import json; d=json.load(open('$f.json')); print('$leg', '$name', 'rep', $rep, d['ms_per_step'])"
     done

@@ -7,7 +7,7 @@
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 3 --warmup 2 --cpu-baseline off --no-e2e --no-timing --no-parity ${BENCH_ARGS:-}"
+ARGS="--steps 3 --warmup 2 --cpu-baseline off --no-e2e --no-timing --no-parity --no-other-format ${BENCH_ARGS:-}"
 for spec in "$@"; do
   label=${spec%%:*}; envs=${spec#*:}
   OUT=$REPO/gpurun_out/$TAG/$label
