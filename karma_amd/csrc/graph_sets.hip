@@ -325,6 +325,7 @@ struct BinArgs {
     uint8_t* dir;       // per chunk: dir_cap bucket ids of the back segments (in flush order)
     int64_t seg_cap;    // segments per chunk: chunk / kBinQ + Bc
     int dir_cap;        // chunk / kBinQ
+    int slotted;        // front runs as whole 128-byte slots, slot b = bucket b (see classify2_kernel's end)
 };
 
 // HIST: per-block code-bucket histograms for code_append_kernel; COMPACT: the
@@ -778,6 +779,12 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             if (BIN)
                 for (int i = 0; i < kBinHdr; ++i) Q.hdr[kBinHdr * chunk + i] = uint4{0u, 0u, 0u, 0u};
         }
+        if (BIN && Q.slotted) {  // the reduce reads every slot: empty ones
+            const BinArgs& Qa = Q;
+            for (uint32_t k = lane; k < (uint32_t)P.Bc * 8u; k += 64)
+                *reinterpret_cast<u32x4*>(Qa.segs + (chunk * Qa.seg_cap + (k >> 3)) * kBinQ + 8 * (k & 7u)) =
+                    u32x4{~0u, ~0u, ~0u, ~0u};
+        }
         return;
     }
     const std::false_type main_pass{};
@@ -866,7 +873,36 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         nc += ok ? 1u : 0u;
         ng += !big && !ok ? 1u : 0u;
     }
-    if (BIN) {
+    if (BIN && Q.slotted) {
+        // slotted (the queues fill well: >= ~40 codes per bucket and chunk):
+        // every bucket's queue as one whole 128-byte segment at slot b of the
+        // chunk's region, past its count 0xFFFF.  The reduce then reads each
+        // bucket's fronts as aligned 128-byte segments at fixed places
+        // (5.7 TB/s in tools/micro/seg_read.hip against 2.8 for ~110-byte
+        // runs at hashed offsets); no granule counts in the header
+        wave_lds_order();
+        const BinArgs& Qa = Q;
+        for (uint32_t k = lane; k < (uint32_t)P.Bc * 8u; k += 64) {
+            const uint32_t bk = k >> 3, i = k & 7u;
+            const uint32_t n = qn[bk];
+            u32x4 v = *reinterpret_cast<const u32x4*>(q + bk * kBinQ + 8 * i);
+            const int k0c = 8 * (int)i;
+            auto pad = [&](uint32_t w, int c) -> uint32_t {
+                const uint32_t lo = k0c + c < (int)n ? (w & 0xFFFFu) : 0xFFFFu;
+                const uint32_t hi = k0c + c + 1 < (int)n ? (w >> 16) : 0xFFFFu;
+                return lo | hi << 16;
+            };
+            v.x = pad(v.x, 0), v.y = pad(v.y, 2), v.z = pad(v.z, 4), v.w = pad(v.w, 6);
+            *reinterpret_cast<u32x4*>(Qa.segs + (chunk * Qa.seg_cap + bk) * kBinQ + 8 * i) = v;
+        }
+        if (lane == 0) {
+            uint4* const h = Q.hdr + kBinHdr * chunk;
+            h[0] = uint4{0u, 0u, 0u, 0u};
+            h[1] = uint4{0u, 0u, 0u, bst[0]};
+            h[2] = uint4{bst[1], bst[2], bst[3], bst[4]};
+            h[3] = uint4{bst[5], bst[6], nc, 0u};
+        }
+    } else if (BIN) {
         // the front runs: every non-empty queue, in bucket order, as 16-byte
         // granules; granule k of the chunk is found through a table in the
         // (now idle) transpose buffer: k -> bucket << 3 | granule
@@ -1630,7 +1666,8 @@ __global__ void __launch_bounds__(kCRT) code_seg_reduce_kernel(const uint16_t* _
                                                                const uint4* __restrict__ hdr,
                                                                const uint8_t* __restrict__ dir, int64_t n_chunks,
                                                                uint32_t seg_cap, int dir_cap, int bwc, int n_cg,
-                                                               uint32_t* __restrict__ part_ch, uint32_t list_cap) {
+                                                               uint32_t* __restrict__ part_ch, uint32_t list_cap,
+                                                               int slotted) {
     __shared__ uint32_t h[kHistMax];
     __shared__ int slots[kCRT];
     __shared__ uint32_t blist[kBackList];
@@ -1652,6 +1689,47 @@ __global__ void __launch_bounds__(kCRT) code_seg_reduce_kernel(const uint16_t* _
         add(v.z & 0xFFFFu), add(v.z >> 16), add(v.w & 0xFFFFu), add(v.w >> 16);
     };
     const int bw_ = bucket >> 3, bs = 4 * (bucket & 7);
+    auto list_back = [&](int64_t c, uint32_t bmw) {  // a chunk whose back mask holds the bucket
+        if ((bmw >> (bucket & 31)) & 1u) {
+            const uint32_t i = __hip_atomic_fetch_add(&nlist, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (i < list_cap) blist[i] = (uint32_t)(c - c_lo);
+        }
+    };
+    if (slotted) {
+        // front slot `bucket` of every chunk: whole 128-byte segments at fixed
+        // places, 8 lanes each, 8 per load instruction; the next 64 chunks'
+        // segments are loaded while these are counted (two register sets);
+        // lane l also reads chunk c0 + l's back mask
+        auto load = [&](u32x4 (&v)[8], int64_t c0) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int64_t c = c0 + 8 * t + (lane >> 3);
+                if (c < c_hi)
+                    v[t] = *reinterpret_cast<const u32x4*>(segs + ((int64_t)c * seg_cap + bucket) * kBinQ + 8 * (lane & 7));
+            }
+        };
+        auto count = [&](const u32x4 (&v)[8], int64_t c0) {
+            if (c0 + lane < c_hi) {
+                const uint4 h2 = hdr[kBinHdr * (c0 + lane) + 2];
+                list_back(c0 + lane, bucket < 32 ? h2.x : h2.y);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                if (c0 + 8 * t + (lane >> 3) < c_hi) add8(v[t]);
+        };
+        u32x4 va[8], vb[8];
+        int64_t c0 = c_lo + (int64_t)wave * 64;
+        if (c0 < c_hi) load(va, c0);
+        while (c0 < c_hi) {
+            if (c0 + kCRT < c_hi) load(vb, c0 + kCRT);
+            count(va, c0);
+            c0 += kCRT;
+            if (c0 >= c_hi) break;
+            if (c0 + kCRT < c_hi) load(va, c0 + kCRT);
+            count(vb, c0);
+            c0 += kCRT;
+        }
+    } else
     // front runs: run r = chunk r's granules of this bucket; a chunk whose
     // back mask holds the bucket is listed for the back pass on the way
     stream_runs(
@@ -1670,11 +1748,7 @@ __global__ void __launch_bounds__(kCRT) code_seg_reduce_kernel(const uint16_t* _
             }
             *beg = c * (int64_t)seg_cap * (kBinQ / 8) + pre;
             *len = mine;
-            const uint32_t bmw = bucket < 32 ? h2.x : h2.y;
-            if ((bmw >> (bucket & 31)) & 1u) {
-                const uint32_t i = __hip_atomic_fetch_add(&nlist, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (i < list_cap) blist[i] = (uint32_t)(c - c_lo);
-            }
+            list_back(c, bucket < 32 ? h2.x : h2.y);
         },
         add8, nullptr, slots);
     __syncthreads();
@@ -2568,6 +2642,7 @@ struct SetsJob {
     bool bin = false;
     uint32_t seg_cap = 0;
     int dir_cap = 0;
+    bool slotted = false;  // binned fronts as whole 128-byte slots (classify2_kernel's end)
     DevArray<uint16_t> bsegs;
     DevArray<uint32_t> bhdr;  // kBinHdr uint4 per chunk
     DevArray<uint8_t> bdir;
@@ -2663,6 +2738,13 @@ int SetsJob::setup() {
     if (bin) {
         dir_cap = (int)(chunk / kBinQ);
         seg_cap = (uint32_t)(dir_cap + g.Bc);
+        // whole slots when a bucket's queue fills well: ~chunk / 3 codes per
+        // chunk (3 records per read) over Bc buckets, >= 40 of 64 (config 3:
+        // 54; the 8-rank preview's 4,096-record chunks: 27, packed granules)
+#ifndef KARMA_BIN_SLOT_MIN
+#define KARMA_BIN_SLOT_MIN 120  // records per chunk per bucket for whole slots (0: never)
+#endif
+        slotted = KARMA_BIN_SLOT_MIN > 0 && A > 0 && chunk >= (int64_t)KARMA_BIN_SLOT_MIN * g.Bc;
         KARMA_CHECK(n_chunks * (int64_t)seg_cap < (int64_t(1) << 32), KARMA_ERR_ARG,
                     "binned classify: %lld chunks exceed 32-bit segment indices", (long long)n_chunks);
         KARMA_TRY(bsegs.alloc(ctx, n_chunks * (int64_t)seg_cap * kBinQ));
@@ -2733,7 +2815,7 @@ int SetsJob::launch() {
                     chunk};
         C.recw = rec.fw;
         const BinArgs Bn = bin ? BinArgs{bsegs.ptr, reinterpret_cast<uint4*>(bhdr.ptr), bdir.ptr, (int64_t)seg_cap,
-                                         dir_cap}
+                                         dir_cap, slotted ? 1 : 0}
                                : BinArgs{};
         auto classify = [&](int64_t c_from, int64_t c_to) -> int {
             C.c0 = c_from;
@@ -2843,7 +2925,7 @@ int SetsJob::launch() {
     if (bin) {
         KARMA_LAUNCH(ctx, "graph_code_reduce", code_seg_reduce_kernel, (int64_t)g.Bc * n_cg, kCRT, 0, bsegs.ptr,
                      reinterpret_cast<const uint4*>(bhdr.ptr), bdir.ptr, n_chunks, seg_cap, dir_cap, g.bwc, n_cg,
-                     part_ch.ptr, back_list_cap());
+                     part_ch.ptr, back_list_cap(), slotted ? 1 : 0);
         // position 2 ("after the code partition": the profile beside the
         // LDS-bound reduce) is after the reduce here: its 132 KB blocks
         // cannot share a CU with the profile's, so a profile started after

@@ -60,6 +60,27 @@ __global__ void __launch_bounds__(1024) runs_read(const u32x4* __restrict__ in, 
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// the back segments' shape: 128-byte aligned segments at random 128-byte slots,
+// 8 lanes per segment (8 segments per load instruction), 8 loads in flight
+__global__ void __launch_bounds__(1024) seg128_read(const u32x4* __restrict__ in, long n_segs, long n_slots,
+                                                    unsigned* __restrict__ sink) {
+    const int lane = threadIdx.x & 63;
+    const long wave = (long)blockIdx.x * 16 + (threadIdx.x >> 6), waves = (long)gridDim.x * 16;
+    unsigned acc = 0;
+    for (long s0 = wave * 64; s0 < n_segs; s0 += waves * 64) {
+        u32x4 v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const long sg = s0 + 8 * t + (lane >> 3);
+            const long slot = (long)((unsigned)(sg * 2654435761u) % (unsigned)n_slots);
+            v[t] = sg < n_segs ? in[slot * 8 + (lane & 7)] : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc ^= v[t].x + v[t].y + v[t].z + v[t].w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 int main(int argc, char** argv) {
     const int L = argc > 1 ? atoi(argv[1]) : 7;
     const long bytes = 2L << 30;  // 2 GiB: well past the 256 MiB Infinity Cache
@@ -89,6 +110,13 @@ int main(int argc, char** argv) {
         hipEventElapsedTime(&ms, a, b);
         const double rb = (double)n_runs * L * 16;
         printf("runs L=%d: %.1f MB in %.3f ms = %.0f GB/s\n", L, rb / 1e6, ms, rb / ms / 1e6);
+        const long n_segs = bytes / 128 / 8;  // 1/8 of the slots, ~ the codes' 207 MB at 2 GiB
+        hipEventRecord(a);
+        seg128_read<<<cu, 1024>>>(in, n_segs, bytes / 128, sink);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        hipEventElapsedTime(&ms, a, b);
+        printf("seg128: %.1f MB in %.3f ms = %.0f GB/s\n", n_segs * 128 / 1e6, ms, n_segs * 128 / ms / 1e6);
     }
     hipFree(in);
     hipFree(sink);
