@@ -9,7 +9,9 @@ wide (16 B/lane) streaming read, so reads are doubled; WRITE_SIZE is exact for
 The code reduces read short runs (~110 B per chunk and bucket) for which
 FETCH_SIZE counts the bytes themselves (calibrated in round 6 with
 tools/micro/seg_read.hip: x 0.986 on a known byte count), so their reads are
-not doubled.
+not doubled -- except where the binned classify writes whole 128-byte slots
+(config 3, "slotted"): the reduce then reads aligned 128-byte segments, the
+wide case (fix such entries by hand; profiles/pmc_traffic.json says which).
 
 The output is keyed by workload (bench.py pmc_traffic(): "<config>[_strong]
 [_shuffled]_n<ranks>"), so a number is only ever reported for the workload
