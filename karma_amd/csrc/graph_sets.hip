@@ -163,9 +163,11 @@ __device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__buil
 
 // ---- classify -------------------------------------------------------------------
 constexpr int kCW = 256;                // classify threads per block (4 independent waves)
-constexpr int kCIter = 512;             // records per wave step (8 per lane)
+constexpr int kCIter = 512;             // records per wave step (8 per lane; flagged records: 64 x KARMA_FLAG_RPL)
 constexpr int kCPer = kCIter / 128;     // 16-byte units per lane per step
-constexpr int kFPer = kCIter / 256;     // ... of flagged records (4 bytes each)
+#ifndef KARMA_FLAG_RPL
+#define KARMA_FLAG_RPL 16  // flagged records per lane and step (16: 1024-record steps, 4 units per lane; 8: 512)
+#endif
 constexpr uint32_t kContigMask = 0x7FFFFFFFu;  // flagged record: contig id; bit 31 starts a read
 constexpr uint32_t kPadW = 0x80000000u;        // flagged padding past a chunk: a read of its own, never emitted
 constexpr int64_t kCChunk = 8192;       // records per wave chunk (16 steps; chunk_records may halve it)
@@ -293,6 +295,9 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 #endif
 constexpr int kRareMax = int(kCChunk / kCIter);  // steps per chunk
 constexpr int kRareW = 5;                        // words per listed step
+#ifndef KARMA_CLS_PIN
+#define KARMA_CLS_PIN 2  // walk state pinned per record (see the walk): 1 with 16 records per lane, 2 always
+#endif
 #ifndef KARMA_CLS_NO_RARE
 #define KARMA_CLS_NO_RARE 0  // measurement only (A/B of the rare pass's register cost): no general / big reads emitted
 #endif
@@ -349,6 +354,15 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         asm volatile("" : "+s"(ka));
         return *reinterpret_cast<const ClassArgs*>(ka);
     };
+    // records per lane and per step: flagged steps hold twice as many records
+    // in the same 16 bytes per lane and unit (the per-step work -- the merge
+    // of tails and heads, the transposes' waits, the carry -- then amortises
+    // over 1024 records)
+    constexpr int RPL = FLAG ? KARMA_FLAG_RPL : 8;
+    constexpr int64_t kIt = 64 * RPL;
+    constexpr int kFPer = RPL / 4;  // FLAG: 16-byte units per lane and step
+    static_assert(RPL == 8 || (FLAG && RPL == 16), "8 or 16 records per lane (16: flagged only)");
+    static_assert(!FLAG || kFPer <= kCPer, "the step's units fit the register set");
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
@@ -462,7 +476,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     auto prefetch = [&](u32x4 (&dst)[kCPer], int64_t t0, int64_t hi) {
         if (FLAG) {  // unit u of lane l = records t0 + 256u + 4l .. + 3; past the chunk: a read start, contig 0
             const int64_t gw = t0 + 4 * lane;
-            if (t0 + kCIter <= hi) {
+            if (t0 + kIt <= hi) {
 #pragma unroll
                 for (int u = 0; u < kFPer; ++u)
                     dst[u] = KARMA_REC_NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(P.recw + gw + 256 * u))
@@ -478,7 +492,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             return;
         }
         const int64_t gb = t0 + 2 * lane;
-        if (t0 + kCIter <= hi) {
+        if (t0 + kIt <= hi) {
 #pragma unroll
             for (int u = 0; u < kCPer; ++u)
                 if (KARMA_REC_NT)
@@ -532,9 +546,36 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     auto step = [&](auto full_tag, auto replay_tag, u32x4 (&buf)[kCPer], u32x4 (&nxt)[kCPer], int64_t t0) {
         constexpr bool FULL = decltype(full_tag)::value;
         constexpr bool REPLAY = decltype(replay_tag)::value;
-        uint32_t rid[8], ctg[8];  // FLAG: rid holds the raw words (bit 31: a read starts here)
+        uint32_t rid[RPL], ctg[RPL];  // FLAG: rid holds the raw words (bit 31: a read starts here)
         // loader lane L, unit u -> lane 16u + L/4, unit L & 3; lane l reads its 8 records back
-        if (FLAG) {
+        if constexpr (FLAG && RPL == 16) {
+            // two passes of 128 granules (2 KB: BIN's half buffer): pass h holds
+            // units 2h, 2h + 1 = the records of lanes 32h .. 32h + 31; local
+            // granule g at slot g ^ ((g >> 4) & 3): the stores' 8-lane groups
+            // stay in one 16-granule row (a permutation of it), and the reads'
+            // 16-lane groups (granules 4j + k) fall on 16 distinct bank quads
+            const int rl = lane & 31;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int g = 64 * u + lane;
+                    tb[g ^ ((g >> 4) & 3)] = buf[2 * h + u];
+                }
+                wave_sync();
+                if ((lane >> 5) == h) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int g = 4 * rl + k;
+                        const u32x4 qv = tb[g ^ ((g >> 4) & 3)];
+                        rid[4 * k] = qv.x, rid[4 * k + 1] = qv.y, rid[4 * k + 2] = qv.z, rid[4 * k + 3] = qv.w;
+                    }
+                }
+                wave_sync();
+            }
+#pragma unroll
+            for (int i = 0; i < RPL; ++i) ctg[i] = rid[i] & kContigMask;
+        } else if (FLAG) {
             // 16-byte granule g = 64u + L (records 4g .. 4g + 3) at slot g ^ ((g >> 3) & 1): lane l
             // reads granules 2l, 2l + 1 (conflict-free on both sides; 2 KB: BIN's half buffer)
 #pragma unroll
@@ -594,22 +635,24 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         }
         if (REPLAY) {
         } else if (REMAP) {
-            if (t0 + kCIter < c_hi) remap_units(nxt);
-            if (t0 + 2 * kCIter < c_hi) prefetch(buf, t0 + 2 * kCIter, c_hi);
-        } else if (t0 + kCIter < c_hi) {
-            prefetch(buf, t0 + kCIter, c_hi);
+            if (t0 + kIt < c_hi) remap_units(nxt);
+            if (t0 + 2 * kIt < c_hi) prefetch(buf, t0 + 2 * kIt, c_hi);
+        } else if (t0 + kIt < c_hi) {
+            prefetch(buf, t0 + kIt, c_hi);
         }
         // valid records of this lane (own reads start at a valid record)
-        const int nval = FULL ? 8 : (int)max<int64_t>(0, min<int64_t>(8, c_hi - (t0 + 8 * lane)));
-        const uint32_t prev_last = FLAG ? 0u : dpp_shr1(prev_rid, rid[7]);
+        const int nval = FULL ? RPL : (int)max<int64_t>(0, min<int64_t>(RPL, c_hi - (t0 + RPL * lane)));
+        const uint32_t prev_last = FLAG ? 0u : dpp_shr1(prev_rid, rid[RPL - 1]);
         // order and range checks as lane masks (padding: read id kEmpty, contig
         // 0); the order of records inside the lane is checked during the walk
         if (!REPLAY) {
             if (!FLAG) bad_order |= lanes(prev_last > rid[0]) & (have_prev ? ~0ull : ~1ull);
-            bad_contig |= lanes(max(max(max(ctg[0], ctg[1]), max(ctg[2], ctg[3])),
-                                    max(max(ctg[4], ctg[5]), max(ctg[6], ctg[7]))) >= P.N);
+            uint32_t cmax = ctg[0];
+#pragma unroll
+            for (int i = 1; i < RPL; ++i) cmax = max(cmax, ctg[i]);
+            bad_contig |= lanes(cmax >= P.N);
         }
-        const uint32_t ubase = (uint32_t)(t0 - c_lo) + 8u * lane;
+        const uint32_t ubase = (uint32_t)(t0 - c_lo) + (uint32_t)RPL * lane;
         // The lane's walk (branch-free: no lane predicate lives across a branch,
         // so the compiler keeps them as SGPR lane masks).  Emission: codes from
         // the front of the chunk's region (BIN: into the bucket queues),
@@ -666,11 +709,15 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             rs_reset(st, ctg[0]);
             hd = st;
             spos = 0;
-            uint32_t hlen = in_mask(S0) ? 0u : 8u;  // head: records before the first start (8: none)
+            uint32_t hlen = in_mask(S0) ? 0u : (uint32_t)RPL;  // head: records before the first start (RPL: none)
             started = S0;
             uint64_t Si = S0;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < RPL; ++i) {
+                // 16 records per lane: <= 64 codes per emit point, 16 of them --
+                // the first eight's codes go into the queues mid-walk (the staging
+                // buffer holds 512)
+                if (!RARE && BIN && RPL > 8 && i == 8) bin_stage();
                 if (i > 0) {
                     const uint64_t cap = Si & ~started;  // the first start: the head ends here
                     hd.win = in_mask(cap) ? st.win : hd.win;
@@ -684,7 +731,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     st.fm3 = fm3;
                     if (!RARE && !FLAG) bad_order |= lanes(rid[i - 1] > rid[i]);
                 }
-                if (i < 7) {
+                if (i < RPL - 1) {
                     // an own read ends at i (the next record starts one); it
                     // started at a valid record iff i < nval
                     const uint64_t Sn = S(i + 1);
@@ -692,7 +739,20 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     Si = Sn;
                     uint32_t code;
                     const uint64_t ok = rs_code_m<COMPACT, BIN>(st, P.N, &code);
-                    emit(e, ok, code, ubase + spos, 0ull);
+                    // an own read of > 8 records (16 per lane) that is not
+                    // compact is a big read (the general path reads 8); a compact
+                    // one is a code like any other (its contig set is the code)
+                    const uint64_t big_own =
+                        RARE && i + 1 > kMaxFast ? lanes((uint32_t)i + 1u - spos > (uint32_t)kMaxFast) & ~ok : 0ull;
+                    emit(e, ok, code, ubase + spos, big_own);
+                }
+                // 16 records: pin the walk's state at each record, or the compiler
+                // sinks the head's selects and the rare mask past the loop and
+                // keeps every record's lane masks alive for them (SGPRs spilled
+                // into VGPR lanes)
+                if (KARMA_CLS_PIN > 1 || (RPL > 8 && KARMA_CLS_PIN)) {
+                    asm volatile("" : "+v"(hd.win), "+v"(hlen), "+v"(spos), "+v"(st.win), "+v"(st.fm3));
+                    asm volatile("" : "+s"(started), "+s"(rare), "+s"(Si));
                 }
             }
             // the head began at record 0 (its first contig is ctg[0]); no read
@@ -702,7 +762,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             // the incoming tail (the previous lane's last read), merged with this
             // lane's head when the read continues (else with itself: the same code)
             const uint64_t t_ok = started & (FULL ? ~0ull : lanes((int)spos < nval));
-            const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
+            const uint32_t t_len = (uint32_t)RPL - spos, t_pos = ubase + spos;
             RState in;
             in.fm3 = dpp_shr1(ct.fm3, st.fm3);
             in.win = dpp_shr1(ct.win, st.win);
@@ -711,12 +771,19 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             const uint64_t have = lanes(in_pk != kEmpty);
             const uint32_t in_len = in_pk & 255u, in_pos = in_pk >> 8;
             const uint64_t cont = ~S0;
-            const uint64_t big = cont & lanes(in_len + hlen > (uint32_t)kMaxFast);
             RState hm;
             hm.fm3 = in_mask(cont) ? hd.fm3 : in.fm3;
             hm.win = in_mask(cont) ? hd.win : in.win;
             uint32_t code;
             const uint64_t ok = rs_code2_m<COMPACT, BIN>(in, hm, P.N, &code);
+            // big: the read runs past this lane (no start in it: its length is
+            // unknown here), or has > 8 records.  16 records per lane: a read
+            // seen whole (tail alone, or tail + head) is a code when compact,
+            // whatever its length, and big only when general and > 8 records
+            const uint64_t big =
+                RPL > 8 ? (cont & lanes(hlen == (uint32_t)RPL)) |
+                              (lanes(in_len + (in_mask(cont) ? hlen : 0u) > (uint32_t)kMaxFast) & ~ok)
+                        : cont & lanes(in_len + hlen > (uint32_t)kMaxFast);
             emit(have, ok, code, in_pos, big);
             return rare;
         };
@@ -731,10 +798,10 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         uint32_t spos;
         uint64_t started;
         const uint64_t rare = walk(std::false_type{}, st, spos, started);
-        // this lane's tail (an own read reaching record 7) -> the next lane;
-        // carry lane 63 into the next step
+        // this lane's tail (an own read reaching its last record) -> the next
+        // lane; carry lane 63 into the next step
         const uint64_t t_ok = started & (FULL ? ~0ull : lanes((int)spos < nval));
-        const uint32_t t_len = 8u - spos, t_pos = ubase + spos;
+        const uint32_t t_len = (uint32_t)RPL - spos, t_pos = ubase + spos;
         const bool ct_ok_next = (t_ok >> 63) != 0;
         RState ct_next;
         ct_next.fm3 = (uint32_t)__builtin_amdgcn_readlane((int)st.fm3, 63);
@@ -745,7 +812,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             // listed with its carry-in (ct* and prev_rid still hold it here)
             if (lane == 0) {
                 uint32_t* const e = rl + kRareW * n_rare;
-                e[0] = (uint32_t)((t0 - c_lo) / kCIter) | (ct_ok ? 256u : 0u) | (have_prev ? 512u : 0u);
+                e[0] = (uint32_t)((t0 - c_lo) / kIt) | (ct_ok ? 256u : 0u) | (have_prev ? 512u : 0u);
                 e[1] = ct.fm3;
                 e[2] = ct.win;
                 e[3] = ct_len | ct_pos << 8;
@@ -763,7 +830,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         ct = ct_next;
         ct_len = ct_len_next;
         ct_pos = ct_pos_next;
-        if (!FLAG) prev_rid = (uint32_t)__builtin_amdgcn_readlane((int)rid[7], 63);
+        if (!FLAG) prev_rid = (uint32_t)__builtin_amdgcn_readlane((int)rid[RPL - 1], 63);
         have_prev = true;
     };
     u32x4 buf[kCPer];
@@ -790,20 +857,20 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     const std::false_type main_pass{};
     if (!REMAP) {
         int64_t t0 = c_lo;
-        for (; t0 + kCIter <= c_hi; t0 += kCIter) step(std::true_type{}, main_pass, buf, buf, t0);
+        for (; t0 + kIt <= c_hi; t0 += kIt) step(std::true_type{}, main_pass, buf, buf, t0);
         if (t0 < c_hi) step(std::false_type{}, main_pass, buf, buf, t0);
     } else {  // two register sets, alternating
         u32x4 buf2[kCPer];
-        if (c_lo + kCIter < c_hi) prefetch(buf2, c_lo + kCIter, c_hi);
+        if (c_lo + kIt < c_hi) prefetch(buf2, c_lo + kIt, c_hi);
         remap_units(buf);
         for (int64_t t0 = c_lo; t0 < c_hi;) {
-            if (t0 + kCIter <= c_hi) step(std::true_type{}, main_pass, buf, buf2, t0);
+            if (t0 + kIt <= c_hi) step(std::true_type{}, main_pass, buf, buf2, t0);
             else step(std::false_type{}, main_pass, buf, buf2, t0);
-            t0 += kCIter;
+            t0 += kIt;
             if (t0 >= c_hi) break;
-            if (t0 + kCIter <= c_hi) step(std::true_type{}, main_pass, buf2, buf, t0);
+            if (t0 + kIt <= c_hi) step(std::true_type{}, main_pass, buf2, buf, t0);
             else step(std::false_type{}, main_pass, buf2, buf, t0);
-            t0 += kCIter;
+            t0 += kIt;
         }
     }
     if (KARMA_CLS_DEFER_RARE && n_rare) {
@@ -825,10 +892,10 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             ct_len = w3 & 255u;
             ct_pos = w3 >> 8;
             prev_rid = (uint32_t)__builtin_amdgcn_readfirstlane((int)e[4]);
-            const int64_t t0 = c_lo + (int64_t)(w0 & 255u) * kCIter;
+            const int64_t t0 = c_lo + (int64_t)(w0 & 255u) * kIt;
             prefetch(buf, t0, c_hi);
             if (REMAP) remap_units(buf);
-            if (t0 + kCIter <= c_hi) step(std::true_type{}, std::true_type{}, buf, buf, t0);
+            if (t0 + kIt <= c_hi) step(std::true_type{}, std::true_type{}, buf, buf, t0);
             else step(std::false_type{}, std::true_type{}, buf, buf, t0);
         }
         ct_ok = s_ok;

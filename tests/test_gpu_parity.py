@@ -343,6 +343,47 @@ def test_flagged_records_first_flag_and_chunk_edges():
         buf.close()
 
 
+@pytest.mark.parametrize("n", [3000, 1_200_000, 2_200_000])  # binned, compact unbinned, no compact path
+def test_flagged_records_sixteen_per_lane(n):
+    """Flagged classify steps hold 16 records per lane (graph_sets.hip
+    KARMA_FLAG_RPL): reads of 9..16 records inside one lane (compact: a code;
+    general: the big list, as the general path reads 8), a read filling a lane
+    exactly (a tail seen whole), reads of 17..40 records (lanes without a
+    start), and runs of one-record reads (1,024 codes per step: the staging
+    buffer's mid-walk flush), each compact and wide."""
+    rng = np.random.default_rng(23)
+    rows, r = [], 0
+
+    def read(m, compact):
+        nonlocal r
+        lo = int(rng.integers(0, n - 200))
+        cs = lo + (rng.integers(0, 4, m) if compact else rng.integers(0, 200, m))
+        rows.extend((r, int(c)) for c in cs)
+        r += 1
+
+    def align(k):  # one-record reads up to a multiple of k records
+        while len(rows) % k:
+            read(1, True)
+
+    while len(rows) < 120_000:
+        kind = int(rng.integers(0, 5))
+        if kind == 0:
+            align(16)
+            for _ in range(int(rng.integers(1, 40))):
+                read(16, bool(rng.random() < 0.6))
+        elif kind == 1:
+            for _ in range(int(rng.integers(1, 2048))):
+                read(1, bool(rng.random() < 0.9))
+        elif kind == 2:
+            read(int(rng.integers(17, 41)), bool(rng.random() < 0.5))
+        else:
+            if rng.random() < 0.5:
+                align(16)
+                read(int(rng.integers(1, 8)), True)
+            read(int(rng.integers(9, 17)), bool(rng.random() < 0.5))
+    check_records(np.array(rows, np.uint32), n)
+
+
 def test_eq_vs_oracle_seeded():
     classes = synth.eq_classes(31, 2000, 300_000, True)
     names = [f"ctg{i}" for i in range(2000)]

@@ -18,7 +18,7 @@ for rep in ${REPS:-1 2}; do
       esac
       f=$OUT/${leg}_${name}_r${rep}
       KARMA_LIB=$lib KARMA_ALLOW_VARIANT=1 timeout -k 10 240 python bench.py --cpu-baseline off --no-e2e --no-other-format ${AB_PARITY:---no-parity} \
-        --steps ${STEPS:-30} $extra > $f.json 2> $f.err || { echo "$leg $name failed"; tail -5 $f.err; exit 1; }
+        --steps ${STEPS:-30} $extra ${AB_EXTRA} > $f.json 2> $f.err || { echo "$leg $name failed"; tail -5 $f.err; exit 1; }
       python -c "import json; d=json.load(open('$f.json')); k=d['kernels_ms_per_step']; print('$leg', '$name', 'rep', $rep, d['ms_per_step'], 'live', (d.get('roofline') or {}).get('avg_launch_ms'), 'ceil', (d.get('profile_write_ceiling') or {}).get('profile_vs_ceiling'), {x: round(k[x], 4) for x in k if k[x] > 0.015})"
     done
   done
