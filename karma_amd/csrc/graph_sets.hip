@@ -262,18 +262,18 @@ __device__ __forceinline__ bool rs_code2(const RState& a, const RState& b, uint3
 // masks, which feed selects through inverse ballots (no 0/1 VGPR round trips)
 __device__ __forceinline__ uint64_t lanes(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 __device__ __forceinline__ bool in_mask(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
-// K23 (the binned classify's staged codes): m0 | rel << 23, one shift-or;
-// rel's bit 0 (always set) lands on bit 23, so M = code >> 24 as in the
-// m0 | M << 24 form and m0 = code & 0x7FFFFF (m0 < 2^21 on the compact path).
-// K23 also drops the m0 < N test: m0 >= N needs a contig >= N, which the range
-// check reports (the call fails), and bin_emit clamps the bucket so that such
-// a code stays inside the queues meanwhile (one op per staged code instead of
-// one compare per record)
+// K23 (the binned classify's staged codes): m0 << 4 | rel, one shift-or
+// (rel < 16 on the compact path, bit 0 always set), so that the bucket queue's
+// u16 value (m0_local << 3 | M) is one bit-field extract and the bucket one
+// shift.  K23 also drops the m0 < N test: m0 >= N needs a contig >= N, which the
+// range check reports (the call fails), and bin_emit clamps the bucket so that
+// such a code stays inside the queues meanwhile (one op per staged code instead
+// of one compare per record)
 template <bool COMPACT, bool K23 = false>
 __device__ __forceinline__ uint64_t rs_code_m(const RState& s, uint32_t N, uint32_t* code) {
     const uint32_t z = (uint32_t)__builtin_ctz(s.win);
     const uint32_t rel = s.win >> z, m0 = s.fm3 + z;
-    *code = K23 ? m0 | rel << 23 : m0 | (rel >> 1) << 24;
+    *code = K23 ? m0 << 4 | rel : m0 | (rel >> 1) << 24;
     return COMPACT ? lanes(rel < 16u) & (K23 ? ~0ull : lanes(m0 < N)) : 0ull;
 }
 template <bool COMPACT, bool K23 = false>
@@ -281,7 +281,7 @@ __device__ __forceinline__ uint64_t rs_code2_m(const RState& a, const RState& b,
     const uint32_t za = (uint32_t)__builtin_ctz(a.win), zb = (uint32_t)__builtin_ctz(b.win);
     const uint32_t ma = a.fm3 + za, mb = b.fm3 + zb, m0 = min(ma, mb);
     const uint32_t rel = ((a.win >> za) << min(ma - m0, 31u)) | ((b.win >> zb) << min(mb - m0, 31u));
-    *code = K23 ? m0 | rel << 23 : m0 | (rel >> 1) << 24;
+    *code = K23 ? m0 << 4 | rel : m0 | (rel >> 1) << 24;
     return COMPACT ? lanes(rel < 16u) & (K23 ? ~0ull : lanes(m0 < N)) : 0ull;
 }
 
@@ -295,6 +295,9 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {  // lan
 #endif
 constexpr int kRareMax = int(kCChunk / kCIter);  // steps per chunk
 constexpr int kRareW = 5;                        // words per listed step
+#ifndef KARMA_CLS_RANGE_CODE
+#define KARMA_CLS_RANGE_CODE 3  // binned flagged classify: 1 the walk on raw words, 2 the range checked per code (RC)
+#endif
 #ifndef KARMA_CLS_PIN
 #define KARMA_CLS_PIN 2  // walk state pinned per record (see the walk): 1 with 16 records per lane, 2 always
 #endif
@@ -363,6 +366,14 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     constexpr int kFPer = RPL / 4;  // FLAG: 16-byte units per lane and step
     static_assert(RPL == 8 || (FLAG && RPL == 16), "8 or 16 records per lane (16: flagged only)");
     static_assert(!FLAG || kFPer <= kCPer, "the step's units fit the register set");
+    // RC: the binned flagged walk reads the raw words (no per-record mask of the
+    // start flag) and checks the contig range per code instead of per record:
+    // a staged compact code with m0 >= N - 3 (its contigs are m0 .. m0 + 3 at
+    // most) lists its step for the replay, which checks the step's compact codes
+    // exactly; general and big reads are checked where their records are read
+    // (general_kernel, big_pairs_kernel); the chunk-end tail read here
+    constexpr bool RC = BIN && FLAG && (KARMA_CLS_RANGE_CODE & 2) && KARMA_CLS_DEFER_RARE;
+    constexpr bool RAW = FLAG && (KARMA_CLS_RANGE_CODE & 1);  // the walk on raw words (measurement split)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
@@ -417,14 +428,19 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // written as a back segment, and the codes that found it full go into the
     // emptied queue (a queue holds < kBinQ codes between calls, so the lane
     // that took slot kBinQ - 1 exists whenever one overflowed)
-    // (code: m0 | M << 24 or the K23 form m0 | rel << 23; m0 < 2^21 either way)
+    // (code: the K23 form m0 << 4 | rel, rel's bit 0 set: bits 1.. are
+    // m0_local << 3 | M, bits bwc + 4.. the bucket)
     auto bin_emit = [&](uint64_t m, uint32_t code) {
-        const uint32_t m0 = code & 0x7FFFFFu, bk = min(m0 >> P.bwc, (uint32_t)P.Bc - 1u);
-        const uint16_t val = (uint16_t)(((m0 & ((1u << P.bwc) - 1u)) << 3) | (code >> 24));
+        const uint32_t bk = min(code >> (P.bwc + 4), (uint32_t)P.Bc - 1u);
+        const uint16_t val = (uint16_t)__builtin_amdgcn_ubfe(code, 1u, (uint32_t)P.bwc + 3u);
         uint32_t pos = 0;
         if (in_mask(m)) {
             pos = __hip_atomic_fetch_add(&qn[bk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (pos < (uint32_t)kBinQ) q[bk * kBinQ | pos] = val;
+            if (pos < (uint32_t)kBinQ) {
+                uint32_t qi = (bk << 6) + pos;
+                asm("" : "+v"(qi));  // two shift-adds, not two shifts and an add
+                q[qi] = val;
+            }
         }
         uint64_t full = m & lanes(pos == (uint32_t)kBinQ - 1u);
         if (!full) return;
@@ -458,14 +474,21 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // into the queues once per step, 64 at a time, instead of at each of the
     // walk's 8 emit points
     uint32_t* const stg = reinterpret_cast<uint32_t*>(tb);
+    const uint32_t* const stg_l = stg + lane;
     uint32_t ns = 0;  // staged codes (uniform)
+    static_assert(kBinQ == 64, "queue slots: bk << 6");
+    // RC: staged codes whose contigs may reach N (m0 >= N - 3), this step
+    uint64_t stage_hi = 0;
+    const uint32_t code_hi = ((uint32_t)max(P.N, 3u) - 3u) << 4;
     auto bin_stage = [&]() {
         if (!ns) return;
         wave_lds_order();
         for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
-            // unpredicated read (ns <= 512 codes per step: the 2 KB buffer; past ns: masked off)
-            const uint32_t j = j0 + lane;
-            bin_emit(lanes(j < ns), stg[min(j, (uint32_t)(kRows * 16 - 1))]);
+            // unpredicated read (ns <= 512 codes: the 2 KB buffer; j0 + lane < 512 always; past ns masked off)
+            const uint32_t cd = stg_l[j0];
+            const uint64_t m = lanes((uint32_t)lane < ns - j0);
+            if (RC) stage_hi |= m & lanes(cd >= code_hi);
+            bin_emit(m, cd);
         }
         ns = 0;
         wave_lds_order();
@@ -647,10 +670,12 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         // 0); the order of records inside the lane is checked during the walk
         if (!REPLAY) {
             if (!FLAG) bad_order |= lanes(prev_last > rid[0]) & (have_prev ? ~0ull : ~1ull);
-            uint32_t cmax = ctg[0];
+            if (!RC) {
+                uint32_t cmax = ctg[0];
 #pragma unroll
-            for (int i = 1; i < RPL; ++i) cmax = max(cmax, ctg[i]);
-            bad_contig |= lanes(cmax >= P.N);
+                for (int i = 1; i < RPL; ++i) cmax = max(cmax, ctg[i]);
+                bad_contig |= lanes(cmax >= P.N);
+            }
         }
         const uint32_t ubase = (uint32_t)(t0 - c_lo) + (uint32_t)RPL * lane;
         // The lane's walk (branch-free: no lane predicate lives across a branch,
@@ -683,6 +708,12 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     nc += __popcll(b);
                     rare |= e & (big | ~ok);
                 } else {
+                    if (RC) {  // the step's compact codes (m0 << 4 | rel): their top contig < N
+                        const uint64_t cm = e & ok & ~big;
+                        if (cm)
+                            bad_contig |= cm & lanes((code >> 4) + 31u - (uint32_t)__builtin_clz(code & 15u) >=
+                                                     PA().N);
+                    }
                     const uint64_t g = e & ~big & ~ok;
                     if (g) {
                         const ClassArgs& Pa = PA();
@@ -724,11 +755,21 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     hlen = in_mask(cap) ? (uint32_t)i : hlen;
                     started |= Si;
                     spos = in_mask(Si) ? (uint32_t)i : spos;
-                    const uint32_t c = ctg[i];
-                    const uint32_t fm3 = in_mask(Si) ? c - 3u : st.fm3;
-                    // a new read: bit 3 alone (c - fm3 = 3)
-                    st.win = (in_mask(Si) ? 0u : st.win) | (1u << min(c - fm3, 31u));
-                    st.fm3 = fm3;
+                    if (RAW) {
+                        // raw word: bit 31 set exactly at a start (i > 0), so a
+                        // start's contig - 3 is w - 0x80000003, and another
+                        // record's w is its contig
+                        const uint32_t w = rid[i];
+                        const uint32_t fm3 = in_mask(Si) ? w - 0x80000003u : st.fm3;
+                        st.win = in_mask(Si) ? 8u : st.win | (1u << min(w - fm3, 31u));
+                        st.fm3 = fm3;
+                    } else {
+                        const uint32_t c = ctg[i];
+                        const uint32_t fm3 = in_mask(Si) ? c - 3u : st.fm3;
+                        // a new read: bit 3 alone (c - fm3 = 3)
+                        st.win = (in_mask(Si) ? 0u : st.win) | (1u << min(c - fm3, 31u));
+                        st.fm3 = fm3;
+                    }
                     if (!RARE && !FLAG) bad_order |= lanes(rid[i - 1] > rid[i]);
                 }
                 if (i < RPL - 1) {
@@ -808,7 +849,8 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         ct_next.win = (uint32_t)__builtin_amdgcn_readlane((int)st.win, 63);
         const uint32_t ct_len_next = (uint32_t)__builtin_amdgcn_readlane((int)t_len, 63);
         const uint32_t ct_pos_next = (uint32_t)__builtin_amdgcn_readlane((int)t_pos, 63);
-        if (KARMA_CLS_DEFER_RARE && rare) {
+        if (RC && BIN) bin_stage();  // (its codes' range test decides the listing too)
+        if (KARMA_CLS_DEFER_RARE && (rare || (RC && stage_hi))) {
             // listed with its carry-in (ct* and prev_rid still hold it here)
             if (lane == 0) {
                 uint32_t* const e = rl + kRareW * n_rare;
@@ -825,7 +867,8 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             uint64_t started2;
             walk(std::true_type{}, st2, spos2, started2);
         }
-        if (BIN) bin_stage();  // before the next step's transpose reuses the buffer
+        if (BIN && !RC) bin_stage();  // before the next step's transpose reuses the buffer
+        if (RC) stage_hi = 0;
         ct_ok = ct_ok_next;
         ct = ct_next;
         ct_len = ct_len_next;
@@ -928,7 +971,12 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
         const bool big = ct_len + hl > (uint32_t)kMaxFast;
         uint32_t code;
         const bool ok = !big && (hl ? rs_code2<COMPACT>(ct, h, P.N, &code) : rs_code<COMPACT>(ct, P.N, &code));
-        if (BIN && ok) bin_emit(1ull, code);  // lane 0's code (uniform values)
+        // lane 0's code (uniform values), in the staged form m0 << 4 | M << 1 | 1
+        if (BIN && ok) {
+            const uint32_t rel = (code >> 24) << 1 | 1u;
+            if (RC && (code & 0xFFFFFFu) + 31u - (uint32_t)__builtin_clz(rel) >= P.N) bad_contig |= 1ull;
+            bin_emit(1ull, (code & 0xFFFFFFu) << 4 | rel);
+        }
         if (lane == 0) {
             const ClassArgs& Pa = P;
             if (big) Pa.big_list[atomicAdd(Pa.big_n, 1u)] = c_lo + ct_pos;
@@ -1080,7 +1128,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(RecIn rec, int64_t A, uint
     uint32_t np = 0;
     uint64_t* out = pairs + chunk * pcap;
     const int64_t c_lo = chunk * chunk_len;
-    bool full = false;
+    bool full = false, bad = false;  // bad: a contig >= N (the binned flagged classify checks codes only)
     for (uint32_t kb = 0; kb < ng; kb += 64) {
         const uint32_t k = kb + lane;
         ReadSet rs;
@@ -1094,6 +1142,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(RecIn rec, int64_t A, uint
             for (int t = 0; t < kMaxFast; ++t) {
                 v = v && s + t < A && (t == 0 || rec.cont(s + t));
                 const uint32_t y = v ? rec.contig(s + t) : kEmpty;
+                bad |= v && y >= N;
                 rs.m[t] = v && y < N ? (remap ? remap[y] : y) : kEmpty;
             }
             sort_dedup(rs);
@@ -1120,6 +1169,7 @@ __global__ void __launch_bounds__(kGW) general_kernel(RecIn rec, int64_t A, uint
         if (np) atomicAdd(blk_items + chunk / lists_per_block, (unsigned long long)np);
         if (full) flags[2] = 1;  // the host reruns with room for every pair
     }
+    if (bad) flags[1] = 1;
     }
 }
 
@@ -2298,12 +2348,22 @@ __global__ void bucket_widen_kernel(const uint32_t* __restrict__ pent, RunDir di
 }
 
 // big reads (> 8 records): pair keys, one thread per read, O(m^3) dedup
+// (count pass: n_out[1] = 1 when a record's contig is >= N; the binned
+// flagged classify checks the range of codes only)
 __global__ void big_pairs_kernel(RecIn rec, int64_t A, const int64_t* __restrict__ big_list,
                                  int64_t n_big, uint32_t N, uint64_t* __restrict__ out,
                                  unsigned long long* __restrict__ n_out, int count_only,
                                  const uint32_t* __restrict__ remap) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_big) return;
+    if (count_only) {
+        const int64_t i = big_list[k];
+        int64_t e = i;
+        bool bad = false;
+        do bad |= rec.contig(e) >= N;
+        while (++e < A && rec.cont(e));
+        if (bad) n_out[1] = 1;
+    }
     unsigned long long c = 0;
     auto map = [&](uint32_t x) { return remap && x < N ? remap[x] : x; };
     read_pairs_slow(rec, A, big_list[k], map, [&](uint32_t a, uint32_t b) {
@@ -2362,13 +2422,15 @@ int finish_pairs(karma_ctx* ctx, RecIn rec, int64_t A, int64_t N, const int64_t*
         return KARMA_OK;
     }
     DevArray<unsigned long long> np;
-    KARMA_TRY(np.alloc(ctx, 1));
-    KARMA_HIP(hipMemsetAsync(np.ptr, 0, 8, ctx->stream));
+    KARMA_TRY(np.alloc(ctx, 2));
+    KARMA_HIP(hipMemsetAsync(np.ptr, 0, 16, ctx->stream));
     KARMA_LAUNCH(ctx, "graph_big_count", big_pairs_kernel, grid_n(n_big, 64), 64, 0, rec, A, big_list,
                  (int64_t)n_big, (uint32_t)N, (uint64_t*)nullptr, np.ptr, 1, remap);
-    unsigned long long hp = 0;
-    KARMA_HIP(hipMemcpyAsync(&hp, np.ptr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned long long hpb[2] = {0, 0};
+    KARMA_HIP(hipMemcpyAsync(hpb, np.ptr, 16, hipMemcpyDeviceToHost, ctx->stream));
     KARMA_HIP(hipStreamSynchronize(ctx->stream));
+    const unsigned long long hp = hpb[0];
+    KARMA_CHECK(!hpb[1], KARMA_ERR_ARG, "a record's contig index is >= n_contigs (%lld)", (long long)N);
     DevArray<uint64_t> allk;
     DevArray<int64_t> allc;
     KARMA_TRY(allk.alloc(ctx, U + hp));

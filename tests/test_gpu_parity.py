@@ -384,6 +384,39 @@ def test_flagged_records_sixteen_per_lane(n):
     check_records(np.array(rows, np.uint32), n)
 
 
+@pytest.mark.parametrize("pos", [0, 1023, 1024, 2047, 4095, 8191, 12_345])
+def test_records_contig_range_per_read_kind(pos):
+    """The binned flagged classify checks the contig range per code (a compact
+    code with m0 >= N - 3 sends its step to the replay, which checks the
+    step's codes exactly) and leaves general and big reads to the kernels that
+    read their records (graph_sets.hip RC).  A read with a contig >= N placed
+    at `pos` (lane, 1,024-record step and 4,096 / 8,192-record chunk edges) as
+    a compact read near N, a wide (general) read and a big read must fail in
+    both record formats; the same reads with every contig < N must match the
+    oracle."""
+    n = 3000
+    rng = np.random.default_rng(pos + 1)
+
+    def build(read):
+        rows = [(r, int(c)) for r, c in enumerate(rng.integers(0, n - 40, pos))]
+        r = pos
+        rows += [(r, c) for c in read]
+        rest = rng.integers(0, n - 40, 30_000)
+        rows += [(r + 1 + i, int(c)) for i, c in enumerate(rest)]
+        return np.array(rows, np.uint32)
+
+    bad_reads = [[n - 2, n], [n - 1, n + 2, n - 1], [5, 900, n + 7], [10 + i for i in range(11)] + [n],
+                 [n + 100], [n - 3, n - 3, n - 1, n - 2, n + 1]]
+    for read in bad_reads:
+        rec = build(read)
+        for flagged in (False, True):
+            x = engine.flag_records(rec) if flagged else rec
+            with pytest.raises(_lib.KarmaError):
+                engine.graph_from_records(x, n, flagged=flagged)
+    for read in ([n - 2, n - 1], [n - 4, n - 1, n - 2], [n - 1], [5, 900, n - 1], [10 + i for i in range(11)] + [n - 1]):
+        check_records(build(read), n)
+
+
 def test_eq_vs_oracle_seeded():
     classes = synth.eq_classes(31, 2000, 300_000, True)
     names = [f"ctg{i}" for i in range(2000)]
