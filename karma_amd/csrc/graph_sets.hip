@@ -269,19 +269,24 @@ __device__ __forceinline__ bool in_mask(uint64_t m) { return __builtin_amdgcn_in
 // range check reports (the call fails), and bin_emit clamps the bucket so that
 // such a code stays inside the queues meanwhile (one op per staged code instead
 // of one compare per record)
+// (*m0_out: the read's first contig at full width -- K23's m0 << 4 drops its
+// top 4 bits -- for the replay's exact range check)
 template <bool COMPACT, bool K23 = false>
-__device__ __forceinline__ uint64_t rs_code_m(const RState& s, uint32_t N, uint32_t* code) {
+__device__ __forceinline__ uint64_t rs_code_m(const RState& s, uint32_t N, uint32_t* code, uint32_t* m0_out) {
     const uint32_t z = (uint32_t)__builtin_ctz(s.win);
     const uint32_t rel = s.win >> z, m0 = s.fm3 + z;
     *code = K23 ? m0 << 4 | rel : m0 | (rel >> 1) << 24;
+    *m0_out = m0;
     return COMPACT ? lanes(rel < 16u) & (K23 ? ~0ull : lanes(m0 < N)) : 0ull;
 }
 template <bool COMPACT, bool K23 = false>
-__device__ __forceinline__ uint64_t rs_code2_m(const RState& a, const RState& b, uint32_t N, uint32_t* code) {
+__device__ __forceinline__ uint64_t rs_code2_m(const RState& a, const RState& b, uint32_t N, uint32_t* code,
+                                               uint32_t* m0_out) {
     const uint32_t za = (uint32_t)__builtin_ctz(a.win), zb = (uint32_t)__builtin_ctz(b.win);
     const uint32_t ma = a.fm3 + za, mb = b.fm3 + zb, m0 = min(ma, mb);
     const uint32_t rel = ((a.win >> za) << min(ma - m0, 31u)) | ((b.win >> zb) << min(mb - m0, 31u));
     *code = K23 ? m0 << 4 | rel : m0 | (rel >> 1) << 24;
+    *m0_out = m0;
     return COMPACT ? lanes(rel < 16u) & (K23 ? ~0ull : lanes(m0 < N)) : 0ull;
 }
 
@@ -297,6 +302,15 @@ constexpr int kRareMax = int(kCChunk / kCIter);  // steps per chunk
 constexpr int kRareW = 5;                        // words per listed step
 #ifndef KARMA_CLS_RANGE_CODE
 #define KARMA_CLS_RANGE_CODE 3  // binned flagged classify: 1 the walk on raw words, 2 the range checked per code (RC)
+#endif
+#ifndef KARMA_CLS_PACKED
+#define KARMA_CLS_PACKED 0  // binned flagged walk: own reads staged as (fm3 << 8 | 8-bit window), coded in bin_stage
+#endif
+#ifndef KARMA_CLS_EMIT_DUMMY
+#define KARMA_CLS_EMIT_DUMMY 0  // binned flagged walk: every lane stores its code (no exec-mask branch per record)
+#endif
+#ifndef KARMA_CLS_HLEN_MAIN
+#define KARMA_CLS_HLEN_MAIN 0  // 1: the main pass tracks the head's length per record too (the round-6 walk)
 #endif
 #ifndef KARMA_CLS_PIN
 #define KARMA_CLS_PIN 2  // walk state pinned per record (see the walk): 1 with 16 records per lane, 2 always
@@ -374,6 +388,13 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // (general_kernel, big_pairs_kernel); the chunk-end tail read here
     constexpr bool RC = BIN && FLAG && (KARMA_CLS_RANGE_CODE & 2) && KARMA_CLS_DEFER_RARE;
     constexpr bool RAW = FLAG && (KARMA_CLS_RANGE_CODE & 1);  // the walk on raw words (measurement split)
+    // PK: the binned flagged walk stages each own read's state as it ends,
+    // (fm3 << 8 | win) with an 8-bit window (bit 7: a contig outside [fm3,
+    // fm3 + 6]), one shift-or per record; bin_stage turns 64 of them at a time
+    // into codes and lists the step when one is not compact.  fm3 keeps 24
+    // bits there, so the range guard lists steps with any contig >= 2^24
+    constexpr bool PK = RC && RAW && RPL > 8 && KARMA_CLS_PACKED;
+    constexpr uint32_t kWinTop = PK ? 7u : 31u;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t chunk = P.c0 + (int64_t)blockIdx.x * (kCW / 64) + wave;
@@ -393,7 +414,9 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // banks mod 64) alike.  BIN: half of it (rows of lanes 0-31, then of lanes
     // 32-63), to leave LDS for the bucket queues at 4 blocks per CU.
     constexpr int kRows = BIN ? 32 : 64;
-    __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][kRows * 4];
+    // (+ 16 granules: the emit's slots for lanes without a code, KARMA_CLS_EMIT_DUMMY)
+    constexpr int kDummy = BIN && FLAG && KARMA_CLS_EMIT_DUMMY ? 16 : 0;
+    __shared__ __attribute__((aligned(16))) u32x4 tbuf[kCW / 64][kRows * 4 + kDummy];
     u32x4* tb = tbuf[wave];
     // the chunk's codes per code bucket, added to its partition block's row at the end
     __shared__ uint32_t whist[kCW / 64][HIST ? kMaxBc : 1];
@@ -475,18 +498,43 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     // walk's 8 emit points
     uint32_t* const stg = reinterpret_cast<uint32_t*>(tb);
     const uint32_t* const stg_l = stg + lane;
+    uint32_t* const stg_dummy = stg + 16 * kRows + lane;  // (kDummy)
     uint32_t ns = 0;  // staged codes (uniform)
+    uint32_t nc = 0, ng = 0;  // the chunk's codes and general reads
+    // one value per lane of `b` into the staging area (kDummy: every lane
+    // stores, the others into a slot of their own past it: no exec-mask branch)
+    auto stage = [&](uint64_t b, uint32_t v) {
+        if (kDummy) {
+            uint32_t r = (uint32_t)rank_below(b);
+            asm volatile("" : "+v"(r));  // in every lane, then one select of the address
+            uint32_t* const sp = in_mask(b) ? stg + ns + r : stg_dummy;
+            *sp = v;
+        } else if (in_mask(b)) {
+            stg[ns + (uint32_t)rank_below(b)] = v;
+        }
+        ns += __popcll(b);
+    };
     static_assert(kBinQ == 64, "queue slots: bk << 6");
     // RC: staged codes whose contigs may reach N (m0 >= N - 3), this step
-    uint64_t stage_hi = 0;
+    uint64_t stage_hi = 0, hi_next = 0;
     const uint32_t code_hi = ((uint32_t)max(P.N, 3u) - 3u) << 4;
     auto bin_stage = [&]() {
         if (!ns) return;
         wave_lds_order();
         for (uint32_t j0 = 0; j0 < ns; j0 += 64) {
             // unpredicated read (ns <= 512 codes: the 2 KB buffer; j0 + lane < 512 always; past ns masked off)
-            const uint32_t cd = stg_l[j0];
-            const uint64_t m = lanes((uint32_t)lane < ns - j0);
+            uint32_t cd = stg_l[j0];
+            uint64_t m = lanes((uint32_t)lane < ns - j0);
+            if (PK) {
+                // (fm3 << 8 | win) -> m0 << 4 | rel: q = m0 << 8 | win (mod 2^32)
+                const uint32_t win = cd & 255u, z = (uint32_t)__builtin_ctz(win), rel = win >> z;
+                const uint32_t q = cd + (z << 8);
+                cd = ((q >> 4) & ~15u) | rel;
+                const uint64_t okm = m & lanes(rel < 16u);
+                stage_hi |= m & ~okm;  // a general or big read: the step goes to the replay
+                m = okm;
+                nc += __popcll(okm);
+            }
             if (RC) stage_hi |= m & lanes(cd >= code_hi);
             bin_emit(m, cd);
         }
@@ -538,7 +586,6 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
     bool ct_ok = false;  // a tail read (started in this chunk) is carried
     RState ct{};
     uint32_t ct_len = 0, ct_pos = 0;
-    uint32_t nc = 0, ng = 0;
     uint64_t bad_order = 0, bad_contig = 0;  // lane masks
     // one 512-record step from `buf`, which then takes the next step's loads
     // (two steps in flight -- a second register set at 4 waves/SIMD -- measured
@@ -675,6 +722,18 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
 #pragma unroll
                 for (int i = 1; i < RPL; ++i) cmax = max(cmax, ctg[i]);
                 bad_contig |= lanes(cmax >= P.N);
+            } else {
+                // a contig >= 2^28 would wrap out of the staged code's m0 << 4
+                // (and pass the per-code test below): its step goes to the
+                // replay, which checks at full width (one OR per record)
+                // (and the next step too when lane 63 holds one: its tail read
+                // is emitted there)
+                uint32_t o = rid[0];
+#pragma unroll
+                for (int i = 1; i < RPL; ++i) o |= rid[i];
+                const uint64_t hi = lanes((o & (PK ? 0x7F000000u : 0x70000000u)) != 0u);
+                stage_hi |= hi | hi_next;
+                hi_next = hi >> 63;
             }
         }
         const uint32_t ubase = (uint32_t)(t0 - c_lo) + (uint32_t)RPL * lane;
@@ -692,12 +751,16 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             constexpr bool RARE = decltype(rare_pass)::value;
             uint64_t rare = 0;
             // e: lanes where a read ends here; ok: ... it is compact (code); big: ... it has > 8 records
-            auto emit = [&](uint64_t e, uint64_t ok, uint32_t code, uint32_t pos, uint64_t big) {
+            auto emit = [&](uint64_t e, uint64_t ok, uint32_t code, uint32_t m0, uint32_t pos, uint64_t big) {
                 if (!RARE) {
                     const uint64_t b = e & ok & ~big;
+                    if (PK) {  // (the merged read; counted in bin_stage) m0 - 3, rel at bit 3
+                        stage(b, (m0 - 3u) << 8 | (code & 15u) << 3);
+                        rare |= e & (big | ~ok);
+                        return;
+                    }
                     if (BIN) {
-                        if (in_mask(b)) stg[ns + (uint32_t)rank_below(b)] = code;
-                        ns += __popcll(b);
+                        stage(b, code);
                     } else {
                         // lanes without a code store past the region (bit 31): dropped
                         const uint32_t boff =
@@ -711,8 +774,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     if (RC) {  // the step's compact codes (m0 << 4 | rel): their top contig < N
                         const uint64_t cm = e & ok & ~big;
                         if (cm)
-                            bad_contig |= cm & lanes((code >> 4) + 31u - (uint32_t)__builtin_clz(code & 15u) >=
-                                                     PA().N);
+                            bad_contig |= cm & lanes(m0 + 31u - (uint32_t)__builtin_clz(code & 15u) >= PA().N);
                     }
                     const uint64_t g = e & ~big & ~ok;
                     if (g) {
@@ -741,6 +803,11 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             hd = st;
             spos = 0;
             uint32_t hlen = in_mask(S0) ? 0u : (uint32_t)RPL;  // head: records before the first start (RPL: none)
+            // the head's length matters only for a non-compact read (general or
+            // big), whose step the main pass lists for the replay anyway: with
+            // 16 records per lane the main pass needs only "no start in the
+            // lane" (~started), one select per record less
+            constexpr bool HLEN = RARE || RPL <= 8 || KARMA_CLS_HLEN_MAIN;
             started = S0;
             uint64_t Si = S0;
 #pragma unroll
@@ -752,7 +819,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                 if (i > 0) {
                     const uint64_t cap = Si & ~started;  // the first start: the head ends here
                     hd.win = in_mask(cap) ? st.win : hd.win;
-                    hlen = in_mask(cap) ? (uint32_t)i : hlen;
+                    if (HLEN) hlen = in_mask(cap) ? (uint32_t)i : hlen;
                     started |= Si;
                     spos = in_mask(Si) ? (uint32_t)i : spos;
                     if (RAW) {
@@ -761,7 +828,7 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                         // record's w is its contig
                         const uint32_t w = rid[i];
                         const uint32_t fm3 = in_mask(Si) ? w - 0x80000003u : st.fm3;
-                        st.win = in_mask(Si) ? 8u : st.win | (1u << min(w - fm3, 31u));
+                        st.win = in_mask(Si) ? 8u : st.win | (1u << min(w - fm3, kWinTop));
                         st.fm3 = fm3;
                     } else {
                         const uint32_t c = ctg[i];
@@ -778,21 +845,26 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
                     const uint64_t Sn = S(i + 1);
                     const uint64_t e = Sn & started & (FULL ? ~0ull : lanes(i < nval));
                     Si = Sn;
-                    uint32_t code;
-                    const uint64_t ok = rs_code_m<COMPACT, BIN>(st, P.N, &code);
-                    // an own read of > 8 records (16 per lane) that is not
-                    // compact is a big read (the general path reads 8); a compact
-                    // one is a code like any other (its contig set is the code)
-                    const uint64_t big_own =
-                        RARE && i + 1 > kMaxFast ? lanes((uint32_t)i + 1u - spos > (uint32_t)kMaxFast) & ~ok : 0ull;
-                    emit(e, ok, code, ubase + spos, big_own);
+                    if (PK && !RARE) {  // the read's state, coded in bin_stage
+                        stage(e, st.fm3 << 8 | st.win);
+                    } else {
+                        uint32_t code, m0;
+                        const uint64_t ok = rs_code_m<COMPACT, BIN>(st, P.N, &code, &m0);
+                        // an own read of > 8 records (16 per lane) that is not
+                        // compact is a big read (the general path reads 8); a compact
+                        // one is a code like any other (its contig set is the code)
+                        const uint64_t big_own =
+                            RARE && i + 1 > kMaxFast ? lanes((uint32_t)i + 1u - spos > (uint32_t)kMaxFast) & ~ok : 0ull;
+                        emit(e, ok, code, m0, ubase + spos, big_own);
+                    }
                 }
                 // 16 records: pin the walk's state at each record, or the compiler
                 // sinks the head's selects and the rare mask past the loop and
                 // keeps every record's lane masks alive for them (SGPRs spilled
                 // into VGPR lanes)
                 if (KARMA_CLS_PIN > 1 || (RPL > 8 && KARMA_CLS_PIN)) {
-                    asm volatile("" : "+v"(hd.win), "+v"(hlen), "+v"(spos), "+v"(st.win), "+v"(st.fm3));
+                    asm volatile("" : "+v"(hd.win), "+v"(spos), "+v"(st.win), "+v"(st.fm3));
+                    if (HLEN) asm volatile("" : "+v"(hlen));
                     asm volatile("" : "+s"(started), "+s"(rare), "+s"(Si));
                 }
             }
@@ -815,17 +887,18 @@ classify2_kernel(ClassArgs P, BinArgs Q) {
             RState hm;
             hm.fm3 = in_mask(cont) ? hd.fm3 : in.fm3;
             hm.win = in_mask(cont) ? hd.win : in.win;
-            uint32_t code;
-            const uint64_t ok = rs_code2_m<COMPACT, BIN>(in, hm, P.N, &code);
+            uint32_t code, m0;
+            const uint64_t ok = rs_code2_m<COMPACT, BIN>(in, hm, P.N, &code, &m0);
             // big: the read runs past this lane (no start in it: its length is
             // unknown here), or has > 8 records.  16 records per lane: a read
             // seen whole (tail alone, or tail + head) is a code when compact,
             // whatever its length, and big only when general and > 8 records
             const uint64_t big =
-                RPL > 8 ? (cont & lanes(hlen == (uint32_t)RPL)) |
-                              (lanes(in_len + (in_mask(cont) ? hlen : 0u) > (uint32_t)kMaxFast) & ~ok)
+                RPL > 8 ? (!HLEN ? cont & ~started
+                                 : (cont & lanes(hlen == (uint32_t)RPL)) |
+                                       (lanes(in_len + (in_mask(cont) ? hlen : 0u) > (uint32_t)kMaxFast) & ~ok))
                         : cont & lanes(in_len + hlen > (uint32_t)kMaxFast);
-            emit(have, ok, code, in_pos, big);
+            emit(have, ok, code, m0, in_pos, big);
             return rare;
         };
         if (REPLAY) {

@@ -405,8 +405,10 @@ def test_records_contig_range_per_read_kind(pos):
         rows += [(r + 1 + i, int(c)) for i, c in enumerate(rest)]
         return np.array(rows, np.uint32)
 
+    # (ids >= 2^28: the staged code's m0 << 4 would wrap them onto small ids)
     bad_reads = [[n - 2, n], [n - 1, n + 2, n - 1], [5, 900, n + 7], [10 + i for i in range(11)] + [n],
-                 [n + 100], [n - 3, n - 3, n - 1, n - 2, n + 1]]
+                 [n + 100], [n - 3, n - 3, n - 1, n - 2, n + 1], [(1 << 28) + 5], [(1 << 28) + 5, (1 << 28) + 7],
+                 [(1 << 30) + 2, (1 << 30) + 2], [(1 << 31) - 1], [7, (1 << 29) + 8]]
     for read in bad_reads:
         rec = build(read)
         for flagged in (False, True):
