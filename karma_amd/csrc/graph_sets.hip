@@ -2021,7 +2021,10 @@ constexpr int kRT = 1024;               // pair-reduce threads (16 waves)
 constexpr int kBand = 8192;             // band counters per bucket (32 KB)
 constexpr int kHashR = 4096;            // hash slots per pair-reduce block
 constexpr int kHashF = 8192;            // hash slots per final (per-bucket) block
-constexpr int kFT = 1024;               // final-kernel threads
+#ifndef KARMA_FINAL_THREADS
+#define KARMA_FINAL_THREADS 512  // 1024: 8-rank strong preview 0.151-0.169 against 0.145-0.148 ms (r06t)
+#endif
+constexpr int kFT = KARMA_FINAL_THREADS;  // final-kernel threads
 constexpr int kSlotCap = kBand + kHashF;  // output pairs per bucket, at most
 
 template <int CAP, int THREADS>

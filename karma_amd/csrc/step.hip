@@ -58,7 +58,10 @@ struct StepStatus {
 };
 static_assert(sizeof(StepStatus) == 64, "status entry");
 
-constexpr int kET = 1024;  // edge-stage tile (elements per block round)
+#ifndef KARMA_EDGE_THREADS
+#define KARMA_EDGE_THREADS 512  // with 512-thread final blocks (graph_sets.hip kFT), profiles/r06/measurements.md (r06t)
+#endif
+constexpr int kET = KARMA_EDGE_THREADS;  // edge-stage tile (elements per block round)
 constexpr int kMaxRuns = 64;
 
 // ---- edge stage on device-sized lists ----------------------------------------
