@@ -1360,8 +1360,14 @@ static int profile_rows(karma_kmer_plan* p, int64_t lo, int64_t hi, double* out,
         const bool p56 = p->kmode == KARMA_KMER_5P6;
         const bool c16 = KARMA_PROF_C16 && c->max_len < 65536;
         const int64_t t_pad = (tab_entries(p56, p->S) + 7) & ~7;
-        const size_t lds = (size_t)(t_pad * tab_copies(t_pad)) * 2 +
-                           (kPBlock / 64) * (size_t)(hist_words(M, c16) + kProfWin) * 4;
+        size_t lds = (size_t)(t_pad * tab_copies(t_pad)) * 2 +
+                     (kPBlock / 64) * (size_t)(hist_words(M, c16) + kProfWin) * 4;
+        // KARMA_PROF_LDS_MIN (A/B): LDS per block at least this many bytes
+        static const size_t lds_min = [] {
+            const char* e = std::getenv("KARMA_PROF_LDS_MIN");
+            return e ? (size_t)std::atoll(e) : (size_t)0;
+        }();
+        lds = std::max(lds, lds_min);
 #define KARMA_WAVE_LAUNCH(P56, C16)                                                                              \
     do {                                                                                                         \
         const int g_ = resident_grid(ctx, reinterpret_cast<const void*>(&profile_wave_kernel<P56, C16>), kPBlock, \
